@@ -1,0 +1,433 @@
+// chess.h — bitboard chess core shared by host and device code of libgpu_nnue.
+//
+// Replaces, for the GPU path, what fishnet relies on the Stockfish process and
+// shakmaty for:
+//   - Position::set / FEN parsing with Chess960 castling (fishnet runs the
+//     engine with UCI_Chess960 = true, /root/reference/src/stockfish.rs:200),
+//   - legal move generation + do_move (children, perft),
+//   - the packed 32-byte board that is the device input format (gn_board).
+//
+// Sliding attacks: hyperbola quintessence on full 64-bit bit reversal
+// (v_bfrev_b32 on gfx950), one subtraction per line, no magics and no PEXT.
+// The line / leaper masks (4 KiB, struct Tables) live in LDS inside kernels
+// and in a static host copy for host callers.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/gpu_nnue.h"
+
+#define GN_HD __host__ __device__ __forceinline__
+
+namespace gn {
+
+typedef uint64_t Bitboard;
+enum { WHITE = 0, BLACK = 1 };
+enum { NO_PT = 0, PAWN = 1, KNIGHT = 2, BISHOP = 3, ROOK = 4, QUEEN = 5, KING = 6 };
+enum { MT_NORMAL = 0, MT_PROMOTION = 1, MT_EN_PASSANT = 2, MT_CASTLING = 3 };
+constexpr int SQ_NONE = 64;
+
+GN_HD Bitboard sqbb(int s) { return 1ull << s; }
+GN_HD int lsb(Bitboard b) { return __builtin_ctzll(b); }
+GN_HD int popcnt(Bitboard b) { return __builtin_popcountll(b); }
+GN_HD int pop_lsb(Bitboard &b) {
+  int s = lsb(b);
+  b &= b - 1;
+  return s;
+}
+GN_HD Bitboard rbit(Bitboard b) { return __builtin_bitreverse64(b); }
+GN_HD int make_piece(int c, int pt) { return (c << 3) | pt; }
+GN_HD int rel_sq(int c, int s) { return c == WHITE ? s : s ^ 56; }
+
+// line masks exclude the square itself: [0] file, [1] rank, [2] a1-h8 diagonal, [3] h1-a8 diagonal
+struct Tables {
+  Bitboard line[4][64];
+  Bitboard knight[64];
+  Bitboard king[64];
+  Bitboard pawn[2][64]; // squares attacked by a pawn of colour c standing on s
+};
+static_assert(sizeof(Tables) == 4096, "tables are 4 KiB");
+
+inline void init_tables(Tables &T) {
+  for (int s = 0; s < 64; ++s) {
+    int f = s & 7, r = s >> 3;
+    Bitboard file = 0x0101010101010101ull << f, rank = 0xFFull << (8 * r), d = 0, a = 0;
+    for (int k = -7; k <= 7; ++k) {
+      if (f + k >= 0 && f + k < 8 && r + k >= 0 && r + k < 8) d |= sqbb((r + k) * 8 + f + k);
+      if (f + k >= 0 && f + k < 8 && r - k >= 0 && r - k < 8) a |= sqbb((r - k) * 8 + f + k);
+    }
+    T.line[0][s] = file & ~sqbb(s);
+    T.line[1][s] = rank & ~sqbb(s);
+    T.line[2][s] = d & ~sqbb(s);
+    T.line[3][s] = a & ~sqbb(s);
+    static const int kn[8][2] = {{1, 2}, {2, 1}, {2, -1}, {1, -2}, {-1, -2}, {-2, -1}, {-2, 1}, {-1, 2}};
+    Bitboard n = 0, k = 0;
+    for (int i = 0; i < 8; ++i) {
+      int nf = f + kn[i][0], nr = r + kn[i][1];
+      if (nf >= 0 && nf < 8 && nr >= 0 && nr < 8) n |= sqbb(nr * 8 + nf);
+    }
+    for (int df = -1; df <= 1; ++df)
+      for (int dr = -1; dr <= 1; ++dr) {
+        int nf = f + df, nr = r + dr;
+        if ((df || dr) && nf >= 0 && nf < 8 && nr >= 0 && nr < 8) k |= sqbb(nr * 8 + nf);
+      }
+    T.knight[s] = n;
+    T.king[s] = k;
+    Bitboard pw = 0, pb = 0;
+    if (r < 7) {
+      if (f > 0) pw |= sqbb(s + 7);
+      if (f < 7) pw |= sqbb(s + 9);
+    }
+    if (r > 0) {
+      if (f > 0) pb |= sqbb(s - 9);
+      if (f < 7) pb |= sqbb(s - 7);
+    }
+    T.pawn[WHITE][s] = pw;
+    T.pawn[BLACK][s] = pb;
+  }
+}
+
+// hyperbola quintessence: attacks along one line with occupancy occ
+GN_HD Bitboard line_attacks(Bitboard occ, int s, Bitboard mask) {
+  Bitboard o = occ & mask;
+  Bitboard f = o - sqbb(s);
+  Bitboard r = rbit(rbit(o) - rbit(sqbb(s)));
+  return (f ^ r) & mask;
+}
+GN_HD Bitboard rook_attacks(const Tables &T, int s, Bitboard occ) {
+  return line_attacks(occ, s, T.line[0][s]) | line_attacks(occ, s, T.line[1][s]);
+}
+GN_HD Bitboard bishop_attacks(const Tables &T, int s, Bitboard occ) {
+  return line_attacks(occ, s, T.line[2][s]) | line_attacks(occ, s, T.line[3][s]);
+}
+// squares strictly between a and b when aligned, else 0
+GN_HD Bitboard between(const Tables &T, int a, int b) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (T.line[k][a] & sqbb(b)) return line_attacks(sqbb(b), a, T.line[k][a]) & line_attacks(sqbb(a), b, T.line[k][b]);
+  return 0;
+}
+// full line through a and b (both included) when aligned, else 0
+GN_HD Bitboard line_through(const Tables &T, int a, int b) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (T.line[k][a] & sqbb(b)) return T.line[k][a] | sqbb(a);
+  return 0;
+}
+
+// Bitboard position.  byType[0] = all occupied squares.
+struct Board {
+  Bitboard byType[7];
+  Bitboard byColor[2];
+  uint8_t stm;
+  uint8_t ep;             // SQ_NONE when none
+  uint8_t castle_rook[4]; // [2c + 0] O-O rook square, [2c + 1] O-O-O rook square, SQ_NONE
+  uint16_t rule50;
+  uint16_t fullmove;
+};
+
+// Runtime-selected bitboards through unrolled constant indices only: keeps a
+// Board in VGPRs on the device (no scratch) and can never index out of range.
+GN_HD Bitboard color_bb(const Board &B, int c) { return c ? B.byColor[1] : B.byColor[0]; }
+GN_HD void xor_color(Board &B, int c, Bitboard b) {
+  if (c) B.byColor[1] ^= b;
+  else B.byColor[0] ^= b;
+}
+GN_HD void or_color(Board &B, int c, Bitboard b) {
+  if (c) B.byColor[1] |= b;
+  else B.byColor[0] |= b;
+}
+GN_HD void xor_type(Board &B, int pt, Bitboard b) {
+#pragma unroll
+  for (int t = PAWN; t <= KING; ++t) B.byType[t] ^= (t == pt) ? b : 0;
+}
+GN_HD void or_type(Board &B, int pt, Bitboard b) {
+#pragma unroll
+  for (int t = PAWN; t <= KING; ++t) B.byType[t] |= (t == pt) ? b : 0;
+}
+
+GN_HD int piece_on(const Board &B, int s) {
+  Bitboard b = sqbb(s);
+  if (!(B.byType[0] & b)) return 0;
+  int c = (B.byColor[BLACK] & b) ? BLACK : WHITE;
+  int pt = PAWN;
+#pragma unroll
+  for (int t = PAWN; t <= KING; ++t)
+    if (B.byType[t] & b) pt = t;
+  return make_piece(c, pt);
+}
+
+GN_HD Bitboard attackers_to(const Board &B, const Tables &T, int s, Bitboard occ) {
+  return (T.pawn[BLACK][s] & B.byColor[WHITE] & B.byType[PAWN]) |
+         (T.pawn[WHITE][s] & B.byColor[BLACK] & B.byType[PAWN]) | (T.knight[s] & B.byType[KNIGHT]) |
+         (T.king[s] & B.byType[KING]) | (rook_attacks(T, s, occ) & (B.byType[ROOK] | B.byType[QUEEN])) |
+         (bishop_attacks(T, s, occ) & (B.byType[BISHOP] | B.byType[QUEEN]));
+}
+
+GN_HD int king_square(const Board &B, int c) { return lsb(B.byType[KING] & color_bb(B, c)); }
+
+GN_HD bool in_check(const Board &B, const Tables &T) {
+  int us = B.stm;
+  return (attackers_to(B, T, king_square(B, us), B.byType[0]) & color_bb(B, us ^ 1)) != 0;
+}
+
+// ------------------------------------------------------------- packing ----
+// piece nibbles of a gn_board as two 64-bit words (nibble k of lo | hi << 64);
+// avoids dynamic indexing into a register-resident byte array on the device
+GN_HD void piece_words(const gn_board &p, uint64_t &lo, uint64_t &hi) {
+  __builtin_memcpy(&lo, p.pc, 8);
+  __builtin_memcpy(&hi, p.pc + 8, 8);
+}
+GN_HD int piece_nibble(uint64_t lo, uint64_t hi, int k) {
+  return (int)(((k < 16 ? lo : hi) >> (4 * (k & 15))) & 15);
+}
+
+// Unpacks and validates a gn_board.  Returns false for anything the device
+// must not touch (bad piece nibble, not exactly one king per side, > 32 pieces,
+// pawns on a back rank, bad en-passant square).  Whether the side not to move
+// is in check is NOT checked here.
+GN_HD bool unpack(const gn_board &p, Board &B) {
+  for (int i = 0; i < 7; ++i) B.byType[i] = 0;
+  B.byColor[0] = B.byColor[1] = 0;
+  Bitboard occ = p.occ;
+  int n = popcnt(occ);
+  if (n < 2 || n > 32) return false;
+  bool ok = true;
+  uint64_t wlo, whi;
+  piece_words(p, wlo, whi);
+  for (int k = 0; occ; ++k) {
+    int s = pop_lsb(occ);
+    int pc = piece_nibble(wlo, whi, k);
+    int pt = pc & 7;
+    ok &= pt >= PAWN && pt <= KING;
+    or_type(B, pt, sqbb(s));
+    or_color(B, pc >> 3, sqbb(s));
+  }
+  B.byType[0] = p.occ;
+  ok &= popcnt(B.byType[KING] & B.byColor[WHITE]) == 1 && popcnt(B.byType[KING] & B.byColor[BLACK]) == 1;
+  ok &= (B.byType[PAWN] & 0xFF000000000000FFull) == 0;
+  B.stm = p.stm_ep >> 7;
+  B.ep = p.stm_ep & 0x7F;
+  if (B.ep > SQ_NONE) ok = false;
+  for (int i = 0; i < 4; ++i) {
+    int nib = (p.castle >> (4 * i)) & 15;
+    B.castle_rook[i] = (nib & 8) ? (uint8_t)(((i >> 1) ? 56 : 0) + (nib & 7)) : (uint8_t)SQ_NONE;
+  }
+  B.rule50 = p.rule50;
+  B.fullmove = p.fullmove;
+  return ok;
+}
+
+GN_HD void pack(const Board &B, gn_board &p) {
+  p.occ = B.byType[0];
+  uint64_t lo = 0, hi = 0;
+  Bitboard occ = B.byType[0];
+  for (int k = 0; occ; ++k) {
+    int s = pop_lsb(occ);
+    uint64_t v = (uint64_t)piece_on(B, s) << (4 * (k & 15));
+    if (k < 16) lo |= v;
+    else hi |= v;
+  }
+  __builtin_memcpy(p.pc, &lo, 8);
+  __builtin_memcpy(p.pc + 8, &hi, 8);
+  p.stm_ep = (uint8_t)((B.stm << 7) | B.ep);
+  p.reserved = 0;
+  uint16_t c = 0;
+  for (int i = 0; i < 4; ++i)
+    if (B.castle_rook[i] != SQ_NONE) c |= (uint16_t)((8 | (B.castle_rook[i] & 7)) << (4 * i));
+  p.castle = c;
+  p.rule50 = B.rule50;
+  p.fullmove = B.fullmove;
+}
+
+// --------------------------------------------------------------- moves ----
+GN_HD uint16_t make_move(int from, int to, int type = MT_NORMAL, int promo = KNIGHT) {
+  return (uint16_t)(to | (from << 6) | ((promo - KNIGHT) << 12) | (type << 14));
+}
+GN_HD int move_from(uint16_t m) { return (m >> 6) & 63; }
+GN_HD int move_to(uint16_t m) { return m & 63; }
+GN_HD int move_type(uint16_t m) { return m >> 14; }
+GN_HD int move_promo(uint16_t m) { return ((m >> 12) & 3) + KNIGHT; }
+
+// Legal move generator.  emit(uint16_t move) is called once per legal move,
+// in a fixed order (king, knights, sliders, pawns, castling).
+template <class F>
+GN_HD void gen_legal(const Board &B, const Tables &T, F &&emit) {
+  const int us = B.stm, them = us ^ 1;
+  const Bitboard occ = B.byType[0], ours = color_bb(B, us), theirs = color_bb(B, them);
+  const int ksq = king_square(B, us);
+  const Bitboard checkers = attackers_to(B, T, ksq, occ) & theirs;
+  // king
+  {
+    Bitboard tg = T.king[ksq] & ~ours, occ_nok = occ ^ sqbb(ksq);
+    while (tg) {
+      int to = pop_lsb(tg);
+      if (!(attackers_to(B, T, to, occ_nok) & theirs)) emit(make_move(ksq, to));
+    }
+  }
+  if (checkers & (checkers - 1)) return; // double check: king moves only
+  // pinned pieces
+  Bitboard pinned = 0;
+  {
+    Bitboard rq = (B.byType[ROOK] | B.byType[QUEEN]) & theirs, bq = (B.byType[BISHOP] | B.byType[QUEEN]) & theirs;
+    Bitboard snipers = ((T.line[0][ksq] | T.line[1][ksq]) & rq) | ((T.line[2][ksq] | T.line[3][ksq]) & bq);
+    while (snipers) {
+      int s = pop_lsb(snipers);
+      Bitboard b = between(T, ksq, s) & occ;
+      if (b && !(b & (b - 1)) && (b & ours)) pinned |= b;
+    }
+  }
+  const Bitboard target = checkers ? (between(T, ksq, lsb(checkers)) | checkers) : ~ours;
+  // knights (a pinned knight never moves)
+  {
+    Bitboard pcs = B.byType[KNIGHT] & ours & ~pinned;
+    while (pcs) {
+      int from = pop_lsb(pcs);
+      Bitboard tg = T.knight[from] & target;
+      while (tg) emit(make_move(from, pop_lsb(tg)));
+    }
+  }
+  // sliders
+  {
+    Bitboard pcs = (B.byType[BISHOP] | B.byType[ROOK] | B.byType[QUEEN]) & ours;
+    while (pcs) {
+      int from = pop_lsb(pcs);
+      Bitboard f = sqbb(from), att = 0;
+      if (f & (B.byType[ROOK] | B.byType[QUEEN])) att |= rook_attacks(T, from, occ);
+      if (f & (B.byType[BISHOP] | B.byType[QUEEN])) att |= bishop_attacks(T, from, occ);
+      att &= target;
+      if (pinned & f) att &= line_through(T, ksq, from);
+      while (att) emit(make_move(from, pop_lsb(att)));
+    }
+  }
+  // pawns
+  {
+    const int up = us == WHITE ? 8 : -8;
+    const Bitboard last = us == WHITE ? 0xFF00000000000000ull : 0xFFull;
+    const Bitboard start = us == WHITE ? 0xFF00ull : 0xFF000000000000ull;
+    Bitboard pcs = B.byType[PAWN] & ours;
+    while (pcs) {
+      int from = pop_lsb(pcs);
+      Bitboard f = sqbb(from), allowed = (pinned & f) ? line_through(T, ksq, from) : ~0ull;
+      Bitboard tg = 0;
+      int one = from + up;
+      if (!(occ & sqbb(one))) {
+        tg |= sqbb(one);
+        if ((f & start) && !(occ & sqbb(one + up))) tg |= sqbb(one + up);
+      }
+      tg |= T.pawn[us][from] & theirs;
+      tg &= target & allowed;
+      while (tg) {
+        int to = pop_lsb(tg);
+        if (sqbb(to) & last) {
+          emit(make_move(from, to, MT_PROMOTION, QUEEN));
+          emit(make_move(from, to, MT_PROMOTION, ROOK));
+          emit(make_move(from, to, MT_PROMOTION, BISHOP));
+          emit(make_move(from, to, MT_PROMOTION, KNIGHT));
+        } else
+          emit(make_move(from, to));
+      }
+      if (B.ep != SQ_NONE && (T.pawn[us][from] & sqbb(B.ep))) {
+        // full simulation: removes both pawns, adds ours on ep, recomputes attackers
+        int cap = B.ep - up;
+        Bitboard occ2 = (occ ^ f ^ sqbb(cap)) | sqbb(B.ep);
+        Bitboard th2 = theirs ^ sqbb(cap);
+        Bitboard att = ((rook_attacks(T, ksq, occ2) & (B.byType[ROOK] | B.byType[QUEEN])) |
+                        (bishop_attacks(T, ksq, occ2) & (B.byType[BISHOP] | B.byType[QUEEN])) |
+                        (T.knight[ksq] & B.byType[KNIGHT]) | (T.pawn[us][ksq] & B.byType[PAWN])) &
+                       th2;
+        if (!att) emit(make_move(from, B.ep, MT_EN_PASSANT));
+      }
+    }
+  }
+  // castling (Chess960 rules; generated only when not in check)
+  if (!checkers) {
+#pragma unroll
+    for (int side = 0; side < 2; ++side) {
+      int rsq = us ? B.castle_rook[2 + side] : B.castle_rook[side];
+      if (rsq == SQ_NONE) continue;
+      if (!(B.byType[ROOK] & ours & sqbb(rsq))) continue;
+      int kto = rel_sq(us, side == 0 ? 6 : 2), rto = rel_sq(us, side == 0 ? 5 : 3);
+      Bitboard kpath = between(T, ksq, kto) | sqbb(kto), rpath = between(T, rsq, rto) | sqbb(rto);
+      if ((kpath | rpath) & occ & ~sqbb(ksq) & ~sqbb(rsq)) continue;
+      Bitboard walk = kto == ksq ? 0 : kpath;
+      bool ok = true;
+      while (walk && ok) ok = !(attackers_to(B, T, pop_lsb(walk), occ) & theirs);
+      if (!ok) continue;
+      Bitboard occ2 = (occ ^ sqbb(ksq) ^ sqbb(rsq)) | sqbb(kto) | sqbb(rto);
+      Bitboard sl = ((rook_attacks(T, kto, occ2) & (B.byType[ROOK] | B.byType[QUEEN])) |
+                     (bishop_attacks(T, kto, occ2) & (B.byType[BISHOP] | B.byType[QUEEN]))) &
+                    theirs;
+      if (sl) continue;
+      emit(make_move(ksq, rsq, MT_CASTLING));
+    }
+  }
+}
+
+// What a move changes, for incremental feature-transformer updates.
+struct Dirty {
+  int n_rem, n_add;
+  int rem_sq[2], rem_pc[2]; // mover at from (or king at from for castling), captured piece
+  int add_sq[2], add_pc[2]; // mover / promoted piece at to, rook at rto
+  bool king_moved;          // mover's perspective needs a refresh
+};
+
+GN_HD Board do_move(const Board &B, uint16_t m, Dirty *d = nullptr) {
+  Board C = B;
+  const int us = B.stm, them = us ^ 1;
+  const int from = move_from(m), to = move_to(m), type = move_type(m);
+  const int pc = piece_on(B, from), pt = pc & 7;
+  const int ksq = king_square(B, us);
+  int captured = 0;
+  if (d) d->n_rem = d->n_add = 0, d->king_moved = pt == KING;
+  if (type == MT_CASTLING) {
+    int kside = to > from;
+    int kto = rel_sq(us, kside ? 6 : 2), rto = rel_sq(us, kside ? 5 : 3);
+    C.byType[KING] ^= sqbb(from) ^ sqbb(kto); // no-op when the king stays (kto == from)
+    C.byType[ROOK] ^= sqbb(to) ^ sqbb(rto);   // no-op when the rook stays (rto == to)
+    xor_color(C, us, sqbb(from) | sqbb(to));
+    or_color(C, us, sqbb(kto) | sqbb(rto));
+    C.byType[0] = C.byColor[0] | C.byColor[1];
+    if (d) {
+      d->n_rem = 2, d->rem_sq[0] = from, d->rem_pc[0] = make_piece(us, KING), d->rem_sq[1] = to,
+      d->rem_pc[1] = make_piece(us, ROOK);
+      d->n_add = 2, d->add_sq[0] = kto, d->add_pc[0] = make_piece(us, KING), d->add_sq[1] = rto,
+      d->add_pc[1] = make_piece(us, ROOK);
+    }
+  } else {
+    int capsq = type == MT_EN_PASSANT ? to - (us == WHITE ? 8 : -8) : to;
+    captured = piece_on(B, capsq);
+    if (captured) {
+      xor_type(C, captured & 7, sqbb(capsq));
+      xor_color(C, them, sqbb(capsq));
+    }
+    int newpt = type == MT_PROMOTION ? move_promo(m) : pt;
+    xor_type(C, pt, sqbb(from));
+    or_type(C, newpt, sqbb(to));
+    xor_color(C, us, sqbb(from) | sqbb(to));
+    C.byType[0] = C.byColor[0] | C.byColor[1];
+    if (d) {
+      d->rem_sq[0] = from, d->rem_pc[0] = pc, d->n_rem = 1;
+      if (captured) d->rem_sq[1] = capsq, d->rem_pc[1] = captured, d->n_rem = 2;
+      d->add_sq[0] = to, d->add_pc[0] = make_piece(us, newpt), d->n_add = 1;
+    }
+  }
+  C.rule50 = (type != MT_CASTLING && (pt == PAWN || captured)) ? 0 : (B.rule50 < 65535 ? B.rule50 + 1 : 65535);
+  C.ep = SQ_NONE;
+  if (pt == PAWN && (to ^ from) == 16) {
+    // ep square only when an enemy pawn stands beside the pushed pawn (it can capture)
+    Bitboard adj = ((sqbb(to) << 1) & ~0x0101010101010101ull) | ((sqbb(to) >> 1) & ~0x8080808080808080ull);
+    if (adj & B.byType[PAWN] & color_bb(B, them)) C.ep = (uint8_t)((from + to) / 2);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    int r = C.castle_rook[i];
+    if (r == SQ_NONE) continue;
+    if (r == from || r == to || ((i >> 1) == us && from == ksq)) C.castle_rook[i] = SQ_NONE;
+  }
+  if (us == BLACK && C.fullmove < 65535) C.fullmove++;
+  C.stm = (uint8_t)them;
+  return C;
+}
+
+} // namespace gn

@@ -1,0 +1,780 @@
+// gpu_nnue.hip — C-ABI of libgpu_nnue.so (see include/gpu_nnue.h).
+//
+// Host side of the boundary that replaces the per-core Stockfish processes'
+// static evaluation for batch workloads (/root/reference/src/stockfish.rs:36-47
+// is the plugin API it sits beside).  Owns: the .nnue loader, device memory,
+// one HIP stream per device, FEN packing, and the launch sequences of the
+// kernels in kernels.hip.
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "host_board.h"
+#include "kernels.h"
+
+using namespace gn;
+
+// ------------------------------------------------------------ errors ------
+static thread_local std::string g_err;
+
+static int fail(int code, const char *fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                               \
+  do {                                                                                              \
+    hipError_t e_ = (expr);                                                                         \
+    if (e_ != hipSuccess) return fail(GN_E_HIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), \
+                                      __FILE__, __LINE__);                                          \
+  } while (0)
+
+namespace gn {
+const Tables &host_tables() {
+  static Tables T = [] {
+    Tables t;
+    init_tables(t);
+    return t;
+  }();
+  return T;
+}
+} // namespace gn
+
+// ----------------------------------------------------------- net file -----
+struct HostNet {
+  int L1 = 0;
+  uint32_t hash = 0;
+  std::vector<uint8_t> ft;    // [22528][2*L1 + 32]
+  std::vector<int16_t> bias;  // [L1], doubled
+  std::vector<int8_t> w0, w1, w2;
+  std::vector<int32_t> b0, b1, b2;
+};
+
+struct Reader {
+  const uint8_t *p;
+  size_t n, off = 0;
+  bool take(void *dst, size_t k) {
+    if (off + k > n) return false;
+    memcpy(dst, p + off, k);
+    off += k;
+    return true;
+  }
+  bool u32(uint32_t &v) {
+    uint8_t b[4];
+    if (!take(b, 4)) return false;
+    v = (uint32_t)b[0] | (uint32_t)b[1] << 8 | (uint32_t)b[2] << 16 | (uint32_t)b[3] << 24;
+    return true;
+  }
+  // signed LEB128 block ("COMPRESSED_LEB128", u32 byte count, payload)
+  template <class Emit>
+  bool leb(int bits, size_t count, Emit &&emit) {
+    char magic[17];
+    uint32_t nbytes;
+    if (!take(magic, 17) || memcmp(magic, "COMPRESSED_LEB128", 17) || !u32(nbytes) || off + nbytes > n) return false;
+    const uint8_t *q = p + off, *end = q + nbytes;
+    for (size_t i = 0; i < count; ++i) {
+      uint32_t r = 0;
+      int shift = 0;
+      for (;;) {
+        if (q >= end || shift >= bits) return false;
+        const uint8_t byte = *q++;
+        r |= (uint32_t)(byte & 0x7f) << shift;
+        shift += 7;
+        if (!(byte & 0x80)) {
+          if (shift < 32 && (byte & 0x40)) r |= ~((1u << shift) - 1u);
+          break;
+        }
+      }
+      emit(i, bits == 16 ? (int32_t)(int16_t)(uint16_t)r : (int32_t)r);
+    }
+    if (q != end) return false;
+    off += nbytes;
+    return true;
+  }
+};
+
+static int parse_net(const uint8_t *data, size_t len, HostNet &h) {
+  Reader r{data, len};
+  uint32_t version, hash, dlen, fth;
+  if (!r.u32(version) || version != NNUE_VERSION) return fail(GN_E_FORMAT, "not a Stockfish .nnue (version)");
+  if (!r.u32(hash) || !r.u32(dlen) || r.off + dlen > len) return fail(GN_E_FORMAT, "bad .nnue header");
+  r.off += dlen;
+  if (!r.u32(fth)) return fail(GN_E_FORMAT, "truncated .nnue");
+  int l1 = 0;
+  for (int c = 32; c <= 4096 && !l1; c += 32)
+    if (ft_hash(c) == fth && (ft_hash(c) ^ arch_hash(c)) == hash) l1 = c;
+  if (!l1) return fail(GN_E_FORMAT, "network hash 0x%08x does not match a HalfKAv2_hm architecture", hash);
+  if (l1 != 3072 && l1 != 1024 && l1 != 128) return fail(GN_E_FORMAT, "unsupported L1 width %d", l1);
+  h.L1 = l1;
+  h.hash = hash;
+  const size_t RS = 2 * (size_t)l1 + 32;
+  h.ft.assign((size_t)FT_INPUTS * RS, 0);
+  h.bias.resize(l1);
+  uint8_t *ft = h.ft.data();
+  if (!r.leb(16, l1, [&](size_t i, int32_t v) { h.bias[i] = (int16_t)(uint16_t)(v * 2); }))
+    return fail(GN_E_FORMAT, "bad feature-transformer biases");
+  if (!r.leb(16, (size_t)l1 * FT_INPUTS, [&](size_t i, int32_t v) {
+        const int16_t d = (int16_t)(uint16_t)(v * 2);
+        memcpy(ft + (i / l1) * RS + 2 * (i % l1), &d, 2);
+      }))
+    return fail(GN_E_FORMAT, "bad feature-transformer weights");
+  if (!r.leb(32, (size_t)PSQT_BUCKETS * FT_INPUTS, [&](size_t i, int32_t v) {
+        memcpy(ft + (i / PSQT_BUCKETS) * RS + 2 * l1 + 4 * (i % PSQT_BUCKETS), &v, 4);
+      }))
+    return fail(GN_E_FORMAT, "bad PSQT weights");
+  h.w0.resize((size_t)LAYER_STACKS * 16 * l1);
+  h.w1.resize(LAYER_STACKS * 32 * 32);
+  h.w2.resize(LAYER_STACKS * 32);
+  h.b0.resize(LAYER_STACKS * 16);
+  h.b1.resize(LAYER_STACKS * 32);
+  h.b2.resize(LAYER_STACKS);
+  const uint32_t ah = arch_hash(l1);
+  for (int s = 0; s < LAYER_STACKS; ++s) {
+    uint32_t hs;
+    if (!r.u32(hs) || hs != ah) return fail(GN_E_FORMAT, "bad layer-stack hash in stack %d", s);
+    bool ok = true;
+    for (int i = 0; i < 16 && ok; ++i) ok = r.u32(reinterpret_cast<uint32_t &>(h.b0[s * 16 + i]));
+    ok = ok && r.take(&h.w0[(size_t)s * 16 * l1], (size_t)16 * l1);
+    for (int i = 0; i < 32 && ok; ++i) ok = r.u32(reinterpret_cast<uint32_t &>(h.b1[s * 32 + i]));
+    ok = ok && r.take(&h.w1[s * 1024], 1024);
+    ok = ok && r.u32(reinterpret_cast<uint32_t &>(h.b2[s]));
+    ok = ok && r.take(&h.w2[s * 32], 32);
+    if (!ok) return fail(GN_E_FORMAT, "truncated layer stack %d", s);
+  }
+  if (r.off != len) return fail(GN_E_FORMAT, "%zu trailing bytes after the network", len - r.off);
+  return GN_OK;
+}
+
+// ----------------------------------------------------------- context ------
+template <class T>
+struct DevBuf {
+  T *p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t n) {
+    if (n <= cap) return hipSuccess;
+    const size_t want = std::max(n, cap + cap / 2);
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    hipError_t e = hipMalloc(&p, std::max<size_t>(want, 1) * sizeof(T));
+    if (e == hipSuccess) cap = want;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr, cap = 0;
+  }
+};
+
+struct Dev {
+  int id = 0;
+  hipStream_t stream = nullptr;
+  void *net_mem[2] = {nullptr, nullptr};
+  NetDevice net[2] = {};
+  bool has[2] = {false, false};
+  Tables *tables = nullptr;
+  DevBuf<int2> osm, obg;
+  DevBuf<uint8_t> nsm, nbg;
+  DevBuf<gn_board> io_boards, frontier[2];
+  DevBuf<gn_eval> io_out, io_out2;
+  DevBuf<uint64_t> counts, offsets;
+  DevBuf<uint32_t> off32;
+  DevBuf<uint16_t> moves;
+  DevBuf<unsigned long long> sum;
+  void *scan_tmp = nullptr;
+  size_t scan_bytes = 0;
+  std::mutex mu;
+};
+
+struct gn_ctx {
+  std::vector<std::unique_ptr<Dev>> devs;
+  gn_eval_params P;
+  int l1[2] = {0, 0};
+  uint32_t hash[2] = {0, 0};
+};
+
+enum { BIG = 0, SMALL = 1 };
+
+static gn_eval_params default_params() {
+  gn_eval_params P;
+  P.small_net_threshold = 962;
+  P.psqt_weight = 125;
+  P.positional_weight = 131;
+  P.reeval_threshold = 236;
+  P.complexity_div_small = 18000;
+  P.complexity_div_big = 18000;
+  P.material_pawn_small = 535;
+  P.material_pawn_big = 535;
+  P.material_base = 77777;
+  P.rule50_div = 212;
+  P.value_clamp = 31506;
+  const int32_t pv[5] = {208, 781, 825, 1276, 2538};
+  memcpy(P.piece_value, pv, sizeof(pv));
+  return P;
+}
+
+static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+static int upload_net(Dev &d, int which, const HostNet &h) {
+  const size_t RS = 2 * (size_t)h.L1 + 32;
+  size_t off[8], o = 0;
+  const size_t sz[8] = {(size_t)FT_INPUTS * RS, h.bias.size() * 2, h.w0.size(), h.b0.size() * 4,
+                        h.w1.size(), h.b1.size() * 4, h.w2.size(), h.b2.size() * 4};
+  const void *src[8] = {h.ft.data(), h.bias.data(), h.w0.data(), h.b0.data(),
+                        h.w1.data(), h.b1.data(), h.w2.data(), h.b2.data()};
+  for (int i = 0; i < 8; ++i) off[i] = o, o += align256(sz[i]);
+  uint8_t *m = nullptr;
+  if (hipMalloc(&m, o) != hipSuccess) return fail(GN_E_NOMEM, "device allocation of %zu bytes failed", o);
+  d.net_mem[which] = m;
+  for (int i = 0; i < 8; ++i) HIP_TRY(hipMemcpy(m + off[i], src[i], sz[i], hipMemcpyHostToDevice));
+  NetDevice &n = d.net[which];
+  n.L1 = h.L1;
+  n.row_stride = (uint32_t)RS;
+  n.ft = m + off[0];
+  n.bias = reinterpret_cast<const int16_t *>(m + off[1]);
+  n.w0 = reinterpret_cast<const int8_t *>(m + off[2]);
+  n.b0 = reinterpret_cast<const int32_t *>(m + off[3]);
+  n.w1 = reinterpret_cast<const int8_t *>(m + off[4]);
+  n.b1 = reinterpret_cast<const int32_t *>(m + off[5]);
+  n.w2 = reinterpret_cast<const int8_t *>(m + off[6]);
+  n.b2 = reinterpret_cast<const int32_t *>(m + off[7]);
+  d.has[which] = true;
+  return GN_OK;
+}
+
+static void destroy(gn_ctx *ctx) {
+  if (!ctx) return;
+  for (auto &dp : ctx->devs) {
+    Dev &d = *dp;
+    (void)hipSetDevice(d.id);
+    if (d.stream) (void)hipStreamSynchronize(d.stream);
+    for (void *m : d.net_mem)
+      if (m) (void)hipFree(m);
+    if (d.tables) (void)hipFree(d.tables);
+    d.osm.release(), d.obg.release(), d.nsm.release(), d.nbg.release();
+    d.io_boards.release(), d.frontier[0].release(), d.frontier[1].release();
+    d.io_out.release(), d.io_out2.release(), d.counts.release(), d.offsets.release();
+    d.off32.release(), d.moves.release(), d.sum.release();
+    if (d.scan_tmp) (void)hipFree(d.scan_tmp);
+    if (d.stream) (void)hipStreamDestroy(d.stream);
+  }
+  delete ctx;
+}
+
+static int create(const uint8_t *big, size_t big_len, const uint8_t *small, size_t small_len, const int *devices,
+                  int n_devices, gn_ctx **out) {
+  if (!out) return fail(GN_E_INVALID, "out is NULL");
+  *out = nullptr;
+  if (!big && !small) return fail(GN_E_INVALID, "no network given");
+  HostNet hn[2];
+  if (big) {
+    int rc = parse_net(big, big_len, hn[BIG]);
+    if (rc) return rc;
+  }
+  if (small) {
+    int rc = parse_net(small, small_len, hn[SMALL]);
+    if (rc) return rc;
+  }
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return fail(GN_E_NODEVICE, "no HIP device visible");
+  std::vector<int> ids;
+  if (devices && n_devices > 0) ids.assign(devices, devices + n_devices);
+  else ids.push_back(0);
+  std::unique_ptr<gn_ctx, void (*)(gn_ctx *)> ctx(new gn_ctx(), destroy);
+  ctx->P = default_params();
+  for (int w = 0; w < 2; ++w) ctx->l1[w] = hn[w].L1, ctx->hash[w] = hn[w].hash;
+  for (int id : ids) {
+    if (id < 0 || id >= count) return fail(GN_E_NODEVICE, "device %d out of range (%d visible)", id, count);
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, id));
+    if (!strstr(prop.gcnArchName, "gfx950"))
+      return fail(GN_E_NODEVICE, "device %d is %s; libgpu_nnue is built for gfx950 only", id, prop.gcnArchName);
+    ctx->devs.emplace_back(new Dev());
+    Dev &d = *ctx->devs.back();
+    d.id = id;
+    HIP_TRY(hipSetDevice(id));
+    HIP_TRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+    HIP_TRY(hipMalloc(&d.tables, sizeof(Tables)));
+    HIP_TRY(hipMemcpy(d.tables, &host_tables(), sizeof(Tables), hipMemcpyHostToDevice));
+    for (int w = 0; w < 2; ++w)
+      if (hn[w].L1) {
+        int rc = upload_net(d, w, hn[w]);
+        if (rc) return rc;
+      }
+  }
+  *out = ctx.release();
+  return GN_OK;
+}
+
+static bool read_file(const char *path, std::vector<uint8_t> &buf) {
+  FILE *f = fopen(path, "rb");
+  if (!f) return false;
+  fseek(f, 0, SEEK_END);
+  long n = ftell(f);
+  fseek(f, 0, SEEK_SET);
+  buf.resize(n > 0 ? (size_t)n : 0);
+  bool ok = n >= 0 && fread(buf.data(), 1, buf.size(), f) == buf.size();
+  fclose(f);
+  return ok;
+}
+
+// ---------------------------------------------------------- launches ------
+struct KernelTimes {
+  hipEvent_t ev[10];
+  bool on = false;
+};
+
+static int evaluate_on(gn_ctx *ctx, Dev &d, const gn_board *b, size_t n, int mode, gn_eval *out, hipStream_t s,
+                       float *kt /* [4] accumulated ms or null */) {
+  if (mode < GN_MODE_FULL || mode > GN_MODE_SMALL) return fail(GN_E_INVALID, "bad mode %d", mode);
+  if ((mode != GN_MODE_SMALL && !d.has[BIG]) || (mode != GN_MODE_BIG && !d.has[SMALL]))
+    return fail(GN_E_NONET, "mode %d needs a network that is not loaded", mode);
+  if (!n) return GN_OK;
+  if (mode != GN_MODE_BIG) HIP_TRY(d.osm.ensure(n));
+  if (mode != GN_MODE_SMALL) HIP_TRY(d.obg.ensure(n));
+  if (mode == GN_MODE_FULL) {
+    HIP_TRY(d.nsm.ensure(n));
+    HIP_TRY(d.nbg.ensure(n));
+  }
+  hipEvent_t ev[6] = {};
+  if (kt)
+    for (auto &e : ev) HIP_TRY(hipEventCreate(&e));
+  auto mark = [&](int k) -> hipError_t { return kt ? hipEventRecord(ev[k], s) : hipSuccess; };
+  const gn_eval_params &P = ctx->P;
+  HIP_TRY(mark(0));
+  if (mode == GN_MODE_FULL) HIP_TRY(launch_classify(b, n, P, d.nsm.p, d.nbg.p, s));
+  HIP_TRY(mark(1));
+  if (mode != GN_MODE_BIG) HIP_TRY(launch_eval_net(d.net[SMALL], b, mode == GN_MODE_FULL ? d.nsm.p : nullptr, n, d.osm.p, s));
+  if (mode == GN_MODE_FULL) HIP_TRY(launch_reeval(d.osm.p, d.nsm.p, n, P, d.nbg.p, s));
+  HIP_TRY(mark(2));
+  if (mode != GN_MODE_SMALL) HIP_TRY(launch_eval_net(d.net[BIG], b, mode == GN_MODE_FULL ? d.nbg.p : nullptr, n, d.obg.p, s));
+  HIP_TRY(mark(3));
+  HIP_TRY(launch_finalize(b, n, mode, d.osm.p, d.obg.p, d.nsm.p, d.nbg.p, P, d.tables, out, s));
+  HIP_TRY(mark(4));
+  if (kt) {
+    HIP_TRY(hipEventSynchronize(ev[4]));
+    for (int k = 0; k < 4; ++k) {
+      float ms = 0;
+      HIP_TRY(hipEventElapsedTime(&ms, ev[k], ev[k + 1]));
+      kt[k] += ms;
+    }
+    for (auto &e : ev) (void)hipEventDestroy(e);
+  }
+  return GN_OK;
+}
+
+static Dev *slot(gn_ctx *ctx, int s) {
+  if (!ctx || s < 0 || s >= (int)ctx->devs.size()) return nullptr;
+  return ctx->devs[s].get();
+}
+
+template <class F>
+static void parallel_for(size_t n, size_t grain, F &&f) {
+  unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  size_t chunks = std::min<size_t>(hw, (n + grain - 1) / std::max<size_t>(grain, 1));
+  if (chunks <= 1) {
+    f(0, n);
+    return;
+  }
+  std::vector<std::thread> th;
+  size_t per = (n + chunks - 1) / chunks;
+  for (size_t c = 0; c < chunks; ++c) {
+    size_t lo = c * per, hi = std::min(n, lo + per);
+    if (lo < hi) th.emplace_back([=, &f] { f(lo, hi); });
+  }
+  for (auto &t : th) t.join();
+}
+
+// expansion on one device with library-owned buffers; fills children boards
+// into d.frontier[1] and moves into d.moves; returns total via *total
+static int expand_children(Dev &d, const gn_board *parents, size_t n, size_t *total, hipStream_t s,
+                           bool want_moves) {
+  HIP_TRY(d.counts.ensure(n + 1));
+  HIP_TRY(d.offsets.ensure(n + 1));
+  HIP_TRY(hipMemsetAsync(d.counts.p + n, 0, sizeof(uint64_t), s));
+  HIP_TRY(launch_count_children(parents, n, d.tables, d.counts.p, s));
+  HIP_TRY(exclusive_scan_u64(d.counts.p, d.offsets.p, n + 1, d.scan_tmp, d.scan_bytes, s));
+  uint64_t t = 0;
+  HIP_TRY(hipMemcpyAsync(&t, d.offsets.p + n, sizeof(t), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  *total = (size_t)t;
+  if (!t) return GN_OK;
+  HIP_TRY(d.frontier[1].ensure(t));
+  if (want_moves) HIP_TRY(d.moves.ensure(t));
+  HIP_TRY(launch_write_children(parents, n, d.tables, d.offsets.p, d.frontier[1].p, want_moves ? d.moves.p : nullptr, s));
+  return GN_OK;
+}
+
+// ============================================================ C-ABI ========
+extern "C" {
+
+int gn_abi_version(void) { return GN_ABI_VERSION; }
+
+const char *gn_last_error(void) { return g_err.c_str(); }
+
+int gn_load_net(const char *big_path, const char *small_path, const int *devices, int n_devices, gn_ctx **out) {
+  try {
+    std::vector<uint8_t> b, s;
+    if (big_path && !read_file(big_path, b)) return fail(GN_E_IO, "cannot read %s", big_path);
+    if (small_path && !read_file(small_path, s)) return fail(GN_E_IO, "cannot read %s", small_path);
+    return create(big_path ? b.data() : nullptr, b.size(), small_path ? s.data() : nullptr, s.size(), devices,
+                  n_devices, out);
+  } catch (const std::bad_alloc &) {
+    return fail(GN_E_NOMEM, "host allocation failed");
+  } catch (...) {
+    return fail(GN_E_INVALID, "unexpected exception");
+  }
+}
+
+int gn_load_net_memory(const uint8_t *big, size_t big_len, const uint8_t *small, size_t small_len, const int *devices,
+                       int n_devices, gn_ctx **out) {
+  try {
+    return create(big, big_len, small, small_len, devices, n_devices, out);
+  } catch (const std::bad_alloc &) {
+    return fail(GN_E_NOMEM, "host allocation failed");
+  } catch (...) {
+    return fail(GN_E_INVALID, "unexpected exception");
+  }
+}
+
+void gn_free(gn_ctx *ctx) { destroy(ctx); }
+
+int gn_get_eval_params(const gn_ctx *ctx, gn_eval_params *out) {
+  if (!out) return fail(GN_E_INVALID, "out is NULL");
+  *out = ctx ? ctx->P : default_params();
+  return GN_OK;
+}
+
+int gn_set_eval_params(gn_ctx *ctx, const gn_eval_params *p) {
+  if (!ctx || !p) return fail(GN_E_INVALID, "NULL argument");
+  if (p->material_base == 0 || p->rule50_div == 0 || p->complexity_div_small == 0 || p->complexity_div_big == 0)
+    return fail(GN_E_INVALID, "zero divisor in eval params");
+  ctx->P = *p;
+  return GN_OK;
+}
+
+int gn_net_info(const gn_ctx *ctx, int *big_l1, uint32_t *big_hash, int *small_l1, uint32_t *small_hash) {
+  if (!ctx) return fail(GN_E_INVALID, "ctx is NULL");
+  if (big_l1) *big_l1 = ctx->l1[BIG];
+  if (big_hash) *big_hash = ctx->hash[BIG];
+  if (small_l1) *small_l1 = ctx->l1[SMALL];
+  if (small_hash) *small_hash = ctx->hash[SMALL];
+  return GN_OK;
+}
+
+int gn_pack_fens(const char *const *fens, size_t n, gn_board *out, uint8_t *ok) {
+  if (n && (!fens || !out)) return fail(GN_E_INVALID, "NULL argument");
+  try {
+    parallel_for(n, 4096, [&](size_t lo, size_t hi) {
+      for (size_t i = lo; i < hi; ++i) {
+        Board B;
+        bool good = parse_fen(fens[i], B);
+        if (good) pack(B, out[i]);
+        else memset(&out[i], 0, sizeof(gn_board));
+        if (ok) ok[i] = good;
+      }
+    });
+  } catch (...) {
+    return fail(GN_E_NOMEM, "thread start failed");
+  }
+  return GN_OK;
+}
+
+int gn_board_to_fen(const gn_board *board, char *buf, size_t buflen) {
+  if (!board || !buf) return fail(GN_E_INVALID, "NULL argument");
+  Board B;
+  if (!unpack(*board, B)) return fail(GN_E_INVALID, "invalid board");
+  if (board_to_fen(B, buf, buflen) < 0) return fail(GN_E_CAPACITY, "buffer too small");
+  return GN_OK;
+}
+
+int gn_random_positions(uint64_t seed, size_t first_index, size_t n, int max_plies, gn_board *out) {
+  if (n && !out) return fail(GN_E_INVALID, "NULL argument");
+  if (max_plies < 0) return fail(GN_E_INVALID, "max_plies < 0");
+  try {
+    parallel_for(n, 256, [&](size_t lo, size_t hi) {
+      for (size_t i = lo; i < hi; ++i) pack(random_playout(seed + first_index + i, max_plies), out[i]);
+    });
+  } catch (...) {
+    return fail(GN_E_NOMEM, "thread start failed");
+  }
+  return GN_OK;
+}
+
+int gn_evaluate_device(gn_ctx *ctx, int device_slot, const gn_board *d_boards, size_t n, int mode, gn_eval *d_out,
+                       void *stream) {
+  Dev *d = slot(ctx, device_slot);
+  if (!d) return fail(GN_E_INVALID, "bad context or device slot");
+  if (n && (!d_boards || !d_out)) return fail(GN_E_INVALID, "NULL buffer");
+  std::lock_guard<std::mutex> lk(d->mu);
+  HIP_TRY(hipSetDevice(d->id));
+  return evaluate_on(ctx, *d, d_boards, n, mode, d_out, stream ? (hipStream_t)stream : d->stream, nullptr);
+}
+
+int gn_time_evaluate_device(gn_ctx *ctx, int device_slot, const gn_board *d_boards, size_t n, int mode,
+                            gn_eval *d_out, int iters, float *ms_total, float *per_kernel_ms) {
+  Dev *d = slot(ctx, device_slot);
+  if (!d) return fail(GN_E_INVALID, "bad context or device slot");
+  if (iters <= 0 || !ms_total) return fail(GN_E_INVALID, "bad iters / ms_total");
+  std::lock_guard<std::mutex> lk(d->mu);
+  HIP_TRY(hipSetDevice(d->id));
+  hipEvent_t a, b;
+  HIP_TRY(hipEventCreate(&a));
+  HIP_TRY(hipEventCreate(&b));
+  HIP_TRY(hipEventRecord(a, d->stream));
+  for (int it = 0; it < iters; ++it) {
+    int rc = evaluate_on(ctx, *d, d_boards, n, mode, d_out, d->stream, nullptr);
+    if (rc) return rc;
+  }
+  HIP_TRY(hipEventRecord(b, d->stream));
+  HIP_TRY(hipEventSynchronize(b));
+  HIP_TRY(hipEventElapsedTime(ms_total, a, b));
+  (void)hipEventDestroy(a);
+  (void)hipEventDestroy(b);
+  if (per_kernel_ms) {
+    float kt[4] = {0, 0, 0, 0};
+    for (int it = 0; it < iters; ++it) {
+      int rc = evaluate_on(ctx, *d, d_boards, n, mode, d_out, d->stream, kt);
+      if (rc) return rc;
+    }
+    for (int k = 0; k < 4; ++k) per_kernel_ms[k] = kt[k] / (float)iters;
+  }
+  return GN_OK;
+}
+
+int gn_device_alloc(gn_ctx *ctx, int device_slot, size_t bytes, void **ptr) {
+  Dev *d = slot(ctx, device_slot);
+  if (!d || !ptr) return fail(GN_E_INVALID, "bad argument");
+  HIP_TRY(hipSetDevice(d->id));
+  if (hipMalloc(ptr, std::max<size_t>(bytes, 1)) != hipSuccess) return fail(GN_E_NOMEM, "hipMalloc(%zu) failed", bytes);
+  return GN_OK;
+}
+
+int gn_device_free(gn_ctx *ctx, int device_slot, void *ptr) {
+  Dev *d = slot(ctx, device_slot);
+  if (!d) return fail(GN_E_INVALID, "bad argument");
+  HIP_TRY(hipSetDevice(d->id));
+  if (ptr) HIP_TRY(hipFree(ptr));
+  return GN_OK;
+}
+
+int gn_memcpy_h2d(gn_ctx *ctx, int device_slot, void *dst, const void *src, size_t bytes) {
+  Dev *d = slot(ctx, device_slot);
+  if (!d) return fail(GN_E_INVALID, "bad argument");
+  HIP_TRY(hipSetDevice(d->id));
+  HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, d->stream));
+  HIP_TRY(hipStreamSynchronize(d->stream));
+  return GN_OK;
+}
+
+int gn_memcpy_d2h(gn_ctx *ctx, int device_slot, void *dst, const void *src, size_t bytes) {
+  Dev *d = slot(ctx, device_slot);
+  if (!d) return fail(GN_E_INVALID, "bad argument");
+  HIP_TRY(hipSetDevice(d->id));
+  HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, d->stream));
+  HIP_TRY(hipStreamSynchronize(d->stream));
+  return GN_OK;
+}
+
+int gn_synchronize(gn_ctx *ctx, int device_slot) {
+  Dev *d = slot(ctx, device_slot);
+  if (!d) return fail(GN_E_INVALID, "bad argument");
+  HIP_TRY(hipSetDevice(d->id));
+  HIP_TRY(hipStreamSynchronize(d->stream));
+  return GN_OK;
+}
+
+int gn_evaluate_batch_mode(gn_ctx *ctx, const char *const *fens, size_t n, int mode, gn_eval *out) {
+  if (!ctx) return fail(GN_E_INVALID, "ctx is NULL");
+  if (n && (!fens || !out)) return fail(GN_E_INVALID, "NULL argument");
+  if (!n) return GN_OK;
+  try {
+    std::vector<gn_board> boards(n);
+    int rc = gn_pack_fens(fens, n, boards.data(), nullptr);
+    if (rc) return rc;
+    const size_t nd = ctx->devs.size(), per = (n + nd - 1) / nd;
+    std::vector<int> rcs(nd, GN_OK);
+    std::vector<std::string> errs(nd);
+    auto work = [&](size_t k) {
+      const size_t lo = k * per, hi = std::min(n, lo + per);
+      if (lo >= hi) return;
+      Dev &d = *ctx->devs[k];
+      std::lock_guard<std::mutex> lk(d.mu);
+      auto run = [&]() -> int {
+        HIP_TRY(hipSetDevice(d.id));
+        HIP_TRY(d.io_boards.ensure(hi - lo));
+        HIP_TRY(d.io_out.ensure(hi - lo));
+        HIP_TRY(hipMemcpyAsync(d.io_boards.p, boards.data() + lo, (hi - lo) * sizeof(gn_board), hipMemcpyHostToDevice,
+                               d.stream));
+        int r = evaluate_on(ctx, d, d.io_boards.p, hi - lo, mode, d.io_out.p, d.stream, nullptr);
+        if (r) return r;
+        HIP_TRY(hipMemcpyAsync(out + lo, d.io_out.p, (hi - lo) * sizeof(gn_eval), hipMemcpyDeviceToHost, d.stream));
+        HIP_TRY(hipStreamSynchronize(d.stream));
+        return GN_OK;
+      };
+      rcs[k] = run();
+      if (rcs[k]) errs[k] = g_err;
+    };
+    if (nd == 1) work(0);
+    else {
+      std::vector<std::thread> th;
+      for (size_t k = 0; k < nd; ++k) th.emplace_back(work, k);
+      for (auto &t : th) t.join();
+    }
+    for (size_t k = 0; k < nd; ++k)
+      if (rcs[k]) {
+        g_err = errs[k];
+        return rcs[k];
+      }
+    return GN_OK;
+  } catch (const std::bad_alloc &) {
+    return fail(GN_E_NOMEM, "host allocation failed");
+  } catch (...) {
+    return fail(GN_E_INVALID, "unexpected exception");
+  }
+}
+
+int gn_evaluate_batch(gn_ctx *ctx, const char *const *fens, size_t n, gn_eval *out) {
+  return gn_evaluate_batch_mode(ctx, fens, n, GN_MODE_FULL, out);
+}
+
+int gn_expand_device(gn_ctx *ctx, int device_slot, const gn_board *d_parents, size_t n, int mode,
+                     gn_eval *d_parent_out, uint32_t *d_offsets, gn_board *d_children, uint16_t *d_moves,
+                     gn_eval *d_child_out, size_t cap, size_t *total, void *stream) {
+  Dev *d = slot(ctx, device_slot);
+  if (!d || !total) return fail(GN_E_INVALID, "bad argument");
+  if (n && (!d_parents || !d_offsets)) return fail(GN_E_INVALID, "NULL buffer");
+  std::lock_guard<std::mutex> lk(d->mu);
+  HIP_TRY(hipSetDevice(d->id));
+  hipStream_t s = stream ? (hipStream_t)stream : d->stream;
+  *total = 0;
+  if (!n) return GN_OK;
+  HIP_TRY(d->counts.ensure(n + 1));
+  HIP_TRY(d->offsets.ensure(n + 1));
+  HIP_TRY(hipMemsetAsync(d->counts.p + n, 0, sizeof(uint64_t), s));
+  HIP_TRY(launch_count_children(d_parents, n, d->tables, d->counts.p, s));
+  HIP_TRY(exclusive_scan_u64(d->counts.p, d->offsets.p, n + 1, d->scan_tmp, d->scan_bytes, s));
+  uint64_t t = 0;
+  HIP_TRY(hipMemcpyAsync(&t, d->offsets.p + n, sizeof(t), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  *total = (size_t)t;
+  if (t > 0xFFFFFFFFull) return fail(GN_E_CAPACITY, "%llu children exceed 32-bit offsets", (unsigned long long)t);
+  HIP_TRY(launch_offsets_u32(d->offsets.p, n + 1, d_offsets, s));
+  if (t > cap) {
+    HIP_TRY(hipStreamSynchronize(s));
+    return fail(GN_E_CAPACITY, "%llu children exceed capacity %zu", (unsigned long long)t, cap);
+  }
+  if (t && (!d_children || !d_moves || !d_child_out)) return fail(GN_E_INVALID, "NULL child buffer");
+  HIP_TRY(launch_write_children(d_parents, n, d->tables, d->offsets.p, d_children, d_moves, s));
+  if (t) {
+    int rc = evaluate_on(ctx, *d, d_children, t, mode, d_child_out, s, nullptr);
+    if (rc) return rc;
+  }
+  if (d_parent_out) {
+    int rc = evaluate_on(ctx, *d, d_parents, n, mode, d_parent_out, s, nullptr);
+    if (rc) return rc;
+  }
+  HIP_TRY(hipStreamSynchronize(s));
+  return GN_OK;
+}
+
+int gn_expand_and_evaluate(gn_ctx *ctx, const char *const *parent_fens, size_t n, int mode, gn_eval *parent_out,
+                           uint32_t *child_offsets, uint16_t *child_moves, gn_eval *child_out, size_t cap) {
+  Dev *d = slot(ctx, 0);
+  if (!d) return fail(GN_E_INVALID, "bad context");
+  if (n && (!parent_fens || !child_offsets)) return fail(GN_E_INVALID, "NULL argument");
+  if (!n) {
+    if (child_offsets) child_offsets[0] = 0;
+    return GN_OK;
+  }
+  try {
+    std::vector<gn_board> boards(n);
+    int rc = gn_pack_fens(parent_fens, n, boards.data(), nullptr);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> lk(d->mu);
+    HIP_TRY(hipSetDevice(d->id));
+    hipStream_t s = d->stream;
+    HIP_TRY(d->io_boards.ensure(n));
+    HIP_TRY(hipMemcpyAsync(d->io_boards.p, boards.data(), n * sizeof(gn_board), hipMemcpyHostToDevice, s));
+    size_t total = 0;
+    rc = expand_children(*d, d->io_boards.p, n, &total, s, true);
+    if (rc) return rc;
+    std::vector<uint64_t> off(n + 1);
+    HIP_TRY(hipMemcpyAsync(off.data(), d->offsets.p, (n + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (total > 0xFFFFFFFFull) return fail(GN_E_CAPACITY, "children exceed 32-bit offsets");
+    for (size_t i = 0; i <= n; ++i) child_offsets[i] = (uint32_t)off[i];
+    if (total > cap) return fail(GN_E_CAPACITY, "%zu children exceed capacity %zu", total, cap);
+    if (total && (!child_moves || !child_out)) return fail(GN_E_INVALID, "NULL child buffer");
+    if (total) {
+      HIP_TRY(d->io_out2.ensure(total));
+      rc = evaluate_on(ctx, *d, d->frontier[1].p, total, mode, d->io_out2.p, s, nullptr);
+      if (rc) return rc;
+      HIP_TRY(hipMemcpyAsync(child_out, d->io_out2.p, total * sizeof(gn_eval), hipMemcpyDeviceToHost, s));
+      HIP_TRY(hipMemcpyAsync(child_moves, d->moves.p, total * sizeof(uint16_t), hipMemcpyDeviceToHost, s));
+    }
+    if (parent_out) {
+      HIP_TRY(d->io_out.ensure(n));
+      rc = evaluate_on(ctx, *d, d->io_boards.p, n, mode, d->io_out.p, s, nullptr);
+      if (rc) return rc;
+      HIP_TRY(hipMemcpyAsync(parent_out, d->io_out.p, n * sizeof(gn_eval), hipMemcpyDeviceToHost, s));
+    }
+    HIP_TRY(hipStreamSynchronize(s));
+    return GN_OK;
+  } catch (const std::bad_alloc &) {
+    return fail(GN_E_NOMEM, "host allocation failed");
+  } catch (...) {
+    return fail(GN_E_INVALID, "unexpected exception");
+  }
+}
+
+int gn_perft(gn_ctx *ctx, const char *fen, int depth, uint64_t *nodes) {
+  Dev *d = slot(ctx, 0);
+  if (!d || !fen || !nodes) return fail(GN_E_INVALID, "bad argument");
+  Board B;
+  if (!parse_fen(fen, B)) return fail(GN_E_INVALID, "bad FEN");
+  if (depth <= 0) {
+    *nodes = 1;
+    return GN_OK;
+  }
+  std::lock_guard<std::mutex> lk(d->mu);
+  HIP_TRY(hipSetDevice(d->id));
+  hipStream_t s = d->stream;
+  gn_board root;
+  pack(B, root);
+  HIP_TRY(d->frontier[0].ensure(1));
+  HIP_TRY(hipMemcpyAsync(d->frontier[0].p, &root, sizeof(root), hipMemcpyHostToDevice, s));
+  size_t n = 1;
+  for (int level = 1; level < depth; ++level) {
+    size_t total = 0;
+    int rc = expand_children(*d, d->frontier[0].p, n, &total, s, false);
+    if (rc) return rc;
+    std::swap(d->frontier[0], d->frontier[1]);
+    n = total;
+    if (!n) break;
+  }
+  unsigned long long sum = 0;
+  if (n) {
+    HIP_TRY(d->sum.ensure(1));
+    HIP_TRY(hipMemsetAsync(d->sum.p, 0, sizeof(unsigned long long), s));
+    HIP_TRY(launch_count_sum(d->frontier[0].p, n, d->tables, d->sum.p, s));
+    HIP_TRY(hipMemcpyAsync(&sum, d->sum.p, sizeof(sum), hipMemcpyDeviceToHost, s));
+  }
+  HIP_TRY(hipStreamSynchronize(s));
+  *nodes = sum;
+  return GN_OK;
+}
+
+} // extern "C"

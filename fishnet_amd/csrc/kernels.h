@@ -1,0 +1,41 @@
+// kernels.h — host-side launchers for the gfx950 kernels in kernels.hip.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "nnue.h"
+
+namespace gn {
+
+// NetworkOutput {psqt / 16, positional / 16} for every position whose
+// need[i] != 0 (need == nullptr: all); other entries of out are untouched.
+hipError_t launch_eval_net(const NetDevice &net, const gn_board *boards, const uint8_t *need, size_t n,
+                           int2 *out, hipStream_t s);
+// GN_MODE_FULL preparation: need_small = valid && |simple_eval| > threshold,
+// need_big = valid && !need_small.
+hipError_t launch_classify(const gn_board *boards, size_t n, const gn_eval_params &P, uint8_t *need_small,
+                           uint8_t *need_big, hipStream_t s);
+// GN_MODE_FULL: marks need_big where the small net's |nnue| < reeval_threshold.
+hipError_t launch_reeval(const int2 *out_small, const uint8_t *need_small, size_t n, const gn_eval_params &P,
+                         uint8_t *need_big, hipStream_t s);
+// Eval::evaluate epilogue -> gn_eval (flags incl. IN_CHECK / BAD_FEN).
+hipError_t launch_finalize(const gn_board *boards, size_t n, int mode, const int2 *out_small,
+                           const int2 *out_big, const uint8_t *need_small, const uint8_t *need_big,
+                           const gn_eval_params &P, const Tables *tables, gn_eval *out, hipStream_t s);
+// legal-move counts per board (invalid boards: 0)
+hipError_t launch_count_children(const gn_board *boards, size_t n, const Tables *tables, uint64_t *counts,
+                                 hipStream_t s);
+// children of every board at offsets[i] (exclusive prefix sums of counts)
+hipError_t launch_write_children(const gn_board *boards, size_t n, const Tables *tables,
+                                 const uint64_t *offsets, gn_board *children, uint16_t *moves, hipStream_t s);
+// sum of legal-move counts over all boards into *total (added; caller zeroes)
+hipError_t launch_count_sum(const gn_board *boards, size_t n, const Tables *tables,
+                            unsigned long long *total, hipStream_t s);
+// narrowing copy of offsets for the C-ABI
+hipError_t launch_offsets_u32(const uint64_t *in, size_t n, uint32_t *out, hipStream_t s);
+// exclusive scan of n + 1 counts (counts[n] must be 0); temp grows on demand
+hipError_t exclusive_scan_u64(const uint64_t *counts, uint64_t *offsets, size_t n1, void *&temp,
+                              size_t &temp_bytes, hipStream_t s);
+
+} // namespace gn

@@ -1,0 +1,473 @@
+// kernels.hip — gfx950 kernels of libgpu_nnue.
+//
+// eval_net<L1, PAR>   the hot path: HalfKAv2_hm feature-transformer gather-
+//                     accumulate (int16 rows, wrapping adds) + transform +
+//                     the bucket-grouped int8 MFMA layer stack, one 16-position
+//                     tile per workgroup.
+// classify / reeval / finalize   Eval::evaluate.
+// count / write children, count_sum   legal movegen for expansion and perft.
+#include <hipcub/hipcub.hpp>
+
+#include "kernels.h"
+
+namespace gn {
+
+typedef unsigned short ushort8 __attribute__((ext_vector_type(8)));
+typedef int int4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ int32_t wmul(int32_t a, int32_t b) { return (int32_t)((uint32_t)a * (uint32_t)b); }
+__device__ __forceinline__ int32_t wadd(int32_t a, int32_t b) { return (int32_t)((uint32_t)a + (uint32_t)b); }
+__device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : v > hi ? hi : v; }
+
+__device__ __forceinline__ void load_tables(Tables &dst, const Tables *src) {
+  const uint4 *s = reinterpret_cast<const uint4 *>(src);
+  uint4 *d = reinterpret_cast<uint4 *>(&dst);
+  for (int i = threadIdx.x; i < (int)(sizeof(Tables) / 16); i += blockDim.x) d[i] = s[i];
+  __syncthreads();
+}
+
+// --------------------------------------------------------------- eval_net --
+// Workgroup = 2 * G * PAR threads, G = L1 / 16 threads per (position,
+// perspective): thread j of a perspective group owns accumulator columns
+// [8j, 8j+8) and [L1/2 + 8j, L1/2 + 8j + 8), so the transform's pairwise
+// product needs no data exchange.  Big net: G = 192, PAR = 1 (384 threads, the
+// 16 positions of the tile one after another); small net: G = 8, PAR = 16
+// (256 threads, all 16 positions at once).
+template <int L1, int PAR>
+__global__ void __launch_bounds__(2 * (L1 / 16) * PAR)
+    eval_net_kernel(NetDevice net, const gn_board *__restrict__ boards, const uint8_t *__restrict__ need,
+                    size_t n, int2 *__restrict__ out) {
+  constexpr int G = L1 / 16;
+  constexpr int NT = 2 * G * PAR;
+  constexpr int NW = NT / 64;
+  constexpr int TILE = 16;
+  constexpr int XS = L1 + 16; // padded LDS row: conflict-free ds_read_b128 across 16 rows
+  constexpr uint32_t RS = 2 * L1 + 32;
+  static_assert(NT % 64 == 0 && TILE % PAR == 0, "geometry");
+
+  // LDS: big net 53.2 KB -> 3 workgroups (18 waves) per CU.  The feature list
+  // (phase 0-1) and the layer-stack scratch (phase 2) share one region.
+  constexpr int ROWS_BYTES = TILE * 2 * 32 * 2;
+  constexpr int LS_BYTES = NW * TILE * 32 + NW * TILE * 4;
+  constexpr int SCRATCH = ROWS_BYTES > LS_BYTES ? ROWS_BYTES : LS_BYTES;
+  __shared__ __attribute__((aligned(16))) uint8_t xt[TILE * XS];
+  __shared__ __attribute__((aligned(16))) uint8_t scratch[SCRATCH];
+  __shared__ int32_t psq[TILE][2];
+  __shared__ int nfeat[TILE];
+  __shared__ int bkt[TILE];
+  __shared__ uint32_t bmask;
+  uint16_t(*rows)[2][32] = reinterpret_cast<uint16_t(*)[2][32]>(scratch);
+  uint8_t(*in1)[TILE][32] = reinterpret_cast<uint8_t(*)[TILE][32]>(scratch);
+  int32_t(*fwd)[TILE] = reinterpret_cast<int32_t(*)[TILE]>(scratch + NW * TILE * 32);
+
+  const int tid = threadIdx.x;
+  const size_t base = (size_t)blockIdx.x * TILE;
+  if (tid == 0) bmask = 0;
+  __syncthreads();
+
+  // ---- phase 0: unpack boards, validate, feature row offsets (both perspectives)
+  if (tid < TILE) {
+    const size_t i = base + tid;
+    int cnt = 0;
+    if (i < n && (!need || need[i])) {
+      const gn_board p = boards[i];
+      uint64_t wlo, whi;
+      piece_words(p, wlo, whi);
+      const int c = popcnt(p.occ);
+      int wk = -1, bk = -1;
+      bool ok = c >= 2 && c <= 32;
+      uint64_t o = p.occ;
+      for (int k = 0; ok && k < c; ++k) {
+        const int s = pop_lsb(o), pc = piece_nibble(wlo, whi, k), pt = pc & 7;
+        ok &= pt >= PAWN && pt <= KING;
+        if (pc == make_piece(WHITE, KING)) ok &= wk < 0, wk = s;
+        if (pc == make_piece(BLACK, KING)) ok &= bk < 0, bk = s;
+      }
+      ok &= wk >= 0 && bk >= 0;
+      if (ok) {
+        const int stm = p.stm_ep >> 7;
+        const int k0 = stm ? bk : wk, k1 = stm ? wk : bk;
+        o = p.occ;
+        for (int k = 0; k < c; ++k) {
+          const int s = pop_lsb(o), pc = piece_nibble(wlo, whi, k);
+          rows[tid][0][k] = (uint16_t)feature_index(stm, s, pc, k0);
+          rows[tid][1][k] = (uint16_t)feature_index(stm ^ 1, s, pc, k1);
+        }
+        cnt = c;
+      }
+    }
+    nfeat[tid] = cnt;
+    bkt[tid] = cnt ? (cnt - 1) / 4 : 0;
+    if (cnt) atomicOr(&bmask, 1u << ((cnt - 1) / 4));
+  }
+  __syncthreads();
+
+  // ---- phase 1: gather-accumulate + transform into the LDS tile
+  {
+    const int q = tid / (2 * G), h = (tid / G) & 1, j = tid % G;
+    const ushort8 bias_lo = *reinterpret_cast<const ushort8 *>(net.bias + 8 * j);
+    const ushort8 bias_hi = *reinterpret_cast<const ushort8 *>(net.bias + L1 / 2 + 8 * j);
+    const uint8_t *ftj = net.ft + 16 * j;
+#pragma unroll 1
+    for (int r = 0; r < TILE / PAR; ++r) {
+      const int p = r * PAR + q;
+      const int cnt = nfeat[p];
+      if (!cnt) continue;
+      ushort8 lo = bias_lo, hi = bias_hi;
+      uint32_t ps = 0;
+      const uint32_t pso = 2 * L1 + ((bkt[p] >> 2) << 4);
+      const int pse = bkt[p] & 3;
+      const uint16_t *rr = rows[p][h];
+      int k = 0;
+      for (; k + 4 <= cnt; k += 4) {
+        const uint32_t o0 = rr[k] * RS, o1 = rr[k + 1] * RS, o2 = rr[k + 2] * RS, o3 = rr[k + 3] * RS;
+        const ushort8 a0 = *reinterpret_cast<const ushort8 *>(ftj + o0);
+        const ushort8 a1 = *reinterpret_cast<const ushort8 *>(ftj + o1);
+        const ushort8 a2 = *reinterpret_cast<const ushort8 *>(ftj + o2);
+        const ushort8 a3 = *reinterpret_cast<const ushort8 *>(ftj + o3);
+        const ushort8 b0 = *reinterpret_cast<const ushort8 *>(ftj + o0 + L1);
+        const ushort8 b1 = *reinterpret_cast<const ushort8 *>(ftj + o1 + L1);
+        const ushort8 b2 = *reinterpret_cast<const ushort8 *>(ftj + o2 + L1);
+        const ushort8 b3 = *reinterpret_cast<const ushort8 *>(ftj + o3 + L1);
+        if (j == 0) {
+          const int4v v0 = *reinterpret_cast<const int4v *>(net.ft + o0 + pso);
+          const int4v v1 = *reinterpret_cast<const int4v *>(net.ft + o1 + pso);
+          const int4v v2 = *reinterpret_cast<const int4v *>(net.ft + o2 + pso);
+          const int4v v3 = *reinterpret_cast<const int4v *>(net.ft + o3 + pso);
+          ps += (uint32_t)v0[pse] + (uint32_t)v1[pse] + (uint32_t)v2[pse] + (uint32_t)v3[pse];
+        }
+        lo += (a0 + a1) + (a2 + a3);
+        hi += (b0 + b1) + (b2 + b3);
+      }
+      for (; k < cnt; ++k) {
+        const uint32_t o0 = rr[k] * RS;
+        lo += *reinterpret_cast<const ushort8 *>(ftj + o0);
+        hi += *reinterpret_cast<const ushort8 *>(ftj + o0 + L1);
+        if (j == 0) ps += (uint32_t)(*reinterpret_cast<const int4v *>(net.ft + o0 + pso))[pse];
+      }
+      // transform: clamp to [0, 254] in the doubled domain, product / 512
+      uint32_t w0 = 0, w1 = 0;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int a = clampi((short)lo[e], 0, 254), b = clampi((short)hi[e], 0, 254);
+        const uint32_t v = (uint32_t)(a * b) >> 9;
+        if (e < 4) w0 |= v << (8 * e);
+        else w1 |= v << (8 * (e - 4));
+      }
+      *reinterpret_cast<uint2 *>(xt + p * XS + h * (L1 / 2) + 8 * j) = make_uint2(w0, w1);
+      if (j == 0) psq[p][h] = (int32_t)ps;
+    }
+  }
+  __syncthreads();
+
+  // ---- phase 2: layer stack, one wave per distinct bucket in the tile
+  const int lane = tid & 63, wave = tid >> 6;
+  const uint32_t bm = bmask;
+  const int nb = popcnt(bm);
+  const int row = lane & 15, kg = lane >> 4;
+  for (int round = 0; round * NW < nb; ++round) {
+    const int slot = round * NW + wave;
+    int b = -1;
+    if (slot < nb) {
+      uint32_t m = bm;
+      for (int t = 0; t < slot; ++t) m &= m - 1;
+      b = __builtin_ctz(m);
+    }
+    if (b >= 0) {
+      // fc_0: [16 pos x L1] u8 . [L1 x 16] i8 -> i32, K in steps of 64
+      int4v acc = {0, 0, 0, 0};
+      const uint8_t *xa = xt + row * XS + kg * 16;
+      const int8_t *wb = net.w0 + ((size_t)b * 16 + row) * L1 + kg * 16;
+#pragma unroll 4
+      for (int ks = 0; ks < L1; ks += 64) {
+        const int4v a = *reinterpret_cast<const int4v *>(xa + ks);
+        const int4v w = *reinterpret_cast<const int4v *>(wb + ks);
+        acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, w, acc, 0, 0, 0);
+      }
+      // acc[i] = fc_0[position 4*kg + i][output row]
+      const int32_t bias0 = net.b0[b * 16 + row];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int pos = 4 * kg + i;
+        const int32_t v = wadd(acc[i], bias0);
+        if (row < 15) {
+          const long long s2 = ((long long)v * v) >> 19;
+          in1[wave][pos][row] = (uint8_t)(s2 < 127 ? s2 : 127);
+          in1[wave][pos][15 + row] = (uint8_t)clampi(v >> 6, 0, 127);
+        } else {
+          fwd[wave][pos] = wmul(v, 600 * 16) / (127 * 64);
+          in1[wave][pos][30] = 0;
+          in1[wave][pos][31] = 0;
+        }
+      }
+    }
+    __syncthreads();
+    if (b >= 0) {
+      // fc_1: [16 x 32(+32 zero)] . [32 x 32] as two 16x16x64 MFMAs
+      const int4v zero = {0, 0, 0, 0};
+      int4v a = zero, wl = zero, wh = zero;
+      if (kg < 2) {
+        a = *reinterpret_cast<const int4v *>(&in1[wave][row][kg * 16]);
+        wl = *reinterpret_cast<const int4v *>(net.w1 + ((size_t)b * 32 + row) * 32 + kg * 16);
+        wh = *reinterpret_cast<const int4v *>(net.w1 + ((size_t)b * 32 + 16 + row) * 32 + kg * 16);
+      }
+      const int4v cl = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, wl, zero, 0, 0, 0);
+      const int4v ch = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, wh, zero, 0, 0, 0);
+      const int32_t b1l = net.b1[b * 32 + row], b1h = net.b1[b * 32 + 16 + row];
+      const int32_t w2l = net.w2[b * 32 + row], w2h = net.w2[b * 32 + 16 + row];
+      int32_t part[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int32_t l = clampi(wadd(cl[i], b1l) >> 6, 0, 127), hh = clampi(wadd(ch[i], b1h) >> 6, 0, 127);
+        part[i] = w2l * l + w2h * hh;
+      }
+#pragma unroll
+      for (int off = 8; off; off >>= 1)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) part[i] = wadd(part[i], __shfl_xor(part[i], off, 16));
+      if (row == 0) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int pos = 4 * kg + i;
+          const size_t gi = base + pos;
+          if (gi < n && nfeat[pos] && bkt[pos] == b) {
+            const int32_t positional = wadd(wadd(net.b2[b], part[i]), fwd[wave][pos]);
+            const int32_t psqt = (int32_t)((uint32_t)psq[pos][0] - (uint32_t)psq[pos][1]) / 2;
+            out[gi] = make_int2(psqt / 16, positional / 16);
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+hipError_t launch_eval_net(const NetDevice &net, const gn_board *boards, const uint8_t *need, size_t n, int2 *out,
+                           hipStream_t s) {
+  if (!n) return hipSuccess;
+  const size_t tiles = (n + 15) / 16;
+  if (net.L1 == 3072) {
+    hipLaunchKernelGGL((eval_net_kernel<3072, 1>), dim3((unsigned)tiles), dim3(384), 0, s, net, boards, need, n, out);
+  } else if (net.L1 == 128) {
+    hipLaunchKernelGGL((eval_net_kernel<128, 16>), dim3((unsigned)tiles), dim3(256), 0, s, net, boards, need, n, out);
+  } else if (net.L1 == 1024) {
+    hipLaunchKernelGGL((eval_net_kernel<1024, 1>), dim3((unsigned)tiles), dim3(128), 0, s, net, boards, need, n, out);
+  } else {
+    return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+// -------------------------------------------------------- Eval::evaluate --
+struct Material {
+  int pawns[2], npm[2];
+};
+
+__device__ __forceinline__ Material material(const Board &B, const gn_eval_params &P) {
+  Material m;
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const Bitboard o = B.byColor[c];
+    m.pawns[c] = popcnt(B.byType[PAWN] & o);
+    m.npm[c] = P.piece_value[1] * popcnt(B.byType[KNIGHT] & o) + P.piece_value[2] * popcnt(B.byType[BISHOP] & o) +
+               P.piece_value[3] * popcnt(B.byType[ROOK] & o) + P.piece_value[4] * popcnt(B.byType[QUEEN] & o);
+  }
+  return m;
+}
+
+__global__ void classify_kernel(const gn_board *__restrict__ boards, size_t n, gn_eval_params P,
+                                uint8_t *__restrict__ need_small, uint8_t *__restrict__ need_big) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  Board B;
+  uint8_t s = 0, b = 0;
+  if (unpack(boards[i], B)) {
+    const Material m = material(B, P);
+    const int us = B.stm;
+    const int simple = P.piece_value[0] * (m.pawns[us] - m.pawns[us ^ 1]) + (m.npm[us] - m.npm[us ^ 1]);
+    s = abs(simple) > P.small_net_threshold;
+    b = !s;
+  }
+  need_small[i] = s;
+  need_big[i] = b;
+}
+
+__global__ void reeval_kernel(const int2 *__restrict__ out_small, const uint8_t *__restrict__ need_small, size_t n,
+                              gn_eval_params P, uint8_t *__restrict__ need_big) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || !need_small[i]) return;
+  const int2 o = out_small[i];
+  const int32_t nnue = wadd(wmul(P.psqt_weight, o.x), wmul(P.positional_weight, o.y)) / 128;
+  if (abs(nnue) < P.reeval_threshold) need_big[i] = 1;
+}
+
+__global__ void finalize_kernel(const gn_board *__restrict__ boards, size_t n, int mode,
+                                const int2 *__restrict__ out_small, const int2 *__restrict__ out_big,
+                                const uint8_t *__restrict__ need_small, const uint8_t *__restrict__ need_big,
+                                gn_eval_params P, const Tables *__restrict__ tables, gn_eval *__restrict__ out) {
+  __shared__ Tables T;
+  load_tables(T, tables);
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  Board B;
+  gn_eval e = {0, 0, 0, 0};
+  if (!unpack(boards[i], B)) {
+    e.flags = GN_FLAG_BAD_FEN;
+    out[i] = e;
+    return;
+  }
+  const Material m = material(B, P);
+  bool small;
+  int2 o;
+  uint32_t flags = 0;
+  if (mode == GN_MODE_SMALL) {
+    small = true, o = out_small[i];
+  } else if (mode == GN_MODE_BIG) {
+    small = false, o = out_big[i];
+  } else if (need_small[i] && !need_big[i]) {
+    small = true, o = out_small[i];
+  } else {
+    small = false, o = out_big[i];
+    if (need_small[i]) flags |= GN_FLAG_REEVAL;
+  }
+  int32_t nnue = wadd(wmul(P.psqt_weight, o.x), wmul(P.positional_weight, o.y)) / 128;
+  const int32_t complexity = abs(wadd(o.x, -o.y));
+  nnue = wadd(nnue, -(wmul(nnue, complexity) / (small ? P.complexity_div_small : P.complexity_div_big)));
+  const int32_t mat = (small ? P.material_pawn_small : P.material_pawn_big) * (m.pawns[0] + m.pawns[1]) +
+                      m.npm[0] + m.npm[1];
+  int32_t v = wmul(nnue, P.material_base + mat) / P.material_base;
+  v = wadd(v, -(wmul(v, (int32_t)B.rule50) / P.rule50_div));
+  v = clampi(v, -P.value_clamp, P.value_clamp);
+  if (small) flags |= GN_FLAG_SMALLNET;
+  if (in_check(B, T)) flags |= GN_FLAG_IN_CHECK;
+  e.psqt = o.x, e.positional = o.y, e.final_v = v, e.flags = flags;
+  out[i] = e;
+}
+
+static inline unsigned blocks_for(size_t n, int bs) { return (unsigned)((n + bs - 1) / bs); }
+
+hipError_t launch_classify(const gn_board *boards, size_t n, const gn_eval_params &P, uint8_t *need_small,
+                           uint8_t *need_big, hipStream_t s) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(classify_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, boards, n, P, need_small, need_big);
+  return hipGetLastError();
+}
+
+hipError_t launch_reeval(const int2 *out_small, const uint8_t *need_small, size_t n, const gn_eval_params &P,
+                         uint8_t *need_big, hipStream_t s) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(reeval_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, out_small, need_small, n, P, need_big);
+  return hipGetLastError();
+}
+
+hipError_t launch_finalize(const gn_board *boards, size_t n, int mode, const int2 *out_small, const int2 *out_big,
+                           const uint8_t *need_small, const uint8_t *need_big, const gn_eval_params &P,
+                           const Tables *tables, gn_eval *out, hipStream_t s) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(finalize_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, boards, n, mode, out_small, out_big,
+                     need_small, need_big, P, tables, out);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------- movegen kernels --
+__global__ void count_children_kernel(const gn_board *__restrict__ boards, size_t n, const Tables *__restrict__ tables,
+                                      uint64_t *__restrict__ counts) {
+  __shared__ Tables T;
+  load_tables(T, tables);
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  Board B;
+  uint64_t c = 0;
+  if (unpack(boards[i], B)) gen_legal(B, T, [&](uint16_t) { ++c; });
+  counts[i] = c;
+}
+
+__global__ void write_children_kernel(const gn_board *__restrict__ boards, size_t n, const Tables *__restrict__ tables,
+                                      const uint64_t *__restrict__ offsets, gn_board *__restrict__ children,
+                                      uint16_t *__restrict__ moves) {
+  __shared__ Tables T;
+  load_tables(T, tables);
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  Board B;
+  if (!unpack(boards[i], B)) return;
+  uint64_t k = offsets[i];
+  gen_legal(B, T, [&](uint16_t m) {
+    gn_board pb;
+    pack(do_move(B, m), pb);
+    children[k] = pb;
+    if (moves) moves[k] = m;
+    ++k;
+  });
+}
+
+__global__ void count_sum_kernel(const gn_board *__restrict__ boards, size_t n, const Tables *__restrict__ tables,
+                                 unsigned long long *__restrict__ total) {
+  __shared__ Tables T;
+  __shared__ unsigned long long part[4];
+  load_tables(T, tables);
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  unsigned long long c = 0;
+  if (i < n) {
+    Board B;
+    if (unpack(boards[i], B)) gen_legal(B, T, [&](uint16_t) { ++c; });
+  }
+  for (int off = 32; off; off >>= 1) c += __shfl_down(c, off, 64);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long s = 0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) s += part[w];
+    if (s) atomicAdd(total, s);
+  }
+}
+
+__global__ void offsets_u32_kernel(const uint64_t *__restrict__ in, size_t n, uint32_t *__restrict__ out) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = (uint32_t)in[i];
+}
+
+hipError_t launch_count_children(const gn_board *boards, size_t n, const Tables *tables, uint64_t *counts,
+                                 hipStream_t s) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(count_children_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, boards, n, tables, counts);
+  return hipGetLastError();
+}
+
+hipError_t launch_write_children(const gn_board *boards, size_t n, const Tables *tables, const uint64_t *offsets,
+                                 gn_board *children, uint16_t *moves, hipStream_t s) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(write_children_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, boards, n, tables, offsets,
+                     children, moves);
+  return hipGetLastError();
+}
+
+hipError_t launch_count_sum(const gn_board *boards, size_t n, const Tables *tables, unsigned long long *total,
+                            hipStream_t s) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(count_sum_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, boards, n, tables, total);
+  return hipGetLastError();
+}
+
+hipError_t launch_offsets_u32(const uint64_t *in, size_t n, uint32_t *out, hipStream_t s) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(offsets_u32_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, in, n, out);
+  return hipGetLastError();
+}
+
+hipError_t exclusive_scan_u64(const uint64_t *counts, uint64_t *offsets, size_t n1, void *&temp, size_t &temp_bytes,
+                              hipStream_t s) {
+  size_t need = 0;
+  hipError_t e = hipcub::DeviceScan::ExclusiveSum(nullptr, need, counts, offsets, n1, s);
+  if (e != hipSuccess) return e;
+  if (need > temp_bytes) {
+    if (temp) (void)hipFree(temp);
+    temp = nullptr;
+    temp_bytes = 0;
+    if ((e = hipMalloc(&temp, need)) != hipSuccess) return e;
+    temp_bytes = need;
+  }
+  return hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, counts, offsets, n1, s);
+}
+
+} // namespace gn

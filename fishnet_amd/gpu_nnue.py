@@ -1,0 +1,274 @@
+"""Python host mirror of the `gpu_nnue` module fishnet would call (ctypes over
+libgpu_nnue.so, include/gpu_nnue.h).
+
+The reference's engine plugin API is `StockfishStub::go_multiple(Chunk)`
+(/root/reference/src/stockfish.rs:36-47); the north-star `gpu_nnue` module adds
+`load_net(.nnue)` and `evaluate_batch(&[Fen]) -> Vec<(psqt, positional, final)>`
+beside it.  This module exposes exactly those two plus expansion, perft and the
+device-resident entry points used by bench.py.  There is no CPU fallback: if
+the HIP library is missing or no gfx950 device is present, calls raise.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("GPU_NNUE_LIB", os.path.join(HERE, "lib", "libgpu_nnue.so"))
+
+MODE_FULL, MODE_BIG, MODE_SMALL = 0, 1, 2
+FLAG_IN_CHECK, FLAG_SMALLNET, FLAG_BAD_FEN, FLAG_REEVAL = 1, 2, 4, 8
+ERRORS = {-1: "INVALID", -2: "IO", -3: "FORMAT", -4: "HIP", -5: "NOMEM", -6: "CAPACITY",
+          -7: "NODEVICE", -8: "NONET"}
+
+EVAL_DTYPE = np.dtype([("psqt", "<i4"), ("positional", "<i4"), ("final_v", "<i4"), ("flags", "<u4")])
+BOARD_DTYPE = np.dtype([("occ", "<u8"), ("pc", "u1", (16,)), ("stm_ep", "u1"), ("reserved", "u1"),
+                        ("castle", "<u2"), ("rule50", "<u2"), ("fullmove", "<u2")])
+assert EVAL_DTYPE.itemsize == 16 and BOARD_DTYPE.itemsize == 32
+
+EXPORTS = ["gn_load_net", "gn_load_net_memory", "gn_free", "gn_last_error", "gn_abi_version",
+           "gn_get_eval_params", "gn_set_eval_params", "gn_net_info", "gn_evaluate_batch",
+           "gn_evaluate_batch_mode", "gn_expand_and_evaluate", "gn_perft", "gn_pack_fens",
+           "gn_board_to_fen", "gn_random_positions", "gn_evaluate_device", "gn_expand_device",
+           "gn_device_alloc", "gn_device_free", "gn_memcpy_h2d", "gn_memcpy_d2h", "gn_synchronize",
+           "gn_time_evaluate_device"]
+
+
+class GnError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"gpu_nnue error {code} ({ERRORS.get(code, '?')}): {msg}")
+        self.code = code
+
+
+class EvalParams(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in (
+        "small_net_threshold", "psqt_weight", "positional_weight", "reeval_threshold",
+        "complexity_div_small", "complexity_div_big", "material_pawn_small", "material_pawn_big",
+        "material_base", "rule50_div", "value_clamp")] + [("piece_value", C.c_int32 * 5)]
+
+
+_lib = None
+
+
+def lib():
+    """Loads libgpu_nnue.so (never falls back to anything else)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"libgpu_nnue.so not built at {LIB_PATH}: run `python -m fishnet_amd.build`")
+    L = C.CDLL(LIB_PATH)
+    vp, sz, i32 = C.c_void_p, C.c_size_t, C.c_int
+    sig = {
+        "gn_load_net": [C.c_char_p, C.c_char_p, vp, i32, C.POINTER(vp)],
+        "gn_load_net_memory": [vp, sz, vp, sz, vp, i32, C.POINTER(vp)],
+        "gn_free": [vp],
+        "gn_last_error": [],
+        "gn_abi_version": [],
+        "gn_get_eval_params": [vp, C.POINTER(EvalParams)],
+        "gn_set_eval_params": [vp, C.POINTER(EvalParams)],
+        "gn_net_info": [vp, C.POINTER(i32), C.POINTER(C.c_uint32), C.POINTER(i32), C.POINTER(C.c_uint32)],
+        "gn_evaluate_batch": [vp, vp, sz, vp],
+        "gn_evaluate_batch_mode": [vp, vp, sz, i32, vp],
+        "gn_expand_and_evaluate": [vp, vp, sz, i32, vp, vp, vp, vp, sz],
+        "gn_perft": [vp, C.c_char_p, i32, C.POINTER(C.c_uint64)],
+        "gn_pack_fens": [vp, sz, vp, vp],
+        "gn_board_to_fen": [vp, C.c_char_p, sz],
+        "gn_random_positions": [C.c_uint64, sz, sz, i32, vp],
+        "gn_evaluate_device": [vp, i32, vp, sz, i32, vp, vp],
+        "gn_expand_device": [vp, i32, vp, sz, i32, vp, vp, vp, vp, vp, sz, C.POINTER(sz), vp],
+        "gn_device_alloc": [vp, i32, sz, C.POINTER(vp)],
+        "gn_device_free": [vp, i32, vp],
+        "gn_memcpy_h2d": [vp, i32, vp, vp, sz],
+        "gn_memcpy_d2h": [vp, i32, vp, vp, sz],
+        "gn_synchronize": [vp, i32],
+        "gn_time_evaluate_device": [vp, i32, vp, sz, i32, vp, i32, C.POINTER(C.c_float), vp],
+    }
+    for name, args in sig.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = i32
+    L.gn_free.restype = None
+    L.gn_last_error.restype = C.c_char_p
+    _lib = L
+    return L
+
+
+def _check(rc):
+    if rc != 0:
+        raise GnError(rc, (lib().gn_last_error() or b"").decode(errors="replace"))
+
+
+def _fen_array(fens):
+    enc = [f.encode() for f in fens]
+    arr = (C.c_char_p * len(enc))(*enc)
+    return arr, enc
+
+
+def pack_fens(fens):
+    """FEN strings -> (boards[BOARD_DTYPE], ok[bool]); host only, no GPU needed."""
+    n = len(fens)
+    boards = np.zeros(n, dtype=BOARD_DTYPE)
+    ok = np.zeros(n, dtype=np.uint8)
+    arr, _keep = _fen_array(fens)
+    _check(lib().gn_pack_fens(arr, n, boards.ctypes.data, ok.ctypes.data))
+    return boards, ok.astype(bool)
+
+
+def board_to_fen(board) -> str:
+    b = np.ascontiguousarray(np.asarray(board, dtype=BOARD_DTYPE).reshape(1))
+    buf = C.create_string_buffer(128)
+    _check(lib().gn_board_to_fen(b.ctypes.data, buf, 128))
+    return buf.value.decode()
+
+
+def random_positions(seed: int, first: int, n: int, max_plies: int = 160):
+    boards = np.zeros(n, dtype=BOARD_DTYPE)
+    _check(lib().gn_random_positions(seed, first, n, max_plies, boards.ctypes.data))
+    return boards
+
+
+def default_eval_params() -> EvalParams:
+    p = EvalParams()
+    _check(lib().gn_get_eval_params(None, C.byref(p)))
+    return p
+
+
+class DeviceBuffer:
+    def __init__(self, ctx: "GpuNnue", nbytes: int, slot: int = 0):
+        self.ctx, self.slot, self.nbytes = ctx, slot, nbytes
+        self.ptr = C.c_void_p()
+        _check(lib().gn_device_alloc(ctx.h, slot, nbytes, C.byref(self.ptr)))
+
+    @property
+    def addr(self):
+        return self.ptr.value
+
+    def upload(self, arr: np.ndarray):
+        a = np.ascontiguousarray(arr)
+        assert a.nbytes <= self.nbytes
+        _check(lib().gn_memcpy_h2d(self.ctx.h, self.slot, self.ptr, a.ctypes.data, a.nbytes))
+
+    def download(self, dtype, count):
+        out = np.empty(count, dtype=dtype)
+        _check(lib().gn_memcpy_d2h(self.ctx.h, self.slot, out.ctypes.data, self.ptr, out.nbytes))
+        return out
+
+    def free(self):
+        if self.ptr and self.ptr.value:
+            lib().gn_device_free(self.ctx.h, self.slot, self.ptr)
+            self.ptr = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class GpuNnue:
+    """load_net + evaluate_batch (the north-star `gpu_nnue` module surface)."""
+
+    def __init__(self, big_path=None, small_path=None, devices=None, big_bytes=None, small_bytes=None):
+        self.h = C.c_void_p()
+        devs = (C.c_int * len(devices))(*devices) if devices else None
+        nd = len(devices) if devices else 0
+        if big_bytes is not None or small_bytes is not None:
+            bb = (C.c_uint8 * len(big_bytes)).from_buffer_copy(big_bytes) if big_bytes is not None else None
+            sb = (C.c_uint8 * len(small_bytes)).from_buffer_copy(small_bytes) if small_bytes is not None else None
+            _check(lib().gn_load_net_memory(bb, len(big_bytes or b""), sb, len(small_bytes or b""), devs, nd,
+                                            C.byref(self.h)))
+        else:
+            _check(lib().gn_load_net(big_path.encode() if big_path else None,
+                                     small_path.encode() if small_path else None, devs, nd, C.byref(self.h)))
+
+    def close(self):
+        if self.h and self.h.value:
+            lib().gn_free(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def net_info(self):
+        a, c = C.c_int(), C.c_int()
+        b, d = C.c_uint32(), C.c_uint32()
+        _check(lib().gn_net_info(self.h, C.byref(a), C.byref(b), C.byref(c), C.byref(d)))
+        return {"big_l1": a.value, "big_hash": b.value, "small_l1": c.value, "small_hash": d.value}
+
+    def eval_params(self) -> EvalParams:
+        p = EvalParams()
+        _check(lib().gn_get_eval_params(self.h, C.byref(p)))
+        return p
+
+    def set_eval_params(self, p: EvalParams):
+        _check(lib().gn_set_eval_params(self.h, C.byref(p)))
+
+    def evaluate_batch(self, fens, mode=MODE_FULL) -> np.ndarray:
+        n = len(fens)
+        out = np.zeros(n, dtype=EVAL_DTYPE)
+        arr, _keep = _fen_array(fens)
+        _check(lib().gn_evaluate_batch_mode(self.h, arr, n, mode, out.ctypes.data))
+        return out
+
+    def expand_and_evaluate(self, fens, mode=MODE_FULL, cap=None):
+        n = len(fens)
+        arr, _keep = _fen_array(fens)
+        offsets = np.zeros(n + 1, dtype=np.uint32)
+        parents = np.zeros(n, dtype=EVAL_DTYPE)
+        cap = cap if cap is not None else 64 * n + 256
+        for _ in range(2):
+            moves = np.zeros(max(cap, 1), dtype=np.uint16)
+            kids = np.zeros(max(cap, 1), dtype=EVAL_DTYPE)
+            rc = lib().gn_expand_and_evaluate(self.h, arr, n, mode, parents.ctypes.data, offsets.ctypes.data,
+                                              moves.ctypes.data, kids.ctypes.data, cap)
+            if rc == -6 and int(offsets[-1]) > cap:
+                cap = int(offsets[-1])
+                continue
+            _check(rc)
+            t = int(offsets[-1])
+            return parents, offsets, moves[:t], kids[:t]
+        raise GnError(-6, "capacity retry failed")
+
+    def perft(self, fen: str, depth: int) -> int:
+        v = C.c_uint64()
+        _check(lib().gn_perft(self.h, fen.encode(), depth, C.byref(v)))
+        return v.value
+
+    # ---- device-resident API -------------------------------------------
+    def alloc(self, nbytes, slot=0) -> DeviceBuffer:
+        return DeviceBuffer(self, nbytes, slot)
+
+    def evaluate_device(self, d_boards: DeviceBuffer, n, mode, d_out: DeviceBuffer, stream=None, slot=0):
+        _check(lib().gn_evaluate_device(self.h, slot, d_boards.ptr, n, mode, d_out.ptr, stream))
+
+    def synchronize(self, slot=0):
+        _check(lib().gn_synchronize(self.h, slot))
+
+    def time_evaluate_device(self, d_boards, n, mode, d_out, iters, per_kernel=True, slot=0):
+        ms = C.c_float()
+        pk = (C.c_float * 4)() if per_kernel else None
+        _check(lib().gn_time_evaluate_device(self.h, slot, d_boards.ptr, n, mode, d_out.ptr, iters,
+                                             C.byref(ms), pk))
+        return ms.value, (list(pk) if per_kernel else None)
+
+    def expand_device(self, d_parents, n, mode, d_parent_out, d_offsets, d_children, d_moves, d_child_out,
+                      cap, stream=None, slot=0):
+        total = C.c_size_t()
+        _check(lib().gn_expand_device(self.h, slot, d_parents.ptr, n, mode,
+                                      d_parent_out.ptr if d_parent_out else None, d_offsets.ptr,
+                                      d_children.ptr, d_moves.ptr, d_child_out.ptr, cap, C.byref(total),
+                                      stream))
+        return total.value
+
+
+def move_to_uci(m: int) -> str:
+    """Stockfish move encoding -> UCI text (castling as king-takes-rook, Chess960 style)."""
+    to, frm, typ = m & 63, (m >> 6) & 63, m >> 14
+    sq = lambda s: "abcdefgh"[s & 7] + str((s >> 3) + 1)
+    return sq(frm) + sq(to) + ("nbrq"[(m >> 12) & 3] if typ == 1 else "")

@@ -1,0 +1,189 @@
+/*
+ * gpu_nnue.h — C-ABI of libgpu_nnue.so, the MI355X (gfx950) batched Stockfish
+ * NNUE evaluator for fishnet.
+ *
+ * Boundary being replaced / extended (reference = ounben/fishnet @ 2025-05-09):
+ *   - StockfishStub::go_multiple(Chunk) -> Result<Vec<PositionResponse>, ChunkFailed>
+ *     /root/reference/src/stockfish.rs:36-47 — the engine plugin API.  A GPU
+ *     backend sits beside it; the Rust `gpu_nnue` module calls
+ *     the functions below from tokio::task::spawn_blocking.
+ *   - The static evaluation those engine processes run at every search leaf
+ *     (Stockfish `Eval::evaluate`, inside the empty Stockfish submodule,
+ *     /root/reference/.gitmodules:1-3) is what gn_evaluate_batch computes.
+ *   - Nets: the reference ships nn-1c0000000000.nnue (big) and
+ *     nn-37f18f62d772.nnue (small) next to the engine (/root/reference/build.rs:8-9,
+ *     src/assets.rs:186-226); gn_load_net takes those files.
+ *
+ * Conventions: plain pointers and sizes; the caller owns every input and output
+ * buffer, the library owns device memory.  Every function returns GN_OK (0) or a
+ * negative GN_E_* code and never aborts or throws across the ABI; the message of
+ * the last failure on the calling thread is gn_last_error().  A gn_ctx may be
+ * shared between threads: calls on one context are serialised internally.
+ */
+#ifndef GPU_NNUE_H
+#define GPU_NNUE_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GN_ABI_VERSION 1
+
+#if defined(__GNUC__)
+#define GN_API __attribute__((visibility("default")))
+#else
+#define GN_API
+#endif
+
+/* return codes */
+#define GN_OK 0
+#define GN_E_INVALID (-1)  /* bad argument                                    */
+#define GN_E_IO (-2)       /* cannot read a net file                          */
+#define GN_E_FORMAT (-3)   /* not a supported .nnue (version/hash/size)       */
+#define GN_E_HIP (-4)      /* HIP runtime error (message has the detail)      */
+#define GN_E_NOMEM (-5)    /* host or device allocation failed                */
+#define GN_E_CAPACITY (-6) /* caller's output buffer too small                */
+#define GN_E_NODEVICE (-7) /* no usable gfx950 device                         */
+#define GN_E_NONET (-8)    /* the requested mode needs a net that is not loaded */
+
+/* evaluation modes */
+#define GN_MODE_FULL 0  /* Eval::evaluate: small net when |simple_eval| > 962,
+                           big-net re-evaluation when |nnue| < 236            */
+#define GN_MODE_BIG 1   /* big net for every position (epilogue: smallNet=false) */
+#define GN_MODE_SMALL 2 /* small net for every position (epilogue: smallNet=true) */
+
+/* per-position flags */
+#define GN_FLAG_IN_CHECK 1u /* side to move in check: Stockfish has no static eval
+                               (Eval::evaluate asserts !checkers); values are still
+                               computed but are not a Stockfish result            */
+#define GN_FLAG_SMALLNET 2u /* final_v came from the small net                    */
+#define GN_FLAG_BAD_FEN 4u  /* unparsable / unsupported position; values are 0     */
+#define GN_FLAG_REEVAL 8u   /* small net was run, then the big net re-evaluated   */
+
+/* One result.  psqt/positional are Network::evaluate's NetworkOutput (already
+ * divided by OutputScale = 16) of the net that produced final_v; final_v is
+ * Eval::evaluate(pos, optimism = 0) in internal Value units; all side-to-move POV. */
+typedef struct gn_eval {
+  int32_t psqt;
+  int32_t positional;
+  int32_t final_v;
+  uint32_t flags;
+} gn_eval;
+
+/* Packed position, 32 bytes, the device input format.
+ *   occ      occupied squares (bit s = square s, a1 = 0 .. h8 = 63)
+ *   pc       piece codes (Stockfish encoding: 1..6 white P N B R Q K, 9..14 black)
+ *            of the occupied squares in ascending square order, two per byte,
+ *            low nibble first
+ *   stm_ep   bit 7 = side to move (1 = black); bits 0..6 = en-passant square
+ *            or 64 when none
+ *   castle   4 nibbles [white O-O, white O-O-O, black O-O, black O-O-O]:
+ *            bit 3 = right present, bits 0..2 = file of the castling rook
+ *   rule50   half-move clock; fullmove = full-move number                    */
+typedef struct gn_board {
+  uint64_t occ;
+  uint8_t pc[16];
+  uint8_t stm_ep;
+  uint8_t reserved;
+  uint16_t castle;
+  uint16_t rule50;
+  uint16_t fullmove;
+} gn_board;
+
+/* Eval::evaluate constants (defaults = Stockfish 17.1). */
+typedef struct gn_eval_params {
+  int32_t small_net_threshold; /* 962   |simple_eval| above which the small net is used */
+  int32_t psqt_weight;         /* 125   nnue = (psqt_w*psqt + pos_w*positional) / 128  */
+  int32_t positional_weight;   /* 131                                                */
+  int32_t reeval_threshold;    /* 236   small-net |nnue| below which big re-evaluates */
+  int32_t complexity_div_small;/* 18000 nnue -= nnue * |psqt - positional| / div      */
+  int32_t complexity_div_big;  /* 18000                                              */
+  int32_t material_pawn_small; /* 535   material = k * pawns + non_pawn_material     */
+  int32_t material_pawn_big;   /* 535                                                */
+  int32_t material_base;       /* 77777 v = nnue * (base + material) / base          */
+  int32_t rule50_div;          /* 212   v -= v * rule50 / div                        */
+  int32_t value_clamp;         /* 31506 |v| <= VALUE_TB_WIN_IN_MAX_PLY - 1           */
+  int32_t piece_value[5];      /* 208 781 825 1276 2538 (P N B R Q)                  */
+} gn_eval_params;
+
+typedef struct gn_ctx gn_ctx;
+
+/* ---- lifecycle ---------------------------------------------------------- */
+/* Load nets and upload them to each listed device (devices = NULL: device 0).
+ * small_path may be NULL (then only GN_MODE_BIG works); big_path may be NULL
+ * (then only GN_MODE_SMALL works). */
+GN_API int gn_load_net(const char *big_path, const char *small_path, const int *devices, int n_devices,
+                gn_ctx **out);
+/* Same from in-memory .nnue images (e.g. after an RCCL broadcast). */
+GN_API int gn_load_net_memory(const uint8_t *big, size_t big_len, const uint8_t *small, size_t small_len,
+                       const int *devices, int n_devices, gn_ctx **out);
+GN_API void gn_free(gn_ctx *ctx);
+GN_API const char *gn_last_error(void); /* thread-local; valid until the next call */
+GN_API int gn_abi_version(void);
+GN_API int gn_get_eval_params(const gn_ctx *ctx, gn_eval_params *out);
+GN_API int gn_set_eval_params(gn_ctx *ctx, const gn_eval_params *params);
+/* network hashes / widths actually loaded (0 when absent) */
+GN_API int gn_net_info(const gn_ctx *ctx, int *big_l1, uint32_t *big_hash, int *small_l1, uint32_t *small_hash);
+
+/* ---- host-buffer API (what the Rust gpu_nnue module calls) -------------- */
+/* Evaluate n FENs (Chess960 castling accepted: KQkq, Shredder and X-FEN).
+ * gn_evaluate_batch == gn_evaluate_batch_mode(..., GN_MODE_FULL, ...).
+ * Bad FENs do not fail the batch: their entry carries GN_FLAG_BAD_FEN. */
+GN_API int gn_evaluate_batch(gn_ctx *ctx, const char *const *fens, size_t n, gn_eval *out);
+GN_API int gn_evaluate_batch_mode(gn_ctx *ctx, const char *const *fens, size_t n, int mode, gn_eval *out);
+
+/* Every parent plus every legal child of it.  child_offsets[n+1] receives the
+ * prefix sums (children of parent i are [child_offsets[i], child_offsets[i+1])),
+ * child_moves / child_out receive one entry per child in the order the device
+ * generator emits them (moves in Stockfish 16-bit encoding; castling = king
+ * takes own rook).  GN_E_CAPACITY when the children exceed cap (child_offsets
+ * is still filled so the caller can retry with the right size). */
+GN_API int gn_expand_and_evaluate(gn_ctx *ctx, const char *const *parent_fens, size_t n, int mode,
+                           gn_eval *parent_out, uint32_t *child_offsets, uint16_t *child_moves,
+                           gn_eval *child_out, size_t cap);
+
+/* Legal-move-tree node count from fen to depth (GPU movegen, breadth-first). */
+GN_API int gn_perft(gn_ctx *ctx, const char *fen, int depth, uint64_t *nodes);
+
+/* ---- packed / device-resident API (benchmarks, multi-GPU shards) -------- */
+/* Host FEN -> packed board; ok[i] = 0 marks a bad FEN (its board is zeroed).
+ * Needs no context and no GPU. */
+GN_API int gn_pack_fens(const char *const *fens, size_t n, gn_board *out, uint8_t *ok);
+/* Packed board -> FEN text (Chess960-aware X-FEN castling); buf >= 100 bytes. */
+GN_API int gn_board_to_fen(const gn_board *board, char *buf, size_t buflen);
+/* Deterministic random-playout positions (xoshiro256**, seed + index): plays
+ * k ~ U{0..max_plies} uniformly random legal plies from the start position
+ * (stopping at mate/stalemate), resampling positions in check. Host only. */
+GN_API int gn_random_positions(uint64_t seed, size_t first_index, size_t n, int max_plies, gn_board *out);
+
+/* Evaluate boards already resident on device `device_slot` (index into the
+ * devices given at load).  d_boards / d_out are device pointers; stream is a
+ * hipStream_t (NULL = the context's own stream).  Asynchronous: returns once
+ * the kernels are queued. */
+GN_API int gn_evaluate_device(gn_ctx *ctx, int device_slot, const gn_board *d_boards, size_t n, int mode,
+                       gn_eval *d_out, void *stream);
+/* Device-resident expansion: counts children (d_counts[n]), writes d_offsets
+ * (n+1 prefix sums), the child boards, moves and evaluations.  Synchronous;
+ * returns the total child count in *total. */
+GN_API int gn_expand_device(gn_ctx *ctx, int device_slot, const gn_board *d_parents, size_t n, int mode,
+                     gn_eval *d_parent_out, uint32_t *d_offsets, gn_board *d_children,
+                     uint16_t *d_moves, gn_eval *d_child_out, size_t cap, size_t *total, void *stream);
+/* Device memory helpers (so callers need no HIP headers). */
+GN_API int gn_device_alloc(gn_ctx *ctx, int device_slot, size_t bytes, void **ptr);
+GN_API int gn_device_free(gn_ctx *ctx, int device_slot, void *ptr);
+GN_API int gn_memcpy_h2d(gn_ctx *ctx, int device_slot, void *dst, const void *src, size_t bytes);
+GN_API int gn_memcpy_d2h(gn_ctx *ctx, int device_slot, void *dst, const void *src, size_t bytes);
+GN_API int gn_synchronize(gn_ctx *ctx, int device_slot);
+/* Time `iters` back-to-back gn_evaluate_device calls with HIP events recorded
+ * on the launch stream; *ms_total = elapsed time.  per_kernel_ms (optional,
+ * length 4) receives the average time of the [classify, small, big, finalize]
+ * kernels measured with events around each launch in a separate pass. */
+GN_API int gn_time_evaluate_device(gn_ctx *ctx, int device_slot, const gn_board *d_boards, size_t n, int mode,
+                            gn_eval *d_out, int iters, float *ms_total, float *per_kernel_ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

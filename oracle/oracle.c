@@ -1,0 +1,810 @@
+/*
+ * oracle.c — CPU restatement of the gpu_nnue hot path.  TEST INFRASTRUCTURE ONLY
+ * (see oracle.h for who may load it and for the parity status).
+ *
+ * Deliberately simple and independent of the product code in fishnet_amd/csrc:
+ * a mailbox board, pseudo-legal generation filtered by make + "is my king
+ * attacked", full-refresh NNUE accumulators (never incremental), scalar loops.
+ *
+ * Restated algorithms (Stockfish is not vendored in the reference: the
+ * `Stockfish/` submodule at /root/reference/.gitmodules:1-3 is empty; the
+ * formulas are the ones listed in SURVEY.md §8a rows a10-a18):
+ *   - .nnue reader: header (version 0x7AF32F20, hash, description), feature
+ *     transformer (3 x COMPRESSED_LEB128 blocks: biases, weights, PSQT weights),
+ *     8 layer stacks (fc_0 / fc_1 / fc_2, little-endian).          [SURVEY a10]
+ *   - Position::set FEN parsing incl. Chess960 castling + ep filter [SURVEY a11]
+ *   - legal move generation and perft                             [SURVEY a12]
+ *   - HalfKAv2_hm feature index                                    [SURVEY a13]
+ *   - feature transformer refresh (weights doubled at load) +
+ *     transform (clamp 0..254, product / 512)                      [SURVEY a14,a15]
+ *   - layer stack propagate (SqrClippedReLU, ClippedReLU, skip)    [SURVEY a16]
+ *   - Network::evaluate bucket + OutputScale                       [SURVEY a17]
+ *   - Eval::evaluate epilogue, Stockfish 17.1 constants            [SURVEY a18]
+ * Integer overflow follows two's complement wrapping, which is what the
+ * reference's compiled x86 code does for these expressions.
+ */
+#include "oracle.h"
+
+#include <ctype.h>
+#include <pthread.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ---------------------------------------------------------------- board -- */
+enum { WHITE = 0, BLACK = 1 };
+enum { PAWN = 1, KNIGHT = 2, BISHOP = 3, ROOK = 4, QUEEN = 5, KING = 6 };
+#define PIECE(c, pt) ((c) * 8 + (pt))
+#define COLOR_OF(pc) ((pc) >> 3)
+#define TYPE_OF(pc) ((pc) & 7)
+#define MT_NORMAL 0
+#define MT_PROMO 1
+#define MT_EP 2
+#define MT_CASTLE 3
+
+typedef struct {
+  uint8_t b[64];
+  int stm;
+  int castle[4]; /* rook square per right: [2c] king side, [2c+1] queen side; -1 none */
+  int ep;        /* en passant target square, -1 none */
+  int rule50;
+  int fullmove;
+} pos_t;
+
+static int rel_sq(int c, int sq) { return c == WHITE ? sq : sq ^ 56; }
+
+static int king_sq(const pos_t *p, int c) {
+  for (int s = 0; s < 64; ++s)
+    if (p->b[s] == PIECE(c, KING)) return s;
+  return -1;
+}
+
+static const int KN_D[8][2] = {{1, 2}, {2, 1}, {2, -1}, {1, -2}, {-1, -2}, {-2, -1}, {-2, 1}, {-1, 2}};
+static const int KG_D[8][2] = {{1, 0}, {1, 1}, {0, 1}, {-1, 1}, {-1, 0}, {-1, -1}, {0, -1}, {1, -1}};
+static const int RK_D[4][2] = {{1, 0}, {-1, 0}, {0, 1}, {0, -1}};
+static const int BS_D[4][2] = {{1, 1}, {1, -1}, {-1, 1}, {-1, -1}};
+
+static int on_board(int f, int r) { return f >= 0 && f < 8 && r >= 0 && r < 8; }
+
+/* is square `sq` attacked by any piece of colour `by`? */
+static int attacked(const pos_t *p, int sq, int by) {
+  int f = sq & 7, r = sq >> 3;
+  int pr = r - (by == WHITE ? 1 : -1);
+  for (int df = -1; df <= 1; df += 2)
+    if (on_board(f + df, pr) && p->b[pr * 8 + f + df] == PIECE(by, PAWN)) return 1;
+  for (int i = 0; i < 8; ++i) {
+    int nf = f + KN_D[i][0], nr = r + KN_D[i][1];
+    if (on_board(nf, nr) && p->b[nr * 8 + nf] == PIECE(by, KNIGHT)) return 1;
+    nf = f + KG_D[i][0], nr = r + KG_D[i][1];
+    if (on_board(nf, nr) && p->b[nr * 8 + nf] == PIECE(by, KING)) return 1;
+  }
+  for (int i = 0; i < 4; ++i) {
+    for (int k = 1;; ++k) {
+      int nf = f + RK_D[i][0] * k, nr = r + RK_D[i][1] * k;
+      if (!on_board(nf, nr)) break;
+      int pc = p->b[nr * 8 + nf];
+      if (!pc) continue;
+      if (pc == PIECE(by, ROOK) || pc == PIECE(by, QUEEN)) return 1;
+      break;
+    }
+    for (int k = 1;; ++k) {
+      int nf = f + BS_D[i][0] * k, nr = r + BS_D[i][1] * k;
+      if (!on_board(nf, nr)) break;
+      int pc = p->b[nr * 8 + nf];
+      if (!pc) continue;
+      if (pc == PIECE(by, BISHOP) || pc == PIECE(by, QUEEN)) return 1;
+      break;
+    }
+  }
+  return 0;
+}
+
+static int in_check(const pos_t *p) {
+  int k = king_sq(p, p->stm);
+  return k >= 0 && attacked(p, k, !p->stm);
+}
+
+static int char_to_piece(char c) {
+  const char *s = strchr("PNBRQK", c);
+  if (s && c) return PIECE(WHITE, (int)(s - "PNBRQK") + 1);
+  s = strchr("pnbrqk", c);
+  if (s && c) return PIECE(BLACK, (int)(s - "pnbrqk") + 1);
+  return 0;
+}
+
+/* Position::set restated: returns 0 ok, -1 malformed / unsupported. */
+static int parse_fen(const char *fen, pos_t *p) {
+  memset(p, 0, sizeof(*p));
+  for (int i = 0; i < 4; ++i) p->castle[i] = -1;
+  p->ep = -1;
+  p->fullmove = 1;
+  const char *s = fen;
+  while (*s == ' ') ++s;
+  int rank = 7, file = 0;
+  while (*s && *s != ' ') {
+    char c = *s++;
+    if (c == '/') {
+      if (file != 8 || rank == 0) return -1;
+      --rank, file = 0;
+    } else if (c >= '1' && c <= '8') {
+      file += c - '0';
+      if (file > 8) return -1;
+    } else {
+      int pc = char_to_piece(c);
+      if (!pc || file > 7) return -1;
+      p->b[rank * 8 + file++] = (uint8_t)pc;
+    }
+  }
+  if (rank != 0 || file != 8) return -1;
+  while (*s == ' ') ++s;
+  if (*s == 'w' || *s == 'b') p->stm = (*s++ == 'b');
+  else if (*s) return -1;
+  while (*s == ' ') ++s;
+  /* validation shared with the product parser: 1 king each, <= 32 pieces,
+   * no pawns on the back ranks */
+  int nk[2] = {0, 0}, npc = 0;
+  for (int sq = 0; sq < 64; ++sq) {
+    int pc = p->b[sq];
+    if (!pc) continue;
+    ++npc;
+    if (TYPE_OF(pc) == KING) ++nk[COLOR_OF(pc)];
+    if (TYPE_OF(pc) == PAWN && ((sq >> 3) == 0 || (sq >> 3) == 7)) return -1;
+  }
+  if (nk[0] != 1 || nk[1] != 1 || npc > 32) return -1;
+  /* castling: KQkq, Shredder-FEN and X-FEN (UCI_Chess960 semantics) */
+  while (*s && *s != ' ') {
+    char t = *s++;
+    if (t == '-') continue;
+    int c = islower((unsigned char)t) ? BLACK : WHITE;
+    char T = (char)toupper((unsigned char)t);
+    int base = c == WHITE ? 0 : 56, rook = PIECE(c, ROOK), rsq = -1;
+    if (T == 'K') {
+      for (int s2 = base + 7; s2 >= base; --s2)
+        if (p->b[s2] == rook) { rsq = s2; break; }
+    } else if (T == 'Q') {
+      for (int s2 = base; s2 <= base + 7; ++s2)
+        if (p->b[s2] == rook) { rsq = s2; break; }
+    } else if (T >= 'A' && T <= 'H') {
+      rsq = base + (T - 'A');
+    } else
+      continue;
+    int ksq = king_sq(p, c);
+    if (rsq < 0 || p->b[rsq] != rook || (ksq >> 3) != (base >> 3)) continue;
+    p->castle[2 * c + (rsq > ksq ? 0 : 1)] = rsq;
+  }
+  while (*s == ' ') ++s;
+  /* en passant: kept only if a pawn of the side to move attacks it, an enemy
+   * pawn stands in front of it and the square and the one behind are empty */
+  if (s[0] >= 'a' && s[0] <= 'h' && s[1] == (p->stm == WHITE ? '6' : '3')) {
+    int ep = (s[1] - '1') * 8 + (s[0] - 'a');
+    int us = p->stm, up = us == WHITE ? 8 : -8;
+    int f = ep & 7, ok = 0;
+    for (int df = -1; df <= 1; df += 2)
+      if (f + df >= 0 && f + df < 8 && p->b[ep - up + df] == PIECE(us, PAWN)) ok = 1;
+    ok = ok && p->b[ep - up] == PIECE(!us, PAWN) && !p->b[ep] && !p->b[ep + up];
+    if (ok) p->ep = ep;
+  }
+  while (*s && *s != ' ') ++s;
+  while (*s == ' ') ++s;
+  if (*s) {
+    p->rule50 = atoi(s);
+    if (p->rule50 < 0) p->rule50 = 0;
+    if (p->rule50 > 65535) p->rule50 = 65535;
+    while (*s && *s != ' ') ++s;
+    while (*s == ' ') ++s;
+    if (*s) p->fullmove = atoi(s) > 0 ? atoi(s) : 1;
+    if (p->fullmove > 65535) p->fullmove = 65535;
+  }
+  /* the side not to move may not be in check */
+  int ok = king_sq(p, !p->stm);
+  if (attacked(p, ok, p->stm)) return -1;
+  return 0;
+}
+
+static void do_move(const pos_t *p, uint16_t m, pos_t *q) {
+  *q = *p;
+  int from = (m >> 6) & 63, to = m & 63, type = m >> 14, promo = ((m >> 12) & 3) + KNIGHT;
+  int us = p->stm, them = !us;
+  int pc = p->b[from], captured = 0;
+  int kfrom = king_sq(p, us);
+  if (type == MT_CASTLE) {
+    int kside = to > from;
+    int kto = rel_sq(us, kside ? 6 : 2), rto = rel_sq(us, kside ? 5 : 3);
+    q->b[from] = 0, q->b[to] = 0;
+    q->b[kto] = (uint8_t)PIECE(us, KING), q->b[rto] = (uint8_t)PIECE(us, ROOK);
+  } else {
+    if (type == MT_EP) {
+      int cap = to - (us == WHITE ? 8 : -8);
+      captured = p->b[cap];
+      q->b[cap] = 0;
+    } else
+      captured = p->b[to];
+    q->b[to] = (uint8_t)(type == MT_PROMO ? PIECE(us, promo) : pc);
+    q->b[from] = 0;
+  }
+  q->rule50 = (type != MT_CASTLE && (TYPE_OF(pc) == PAWN || captured)) ? 0 : p->rule50 + 1;
+  if (q->rule50 > 65535) q->rule50 = 65535;
+  q->ep = -1;
+  if (TYPE_OF(pc) == PAWN && (to ^ from) == 16) {
+    int f = to & 7;
+    for (int df = -1; df <= 1; df += 2)
+      if (f + df >= 0 && f + df < 8 && p->b[to + df] == PIECE(them, PAWN)) q->ep = (from + to) / 2;
+  }
+  for (int i = 0; i < 4; ++i) {
+    if (q->castle[i] < 0) continue;
+    if (from == q->castle[i] || to == q->castle[i]) q->castle[i] = -1;
+    else if (i / 2 == us && from == kfrom) q->castle[i] = -1;
+  }
+  if (us == BLACK && q->fullmove < 65535) q->fullmove++;
+  q->stm = them;
+}
+
+static int mk(int from, int to, int type, int promo) {
+  return to | (from << 6) | (type == MT_PROMO ? (promo - KNIGHT) << 12 : 0) | (type << 14);
+}
+
+static int gen_pseudo(const pos_t *p, uint16_t *mv) {
+  int n = 0, us = p->stm, them = !us;
+  int up = us == WHITE ? 8 : -8;
+  for (int sq = 0; sq < 64; ++sq) {
+    int pc = p->b[sq];
+    if (!pc || COLOR_OF(pc) != us) continue;
+    int pt = TYPE_OF(pc), f = sq & 7, r = sq >> 3;
+    if (pt == PAWN) {
+      int to = sq + up, last = (to >> 3) == (us == WHITE ? 7 : 0);
+      if (!p->b[to]) {
+        if (last)
+          for (int pr = QUEEN; pr >= KNIGHT; --pr) mv[n++] = (uint16_t)mk(sq, to, MT_PROMO, pr);
+        else {
+          mv[n++] = (uint16_t)mk(sq, to, MT_NORMAL, 0);
+          if (r == (us == WHITE ? 1 : 6) && !p->b[to + up]) mv[n++] = (uint16_t)mk(sq, to + up, MT_NORMAL, 0);
+        }
+      }
+      for (int df = -1; df <= 1; df += 2) {
+        if (f + df < 0 || f + df > 7) continue;
+        int t = sq + up + df, tp = p->b[t];
+        if (tp && COLOR_OF(tp) == them) {
+          if (last)
+            for (int pr = QUEEN; pr >= KNIGHT; --pr) mv[n++] = (uint16_t)mk(sq, t, MT_PROMO, pr);
+          else
+            mv[n++] = (uint16_t)mk(sq, t, MT_NORMAL, 0);
+        } else if (t == p->ep)
+          mv[n++] = (uint16_t)mk(sq, t, MT_EP, 0);
+      }
+      continue;
+    }
+    if (pt == KNIGHT || pt == KING) {
+      const int(*d)[2] = pt == KNIGHT ? KN_D : KG_D;
+      for (int i = 0; i < 8; ++i) {
+        int nf = f + d[i][0], nr = r + d[i][1];
+        if (!on_board(nf, nr)) continue;
+        int tp = p->b[nr * 8 + nf];
+        if (!tp || COLOR_OF(tp) == them) mv[n++] = (uint16_t)mk(sq, nr * 8 + nf, MT_NORMAL, 0);
+      }
+      continue;
+    }
+    for (int pass = 0; pass < 2; ++pass) {
+      const int(*d)[2] = pass == 0 ? RK_D : BS_D;
+      if (pass == 0 && pt == BISHOP) continue;
+      if (pass == 1 && pt == ROOK) continue;
+      for (int i = 0; i < 4; ++i)
+        for (int k = 1;; ++k) {
+          int nf = f + d[i][0] * k, nr = r + d[i][1] * k;
+          if (!on_board(nf, nr)) break;
+          int tp = p->b[nr * 8 + nf];
+          if (tp && COLOR_OF(tp) == us) break;
+          mv[n++] = (uint16_t)mk(sq, nr * 8 + nf, MT_NORMAL, 0);
+          if (tp) break;
+        }
+    }
+  }
+  /* castling (Chess960 rules: king to g/c file, rook to f/d file) */
+  int ksq = king_sq(p, us);
+  if (!attacked(p, ksq, them))
+    for (int side = 0; side < 2; ++side) {
+      int rsq = p->castle[2 * us + side];
+      if (rsq < 0) continue;
+      int kto = rel_sq(us, side == 0 ? 6 : 2), rto = rel_sq(us, side == 0 ? 5 : 3);
+      int ok = 1;
+      int lo = ksq < kto ? ksq : kto, hi = ksq < kto ? kto : ksq;
+      for (int s = lo; s <= hi && ok; ++s)
+        if (s != ksq && s != rsq && p->b[s]) ok = 0;
+      lo = rsq < rto ? rsq : rto, hi = rsq < rto ? rto : rsq;
+      for (int s = lo; s <= hi && ok; ++s)
+        if (s != ksq && s != rsq && p->b[s]) ok = 0;
+      int step = kto > ksq ? 1 : -1;
+      for (int s = ksq + step; ok && s != kto + step; s += step)
+        if (attacked(p, s, them)) ok = 0;
+      if (kto == ksq && ok && attacked(p, kto, them)) ok = 0;
+      if (ok) mv[n++] = (uint16_t)mk(ksq, rsq, MT_CASTLE, 0);
+    }
+  return n;
+}
+
+static int gen_legal(const pos_t *p, uint16_t *mv) {
+  uint16_t ps[256];
+  int np = gen_pseudo(p, ps), n = 0;
+  for (int i = 0; i < np; ++i) {
+    pos_t q;
+    do_move(p, ps[i], &q);
+    int k = king_sq(&q, p->stm);
+    if (!attacked(&q, k, q.stm)) mv[n++] = ps[i];
+  }
+  return n;
+}
+
+static uint64_t perft_rec(const pos_t *p, int depth) {
+  uint16_t mv[256];
+  int n = gen_legal(p, mv);
+  if (depth <= 1) return (uint64_t)n;
+  uint64_t sum = 0;
+  for (int i = 0; i < n; ++i) {
+    pos_t q;
+    do_move(p, mv[i], &q);
+    sum += perft_rec(&q, depth - 1);
+  }
+  return sum;
+}
+
+uint64_t or_perft(const char *fen, int depth) {
+  pos_t p;
+  if (parse_fen(fen, &p)) return UINT64_MAX;
+  if (depth <= 0) return 1;
+  return perft_rec(&p, depth);
+}
+
+int or_legal_moves(const char *fen, uint16_t *moves, int cap) {
+  pos_t p;
+  uint16_t mv[256];
+  if (parse_fen(fen, &p)) return -1;
+  int n = gen_legal(&p, mv);
+  if (n > cap) return -2;
+  memcpy(moves, mv, (size_t)n * sizeof(uint16_t));
+  return n;
+}
+
+static int write_fen(const pos_t *p, char *out, int cap) {
+  char buf[128];
+  int k = 0;
+  for (int r = 7; r >= 0; --r) {
+    int empty = 0;
+    for (int f = 0; f < 8; ++f) {
+      int pc = p->b[r * 8 + f];
+      if (!pc) { ++empty; continue; }
+      if (empty) buf[k++] = (char)('0' + empty), empty = 0;
+      char c = "?PNBRQK?"[TYPE_OF(pc)];
+      buf[k++] = COLOR_OF(pc) == BLACK ? (char)tolower(c) : c;
+    }
+    if (empty) buf[k++] = (char)('0' + empty);
+    if (r) buf[k++] = '/';
+  }
+  buf[k++] = ' ', buf[k++] = p->stm ? 'b' : 'w', buf[k++] = ' ';
+  int any = 0;
+  for (int i = 0; i < 4; ++i) {
+    int rsq = p->castle[i];
+    if (rsq < 0) continue;
+    int c = i / 2, base = c == WHITE ? 0 : 56, outer = 1;
+    /* X-FEN: K/Q when the castling rook is the outermost rook on its side */
+    if (i % 2 == 0) {
+      for (int s = rsq + 1; s <= base + 7; ++s)
+        if (p->b[s] == PIECE(c, ROOK)) outer = 0;
+    } else {
+      for (int s = base; s < rsq; ++s)
+        if (p->b[s] == PIECE(c, ROOK)) outer = 0;
+    }
+    char ch = outer ? (i % 2 == 0 ? 'K' : 'Q') : (char)('A' + (rsq & 7));
+    buf[k++] = c == BLACK ? (char)tolower(ch) : ch;
+    any = 1;
+  }
+  if (!any) buf[k++] = '-';
+  buf[k++] = ' ';
+  if (p->ep >= 0) buf[k++] = (char)('a' + (p->ep & 7)), buf[k++] = (char)('1' + (p->ep >> 3));
+  else buf[k++] = '-';
+  k += snprintf(buf + k, sizeof(buf) - (size_t)k, " %d %d", p->rule50, p->fullmove);
+  if (k + 1 > cap) return -1;
+  memcpy(out, buf, (size_t)k + 1);
+  return k;
+}
+
+int or_child_fen(const char *fen, uint16_t move, char *out, int cap) {
+  pos_t p, q;
+  if (parse_fen(fen, &p)) return -1;
+  do_move(&p, move, &q);
+  return write_fen(&q, out, cap);
+}
+
+int or_normalize_fen(const char *fen, char *out, int cap) {
+  pos_t p;
+  if (parse_fen(fen, &p)) return -1;
+  return write_fen(&p, out, cap);
+}
+
+/* ------------------------------------------------------------------ net -- */
+#define FT_INPUTS 22528
+#define PSQT_BUCKETS 8
+#define STACKS 8
+#define NNUE_VERSION 0x7AF32F20u
+
+struct or_net {
+  int L1;
+  uint32_t hash;
+  int16_t *ft_b;   /* [L1], doubled at load */
+  int16_t *ft_w;   /* [FT_INPUTS][L1], doubled at load */
+  int32_t *psqt_w; /* [FT_INPUTS][8] */
+  int32_t b0[STACKS][16];
+  int8_t *w0[STACKS]; /* [16][L1] */
+  int32_t b1[STACKS][32];
+  int8_t w1[STACKS][32 * 32];
+  int32_t b2[STACKS];
+  int8_t w2[STACKS][32];
+};
+
+static uint32_t affine_hash(uint32_t prev, uint32_t outs) {
+  uint32_t h = 0xCC03DAE4u + outs;
+  h ^= prev >> 1;
+  h ^= prev << 31;
+  return h;
+}
+
+uint32_t or_expected_hash(int l1, uint32_t *ft_hash, uint32_t *arch_hash) {
+  uint32_t ft = 0x7f234cb8u ^ (uint32_t)(l1 * 2);
+  uint32_t h = 0xEC42E90Du ^ (uint32_t)(l1 * 2);
+  h = affine_hash(h, 16);
+  h = 0x538D24C7u + h;
+  h = affine_hash(h, 32);
+  h = 0x538D24C7u + h;
+  h = affine_hash(h, 1);
+  if (ft_hash) *ft_hash = ft;
+  if (arch_hash) *arch_hash = h;
+  return ft ^ h;
+}
+
+typedef struct {
+  const uint8_t *p;
+  size_t n, off;
+} rd_t;
+
+static int rd_bytes(rd_t *r, void *dst, size_t k) {
+  if (r->off + k > r->n) return -1;
+  memcpy(dst, r->p + r->off, k);
+  r->off += k;
+  return 0;
+}
+
+static int rd_u32(rd_t *r, uint32_t *v) {
+  uint8_t b[4];
+  if (rd_bytes(r, b, 4)) return -1;
+  *v = (uint32_t)b[0] | (uint32_t)b[1] << 8 | (uint32_t)b[2] << 16 | (uint32_t)b[3] << 24;
+  return 0;
+}
+
+/* signed LEB128 block: "COMPRESSED_LEB128" + u32 byte count + payload */
+static int rd_leb(rd_t *r, int bits, void *out, size_t count) {
+  char magic[17];
+  uint32_t nbytes;
+  if (rd_bytes(r, magic, 17) || memcmp(magic, "COMPRESSED_LEB128", 17)) return -1;
+  if (rd_u32(r, &nbytes) || r->off + nbytes > r->n) return -1;
+  const uint8_t *p = r->p + r->off, *end = p + nbytes;
+  for (size_t i = 0; i < count; ++i) {
+    uint32_t result = 0;
+    int shift = 0;
+    for (;;) {
+      if (p >= end || shift >= bits) return -1;
+      uint8_t byte = *p++;
+      result |= (uint32_t)(byte & 0x7f) << shift;
+      shift += 7;
+      if (!(byte & 0x80)) {
+        if (shift < 32 && (byte & 0x40)) result |= ~((1u << shift) - 1u);
+        break;
+      }
+    }
+    if (bits == 16) ((int16_t *)out)[i] = (int16_t)(uint16_t)result;
+    else ((int32_t *)out)[i] = (int32_t)result;
+  }
+  if (p != end) return -1;
+  r->off += nbytes;
+  return 0;
+}
+
+static int rd_i32s(rd_t *r, int32_t *o, size_t k) {
+  for (size_t i = 0; i < k; ++i) {
+    uint32_t v;
+    if (rd_u32(r, &v)) return -1;
+    o[i] = (int32_t)v;
+  }
+  return 0;
+}
+
+void or_net_free(or_net *net) {
+  if (!net) return;
+  free(net->ft_b), free(net->ft_w), free(net->psqt_w);
+  for (int i = 0; i < STACKS; ++i) free(net->w0[i]);
+  free(net);
+}
+
+#define FAIL(msg)                                     \
+  do {                                                \
+    if (err && errlen > 0) snprintf(err, (size_t)errlen, "%s", msg); \
+    or_net_free(net);                                 \
+    return -1;                                        \
+  } while (0)
+
+int or_net_load_mem(const uint8_t *buf, size_t len, or_net **out, char *err, int errlen) {
+  rd_t r = {buf, len, 0};
+  or_net *net = (or_net *)calloc(1, sizeof(or_net));
+  uint32_t version, hash, dlen;
+  if (!net) FAIL("out of memory");
+  if (rd_u32(&r, &version) || version != NNUE_VERSION) FAIL("bad version");
+  if (rd_u32(&r, &hash) || rd_u32(&r, &dlen) || r.off + dlen > len) FAIL("bad header");
+  r.off += dlen;
+  uint32_t fth;
+  if (rd_u32(&r, &fth)) FAIL("truncated");
+  int l1 = 0;
+  for (int cand = 32; cand <= 4096; cand += 32) {
+    uint32_t f, a;
+    uint32_t h = or_expected_hash(cand, &f, &a);
+    if (f == fth && h == hash) { l1 = cand; break; }
+  }
+  if (!l1) FAIL("hash mismatch (unsupported architecture)");
+  net->L1 = l1, net->hash = hash;
+  net->ft_b = (int16_t *)malloc(sizeof(int16_t) * (size_t)l1);
+  net->ft_w = (int16_t *)malloc(sizeof(int16_t) * (size_t)l1 * FT_INPUTS);
+  net->psqt_w = (int32_t *)malloc(sizeof(int32_t) * PSQT_BUCKETS * FT_INPUTS);
+  if (!net->ft_b || !net->ft_w || !net->psqt_w) FAIL("out of memory");
+  if (rd_leb(&r, 16, net->ft_b, (size_t)l1)) FAIL("bad FT biases");
+  if (rd_leb(&r, 16, net->ft_w, (size_t)l1 * FT_INPUTS)) FAIL("bad FT weights");
+  if (rd_leb(&r, 32, net->psqt_w, (size_t)PSQT_BUCKETS * FT_INPUTS)) FAIL("bad PSQT weights");
+  /* weights and biases are doubled at load (transform works in the x2 domain) */
+  for (int i = 0; i < l1; ++i) net->ft_b[i] = (int16_t)(net->ft_b[i] * 2);
+  for (size_t i = 0; i < (size_t)l1 * FT_INPUTS; ++i) net->ft_w[i] = (int16_t)(net->ft_w[i] * 2);
+  uint32_t arch;
+  or_expected_hash(l1, NULL, &arch);
+  for (int s = 0; s < STACKS; ++s) {
+    uint32_t h;
+    if (rd_u32(&r, &h) || h != arch) FAIL("bad layer-stack hash");
+    net->w0[s] = (int8_t *)malloc((size_t)16 * l1);
+    if (!net->w0[s]) FAIL("out of memory");
+    if (rd_i32s(&r, net->b0[s], 16) || rd_bytes(&r, net->w0[s], (size_t)16 * l1)) FAIL("bad fc_0");
+    if (rd_i32s(&r, net->b1[s], 32) || rd_bytes(&r, net->w1[s], 32 * 32)) FAIL("bad fc_1");
+    if (rd_i32s(&r, &net->b2[s], 1) || rd_bytes(&r, net->w2[s], 32)) FAIL("bad fc_2");
+  }
+  if (r.off != len) FAIL("trailing bytes after network");
+  *out = net;
+  return 0;
+}
+
+int or_net_load(const char *path, or_net **out, char *err, int errlen) {
+  FILE *f = fopen(path, "rb");
+  if (!f) {
+    if (err && errlen > 0) snprintf(err, (size_t)errlen, "cannot open %s", path);
+    return -1;
+  }
+  fseek(f, 0, SEEK_END);
+  long n = ftell(f);
+  fseek(f, 0, SEEK_SET);
+  uint8_t *buf = (uint8_t *)malloc((size_t)n);
+  if (!buf || fread(buf, 1, (size_t)n, f) != (size_t)n) {
+    fclose(f), free(buf);
+    if (err && errlen > 0) snprintf(err, (size_t)errlen, "read failed");
+    return -1;
+  }
+  fclose(f);
+  int rc = or_net_load_mem(buf, (size_t)n, out, err, errlen);
+  free(buf);
+  return rc;
+}
+
+int or_net_l1(const or_net *net) { return net->L1; }
+uint32_t or_net_hash(const or_net *net) { return net->hash; }
+
+/* HalfKAv2_hm: idx = (sq ^ orient) + PieceSquareIndex[persp][pc] + KingBucket * 704 */
+static int make_index(int persp, int sq, int pc, int ksq) {
+  int orient = ((ksq & 7) < 4 ? 7 : 0) ^ (persp == BLACK ? 56 : 0);
+  int rel_rank = persp == WHITE ? (ksq >> 3) : 7 - (ksq >> 3);
+  int f = ksq & 7;
+  int bucket = 4 * (7 - rel_rank) + (f < 4 ? f : 7 - f);
+  int pt = TYPE_OF(pc), plane;
+  if (pt == KING) plane = 10;
+  else plane = 2 * (pt - 1) + (COLOR_OF(pc) != persp);
+  return (sq ^ orient) + plane * 64 + bucket * 704;
+}
+
+static void accumulate(const or_net *net, const pos_t *p, int persp, int16_t *acc, int32_t *ps) {
+  int L1 = net->L1, ksq = king_sq(p, persp);
+  memcpy(acc, net->ft_b, sizeof(int16_t) * (size_t)L1);
+  for (int b = 0; b < 8; ++b) ps[b] = 0;
+  for (int sq = 0; sq < 64; ++sq) {
+    if (!p->b[sq]) continue;
+    int idx = make_index(persp, sq, p->b[sq], ksq);
+    const int16_t *w = net->ft_w + (size_t)idx * L1;
+    for (int i = 0; i < L1; ++i) acc[i] = (int16_t)(uint16_t)((uint16_t)acc[i] + (uint16_t)w[i]);
+    for (int b = 0; b < 8; ++b) ps[b] = (int32_t)((uint32_t)ps[b] + (uint32_t)net->psqt_w[(size_t)idx * 8 + b]);
+  }
+}
+
+static int clampi(int v, int lo, int hi) { return v < lo ? lo : v > hi ? hi : v; }
+static int32_t wmul(int32_t a, int32_t b) { return (int32_t)((uint32_t)a * (uint32_t)b); }
+static int32_t wadd(int32_t a, int32_t b) { return (int32_t)((uint32_t)a + (uint32_t)b); }
+
+/* Network::evaluate: returns {psqt / 16, positional / 16} (side-to-move POV) */
+static void net_output(const or_net *net, const pos_t *p, int32_t *psqt_out, int32_t *pos_out) {
+  int L1 = net->L1, H = L1 / 2;
+  int16_t acc[2][4096];
+  int32_t ps[2][8];
+  uint8_t x[4096];
+  accumulate(net, p, WHITE, acc[WHITE], ps[WHITE]);
+  accumulate(net, p, BLACK, acc[BLACK], ps[BLACK]);
+  int persp[2] = {p->stm, !p->stm};
+  for (int k = 0; k < 2; ++k)
+    for (int j = 0; j < H; ++j) {
+      int a = clampi(acc[persp[k]][j], 0, 254), b = clampi(acc[persp[k]][j + H], 0, 254);
+      x[k * H + j] = (uint8_t)((unsigned)(a * b) / 512u);
+    }
+  int count = 0;
+  for (int sq = 0; sq < 64; ++sq) count += p->b[sq] != 0;
+  int bucket = (count - 1) / 4;
+  int32_t psqt = (int32_t)((uint32_t)ps[p->stm][bucket] - (uint32_t)ps[!p->stm][bucket]) / 2;
+  int32_t fc0[16], fc1[32], in1[32];
+  for (int o = 0; o < 16; ++o) {
+    int32_t s = net->b0[bucket][o];
+    const int8_t *w = net->w0[bucket] + (size_t)o * L1;
+    for (int j = 0; j < L1; ++j) s = wadd(s, (int32_t)w[j] * x[j]);
+    fc0[o] = s;
+  }
+  for (int i = 0; i < 15; ++i) {
+    long long sq = ((long long)fc0[i] * fc0[i]) >> 19;
+    in1[i] = (int32_t)(sq < 127 ? sq : 127);
+    in1[15 + i] = clampi(fc0[i] >> 6, 0, 127);
+  }
+  in1[30] = in1[31] = 0;
+  for (int o = 0; o < 32; ++o) {
+    int32_t s = net->b1[bucket][o];
+    for (int j = 0; j < 32; ++j) s = wadd(s, (int32_t)net->w1[bucket][o * 32 + j] * in1[j]);
+    fc1[o] = clampi(s >> 6, 0, 127);
+  }
+  int32_t fc2 = net->b2[bucket];
+  for (int j = 0; j < 32; ++j) fc2 = wadd(fc2, (int32_t)net->w2[bucket][j] * fc1[j]);
+  int32_t fwd = wmul(fc0[15], 600 * 16) / (127 * (1 << 6));
+  int32_t positional = wadd(fc2, fwd);
+  *psqt_out = psqt / 16;
+  *pos_out = positional / 16;
+}
+
+/* ------------------------------------------------------------ evaluate -- */
+static const int PIECE_VALUE[7] = {0, 208, 781, 825, 1276, 2538, 0};
+
+static void material(const pos_t *p, int *pawns, int npm[2]) {
+  int np[2] = {0, 0};
+  npm[0] = npm[1] = 0;
+  for (int sq = 0; sq < 64; ++sq) {
+    int pc = p->b[sq];
+    if (!pc) continue;
+    if (TYPE_OF(pc) == PAWN) np[COLOR_OF(pc)]++;
+    else npm[COLOR_OF(pc)] += PIECE_VALUE[TYPE_OF(pc)];
+  }
+  pawns[0] = np[0], pawns[1] = np[1];
+}
+
+static void evaluate(const or_net *big, const or_net *small, const pos_t *p, int mode, or_eval *out) {
+  int pawns[2], npm[2], us = p->stm;
+  material(p, pawns, npm);
+  int simple = 208 * (pawns[us] - pawns[!us]) + (npm[us] - npm[!us]);
+  int small_net = mode == OR_MODE_SMALL ? 1 : mode == OR_MODE_BIG ? 0 : (abs(simple) > 962);
+  uint32_t flags = 0;
+  int32_t psqt, positional, nnue;
+  if (small_net) net_output(small, p, &psqt, &positional);
+  else net_output(big, p, &psqt, &positional);
+  nnue = wadd(wmul(125, psqt), wmul(131, positional)) / 128;
+  if (mode == OR_MODE_FULL && small_net && abs(nnue) < 236) {
+    net_output(big, p, &psqt, &positional);
+    nnue = wadd(wmul(125, psqt), wmul(131, positional)) / 128;
+    small_net = 0;
+    flags |= OR_FLAG_REEVAL;
+  }
+  int32_t complexity = abs(psqt - positional);
+  nnue = wadd(nnue, -(wmul(nnue, complexity) / 18000));
+  int32_t mat = 535 * (pawns[0] + pawns[1]) + npm[0] + npm[1];
+  int32_t v = wmul(nnue, 77777 + mat) / 77777;
+  v = wadd(v, -(wmul(v, p->rule50) / 212));
+  v = clampi(v, -31506, 31506);
+  if (small_net) flags |= OR_FLAG_SMALLNET;
+  if (in_check(p)) flags |= OR_FLAG_IN_CHECK;
+  out->psqt = psqt, out->positional = positional, out->final_v = v, out->flags = flags;
+}
+
+int or_eval_fen(const or_net *big, const or_net *small, const char *fen, int mode, or_eval *out) {
+  pos_t p;
+  memset(out, 0, sizeof(*out));
+  if (parse_fen(fen, &p)) {
+    out->flags = OR_FLAG_BAD_FEN;
+    return -1;
+  }
+  if ((mode != OR_MODE_SMALL && !big) || (mode != OR_MODE_BIG && !small)) return -2;
+  evaluate(big, small, &p, mode, out);
+  return 0;
+}
+
+typedef struct {
+  const or_net *big, *small;
+  const char *const *fens;
+  size_t lo, hi;
+  int mode;
+  or_eval *out;
+} job_t;
+
+static void *eval_worker(void *arg) {
+  job_t *j = (job_t *)arg;
+  for (size_t i = j->lo; i < j->hi; ++i) or_eval_fen(j->big, j->small, j->fens[i], j->mode, &j->out[i]);
+  return NULL;
+}
+
+int or_eval_fens(const or_net *big, const or_net *small, const char *const *fens, size_t n, int mode,
+                 or_eval *out, int threads) {
+  if (threads <= 1 || n < 2) {
+    job_t j = {big, small, fens, 0, n, mode, out};
+    eval_worker(&j);
+    return 0;
+  }
+  if (threads > 256) threads = 256;
+  pthread_t th[256];
+  job_t jobs[256];
+  int created[256] = {0};
+  size_t per = (n + (size_t)threads - 1) / (size_t)threads;
+  for (int t = 0; t < threads; ++t) {
+    size_t lo = (size_t)t * per, hi = lo + per < n ? lo + per : n;
+    if (lo >= hi) break;
+    jobs[t] = (job_t){big, small, fens, lo, hi, mode, out};
+    if (pthread_create(&th[t], NULL, eval_worker, &jobs[t])) eval_worker(&jobs[t]);
+    else created[t] = 1;
+  }
+  for (int t = 0; t < threads; ++t)
+    if (created[t]) pthread_join(th[t], NULL);
+  return 0;
+}
+
+int or_features(const char *fen, int perspective, uint32_t *idx, int cap) {
+  pos_t p;
+  if (parse_fen(fen, &p)) return -1;
+  int n = 0, ksq = king_sq(&p, perspective);
+  for (int sq = 0; sq < 64; ++sq) {
+    if (!p.b[sq]) continue;
+    if (n >= cap) return -2;
+    idx[n++] = (uint32_t)make_index(perspective, sq, p.b[sq], ksq);
+  }
+  return n;
+}
+
+int or_accumulate(const or_net *net, const char *fen, int perspective, int16_t *acc, int32_t *psqt8) {
+  pos_t p;
+  if (parse_fen(fen, &p)) return -1;
+  accumulate(net, &p, perspective, acc, psqt8);
+  return 0;
+}
+
+int or_net_output(const or_net *net, const char *fen, int32_t *psqt, int32_t *positional) {
+  pos_t p;
+  if (parse_fen(fen, &p)) return -1;
+  net_output(net, &p, psqt, positional);
+  return 0;
+}
+
+int or_expand_eval(const or_net *big, const or_net *small, const char *fen, int mode, or_eval *parent,
+                   uint16_t *moves, or_eval *children, int cap) {
+  pos_t p;
+  uint16_t mv[256];
+  if (parse_fen(fen, &p)) {
+    memset(parent, 0, sizeof(*parent));
+    parent->flags = OR_FLAG_BAD_FEN;
+    return -1;
+  }
+  evaluate(big, small, &p, mode, parent);
+  int n = gen_legal(&p, mv);
+  if (n > cap) return -2;
+  for (int i = 0; i < n; ++i) {
+    pos_t q;
+    do_move(&p, mv[i], &q);
+    moves[i] = mv[i];
+    evaluate(big, small, &q, mode, &children[i]);
+  }
+  return n;
+}

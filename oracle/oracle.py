@@ -1,0 +1,193 @@
+"""ctypes wrapper over oracle/_build/liboracle.so — TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import
+this module.  It is the checker for the product path (libgpu_nnue.so); the
+product never imports it.  See oracle.h for what is restated and the parity
+status (perft pinned by public known answers; NNUE "parity unpinned").
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_build", "liboracle.so")
+
+MODE_FULL, MODE_BIG, MODE_SMALL = 0, 1, 2
+FLAG_IN_CHECK, FLAG_SMALLNET, FLAG_BAD_FEN, FLAG_REEVAL = 1, 2, 4, 8
+
+
+class OrEval(C.Structure):
+    _fields_ = [("psqt", C.c_int32), ("positional", C.c_int32),
+                ("final_v", C.c_int32), ("flags", C.c_uint32)]
+
+
+EVAL_DTYPE = np.dtype([("psqt", "<i4"), ("positional", "<i4"),
+                       ("final_v", "<i4"), ("flags", "<u4")])
+
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = C.CDLL(LIB_PATH)
+        L.or_net_load.argtypes = [C.c_char_p, C.POINTER(C.c_void_p), C.c_char_p, C.c_int]
+        L.or_net_load_mem.argtypes = [C.c_void_p, C.c_size_t, C.POINTER(C.c_void_p), C.c_char_p, C.c_int]
+        L.or_net_free.argtypes = [C.c_void_p]
+        L.or_net_l1.argtypes = [C.c_void_p]
+        L.or_net_hash.argtypes = [C.c_void_p]
+        L.or_net_hash.restype = C.c_uint32
+        L.or_expected_hash.argtypes = [C.c_int, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
+        L.or_expected_hash.restype = C.c_uint32
+        L.or_eval_fen.argtypes = [C.c_void_p, C.c_void_p, C.c_char_p, C.c_int, C.POINTER(OrEval)]
+        L.or_eval_fens.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(C.c_char_p), C.c_size_t,
+                                   C.c_int, C.c_void_p, C.c_int]
+        L.or_features.argtypes = [C.c_char_p, C.c_int, C.POINTER(C.c_uint32), C.c_int]
+        L.or_accumulate.argtypes = [C.c_void_p, C.c_char_p, C.c_int, C.c_void_p, C.c_void_p]
+        L.or_net_output.argtypes = [C.c_void_p, C.c_char_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
+        L.or_legal_moves.argtypes = [C.c_char_p, C.POINTER(C.c_uint16), C.c_int]
+        L.or_child_fen.argtypes = [C.c_char_p, C.c_uint16, C.c_char_p, C.c_int]
+        L.or_normalize_fen.argtypes = [C.c_char_p, C.c_char_p, C.c_int]
+        L.or_perft.argtypes = [C.c_char_p, C.c_int]
+        L.or_perft.restype = C.c_uint64
+        L.or_expand_eval.argtypes = [C.c_void_p, C.c_void_p, C.c_char_p, C.c_int, C.POINTER(OrEval),
+                                     C.POINTER(C.c_uint16), C.c_void_p, C.c_int]
+        _lib = L
+    return _lib
+
+
+class Net:
+    """A loaded .nnue network (oracle side)."""
+
+    def __init__(self, path=None, data: bytes | None = None):
+        err = C.create_string_buffer(256)
+        h = C.c_void_p()
+        if data is not None:
+            buf = (C.c_uint8 * len(data)).from_buffer_copy(data)
+            rc = lib().or_net_load_mem(buf, len(data), C.byref(h), err, 256)
+        else:
+            rc = lib().or_net_load(str(path).encode(), C.byref(h), err, 256)
+        if rc != 0:
+            raise ValueError(f"oracle net load failed: {err.value.decode()}")
+        self.h = h
+
+    @property
+    def l1(self):
+        return lib().or_net_l1(self.h)
+
+    @property
+    def hash(self):
+        return lib().or_net_hash(self.h)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().or_net_free(self.h)
+            self.h = None
+
+
+def expected_hash(l1):
+    ft, arch = C.c_uint32(), C.c_uint32()
+    h = lib().or_expected_hash(l1, C.byref(ft), C.byref(arch))
+    return h, ft.value, arch.value
+
+
+def _h(net):
+    return net.h if net is not None else None
+
+
+def eval_fen(big, small, fen, mode=MODE_FULL):
+    out = OrEval()
+    lib().or_eval_fen(_h(big), _h(small), fen.encode(), mode, C.byref(out))
+    return (out.psqt, out.positional, out.final_v, out.flags)
+
+
+def eval_fens(big, small, fens, mode=MODE_FULL, threads=1):
+    n = len(fens)
+    arr = (C.c_char_p * n)(*[f.encode() for f in fens])
+    out = np.zeros(n, dtype=EVAL_DTYPE)
+    lib().or_eval_fens(_h(big), _h(small), arr, n, mode, out.ctypes.data, threads)
+    return out
+
+
+def features(fen, perspective):
+    buf = (C.c_uint32 * 64)()
+    n = lib().or_features(fen.encode(), perspective, buf, 64)
+    if n < 0:
+        raise ValueError("bad fen")
+    return list(buf[:n])
+
+
+def accumulate(net, fen, perspective):
+    acc = np.zeros(net.l1, dtype=np.int16)
+    ps = np.zeros(8, dtype=np.int32)
+    if lib().or_accumulate(net.h, fen.encode(), perspective, acc.ctypes.data, ps.ctypes.data):
+        raise ValueError("bad fen")
+    return acc, ps
+
+
+def net_output(net, fen):
+    a, b = C.c_int32(), C.c_int32()
+    if lib().or_net_output(net.h, fen.encode(), C.byref(a), C.byref(b)):
+        raise ValueError("bad fen")
+    return a.value, b.value
+
+
+def legal_moves(fen):
+    buf = (C.c_uint16 * 256)()
+    n = lib().or_legal_moves(fen.encode(), buf, 256)
+    if n < 0:
+        raise ValueError("bad fen")
+    return list(buf[:n])
+
+
+def child_fen(fen, move):
+    out = C.create_string_buffer(128)
+    if lib().or_child_fen(fen.encode(), move, out, 128) < 0:
+        raise ValueError("bad fen")
+    return out.value.decode()
+
+
+def normalize_fen(fen):
+    out = C.create_string_buffer(128)
+    if lib().or_normalize_fen(fen.encode(), out, 128) < 0:
+        raise ValueError("bad fen")
+    return out.value.decode()
+
+
+def perft(fen, depth):
+    v = lib().or_perft(fen.encode(), depth)
+    if v == 2**64 - 1:
+        raise ValueError("bad fen")
+    return v
+
+
+def expand_eval(big, small, fen, mode=MODE_FULL):
+    parent = OrEval()
+    moves = (C.c_uint16 * 256)()
+    kids = np.zeros(256, dtype=EVAL_DTYPE)
+    n = lib().or_expand_eval(_h(big), _h(small), fen.encode(), mode, C.byref(parent), moves,
+                             kids.ctypes.data, 256)
+    if n < 0:
+        raise ValueError("bad fen")
+    return ((parent.psqt, parent.positional, parent.final_v, parent.flags),
+            list(moves[:n]), kids[:n].copy())
+
+
+def move_to_uci(m):
+    """Stockfish move encoding -> UCI text (Chess960 castling: king takes rook)."""
+    to, frm, typ = m & 63, (m >> 6) & 63, m >> 14
+    sq = lambda s: "abcdefgh"[s & 7] + str((s >> 3) + 1)
+    u = sq(frm) + sq(to)
+    if typ == 1:
+        u += "nbrq"[(m >> 12) & 3]
+    return u

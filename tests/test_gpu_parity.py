@@ -1,0 +1,139 @@
+"""GPU parity: libgpu_nnue (HIP, gfx950) against the CPU oracle, bit-exact.
+
+Every check here compares integers, so the bar is exact equality (north star:
+"Results must match ... bit-exactly, since all arithmetic is integer").
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def special_fens():
+    with open(os.path.join(HERE, "golden", "special_fens.txt")) as f:
+        return [l.strip() for l in f if l.strip() and not l.startswith("#")]
+
+
+def random_fens(n, seed, max_plies=160):
+    from fishnet_amd import gpu_nnue as G
+    boards = G.random_positions(seed, 0, n, max_plies)
+    return [G.board_to_fen(b) for b in boards]
+
+
+def _cmp(got, exp, fens):
+    bad = np.nonzero(got != exp)[0]
+    if len(bad):
+        i = bad[0]
+        raise AssertionError(f"{len(bad)} mismatches; first {fens[i]!r}: gpu={got[i]} oracle={exp[i]}")
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_special_fens_all_modes(gpu_ctx, oracle_nets, oracle_lib, mode):
+    big, small = oracle_nets
+    fens = special_fens()
+    _cmp(gpu_ctx.evaluate_batch(fens, mode), oracle_lib.eval_fens(big, small, fens, mode, threads=8), fens)
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_random_playouts_all_modes(gpu_ctx, oracle_nets, oracle_lib, mode):
+    big, small = oracle_nets
+    fens = random_fens(3000, 0x5EED0000 + 17 * mode)
+    got = gpu_ctx.evaluate_batch(fens, mode)
+    _cmp(got, oracle_lib.eval_fens(big, small, fens, mode, threads=8), fens)
+    if mode == 0:  # the FULL pipeline exercised every branch
+        flags = got["flags"]
+        assert (flags & 2).any() and (flags & 8).any() and ((flags & 10) == 0).any()
+
+
+def test_golden_vectors(gpu_ctx):
+    """The committed oracle goldens (tests/golden/eval_goldens.json) on the GPU."""
+    g = json.load(open(os.path.join(HERE, "golden", "eval_goldens.json")))
+    for mode_name, rows in g["results"].items():
+        mode = {"full": 0, "big": 1, "small": 2}[mode_name]
+        fens = [r[0] for r in rows]
+        exp = np.array([tuple(r[1:]) for r in rows], dtype=gpu_ctx.evaluate_batch([], mode).dtype)
+        _cmp(gpu_ctx.evaluate_batch(fens, mode), exp, fens)
+
+
+def test_bad_fens_flagged(gpu_ctx):
+    fens = ["", "garbage", "8/8/8/8/8/8/8/8 w - - 0 1", "K7/8/8/8/8/8/8/7K w - - 0 1",
+            "rnbqkbnr/pppppppp/8/8/8/8/PPPPPPPP/RNBQKBNR w KQkq - 0 1", "P3k3/8/8/8/8/8/8/4K3 w - - 0 1",
+            "4k3/8/8/8/8/8/8/R3K3 b - - 0 1x", "4k3/4R3/8/8/8/8/8/4K3 w - - 0 1"]
+    out = gpu_ctx.evaluate_batch(fens, 0)
+    assert [bool(f & 4) for f in out["flags"]] == [True, True, True, True, False, True, False, True]
+    assert (out[out["flags"] & 4 != 0][["psqt", "positional", "final_v"]].tolist()
+            == [(0, 0, 0)] * 6)
+
+
+def test_stress_net_wraps(oracle_lib):
+    """FT weights large enough that the int16 accumulators wrap constantly."""
+    from fishnet_amd import gpu_nnue as G, synthnet
+    p = synthnet.cached_synth_net(128, 7, stress=True)
+    ctx = G.GpuNnue(None, p)
+    on = oracle_lib.Net(p)
+    fens = special_fens() + random_fens(2000, 99)
+    acc, _ = oracle_lib.accumulate(on, fens[2], 0)
+    _cmp(ctx.evaluate_batch(fens, 2), oracle_lib.eval_fens(None, on, fens, 2, threads=8), fens)
+    # sanity: the wrap really happens (|x2 accumulator| > 32767 before wrapping)
+    assert np.abs(acc.astype(np.int32)).max() > 8000
+
+
+def test_big_stress_net(oracle_lib):
+    from fishnet_amd import gpu_nnue as G, synthnet
+    p = synthnet.cached_synth_net(3072, 11, stress=True)
+    ctx = G.GpuNnue(p, None)
+    on = oracle_lib.Net(p)
+    fens = special_fens() + random_fens(500, 1234)
+    _cmp(ctx.evaluate_batch(fens, 1), oracle_lib.eval_fens(on, None, fens, 1, threads=8), fens)
+
+
+def test_device_api_matches_host_api(gpu_ctx):
+    from fishnet_amd import gpu_nnue as G
+    boards = G.random_positions(42, 1000, 4099, 160)
+    fens = [G.board_to_fen(b) for b in boards]
+    d_b = gpu_ctx.alloc(boards.nbytes)
+    d_o = gpu_ctx.alloc(len(boards) * 16)
+    d_b.upload(boards)
+    for mode in (0, 1, 2):
+        gpu_ctx.evaluate_device(d_b, len(boards), mode, d_o)
+        gpu_ctx.synchronize()
+        got = d_o.download(G.EVAL_DTYPE, len(boards))
+        assert np.array_equal(got, gpu_ctx.evaluate_batch(fens, mode))
+    ms, per = gpu_ctx.time_evaluate_device(d_b, len(boards), 1, d_o, 3)
+    assert ms > 0 and per[2] > 0
+
+
+def test_perft_known_answers(gpu_ctx):
+    g = json.load(open(os.path.join(HERE, "golden", "perft.json")))
+    for c in g["cases"]:
+        for d, nodes in enumerate(c["nodes"], start=1):
+            if nodes > 200_000_000:
+                break
+            assert gpu_ctx.perft(c["fen"], d) == nodes, (c["name"], d)
+
+
+def test_perft_special_vs_oracle(gpu_ctx, oracle_lib):
+    for fen in special_fens():
+        for d in (1, 2, 3):
+            assert gpu_ctx.perft(fen, d) == oracle_lib.perft(fen, d), (fen, d)
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_expand_vs_oracle(gpu_ctx, oracle_nets, oracle_lib, mode):
+    from fishnet_amd.gpu_nnue import move_to_uci
+    big, small = oracle_nets
+    fens = special_fens() + random_fens(150, 777)
+    parents, offs, moves, kids = gpu_ctx.expand_and_evaluate(fens, mode)
+    for i, fen in enumerate(fens):
+        p_exp, m_exp, k_exp = oracle_lib.expand_eval(big, small, fen, mode)
+        assert tuple(parents[i]) == p_exp, fen
+        lo, hi = int(offs[i]), int(offs[i + 1])
+        got = {int(m): tuple(k) for m, k in zip(moves[lo:hi], kids[lo:hi])}
+        exp = {int(m): tuple(k) for m, k in zip(m_exp, k_exp)}
+        assert set(got) == set(exp), (fen, sorted(map(move_to_uci, set(got) ^ set(exp))))
+        assert got == exp, fen

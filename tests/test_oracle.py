@@ -1,0 +1,157 @@
+"""The CPU oracle pinned before it is trusted (CPU only).
+
+- movegen: public perft known answers (tests/golden/perft.json), incl. Chess960;
+- NNUE: "parity unpinned" against Stockfish (no source, binary or net exists in
+  the container).  What IS pinned: the committed goldens
+  (regression), hand-derived HalfKAv2_hm indices, the file format round trip,
+  and a third, independent numpy restatement written here in the test.
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+START = "rnbqkbnr/pppppppp/8/8/8/8/PPPPPPPP/RNBQKBNR w KQkq - 0 1"
+
+
+def test_perft_known_answers(oracle_lib):
+    g = json.load(open(os.path.join(HERE, "golden", "perft.json")))
+    for c in g["cases"]:
+        for d, nodes in enumerate(c["nodes"], start=1):
+            if nodes > 3_000_000:
+                break
+            assert oracle_lib.perft(c["fen"], d) == nodes, (c["name"], d)
+
+
+def test_hashes_two_implementations(oracle_lib):
+    from fishnet_amd import synthnet
+    for l1 in (128, 1024, 3072):
+        assert oracle_lib.expected_hash(l1) == synthnet.hashes(l1)
+
+
+def test_leb128_roundtrip():
+    from fishnet_amd import synthnet
+    rng = np.random.default_rng(0)
+    for bits in (16, 32):
+        lo, hi = -(1 << (bits - 1)), (1 << (bits - 1)) - 1
+        v = np.concatenate([np.array([0, 1, -1, 63, 64, -64, -65, lo, hi]),
+                            rng.integers(lo, hi, 2000)]).astype(np.int64)
+        assert np.array_equal(synthnet.leb128_decode(synthnet.leb128_encode(v), len(v), bits), v)
+
+
+def test_feature_index_hand_derived(oracle_lib):
+    # white perspective, white king e1 (file e: no mirror, bucket 31 -> 21824)
+    w = oracle_lib.features(START, 0)
+    assert 8 + 21824 in w          # own pawn a2: plane 0
+    assert 60 + 640 + 21824 in w   # their king e8: plane 10
+    assert 57 + 3 * 64 + 21824 in w  # their knight b8: plane 3
+    # black perspective is the mirror image of white's at the start position
+    assert sorted(oracle_lib.features(START, 1)) == sorted(w)
+    # king on d1 (file d) mirrors files: own rook a1 -> a1 ^ 7 = h1 (7), bucket 28+3=31
+    f = oracle_lib.features("4k3/8/8/8/8/8/8/R2K4 w - - 0 1", 0)
+    assert 7 + 6 * 64 + 31 * 704 in f
+    # white king on h1: file h (no mirror), bucket 4*7 + min(7, 0) = 28
+    f = oracle_lib.features("k7/8/8/8/8/8/8/7K w - - 0 1", 0)
+    assert 7 + 640 + 28 * 704 in f and 56 + 640 + 28 * 704 in f
+    # black perspective, black king a8: files a-d mirror, ranks flip -> a8 ^ 63 = h1, bucket 28
+    f = oracle_lib.features("k7/8/8/8/8/8/8/7K w - - 0 1", 1)
+    assert (56 ^ 63) + 640 + 28 * 704 in f and (7 ^ 63) + 640 + 28 * 704 in f
+    assert all(0 <= x < 22528 for x in f)
+
+
+def test_goldens_regenerate_identically(oracle_lib, oracle_nets, synth_big_path, synth_small_path):
+    g = json.load(open(os.path.join(HERE, "golden", "eval_goldens.json")))
+    sha = lambda p: hashlib.sha256(open(p, "rb").read()).hexdigest()
+    assert g["nets"]["big"]["sha256"] == sha(synth_big_path)
+    assert g["nets"]["small"]["sha256"] == sha(synth_small_path)
+    big, small = oracle_nets
+    for name, mode in (("full", 0), ("big", 1), ("small", 2)):
+        rows = g["results"][name]
+        got = oracle_lib.eval_fens(big, small, [r[0] for r in rows], mode, threads=4)
+        assert [list(map(int, r)) for r in got.tolist()] == [r[1:] for r in rows]
+
+
+def test_goldens_cover_every_branch():
+    g = json.load(open(os.path.join(HERE, "golden", "eval_goldens.json")))
+    flags = [r[4] for r in g["results"]["full"]]
+    assert any(f & 1 for f in flags) and any(f & 2 for f in flags) and any(f & 8 for f in flags)
+    assert any(f & 10 == 0 for f in flags)
+
+
+# ---------------------------------------------------------------- numpy ----
+PT = {"p": 1, "n": 2, "b": 3, "r": 4, "q": 5, "k": 6}
+
+
+def np_board(fen):
+    rows, stm = fen.split()[0].split("/"), fen.split()[1]
+    pcs = {}
+    for r, row in enumerate(rows):
+        f = 0
+        for ch in row:
+            if ch.isdigit():
+                f += int(ch)
+            else:
+                pcs[(7 - r) * 8 + f] = (0 if ch.isupper() else 1, PT[ch.lower()])
+                f += 1
+    rule50 = int(fen.split()[4]) if len(fen.split()) > 4 else 0
+    return pcs, (1 if stm == "b" else 0), rule50
+
+
+def np_index(persp, sq, color, pt, ksq):
+    kf = ksq % 8
+    orient = (7 if kf < 4 else 0) ^ (56 if persp else 0)
+    rr = (ksq // 8) ^ (7 if persp else 0)
+    bucket = 4 * (7 - rr) + min(kf, 7 - kf)
+    plane = 10 if pt == 6 else 2 * (pt - 1) + (color != persp)
+    return (sq ^ orient) + 64 * plane + 704 * bucket
+
+
+def np_net_output(a, fen):
+    """numpy restatement of Network::evaluate for a synthetic net's arrays."""
+    pcs, stm, _ = np_board(fen)
+    l1 = a["ft_bias"].shape[0]
+    h = l1 // 2
+    acc, ps = {}, {}
+    for persp in (0, 1):
+        ksq = [s for s, (c, t) in pcs.items() if c == persp and t == 6][0]
+        idx = [np_index(persp, s, c, t, ksq) for s, (c, t) in pcs.items()]
+        w = a["ft_w"][idx].astype(np.int64).sum(axis=0) * 2 + a["ft_bias"].astype(np.int64) * 2
+        acc[persp] = ((w + 32768) % 65536 - 32768)  # int16 wrap of the doubled sum
+        ps[persp] = a["psqt"][idx].astype(np.int64).sum(axis=0)
+    x = np.concatenate([np.clip(acc[p][:h], 0, 254) * np.clip(acc[p][h:], 0, 254) // 512 for p in (stm, 1 - stm)])
+    bucket = (len(pcs) - 1) // 4
+    psqt = int(ps[stm][bucket] - ps[1 - stm][bucket])
+    psqt = int(psqt / 2)  # C truncation
+    fc0 = a["b0"][bucket].astype(np.int64) + a["w0"][bucket].astype(np.int64) @ x
+    in1 = np.zeros(32, dtype=np.int64)
+    in1[:15] = np.minimum(127, (fc0[:15] * fc0[:15]) >> 19)
+    in1[15:30] = np.clip(fc0[:15] >> 6, 0, 127)
+    fc1 = np.clip((a["b1"][bucket].astype(np.int64) + a["w1"][bucket].astype(np.int64) @ in1) >> 6, 0, 127)
+    fc2 = int(a["b2"][bucket][0] + a["w2"][bucket].astype(np.int64) @ fc1)
+    fwd = int(fc0[15] * 9600 / 8128) if fc0[15] >= 0 else -int(-fc0[15] * 9600 / 8128)
+    pos = fc2 + fwd
+    trunc = lambda v: int(v / 16) if v >= 0 else -int(-v / 16)
+    return trunc(psqt), trunc(pos)
+
+
+@pytest.mark.parametrize("stress", [False, True])
+def test_numpy_restatement_agrees(oracle_lib, stress):
+    from fishnet_amd import synthnet
+    seed = 7 if stress else 2
+    a = synthnet.synth_net_arrays(128, seed, stress)
+    net = oracle_lib.Net(synthnet.cached_synth_net(128, seed, stress))
+    fens = [l.strip() for l in open(os.path.join(HERE, "golden", "special_fens.txt"))
+            if l.strip() and not l.startswith("#")]
+    for fen in fens:
+        assert oracle_lib.net_output(net, fen) == np_net_output(a, fen), fen
+
+
+def test_net_parser_rejects_corruption(oracle_lib, synth_small_path):
+    data = open(synth_small_path, "rb").read()
+    for bad in (data[:-1], data + b"\0", data[:4] + b"\1\2\3\4" + data[8:], b"\0" * 64):
+        with pytest.raises(ValueError):
+            oracle_lib.Net(data=bad)
+    assert oracle_lib.Net(data=data).l1 == 128
