@@ -430,4 +430,86 @@ GN_HD Board do_move(const Board &B, uint16_t m, Dirty *d = nullptr) {
   return C;
 }
 
+// ------------------------------------------------------ random playouts ----
+// xoshiro256** (Blackman & Vigna), seeded through splitmix64
+struct Xoshiro {
+  uint64_t s0, s1, s2, s3;
+  GN_HD explicit Xoshiro(uint64_t seed) {
+    s0 = mix(seed += 0x9E3779B97F4A7C15ull);
+    s1 = mix(seed += 0x9E3779B97F4A7C15ull);
+    s2 = mix(seed += 0x9E3779B97F4A7C15ull);
+    s3 = mix(seed += 0x9E3779B97F4A7C15ull);
+  }
+  GN_HD static uint64_t mix(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+  }
+  GN_HD static uint64_t rotl(uint64_t x, int k) { return (x << k) | (x >> (64 - k)); }
+  GN_HD uint64_t next() {
+    uint64_t r = rotl(s1 * 5, 7) * 9, t = s1 << 17;
+    s2 ^= s0, s3 ^= s1, s1 ^= s2, s0 ^= s3, s2 ^= t, s3 = rotl(s3, 45);
+    return r;
+  }
+  GN_HD uint32_t below(uint32_t n) { return (uint32_t)((next() >> 32) * n >> 32); }
+};
+
+GN_HD Board start_position() {
+  Board B;
+  B.byType[PAWN] = 0x00FF00000000FF00ull;
+  B.byType[KNIGHT] = 0x4200000000000042ull;
+  B.byType[BISHOP] = 0x2400000000000024ull;
+  B.byType[ROOK] = 0x8100000000000081ull;
+  B.byType[QUEEN] = 0x0800000000000008ull;
+  B.byType[KING] = 0x1000000000000010ull;
+  B.byColor[WHITE] = 0xFFFFull;
+  B.byColor[BLACK] = 0xFFFF000000000000ull;
+  B.byType[0] = B.byColor[WHITE] | B.byColor[BLACK];
+  B.stm = WHITE, B.ep = SQ_NONE;
+  B.castle_rook[0] = 7, B.castle_rook[1] = 0, B.castle_rook[2] = 63, B.castle_rook[3] = 56;
+  B.rule50 = 0, B.fullmove = 1;
+  return B;
+}
+
+GN_HD int count_legal(const Board &B, const Tables &T) {
+  int n = 0;
+  gen_legal(B, T, [&](uint16_t) { ++n; });
+  return n;
+}
+
+GN_HD uint16_t nth_legal(const Board &B, const Tables &T, int r) {
+  uint16_t pick = 0;
+  int k = 0;
+  gen_legal(B, T, [&](uint16_t m) {
+    if (k++ == r) pick = m;
+  });
+  return pick;
+}
+
+// Random playout from the start position (SURVEY.md §8d workload): k ~
+// U{0..max_plies} uniformly random legal plies, stopping at mate / stalemate /
+// rule50 >= 100; a final position in check is played on (<= 8 plies) or the
+// playout restarts (bounded: 64 attempts).  Host and device run this same code,
+// so a seed gives the same position everywhere.
+GN_HD Board random_playout(uint64_t seed, int max_plies, const Tables &T) {
+  Xoshiro rng(seed);
+  Board B = start_position();
+  for (int attempt = 0; attempt < 64; ++attempt) {
+    B = start_position();
+    const int k = (int)rng.below((uint32_t)max_plies + 1);
+    for (int ply = 0; ply < k; ++ply) {
+      const int n = count_legal(B, T);
+      if (!n || B.rule50 >= 100) break;
+      B = do_move(B, nth_legal(B, T, (int)rng.below((uint32_t)n)));
+    }
+    for (int extra = 0; extra < 8 && in_check(B, T); ++extra) {
+      const int n = count_legal(B, T);
+      if (!n) break;
+      B = do_move(B, nth_legal(B, T, (int)rng.below((uint32_t)n)));
+    }
+    if (!in_check(B, T)) break;
+  }
+  return B;
+}
+
 } // namespace gn

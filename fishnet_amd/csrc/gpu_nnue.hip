@@ -336,8 +336,10 @@ struct KernelTimes {
   bool on = false;
 };
 
+// Launch sequence of one evaluation.  ev (optional) = 5 events recorded between
+// the stages [classify(+)] [small net (+reeval)] [big net] [finalize].
 static int evaluate_on(gn_ctx *ctx, Dev &d, const gn_board *b, size_t n, int mode, gn_eval *out, hipStream_t s,
-                       float *kt /* [4] accumulated ms or null */) {
+                       hipEvent_t *ev) {
   if (mode < GN_MODE_FULL || mode > GN_MODE_SMALL) return fail(GN_E_INVALID, "bad mode %d", mode);
   if ((mode != GN_MODE_SMALL && !d.has[BIG]) || (mode != GN_MODE_BIG && !d.has[SMALL]))
     return fail(GN_E_NONET, "mode %d needs a network that is not loaded", mode);
@@ -348,10 +350,7 @@ static int evaluate_on(gn_ctx *ctx, Dev &d, const gn_board *b, size_t n, int mod
     HIP_TRY(d.nsm.ensure(n));
     HIP_TRY(d.nbg.ensure(n));
   }
-  hipEvent_t ev[6] = {};
-  if (kt)
-    for (auto &e : ev) HIP_TRY(hipEventCreate(&e));
-  auto mark = [&](int k) -> hipError_t { return kt ? hipEventRecord(ev[k], s) : hipSuccess; };
+  auto mark = [&](int k) -> hipError_t { return ev ? hipEventRecord(ev[k], s) : hipSuccess; };
   const gn_eval_params &P = ctx->P;
   HIP_TRY(mark(0));
   if (mode == GN_MODE_FULL) HIP_TRY(launch_classify(b, n, P, d.nsm.p, d.nbg.p, s));
@@ -363,15 +362,6 @@ static int evaluate_on(gn_ctx *ctx, Dev &d, const gn_board *b, size_t n, int mod
   HIP_TRY(mark(3));
   HIP_TRY(launch_finalize(b, n, mode, d.osm.p, d.obg.p, d.nsm.p, d.nbg.p, P, d.tables, out, s));
   HIP_TRY(mark(4));
-  if (kt) {
-    HIP_TRY(hipEventSynchronize(ev[4]));
-    for (int k = 0; k < 4; ++k) {
-      float ms = 0;
-      HIP_TRY(hipEventElapsedTime(&ms, ev[k], ev[k + 1]));
-      kt[k] += ms;
-    }
-    for (auto &e : ev) (void)hipEventDestroy(e);
-  }
   return GN_OK;
 }
 
@@ -530,27 +520,49 @@ int gn_time_evaluate_device(gn_ctx *ctx, int device_slot, const gn_board *d_boar
   if (iters <= 0 || !ms_total) return fail(GN_E_INVALID, "bad iters / ms_total");
   std::lock_guard<std::mutex> lk(d->mu);
   HIP_TRY(hipSetDevice(d->id));
-  hipEvent_t a, b;
-  HIP_TRY(hipEventCreate(&a));
-  HIP_TRY(hipEventCreate(&b));
-  HIP_TRY(hipEventRecord(a, d->stream));
-  for (int it = 0; it < iters; ++it) {
-    int rc = evaluate_on(ctx, *d, d_boards, n, mode, d_out, d->stream, nullptr);
-    if (rc) return rc;
-  }
-  HIP_TRY(hipEventRecord(b, d->stream));
-  HIP_TRY(hipEventSynchronize(b));
-  HIP_TRY(hipEventElapsedTime(ms_total, a, b));
-  (void)hipEventDestroy(a);
-  (void)hipEventDestroy(b);
-  if (per_kernel_ms) {
-    float kt[4] = {0, 0, 0, 0};
-    for (int it = 0; it < iters; ++it) {
-      int rc = evaluate_on(ctx, *d, d_boards, n, mode, d_out, d->stream, kt);
-      if (rc) return rc;
+  std::vector<hipEvent_t> ev((size_t)iters * 5 + 2, nullptr);
+  auto cleanup = [&] {
+    for (auto &e : ev)
+      if (e) (void)hipEventDestroy(e);
+  };
+  for (auto &e : ev)
+    if (hipEventCreate(&e) != hipSuccess) {
+      cleanup();
+      return fail(GN_E_HIP, "hipEventCreate failed");
     }
-    for (int k = 0; k < 4; ++k) per_kernel_ms[k] = kt[k] / (float)iters;
+  int rc = GN_OK;
+  hipError_t he = hipEventRecord(ev[0], d->stream);
+  for (int it = 0; it < iters && rc == GN_OK && he == hipSuccess; ++it)
+    rc = evaluate_on(ctx, *d, d_boards, n, mode, d_out, d->stream, per_kernel_ms ? &ev[2 + 5 * it] : nullptr);
+  if (rc == GN_OK && he == hipSuccess) he = hipEventRecord(ev[1], d->stream);
+  if (rc == GN_OK && he == hipSuccess) he = hipEventSynchronize(ev[1]);
+  if (rc == GN_OK && he == hipSuccess) he = hipEventElapsedTime(ms_total, ev[0], ev[1]);
+  if (rc == GN_OK && he == hipSuccess && per_kernel_ms) {
+    float acc[4] = {0, 0, 0, 0};
+    for (int it = 0; it < iters && he == hipSuccess; ++it)
+      for (int k = 0; k < 4 && he == hipSuccess; ++k) {
+        float ms = 0;
+        he = hipEventElapsedTime(&ms, ev[2 + 5 * it + k], ev[2 + 5 * it + k + 1]);
+        acc[k] += ms;
+      }
+    for (int k = 0; k < 4; ++k) per_kernel_ms[k] = acc[k] / (float)iters;
   }
+  cleanup();
+  if (rc) return rc;
+  if (he != hipSuccess) return fail(GN_E_HIP, "timing failed: %s", hipGetErrorString(he));
+  return GN_OK;
+}
+
+int gn_random_positions_device(gn_ctx *ctx, int device_slot, uint64_t seed, size_t first_index, size_t n,
+                               int max_plies, gn_board *d_out, void *stream) {
+  Dev *d = slot(ctx, device_slot);
+  if (!d) return fail(GN_E_INVALID, "bad context or device slot");
+  if (n && !d_out) return fail(GN_E_INVALID, "NULL buffer");
+  if (max_plies < 0) return fail(GN_E_INVALID, "max_plies < 0");
+  std::lock_guard<std::mutex> lk(d->mu);
+  HIP_TRY(hipSetDevice(d->id));
+  HIP_TRY(launch_random_positions(seed, first_index, n, max_plies, d->tables, d_out,
+                                  stream ? (hipStream_t)stream : d->stream));
   return GN_OK;
 }
 

@@ -155,54 +155,12 @@ inline int board_to_fen(const Board &B, char *out, size_t cap) {
   return k;
 }
 
-// xoshiro256** (Blackman & Vigna), seeded through splitmix64
-struct Xoshiro {
-  uint64_t s[4];
-  explicit Xoshiro(uint64_t seed) {
-    for (int i = 0; i < 4; ++i) {
-      uint64_t z = (seed += 0x9E3779B97F4A7C15ull);
-      z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-      z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-      s[i] = z ^ (z >> 31);
-    }
-  }
-  static uint64_t rotl(uint64_t x, int k) { return (x << k) | (x >> (64 - k)); }
-  uint64_t next() {
-    uint64_t r = rotl(s[1] * 5, 7) * 9, t = s[1] << 17;
-    s[2] ^= s[0], s[3] ^= s[1], s[1] ^= s[2], s[0] ^= s[3], s[2] ^= t, s[3] = rotl(s[3], 45);
-    return r;
-  }
-  uint32_t below(uint32_t n) { return (uint32_t)((next() >> 32) * n >> 32); }
-};
-
 inline int legal_moves(const Board &B, uint16_t *mv) {
   int n = 0;
   gen_legal(B, host_tables(), [&](uint16_t m) { mv[n++] = m; });
   return n;
 }
 
-// Random playout from the start position: k ~ U{0..max_plies} plies; stop on
-// mate / stalemate / rule50 >= 100; never return a position in check.
-inline Board random_playout(uint64_t seed, int max_plies) {
-  Xoshiro rng(seed);
-  for (;;) {
-    Board B;
-    parse_fen("rnbqkbnr/pppppppp/8/8/8/8/PPPPPPPP/RNBQKBNR w KQkq - 0 1", B);
-    int k = (int)rng.below((uint32_t)max_plies + 1);
-    uint16_t mv[256];
-    for (int ply = 0; ply < k; ++ply) {
-      int n = legal_moves(B, mv);
-      if (!n || B.rule50 >= 100) break;
-      B = do_move(B, mv[rng.below((uint32_t)n)]);
-    }
-    // resample a position in check by playing on (bounded), else restart
-    for (int extra = 0; extra < 8 && in_check(B, host_tables()); ++extra) {
-      int n = legal_moves(B, mv);
-      if (!n) break;
-      B = do_move(B, mv[rng.below((uint32_t)n)]);
-    }
-    if (!in_check(B, host_tables())) return B;
-  }
-}
+inline Board random_playout(uint64_t seed, int max_plies) { return random_playout(seed, max_plies, host_tables()); }
 
 } // namespace gn

@@ -32,6 +32,9 @@ hipError_t launch_write_children(const gn_board *boards, size_t n, const Tables 
 // sum of legal-move counts over all boards into *total (added; caller zeroes)
 hipError_t launch_count_sum(const gn_board *boards, size_t n, const Tables *tables,
                             unsigned long long *total, hipStream_t s);
+// random playouts (chess.h random_playout), one thread per position
+hipError_t launch_random_positions(uint64_t seed, size_t first, size_t n, int max_plies, const Tables *tables,
+                                   gn_board *out, hipStream_t s);
 // narrowing copy of offsets for the C-ABI
 hipError_t launch_offsets_u32(const uint64_t *in, size_t n, uint32_t *out, hipStream_t s);
 // exclusive scan of n + 1 counts (counts[n] must be 0); temp grows on demand

@@ -422,6 +422,17 @@ __global__ void count_sum_kernel(const gn_board *__restrict__ boards, size_t n, 
   }
 }
 
+__global__ void random_positions_kernel(uint64_t seed, size_t first, size_t n, int max_plies,
+                                        const Tables *__restrict__ tables, gn_board *__restrict__ out) {
+  __shared__ Tables T;
+  load_tables(T, tables);
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  gn_board pb;
+  pack(random_playout(seed + first + i, max_plies, T), pb);
+  out[i] = pb;
+}
+
 __global__ void offsets_u32_kernel(const uint64_t *__restrict__ in, size_t n, uint32_t *__restrict__ out) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) out[i] = (uint32_t)in[i];
@@ -446,6 +457,14 @@ hipError_t launch_count_sum(const gn_board *boards, size_t n, const Tables *tabl
                             hipStream_t s) {
   if (!n) return hipSuccess;
   hipLaunchKernelGGL(count_sum_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, boards, n, tables, total);
+  return hipGetLastError();
+}
+
+hipError_t launch_random_positions(uint64_t seed, size_t first, size_t n, int max_plies, const Tables *tables,
+                                   gn_board *out, hipStream_t s) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(random_positions_kernel, dim3(blocks_for(n, 128)), dim3(128), 0, s, seed, first, n, max_plies,
+                     tables, out);
   return hipGetLastError();
 }
 

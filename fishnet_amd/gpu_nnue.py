@@ -33,7 +33,7 @@ EXPORTS = ["gn_load_net", "gn_load_net_memory", "gn_free", "gn_last_error", "gn_
            "gn_evaluate_batch_mode", "gn_expand_and_evaluate", "gn_perft", "gn_pack_fens",
            "gn_board_to_fen", "gn_random_positions", "gn_evaluate_device", "gn_expand_device",
            "gn_device_alloc", "gn_device_free", "gn_memcpy_h2d", "gn_memcpy_d2h", "gn_synchronize",
-           "gn_time_evaluate_device"]
+           "gn_time_evaluate_device", "gn_random_positions_device"]
 
 
 class GnError(RuntimeError):
@@ -85,6 +85,7 @@ def lib():
         "gn_memcpy_d2h": [vp, i32, vp, vp, sz],
         "gn_synchronize": [vp, i32],
         "gn_time_evaluate_device": [vp, i32, vp, sz, i32, vp, i32, C.POINTER(C.c_float), vp],
+        "gn_random_positions_device": [vp, i32, C.c_uint64, sz, sz, i32, vp, vp],
     }
     for name, args in sig.items():
         f = getattr(L, name)
@@ -246,6 +247,9 @@ class GpuNnue:
 
     def evaluate_device(self, d_boards: DeviceBuffer, n, mode, d_out: DeviceBuffer, stream=None, slot=0):
         _check(lib().gn_evaluate_device(self.h, slot, d_boards.ptr, n, mode, d_out.ptr, stream))
+
+    def random_positions_device(self, seed, first, n, max_plies, d_out: DeviceBuffer, stream=None, slot=0):
+        _check(lib().gn_random_positions_device(self.h, slot, seed, first, n, max_plies, d_out.ptr, stream))
 
     def synchronize(self, slot=0):
         _check(lib().gn_synchronize(self.h, slot))

@@ -158,6 +158,11 @@ GN_API int gn_board_to_fen(const gn_board *board, char *buf, size_t buflen);
  * (stopping at mate/stalemate), resampling positions in check. Host only. */
 GN_API int gn_random_positions(uint64_t seed, size_t first_index, size_t n, int max_plies, gn_board *out);
 
+/* Same generator on the GPU (identical boards for identical seeds): writes n
+ * boards to device memory d_out; asynchronous on `stream` (NULL = context stream). */
+GN_API int gn_random_positions_device(gn_ctx *ctx, int device_slot, uint64_t seed, size_t first_index, size_t n,
+                                      int max_plies, gn_board *d_out, void *stream);
+
 /* Evaluate boards already resident on device `device_slot` (index into the
  * devices given at load).  d_boards / d_out are device pointers; stream is a
  * hipStream_t (NULL = the context's own stream).  Asynchronous: returns once
@@ -178,8 +183,9 @@ GN_API int gn_memcpy_d2h(gn_ctx *ctx, int device_slot, void *dst, const void *sr
 GN_API int gn_synchronize(gn_ctx *ctx, int device_slot);
 /* Time `iters` back-to-back gn_evaluate_device calls with HIP events recorded
  * on the launch stream; *ms_total = elapsed time.  per_kernel_ms (optional,
- * length 4) receives the average time of the [classify, small, big, finalize]
- * kernels measured with events around each launch in a separate pass. */
+ * length 4) receives the average per-call time of the [classify(+reeval),
+ * small net, big net, finalize] stages, from events recorded between the
+ * launches of that same timed pass (one host sync at the end). */
 GN_API int gn_time_evaluate_device(gn_ctx *ctx, int device_slot, const gn_board *d_boards, size_t n, int mode,
                             gn_eval *d_out, int iters, float *ms_total, float *per_kernel_ms);
 
