@@ -44,6 +44,8 @@ WORKLOADS = {
                     "1M random-playout positions per MI355X"),
     "full16m": dict(mode=0, n=1 << 24, l1=3072, config="Eval::evaluate pipeline (small net, big-net re-eval "
                     "when |nnue| < 236) on 16M random-playout positions per MI355X"),
+    "children": dict(mode=1, n=8192, l1=3072, config="configs[3] shape: 8192 random 80-ply games per MI355X "
+                     "(81 parents each) x every legal child; GPU movegen + incremental big-net accumulators"),
 }
 STAGES = ["classify", "small_net", "big_net", "finalize"]
 
@@ -86,6 +88,77 @@ def cpu_baseline(G, boards_sample, mode, budget_s):
             "sample": f"{len(fens)} positions (first {len(fens)} of rank 0's batch, same nets, same mode) x {reps} "
                       f"passes = {done} evals in {dt:.1f} s; oracle/oracle.c scalar C -O3 -march=x86-64-v3 "
                       f"(AVX2 build class), {threads} POSIX threads on {cpu_model()}"}
+
+
+def run_children(args, ctx, wl, world, rank, dist, torch, net_label, big_p, small_p):
+    """configs[3] shape: games x 81 parents, every legal child, incremental."""
+    from fishnet_amd import gpu_nnue as G
+    games, plies, mode = (args.positions or wl["n"]), 80, wl["mode"]
+    n = games * (plies + 1)
+    d_par = ctx.alloc(n * 32)
+    t = time.perf_counter()
+    ctx.random_games_device(SEED, rank * games, games, plies, d_par)
+    ctx.synchronize()
+    gen_s = time.perf_counter() - t
+    if args.warmup:
+        ctx.time_expand_device(d_par, n, mode, args.warmup)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ms, children, stages, rows = ctx.time_expand_device(d_par, n, mode, args.steps)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    if world > 1:
+        w = torch.tensor([wall], dtype=torch.float64, device="cuda")
+        dist.all_reduce(w, op=dist.ReduceOp.MAX)
+        wall = float(w.item())
+    evals = n + children
+    value = world * evals * args.steps / wall
+    l1 = 3072 if mode != 2 else 128
+    stage = 5 if mode != 2 else 4
+    alg = rows * (2 * l1 + 4) + n * 32 + children * (24 + 8)
+    kern_ms = stages[stage]
+    achieved = alg / (kern_ms * 1e-3) / 1e9
+    line = {
+        "metric": METRIC, "value": round(value, 1), "unit": "evals/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(wall * 1e3 / args.steps, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "int16/int8",
+        "data": f"synthetic: seeded random 80-ply games generated on the GPU; nets {net_label}",
+        "config": {"workload": wl["config"], "games_per_gpu": games, "parents_per_gpu": n,
+                   "children_per_gpu": children, "evals_per_step_per_gpu": evals,
+                   "mode": ["full", "big", "small"][mode], "incremental": True,
+                   "parallelism": f"dp{world} (games sharded, no collective)"},
+        "roofline": {"bound": "hbm", "kernel": f"expand_eval<{l1}>", "achieved": round(achieved, 1),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": None, "alg_bytes_per_launch": alg, "ft_rows_per_launch": rows,
+                     "kernel_ms_per_launch": round(kern_ms, 4),
+                     "stage_ms": {k: round(v, 4) for k, v in zip(G.EXPAND_STAGES, stages)}},
+        "gen_games_s": round(gen_s, 3),
+    }
+    if rank == 0 and args.check:
+        from oracle import oracle as O
+        boards = d_par.download(G.BOARD_DTYPE, n)
+        idx = np.linspace(0, n - 1, 24).astype(int)
+        fens = [G.board_to_fen(boards[i]) for i in idx]
+        parents, offs, moves, kids = ctx.expand_and_evaluate(fens, mode)
+        big = O.Net(big_p) if mode != 2 else None
+        small = O.Net(small_p) if mode != 1 else None
+        bad = 0
+        for i, fen in enumerate(fens):
+            _, m_exp, k_exp = O.expand_eval(big, small, fen, mode)
+            got = dict(zip(moves[offs[i]:offs[i + 1]].tolist(), map(tuple, kids[offs[i]:offs[i + 1]].tolist())))
+            bad += got != dict(zip(m_exp, map(tuple, k_exp.tolist())))
+        line["oracle_check"] = {"parents": len(fens), "children": int(offs[-1]), "mismatching_parents": bad}
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    d_par.free()
+    ctx.close()
 
 
 def main():
@@ -166,6 +239,10 @@ def main():
         d_boards.free()
         d_out.free()
         return res
+
+    if args.workload == "children":
+        run_children(args, ctx, wl, world, rank, dist, torch, net_label, big_p, small_p)
+        return
 
     r = run_workload(mode, n, args.steps, args.warmup, True)
     total = world * n * args.steps

@@ -192,6 +192,9 @@ struct Dev {
   DevBuf<uint64_t> counts, offsets;
   DevBuf<uint32_t> off32;
   DevBuf<uint16_t> moves;
+  DevBuf<ChildDelta> deltas;
+  DevBuf<int2> p_osm, p_obg;     // parent-side net outputs during expansion
+  DevBuf<uint8_t> p_nsm, p_nbg;  // parent-side net selection during expansion
   DevBuf<unsigned long long> sum;
   void *scan_tmp = nullptr;
   size_t scan_bytes = 0;
@@ -201,6 +204,7 @@ struct Dev {
 struct gn_ctx {
   std::vector<std::unique_ptr<Dev>> devs;
   gn_eval_params P;
+  bool incremental = true; // GN_OPT_INCREMENTAL_CHILDREN
   int l1[2] = {0, 0};
   uint32_t hash[2] = {0, 0};
 };
@@ -266,7 +270,8 @@ static void destroy(gn_ctx *ctx) {
     d.osm.release(), d.obg.release(), d.nsm.release(), d.nbg.release();
     d.io_boards.release(), d.frontier[0].release(), d.frontier[1].release();
     d.io_out.release(), d.io_out2.release(), d.counts.release(), d.offsets.release();
-    d.off32.release(), d.moves.release(), d.sum.release();
+    d.off32.release(), d.moves.release(), d.sum.release(), d.deltas.release();
+    d.p_osm.release(), d.p_obg.release(), d.p_nsm.release(), d.p_nbg.release();
     if (d.scan_tmp) (void)hipFree(d.scan_tmp);
     if (d.stream) (void)hipStreamDestroy(d.stream);
   }
@@ -387,23 +392,100 @@ static void parallel_for(size_t n, size_t grain, F &&f) {
   for (auto &t : th) t.join();
 }
 
-// expansion on one device with library-owned buffers; fills children boards
-// into d.frontier[1] and moves into d.moves; returns total via *total
-static int expand_children(Dev &d, const gn_board *parents, size_t n, size_t *total, hipStream_t s,
-                           bool want_moves) {
+// Child generation: counts -> exclusive scan (d.offsets, n + 1) -> children
+// boards (+ moves, + ChildDelta when deltas is non-null).  *total = children.
+// ev (optional) gets 3 events: after count+scan, after the host read of the
+// total, after write_children.
+static int generate_children(Dev &d, const gn_board *parents, size_t n, gn_board *children_or_null, size_t cap,
+                             uint16_t *moves, bool want_deltas, size_t *total, hipStream_t s, hipEvent_t *ev,
+                             unsigned long long *rows = nullptr) {
   HIP_TRY(d.counts.ensure(n + 1));
   HIP_TRY(d.offsets.ensure(n + 1));
   HIP_TRY(hipMemsetAsync(d.counts.p + n, 0, sizeof(uint64_t), s));
   HIP_TRY(launch_count_children(parents, n, d.tables, d.counts.p, s));
   HIP_TRY(exclusive_scan_u64(d.counts.p, d.offsets.p, n + 1, d.scan_tmp, d.scan_bytes, s));
+  if (ev) HIP_TRY(hipEventRecord(ev[0], s));
   uint64_t t = 0;
   HIP_TRY(hipMemcpyAsync(&t, d.offsets.p + n, sizeof(t), hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
   *total = (size_t)t;
-  if (!t) return GN_OK;
-  HIP_TRY(d.frontier[1].ensure(t));
-  if (want_moves) HIP_TRY(d.moves.ensure(t));
-  HIP_TRY(launch_write_children(parents, n, d.tables, d.offsets.p, d.frontier[1].p, want_moves ? d.moves.p : nullptr, s));
+  if (ev) HIP_TRY(hipEventRecord(ev[1], s));
+  gn_board *children = children_or_null;
+  if (!children) {
+    HIP_TRY(d.frontier[1].ensure(std::max<size_t>(t, 1)));
+    children = d.frontier[1].p;
+  } else if (t > cap) {
+    return fail(GN_E_CAPACITY, "%zu children exceed capacity %zu", (size_t)t, cap);
+  }
+  if (want_deltas) HIP_TRY(d.deltas.ensure(std::max<size_t>(t, 1)));
+  if (t) HIP_TRY(launch_write_children(parents, n, d.tables, d.offsets.p, children, moves,
+                                        want_deltas ? d.deltas.p : nullptr, rows, s));
+  if (ev) HIP_TRY(hipEventRecord(ev[2], s));
+  return GN_OK;
+}
+
+// Evaluate parents + children after generate_children.  Incremental: the
+// expand_eval kernels (one workgroup per parent, children from the parent
+// accumulators); otherwise every child is a full refresh (evaluate_on).
+// ev (optional) gets 4 events: after classify, after the small net (+reeval),
+// after the big net, after finalize.
+static int expand_evaluate(gn_ctx *ctx, Dev &d, const gn_board *parents, size_t n, const gn_board *children,
+                           size_t total, int mode, gn_eval *parent_out, gn_eval *child_out, hipStream_t s,
+                           hipEvent_t *ev) {
+  if (mode < GN_MODE_FULL || mode > GN_MODE_SMALL) return fail(GN_E_INVALID, "bad mode %d", mode);
+  if ((mode != GN_MODE_SMALL && !d.has[BIG]) || (mode != GN_MODE_BIG && !d.has[SMALL]))
+    return fail(GN_E_NONET, "mode %d needs a network that is not loaded", mode);
+  if (!ctx->incremental) {
+    if (total) {
+      int rc = evaluate_on(ctx, d, children, total, mode, child_out, s, nullptr);
+      if (rc) return rc;
+    }
+    return parent_out ? evaluate_on(ctx, d, parents, n, mode, parent_out, s, nullptr) : GN_OK;
+  }
+  const size_t nt = std::max<size_t>(total, 1);
+  if (mode != GN_MODE_BIG) {
+    HIP_TRY(d.osm.ensure(nt));
+    HIP_TRY(d.p_osm.ensure(n));
+  }
+  if (mode != GN_MODE_SMALL) {
+    HIP_TRY(d.obg.ensure(nt));
+    HIP_TRY(d.p_obg.ensure(n));
+  }
+  if (mode == GN_MODE_FULL) {
+    HIP_TRY(d.nsm.ensure(nt));
+    HIP_TRY(d.nbg.ensure(nt));
+    HIP_TRY(d.p_nsm.ensure(n));
+    HIP_TRY(d.p_nbg.ensure(n));
+  }
+  auto mark = [&](int k) -> hipError_t { return ev ? hipEventRecord(ev[k], s) : hipSuccess; };
+  const gn_eval_params &P = ctx->P;
+  const uint64_t *off = d.offsets.p;
+  const ChildDelta *dl = d.deltas.p;
+  if (mode == GN_MODE_FULL) {
+    HIP_TRY(launch_classify(parents, n, P, d.p_nsm.p, d.p_nbg.p, s));
+    HIP_TRY(launch_classify(children, total, P, d.nsm.p, d.nbg.p, s));
+  }
+  HIP_TRY(mark(0));
+  if (mode != GN_MODE_BIG) {
+    const bool f = mode == GN_MODE_FULL;
+    HIP_TRY(launch_expand_net(d.net[SMALL], parents, n, off, children, dl, f ? d.p_nsm.p : nullptr,
+                              f ? d.nsm.p : nullptr, d.p_osm.p, d.osm.p, s));
+    if (f) {
+      HIP_TRY(launch_reeval(d.p_osm.p, d.p_nsm.p, n, P, d.p_nbg.p, s));
+      HIP_TRY(launch_reeval(d.osm.p, d.nsm.p, total, P, d.nbg.p, s));
+    }
+  }
+  HIP_TRY(mark(1));
+  if (mode != GN_MODE_SMALL) {
+    const bool f = mode == GN_MODE_FULL;
+    HIP_TRY(launch_expand_net(d.net[BIG], parents, n, off, children, dl, f ? d.p_nbg.p : nullptr,
+                              f ? d.nbg.p : nullptr, d.p_obg.p, d.obg.p, s));
+  }
+  HIP_TRY(mark(2));
+  HIP_TRY(launch_finalize(children, total, mode, d.osm.p, d.obg.p, d.nsm.p, d.nbg.p, P, d.tables, child_out, s));
+  if (parent_out)
+    HIP_TRY(launch_finalize(parents, n, mode, d.p_osm.p, d.p_obg.p, d.p_nsm.p, d.p_nbg.p, P, d.tables, parent_out, s));
+  HIP_TRY(mark(3));
   return GN_OK;
 }
 
@@ -673,33 +755,114 @@ int gn_expand_device(gn_ctx *ctx, int device_slot, const gn_board *d_parents, si
   hipStream_t s = stream ? (hipStream_t)stream : d->stream;
   *total = 0;
   if (!n) return GN_OK;
-  HIP_TRY(d->counts.ensure(n + 1));
-  HIP_TRY(d->offsets.ensure(n + 1));
-  HIP_TRY(hipMemsetAsync(d->counts.p + n, 0, sizeof(uint64_t), s));
-  HIP_TRY(launch_count_children(d_parents, n, d->tables, d->counts.p, s));
-  HIP_TRY(exclusive_scan_u64(d->counts.p, d->offsets.p, n + 1, d->scan_tmp, d->scan_bytes, s));
-  uint64_t t = 0;
-  HIP_TRY(hipMemcpyAsync(&t, d->offsets.p + n, sizeof(t), hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipStreamSynchronize(s));
-  *total = (size_t)t;
-  if (t > 0xFFFFFFFFull) return fail(GN_E_CAPACITY, "%llu children exceed 32-bit offsets", (unsigned long long)t);
+  if (!d_children || !d_moves || !d_child_out) return fail(GN_E_INVALID, "NULL child buffer");
+  size_t t = 0;
+  int rc = generate_children(*d, d_parents, n, d_children, cap, d_moves, ctx->incremental, &t, s, nullptr);
+  *total = t;
+  if (t > 0xFFFFFFFFull) return fail(GN_E_CAPACITY, "%zu children exceed 32-bit offsets", t);
   HIP_TRY(launch_offsets_u32(d->offsets.p, n + 1, d_offsets, s));
-  if (t > cap) {
+  if (rc) {
     HIP_TRY(hipStreamSynchronize(s));
-    return fail(GN_E_CAPACITY, "%llu children exceed capacity %zu", (unsigned long long)t, cap);
+    return rc;
   }
-  if (t && (!d_children || !d_moves || !d_child_out)) return fail(GN_E_INVALID, "NULL child buffer");
-  HIP_TRY(launch_write_children(d_parents, n, d->tables, d->offsets.p, d_children, d_moves, s));
-  if (t) {
-    int rc = evaluate_on(ctx, *d, d_children, t, mode, d_child_out, s, nullptr);
-    if (rc) return rc;
-  }
-  if (d_parent_out) {
-    int rc = evaluate_on(ctx, *d, d_parents, n, mode, d_parent_out, s, nullptr);
-    if (rc) return rc;
-  }
+  rc = expand_evaluate(ctx, *d, d_parents, n, d_children, t, mode, d_parent_out, d_child_out, s, nullptr);
+  if (rc) return rc;
   HIP_TRY(hipStreamSynchronize(s));
   return GN_OK;
+}
+
+int gn_time_expand_device(gn_ctx *ctx, int device_slot, const gn_board *d_parents, size_t n, int mode, int iters,
+                          float *ms_total, size_t *total, float *stage_ms, uint64_t *ft_rows) {
+  Dev *d = slot(ctx, device_slot);
+  if (!d || !ms_total || !total || iters <= 0) return fail(GN_E_INVALID, "bad argument");
+  std::lock_guard<std::mutex> lk(d->mu);
+  HIP_TRY(hipSetDevice(d->id));
+  hipStream_t s = d->stream;
+  const int NE = 8; // start, [count+scan], [total read], [write], [classify], [small], [big], [finalize]
+  std::vector<hipEvent_t> ev((size_t)iters * NE + 2, nullptr);
+  auto cleanup = [&] {
+    for (auto &e : ev)
+      if (e) (void)hipEventDestroy(e);
+  };
+  for (auto &e : ev)
+    if (hipEventCreate(&e) != hipSuccess) {
+      cleanup();
+      return fail(GN_E_HIP, "hipEventCreate failed");
+    }
+  int rc = GN_OK;
+  size_t t = 0;
+  HIP_TRY(d->sum.ensure(1));
+  HIP_TRY(hipMemsetAsync(d->sum.p, 0, sizeof(unsigned long long), s));
+  hipError_t he = hipEventRecord(ev[0], s);
+  for (int it = 0; it < iters && rc == GN_OK && he == hipSuccess; ++it) {
+    hipEvent_t *e = &ev[2 + (size_t)NE * it];
+    he = hipEventRecord(e[0], s);
+    if (he != hipSuccess) break;
+    rc = generate_children(*d, d_parents, n, nullptr, 0, nullptr, ctx->incremental, &t, s, e + 1,
+                           it == 0 ? d->sum.p : nullptr);
+    if (rc) break;
+    HIP_TRY(d->io_out.ensure(n));
+    HIP_TRY(d->io_out2.ensure(std::max<size_t>(t, 1)));
+    rc = expand_evaluate(ctx, *d, d_parents, n, d->frontier[1].p, t, mode, d->io_out.p, d->io_out2.p, s, e + 4);
+  }
+  if (rc == GN_OK && he == hipSuccess) he = hipEventRecord(ev[1], s);
+  if (rc == GN_OK && he == hipSuccess) he = hipEventSynchronize(ev[1]);
+  if (rc == GN_OK && he == hipSuccess) he = hipEventElapsedTime(ms_total, ev[0], ev[1]);
+  if (rc == GN_OK && he == hipSuccess && stage_ms) {
+    float acc[7] = {0, 0, 0, 0, 0, 0, 0};
+    for (int it = 0; it < iters && he == hipSuccess; ++it)
+      for (int k = 0; k < 7 && he == hipSuccess; ++k) {
+        float ms = 0;
+        he = hipEventElapsedTime(&ms, ev[2 + (size_t)NE * it + k], ev[2 + (size_t)NE * it + k + 1]);
+        acc[k] += ms;
+      }
+    for (int k = 0; k < 7; ++k) stage_ms[k] = acc[k] / (float)iters;
+  }
+  cleanup();
+  *total = t;
+  if (rc) return rc;
+  if (ft_rows && he == hipSuccess) {
+    unsigned long long r = 0;
+    he = hipMemcpy(&r, d->sum.p, sizeof(r), hipMemcpyDeviceToHost);
+    *ft_rows = ctx->incremental ? r : 0;
+  }
+  if (he != hipSuccess) return fail(GN_E_HIP, "timing failed: %s", hipGetErrorString(he));
+  return GN_OK;
+}
+
+int gn_random_games_device(gn_ctx *ctx, int device_slot, uint64_t seed, size_t first_game, size_t n_games, int plies,
+                           gn_board *d_out, void *stream) {
+  Dev *d = slot(ctx, device_slot);
+  if (!d) return fail(GN_E_INVALID, "bad context or device slot");
+  if (n_games && !d_out) return fail(GN_E_INVALID, "NULL buffer");
+  if (plies < 0 || plies > 1000) return fail(GN_E_INVALID, "plies out of range");
+  std::lock_guard<std::mutex> lk(d->mu);
+  HIP_TRY(hipSetDevice(d->id));
+  HIP_TRY(launch_random_games(seed, first_game, n_games, plies, d->tables, d_out,
+                              stream ? (hipStream_t)stream : d->stream));
+  return GN_OK;
+}
+
+int gn_set_option(gn_ctx *ctx, int option, int64_t value) {
+  if (!ctx) return fail(GN_E_INVALID, "ctx is NULL");
+  switch (option) {
+  case GN_OPT_INCREMENTAL_CHILDREN:
+    ctx->incremental = value != 0;
+    return GN_OK;
+  default:
+    return fail(GN_E_INVALID, "unknown option %d", option);
+  }
+}
+
+int gn_get_option(const gn_ctx *ctx, int option, int64_t *value) {
+  if (!ctx || !value) return fail(GN_E_INVALID, "NULL argument");
+  switch (option) {
+  case GN_OPT_INCREMENTAL_CHILDREN:
+    *value = ctx->incremental;
+    return GN_OK;
+  default:
+    return fail(GN_E_INVALID, "unknown option %d", option);
+  }
 }
 
 int gn_expand_and_evaluate(gn_ctx *ctx, const char *const *parent_fens, size_t n, int mode, gn_eval *parent_out,
@@ -720,29 +883,33 @@ int gn_expand_and_evaluate(gn_ctx *ctx, const char *const *parent_fens, size_t n
     hipStream_t s = d->stream;
     HIP_TRY(d->io_boards.ensure(n));
     HIP_TRY(hipMemcpyAsync(d->io_boards.p, boards.data(), n * sizeof(gn_board), hipMemcpyHostToDevice, s));
-    size_t total = 0;
-    rc = expand_children(*d, d->io_boards.p, n, &total, s, true);
-    if (rc) return rc;
+    // size the move buffer from the counts first (generate_children syncs for the total)
+    HIP_TRY(d->counts.ensure(n + 1));
+    HIP_TRY(d->offsets.ensure(n + 1));
+    HIP_TRY(hipMemsetAsync(d->counts.p + n, 0, sizeof(uint64_t), s));
+    HIP_TRY(launch_count_children(d->io_boards.p, n, d->tables, d->counts.p, s));
+    HIP_TRY(exclusive_scan_u64(d->counts.p, d->offsets.p, n + 1, d->scan_tmp, d->scan_bytes, s));
     std::vector<uint64_t> off(n + 1);
     HIP_TRY(hipMemcpyAsync(off.data(), d->offsets.p, (n + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
+    const size_t total = (size_t)off[n];
     if (total > 0xFFFFFFFFull) return fail(GN_E_CAPACITY, "children exceed 32-bit offsets");
     for (size_t i = 0; i <= n; ++i) child_offsets[i] = (uint32_t)off[i];
     if (total > cap) return fail(GN_E_CAPACITY, "%zu children exceed capacity %zu", total, cap);
     if (total && (!child_moves || !child_out)) return fail(GN_E_INVALID, "NULL child buffer");
-    if (total) {
-      HIP_TRY(d->io_out2.ensure(total));
-      rc = evaluate_on(ctx, *d, d->frontier[1].p, total, mode, d->io_out2.p, s, nullptr);
-      if (rc) return rc;
-      HIP_TRY(hipMemcpyAsync(child_out, d->io_out2.p, total * sizeof(gn_eval), hipMemcpyDeviceToHost, s));
-      HIP_TRY(hipMemcpyAsync(child_moves, d->moves.p, total * sizeof(uint16_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(d->moves.ensure(std::max<size_t>(total, 1)));
+    size_t t = 0;
+    rc = generate_children(*d, d->io_boards.p, n, nullptr, 0, d->moves.p, ctx->incremental, &t, s, nullptr);
+    if (rc) return rc;
+    HIP_TRY(d->io_out.ensure(n));
+    HIP_TRY(d->io_out2.ensure(std::max<size_t>(t, 1)));
+    rc = expand_evaluate(ctx, *d, d->io_boards.p, n, d->frontier[1].p, t, mode, d->io_out.p, d->io_out2.p, s, nullptr);
+    if (rc) return rc;
+    if (t) {
+      HIP_TRY(hipMemcpyAsync(child_out, d->io_out2.p, t * sizeof(gn_eval), hipMemcpyDeviceToHost, s));
+      HIP_TRY(hipMemcpyAsync(child_moves, d->moves.p, t * sizeof(uint16_t), hipMemcpyDeviceToHost, s));
     }
-    if (parent_out) {
-      HIP_TRY(d->io_out.ensure(n));
-      rc = evaluate_on(ctx, *d, d->io_boards.p, n, mode, d->io_out.p, s, nullptr);
-      if (rc) return rc;
-      HIP_TRY(hipMemcpyAsync(parent_out, d->io_out.p, n * sizeof(gn_eval), hipMemcpyDeviceToHost, s));
-    }
+    if (parent_out) HIP_TRY(hipMemcpyAsync(parent_out, d->io_out.p, n * sizeof(gn_eval), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     return GN_OK;
   } catch (const std::bad_alloc &) {
@@ -771,7 +938,7 @@ int gn_perft(gn_ctx *ctx, const char *fen, int depth, uint64_t *nodes) {
   size_t n = 1;
   for (int level = 1; level < depth; ++level) {
     size_t total = 0;
-    int rc = expand_children(*d, d->frontier[0].p, n, &total, s, false);
+    int rc = generate_children(*d, d->frontier[0].p, n, nullptr, 0, nullptr, false, &total, s, nullptr);
     if (rc) return rc;
     std::swap(d->frontier[0], d->frontier[1]);
     n = total;

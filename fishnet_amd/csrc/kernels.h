@@ -12,6 +12,12 @@ namespace gn {
 // need[i] != 0 (need == nullptr: all); other entries of out are untouched.
 hipError_t launch_eval_net(const NetDevice &net, const gn_board *boards, const uint8_t *need, size_t n,
                            int2 *out, hipStream_t s);
+// Incremental evaluation of parents + all their children (children of parent
+// p are [offsets[p], offsets[p+1]) with moves[]); need_* select what this net
+// evaluates (nullptr: all).
+hipError_t launch_expand_net(const NetDevice &net, const gn_board *parents, size_t n, const uint64_t *offsets,
+                             const gn_board *children, const ChildDelta *deltas, const uint8_t *need_parent,
+                             const uint8_t *need_child, int2 *out_parent, int2 *out_child, hipStream_t s);
 // GN_MODE_FULL preparation: need_small = valid && |simple_eval| > threshold,
 // need_big = valid && !need_small.
 hipError_t launch_classify(const gn_board *boards, size_t n, const gn_eval_params &P, uint8_t *need_small,
@@ -28,13 +34,17 @@ hipError_t launch_count_children(const gn_board *boards, size_t n, const Tables 
                                  hipStream_t s);
 // children of every board at offsets[i] (exclusive prefix sums of counts)
 hipError_t launch_write_children(const gn_board *boards, size_t n, const Tables *tables,
-                                 const uint64_t *offsets, gn_board *children, uint16_t *moves, hipStream_t s);
+                                 const uint64_t *offsets, gn_board *children, uint16_t *moves, ChildDelta *deltas,
+                                 unsigned long long *rows, hipStream_t s);
 // sum of legal-move counts over all boards into *total (added; caller zeroes)
 hipError_t launch_count_sum(const gn_board *boards, size_t n, const Tables *tables,
                             unsigned long long *total, hipStream_t s);
 // random playouts (chess.h random_playout), one thread per position
 hipError_t launch_random_positions(uint64_t seed, size_t first, size_t n, int max_plies, const Tables *tables,
                                    gn_board *out, hipStream_t s);
+// random games: out[g * (plies + 1) + k] = position after k plies of game g
+hipError_t launch_random_games(uint64_t seed, size_t first_game, size_t n_games, int plies, const Tables *tables,
+                               gn_board *out, hipStream_t s);
 // narrowing copy of offsets for the C-ABI
 hipError_t launch_offsets_u32(const uint64_t *in, size_t n, uint32_t *out, hipStream_t s);
 // exclusive scan of n + 1 counts (counts[n] must be 0); temp grows on demand

@@ -26,6 +26,98 @@ __device__ __forceinline__ void load_tables(Tables &dst, const Tables *src) {
   __syncthreads();
 }
 
+// ------------------------------------------------------------ layer stack --
+// NetworkArchitecture::propagate for a 16-position tile held in LDS as
+// transformed features xt[16][L1 + 16] (u8), one wave per distinct bucket:
+//   fc_0  [16 x L1] . [L1 x 16]  -> int8 MFMA 16x16x64, K = L1 / 64 steps
+//   SqrClippedReLU / ClippedReLU -> in1[16][32] (LDS, per wave)
+//   fc_1  [16 x 32] . [32 x 32]  -> two int8 MFMAs (K padded to 64 with zeros)
+//   fc_2  32 -> 1 by a 16-lane shuffle reduction, + skip term from fc_0[15]
+// Lane layout of v_mfma_i32_16x16x64_i8: lane l holds A[row l&15][16(l>>4)..+16],
+// B[16(l>>4)..+16][col l&15]; C[4(l>>4)+i][l&15] in acc[i].  The K grouping
+// inside a lane is irrelevant to the result as long as A and B use the same.
+// valid(pos, b): slot pos holds a position of bucket b; emit(pos, {psqt/16, positional/16}).
+template <int L1, int NW, class Valid, class Emit>
+__device__ __forceinline__ void layer_stack_tile(const NetDevice &net, const uint8_t *xt, uint8_t (*in1)[16][32],
+                                                 int32_t (*fwd)[16], const int32_t (*psq)[2], const int *bkt,
+                                                 uint32_t bm, Valid &&valid, Emit &&emit) {
+  constexpr int XS = L1 + 16;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nb = popcnt(bm);
+  const int row = lane & 15, kg = lane >> 4;
+  for (int round = 0; round * NW < nb; ++round) {
+    const int slot = round * NW + wave;
+    int b = -1;
+    if (slot < nb) {
+      uint32_t m = bm;
+      for (int t = 0; t < slot; ++t) m &= m - 1;
+      b = __builtin_ctz(m);
+    }
+    if (b >= 0) {
+      int4v acc = {0, 0, 0, 0};
+      const uint8_t *xa = xt + row * XS + kg * 16;
+      const int8_t *wb = net.w0 + ((size_t)b * 16 + row) * L1 + kg * 16;
+#pragma unroll 4
+      for (int ks = 0; ks < L1; ks += 64) {
+        const int4v a = *reinterpret_cast<const int4v *>(xa + ks);
+        const int4v w = *reinterpret_cast<const int4v *>(wb + ks);
+        acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, w, acc, 0, 0, 0);
+      }
+      const int32_t bias0 = net.b0[b * 16 + row];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int pos = 4 * kg + i;
+        const int32_t v = wadd(acc[i], bias0);
+        if (row < 15) {
+          const long long s2 = ((long long)v * v) >> 19;
+          in1[wave][pos][row] = (uint8_t)(s2 < 127 ? s2 : 127);
+          in1[wave][pos][15 + row] = (uint8_t)clampi(v >> 6, 0, 127);
+        } else {
+          fwd[wave][pos] = wmul(v, 600 * 16) / (127 * 64);
+          in1[wave][pos][30] = 0;
+          in1[wave][pos][31] = 0;
+        }
+      }
+    }
+    __syncthreads();
+    if (b >= 0) {
+      const int4v zero = {0, 0, 0, 0};
+      int4v a = zero, wl = zero, wh = zero;
+      if (kg < 2) {
+        a = *reinterpret_cast<const int4v *>(&in1[wave][row][kg * 16]);
+        wl = *reinterpret_cast<const int4v *>(net.w1 + ((size_t)b * 32 + row) * 32 + kg * 16);
+        wh = *reinterpret_cast<const int4v *>(net.w1 + ((size_t)b * 32 + 16 + row) * 32 + kg * 16);
+      }
+      const int4v cl = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, wl, zero, 0, 0, 0);
+      const int4v ch = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, wh, zero, 0, 0, 0);
+      const int32_t b1l = net.b1[b * 32 + row], b1h = net.b1[b * 32 + 16 + row];
+      const int32_t w2l = net.w2[b * 32 + row], w2h = net.w2[b * 32 + 16 + row];
+      int32_t part[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int32_t l = clampi(wadd(cl[i], b1l) >> 6, 0, 127), hh = clampi(wadd(ch[i], b1h) >> 6, 0, 127);
+        part[i] = w2l * l + w2h * hh;
+      }
+#pragma unroll
+      for (int off = 8; off; off >>= 1)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) part[i] = wadd(part[i], __shfl_xor(part[i], off, 16));
+      if (row == 0) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int pos = 4 * kg + i;
+          if (valid(pos, b)) {
+            const int32_t positional = wadd(wadd(net.b2[b], part[i]), fwd[wave][pos]);
+            const int32_t psqt = (int32_t)((uint32_t)psq[pos][0] - (uint32_t)psq[pos][1]) / 2;
+            emit(pos, make_int2(psqt / 16, positional / 16));
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
 // --------------------------------------------------------------- eval_net --
 // Workgroup = 2 * G * PAR threads, G = L1 / 16 threads per (position,
 // perspective): thread j of a perspective group owns accumulator columns
@@ -65,36 +157,14 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR)
   if (tid == 0) bmask = 0;
   __syncthreads();
 
-  // ---- phase 0: unpack boards, validate, feature row offsets (both perspectives)
+  // ---- phase 0: feature rows of both perspectives (slot 0 = side to move)
   if (tid < TILE) {
     const size_t i = base + tid;
     int cnt = 0;
     if (i < n && (!need || need[i])) {
       const gn_board p = boards[i];
-      uint64_t wlo, whi;
-      piece_words(p, wlo, whi);
-      const int c = popcnt(p.occ);
-      int wk = -1, bk = -1;
-      bool ok = c >= 2 && c <= 32;
-      uint64_t o = p.occ;
-      for (int k = 0; ok && k < c; ++k) {
-        const int s = pop_lsb(o), pc = piece_nibble(wlo, whi, k), pt = pc & 7;
-        ok &= pt >= PAWN && pt <= KING;
-        if (pc == make_piece(WHITE, KING)) ok &= wk < 0, wk = s;
-        if (pc == make_piece(BLACK, KING)) ok &= bk < 0, bk = s;
-      }
-      ok &= wk >= 0 && bk >= 0;
-      if (ok) {
-        const int stm = p.stm_ep >> 7;
-        const int k0 = stm ? bk : wk, k1 = stm ? wk : bk;
-        o = p.occ;
-        for (int k = 0; k < c; ++k) {
-          const int s = pop_lsb(o), pc = piece_nibble(wlo, whi, k);
-          rows[tid][0][k] = (uint16_t)feature_index(stm, s, pc, k0);
-          rows[tid][1][k] = (uint16_t)feature_index(stm ^ 1, s, pc, k1);
-        }
-        cnt = c;
-      }
+      const int stm = p.stm_ep >> 7;
+      cnt = packed_features(p, rows[tid][stm], rows[tid][stm ^ 1]);
     }
     nfeat[tid] = cnt;
     bkt[tid] = cnt ? (cnt - 1) / 4 : 0;
@@ -160,86 +230,233 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR)
   }
   __syncthreads();
 
-  // ---- phase 2: layer stack, one wave per distinct bucket in the tile
-  const int lane = tid & 63, wave = tid >> 6;
-  const uint32_t bm = bmask;
-  const int nb = popcnt(bm);
-  const int row = lane & 15, kg = lane >> 4;
-  for (int round = 0; round * NW < nb; ++round) {
-    const int slot = round * NW + wave;
-    int b = -1;
-    if (slot < nb) {
-      uint32_t m = bm;
-      for (int t = 0; t < slot; ++t) m &= m - 1;
-      b = __builtin_ctz(m);
-    }
-    if (b >= 0) {
-      // fc_0: [16 pos x L1] u8 . [L1 x 16] i8 -> i32, K in steps of 64
-      int4v acc = {0, 0, 0, 0};
-      const uint8_t *xa = xt + row * XS + kg * 16;
-      const int8_t *wb = net.w0 + ((size_t)b * 16 + row) * L1 + kg * 16;
-#pragma unroll 4
-      for (int ks = 0; ks < L1; ks += 64) {
-        const int4v a = *reinterpret_cast<const int4v *>(xa + ks);
-        const int4v w = *reinterpret_cast<const int4v *>(wb + ks);
-        acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, w, acc, 0, 0, 0);
+  // ---- phase 2: layer stack (MFMA), one wave per distinct bucket in the tile
+  layer_stack_tile<L1, NW>(net, xt, in1, fwd, psq, bkt, bmask, [&](int pos, int b) {
+    return base + pos < n && nfeat[pos] && bkt[pos] == b;
+  }, [&](int pos, int2 v) { out[base + pos] = v; });
+}
+
+// ---------------------------------------------------------- expand_eval --
+// Incremental evaluation of every legal child of a parent (SURVEY.md §8a row
+// a14, "children are derived from the parent accumulator by incremental
+// add/sub deltas").  One workgroup per parent; slot list = [parent, child_0 ..
+// child_{nc-1}] in tiles of 16.  Threads are split by ABSOLUTE perspective
+// (h = 0 white, 1 black) because the side to move alternates between parent
+// and children; h is mapped to the stm / ~stm half of the transformed
+// features per slot.  The parent accumulators (refreshed once) stay in
+// registers (big net) or LDS (small net, PAR > 1); a child perspective is
+//   parent_acc - rows(removed) + rows(added)   (1-3 rows each, Dirty),
+// or a refresh from the bias when that perspective's own king moved.
+template <int L1, int PAR>
+__global__ void __launch_bounds__(2 * (L1 / 16) * PAR)
+    expand_eval_kernel(NetDevice net, const gn_board *__restrict__ parents, const uint64_t *__restrict__ offsets,
+                       const gn_board *__restrict__ children, const ChildDelta *__restrict__ deltas,
+                       const uint8_t *__restrict__ need_parent,
+                       const uint8_t *__restrict__ need_child, int2 *__restrict__ out_parent,
+                       int2 *__restrict__ out_child) {
+  constexpr int G = L1 / 16;
+  constexpr int NT = 2 * G * PAR;
+  constexpr int NW = NT / 64;
+  constexpr int TILE = 16;
+  constexpr int XS = L1 + 16;
+  constexpr uint32_t RS = 2 * L1 + 32;
+  constexpr int ROWS_BYTES = TILE * 2 * 32 * 2;
+  constexpr int LS_BYTES = NW * TILE * 32 + NW * TILE * 4;
+  constexpr int SCRATCH = ROWS_BYTES > LS_BYTES ? ROWS_BYTES : LS_BYTES;
+  constexpr int PACC = PAR > 1 ? 2 * L1 : 8; // shared parent accumulators (small net only)
+  __shared__ __attribute__((aligned(16))) uint8_t xt[TILE * XS];
+  __shared__ __attribute__((aligned(16))) uint8_t scratch[SCRATCH];
+  __shared__ __attribute__((aligned(16))) uint16_t pacc_lds[PACC];
+  __shared__ __attribute__((aligned(16))) int32_t pps_lds[2][8];
+  __shared__ uint16_t prow[2][32];
+  __shared__ int32_t psq[TILE][2];
+  __shared__ int nsub[TILE][2], nadd[TILE][2], usep[TILE][2], sstm[TILE], bkt[TILE], valid[TILE];
+  __shared__ int pcount;
+  __shared__ uint32_t bmask;
+  uint16_t(*rows)[2][32] = reinterpret_cast<uint16_t(*)[2][32]>(scratch);
+  uint8_t(*in1)[TILE][32] = reinterpret_cast<uint8_t(*)[TILE][32]>(scratch);
+  int32_t(*fwd)[TILE] = reinterpret_cast<int32_t(*)[TILE]>(scratch + NW * TILE * 32);
+
+  const int tid = threadIdx.x;
+  const size_t p = blockIdx.x;
+  const uint64_t off = offsets[p];
+  const int nc = (int)(offsets[p + 1] - off);
+  const int total = 1 + nc;
+
+  // ---- pre-phase: is any slot needed?  parent feature rows (both perspectives)
+  int want = 0;
+  for (int q = tid; q < total; q += NT)
+    want |= q == 0 ? (need_parent ? need_parent[p] : 1) : (need_child ? need_child[off + q - 1] : 1);
+  if (tid == 0) pcount = packed_features(parents[p], prow[0], prow[1]);
+  if (!__syncthreads_or(want)) return;
+  if (!pcount) return;
+
+  const int q = tid / (2 * G), h = (tid / G) & 1, j = tid % G;
+  const ushort8 bias_lo = *reinterpret_cast<const ushort8 *>(net.bias + 8 * j);
+  const ushort8 bias_hi = *reinterpret_cast<const ushort8 *>(net.bias + L1 / 2 + 8 * j);
+  const uint8_t *ftj = net.ft + 16 * j;
+  const uint32_t pso = 2 * L1 + 16 * (j & 1); // this thread's 4 PSQT buckets (j < 2 only)
+  const int4v zero4 = {0, 0, 0, 0};
+
+  // parent accumulators: bias + all rows (group q == 0), kept for every child
+  ushort8 pacc_lo = bias_lo, pacc_hi = bias_hi;
+  int4v pps = zero4;
+  if (q == 0) {
+    const int cnt = pcount;
+    int k = 0;
+    for (; k + 4 <= cnt; k += 4) {
+      const uint32_t o0 = prow[h][k] * RS, o1 = prow[h][k + 1] * RS, o2 = prow[h][k + 2] * RS, o3 = prow[h][k + 3] * RS;
+      const ushort8 a0 = *reinterpret_cast<const ushort8 *>(ftj + o0), a1 = *reinterpret_cast<const ushort8 *>(ftj + o1);
+      const ushort8 a2 = *reinterpret_cast<const ushort8 *>(ftj + o2), a3 = *reinterpret_cast<const ushort8 *>(ftj + o3);
+      const ushort8 b0 = *reinterpret_cast<const ushort8 *>(ftj + o0 + L1), b1 = *reinterpret_cast<const ushort8 *>(ftj + o1 + L1);
+      const ushort8 b2 = *reinterpret_cast<const ushort8 *>(ftj + o2 + L1), b3 = *reinterpret_cast<const ushort8 *>(ftj + o3 + L1);
+      if (j < 2) {
+        pps += *reinterpret_cast<const int4v *>(net.ft + o0 + pso) + *reinterpret_cast<const int4v *>(net.ft + o1 + pso);
+        pps += *reinterpret_cast<const int4v *>(net.ft + o2 + pso) + *reinterpret_cast<const int4v *>(net.ft + o3 + pso);
       }
-      // acc[i] = fc_0[position 4*kg + i][output row]
-      const int32_t bias0 = net.b0[b * 16 + row];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int pos = 4 * kg + i;
-        const int32_t v = wadd(acc[i], bias0);
-        if (row < 15) {
-          const long long s2 = ((long long)v * v) >> 19;
-          in1[wave][pos][row] = (uint8_t)(s2 < 127 ? s2 : 127);
-          in1[wave][pos][15 + row] = (uint8_t)clampi(v >> 6, 0, 127);
-        } else {
-          fwd[wave][pos] = wmul(v, 600 * 16) / (127 * 64);
-          in1[wave][pos][30] = 0;
-          in1[wave][pos][31] = 0;
-        }
-      }
+      pacc_lo += (a0 + a1) + (a2 + a3);
+      pacc_hi += (b0 + b1) + (b2 + b3);
     }
+    for (; k < cnt; ++k) {
+      const uint32_t o0 = prow[h][k] * RS;
+      pacc_lo += *reinterpret_cast<const ushort8 *>(ftj + o0);
+      pacc_hi += *reinterpret_cast<const ushort8 *>(ftj + o0 + L1);
+      if (j < 2) pps += *reinterpret_cast<const int4v *>(net.ft + o0 + pso);
+    }
+    if (PAR > 1) {
+      *reinterpret_cast<ushort8 *>(pacc_lds + h * L1 + 8 * j) = pacc_lo;
+      *reinterpret_cast<ushort8 *>(pacc_lds + h * L1 + L1 / 2 + 8 * j) = pacc_hi;
+      if (j < 2) *reinterpret_cast<int4v *>(&pps_lds[h][4 * j]) = pps;
+    }
+  }
+  if (PAR > 1) {
     __syncthreads();
-    if (b >= 0) {
-      // fc_1: [16 x 32(+32 zero)] . [32 x 32] as two 16x16x64 MFMAs
-      const int4v zero = {0, 0, 0, 0};
-      int4v a = zero, wl = zero, wh = zero;
-      if (kg < 2) {
-        a = *reinterpret_cast<const int4v *>(&in1[wave][row][kg * 16]);
-        wl = *reinterpret_cast<const int4v *>(net.w1 + ((size_t)b * 32 + row) * 32 + kg * 16);
-        wh = *reinterpret_cast<const int4v *>(net.w1 + ((size_t)b * 32 + 16 + row) * 32 + kg * 16);
-      }
-      const int4v cl = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, wl, zero, 0, 0, 0);
-      const int4v ch = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, wh, zero, 0, 0, 0);
-      const int32_t b1l = net.b1[b * 32 + row], b1h = net.b1[b * 32 + 16 + row];
-      const int32_t w2l = net.w2[b * 32 + row], w2h = net.w2[b * 32 + 16 + row];
-      int32_t part[4];
+    pacc_lo = *reinterpret_cast<const ushort8 *>(pacc_lds + h * L1 + 8 * j);
+    pacc_hi = *reinterpret_cast<const ushort8 *>(pacc_lds + h * L1 + L1 / 2 + 8 * j);
+    if (j < 2) pps = *reinterpret_cast<const int4v *>(&pps_lds[h][4 * j]);
+  }
+
+  for (int t0 = 0; t0 < total; t0 += TILE) {
+    if (tid == 0) bmask = 0;
+    __syncthreads();
+    // ---- phase 0: slot descriptors (one thread per slot) from ChildDelta
+    if (tid < TILE) {
+      const int qq = t0 + tid;
+      int v = 0, stm = 0, cnt = 2;
+      if (qq < total) {
+        if (qq == 0) {
+          v = need_parent ? need_parent[p] : 1;
+          stm = parents[p].stm_ep >> 7, cnt = pcount;
+          nsub[tid][0] = nsub[tid][1] = nadd[tid][0] = nadd[tid][1] = 0;
+          usep[tid][0] = usep[tid][1] = 1;
+        } else if ((v = need_child ? need_child[off + qq - 1] : 1)) {
+          const ChildDelta cd = deltas[off + qq - 1];
+          stm = (cd.meta >> 10) & 1;
+          cnt = 4 * ((cd.meta >> 11) & 7) + 1;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int32_t l = clampi(wadd(cl[i], b1l) >> 6, 0, 127), hh = clampi(wadd(ch[i], b1h) >> 6, 0, 127);
-        part[i] = w2l * l + w2h * hh;
-      }
-#pragma unroll
-      for (int off = 8; off; off >>= 1)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) part[i] = wadd(part[i], __shfl_xor(part[i], off, 16));
-      if (row == 0) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int pos = 4 * kg + i;
-          const size_t gi = base + pos;
-          if (gi < n && nfeat[pos] && bkt[pos] == b) {
-            const int32_t positional = wadd(wadd(net.b2[b], part[i]), fwd[wave][pos]);
-            const int32_t psqt = (int32_t)((uint32_t)psq[pos][0] - (uint32_t)psq[pos][1]) / 2;
-            out[gi] = make_int2(psqt / 16, positional / 16);
+          for (int hh = 0; hh < 2; ++hh) {
+            if (cd.meta & (1u << (8 + hh))) {
+              const gn_board cb = children[off + qq - 1];
+              const int c = packed_features(cb, hh == 0 ? rows[tid][0] : nullptr, hh == 1 ? rows[tid][1] : nullptr);
+              usep[tid][hh] = 0, nsub[tid][hh] = 0, nadd[tid][hh] = c;
+              if (!c) v = 0;
+            } else {
+              const int ns = (cd.meta >> (4 * hh)) & 3, na = (cd.meta >> (4 * hh + 2)) & 3;
+              rows[tid][hh][0] = cd.idx[hh][0];
+              rows[tid][hh][1] = cd.idx[hh][1];
+              rows[tid][hh][ns] = cd.idx[hh][2];
+              rows[tid][hh][ns + 1] = cd.idx[hh][3];
+              usep[tid][hh] = 1, nsub[tid][hh] = ns, nadd[tid][hh] = na;
+            }
           }
         }
       }
+      valid[tid] = v;
+      sstm[tid] = stm;
+      bkt[tid] = (cnt - 1) / 4;
+      if (v) atomicOr(&bmask, 1u << ((cnt - 1) / 4));
     }
     __syncthreads();
+
+    // ---- phase 1: accumulators + transform
+#pragma unroll 1
+    for (int r = 0; r < TILE / PAR; ++r) {
+      const int sl = r * PAR + q;
+      if (!valid[sl]) continue;
+      const bool fromp = usep[sl][h];
+      ushort8 lo = fromp ? pacc_lo : bias_lo, hi = fromp ? pacc_hi : bias_hi;
+      int4v ps = fromp ? pps : zero4;
+      const uint16_t *rr = rows[sl][h];
+      const int ns = nsub[sl][h], na = nadd[sl][h];
+      int k = 0;
+      for (; k < ns; ++k) {
+        const uint32_t o0 = rr[k] * RS;
+        lo -= *reinterpret_cast<const ushort8 *>(ftj + o0);
+        hi -= *reinterpret_cast<const ushort8 *>(ftj + o0 + L1);
+        if (j < 2) ps -= *reinterpret_cast<const int4v *>(net.ft + o0 + pso);
+      }
+      const int end = ns + na;
+      for (; k + 4 <= end; k += 4) {
+        const uint32_t o0 = rr[k] * RS, o1 = rr[k + 1] * RS, o2 = rr[k + 2] * RS, o3 = rr[k + 3] * RS;
+        const ushort8 a0 = *reinterpret_cast<const ushort8 *>(ftj + o0), a1 = *reinterpret_cast<const ushort8 *>(ftj + o1);
+        const ushort8 a2 = *reinterpret_cast<const ushort8 *>(ftj + o2), a3 = *reinterpret_cast<const ushort8 *>(ftj + o3);
+        const ushort8 b0 = *reinterpret_cast<const ushort8 *>(ftj + o0 + L1), b1 = *reinterpret_cast<const ushort8 *>(ftj + o1 + L1);
+        const ushort8 b2 = *reinterpret_cast<const ushort8 *>(ftj + o2 + L1), b3 = *reinterpret_cast<const ushort8 *>(ftj + o3 + L1);
+        if (j < 2) {
+          ps += *reinterpret_cast<const int4v *>(net.ft + o0 + pso) + *reinterpret_cast<const int4v *>(net.ft + o1 + pso);
+          ps += *reinterpret_cast<const int4v *>(net.ft + o2 + pso) + *reinterpret_cast<const int4v *>(net.ft + o3 + pso);
+        }
+        lo += (a0 + a1) + (a2 + a3);
+        hi += (b0 + b1) + (b2 + b3);
+      }
+      for (; k < end; ++k) {
+        const uint32_t o0 = rr[k] * RS;
+        lo += *reinterpret_cast<const ushort8 *>(ftj + o0);
+        hi += *reinterpret_cast<const ushort8 *>(ftj + o0 + L1);
+        if (j < 2) ps += *reinterpret_cast<const int4v *>(net.ft + o0 + pso);
+      }
+      const int side = h == sstm[sl] ? 0 : 1;
+      uint32_t w0 = 0, w1 = 0;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int a = clampi((short)lo[e], 0, 254), b = clampi((short)hi[e], 0, 254);
+        const uint32_t v = (uint32_t)(a * b) >> 9;
+        if (e < 4) w0 |= v << (8 * e);
+        else w1 |= v << (8 * (e - 4));
+      }
+      *reinterpret_cast<uint2 *>(xt + sl * XS + side * (L1 / 2) + 8 * j) = make_uint2(w0, w1);
+      const int b = bkt[sl];
+      if (j == (b >> 2)) psq[sl][side] = ps[b & 3];
+    }
+    __syncthreads();
+
+    // ---- phase 2: layer stack
+    layer_stack_tile<L1, NW>(net, xt, in1, fwd, psq, bkt, bmask, [&](int pos, int b) {
+      return t0 + pos < total && valid[pos] && bkt[pos] == b;
+    }, [&](int pos, int2 v) {
+      if (t0 + pos == 0) out_parent[p] = v;
+      else out_child[off + t0 + pos - 1] = v;
+    });
   }
+}
+
+hipError_t launch_expand_net(const NetDevice &net, const gn_board *parents, size_t n, const uint64_t *offsets,
+                             const gn_board *children, const ChildDelta *deltas, const uint8_t *need_parent,
+                             const uint8_t *need_child, int2 *out_parent, int2 *out_child, hipStream_t s) {
+  if (!n) return hipSuccess;
+  if (net.L1 == 3072) {
+    hipLaunchKernelGGL((expand_eval_kernel<3072, 1>), dim3((unsigned)n), dim3(384), 0, s, net, parents, offsets, children,
+                       deltas, need_parent, need_child, out_parent, out_child);
+  } else if (net.L1 == 128) {
+    hipLaunchKernelGGL((expand_eval_kernel<128, 16>), dim3((unsigned)n), dim3(256), 0, s, net, parents, offsets, children,
+                       deltas, need_parent, need_child, out_parent, out_child);
+  } else if (net.L1 == 1024) {
+    hipLaunchKernelGGL((expand_eval_kernel<1024, 1>), dim3((unsigned)n), dim3(128), 0, s, net, parents, offsets, children,
+                       deltas, need_parent, need_child, out_parent, out_child);
+  } else {
+    return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
 }
 
 hipError_t launch_eval_net(const NetDevice &net, const gn_board *boards, const uint8_t *need, size_t n, int2 *out,
@@ -384,7 +601,8 @@ __global__ void count_children_kernel(const gn_board *__restrict__ boards, size_
 
 __global__ void write_children_kernel(const gn_board *__restrict__ boards, size_t n, const Tables *__restrict__ tables,
                                       const uint64_t *__restrict__ offsets, gn_board *__restrict__ children,
-                                      uint16_t *__restrict__ moves) {
+                                      uint16_t *__restrict__ moves, ChildDelta *__restrict__ deltas,
+                                      unsigned long long *__restrict__ rows) {
   __shared__ Tables T;
   load_tables(T, tables);
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -392,13 +610,22 @@ __global__ void write_children_kernel(const gn_board *__restrict__ boards, size_
   Board B;
   if (!unpack(boards[i], B)) return;
   uint64_t k = offsets[i];
+  // feature-transformer rows the incremental evaluation will gather: the
+  // parent's refresh (both perspectives) + per child either the delta rows or
+  // a refresh of the perspective whose king moved
+  unsigned long long nrows = 2ull * popcnt(B.byType[0]);
   gen_legal(B, T, [&](uint16_t m) {
     gn_board pb;
-    pack(do_move(B, m), pb);
+    Dirty d;
+    const Board C = do_move(B, m, &d);
+    pack(C, pb);
     children[k] = pb;
     if (moves) moves[k] = m;
+    if (deltas) deltas[k] = make_child_delta(B, C, d);
+    nrows += d.king_moved ? popcnt(C.byType[0]) + d.n_rem + d.n_add : 2 * (d.n_rem + d.n_add);
     ++k;
   });
+  if (rows) atomicAdd(rows, nrows);
 }
 
 __global__ void count_sum_kernel(const gn_board *__restrict__ boards, size_t n, const Tables *__restrict__ tables,
@@ -433,6 +660,28 @@ __global__ void random_positions_kernel(uint64_t seed, size_t first, size_t n, i
   out[i] = pb;
 }
 
+__global__ void random_games_kernel(uint64_t seed, size_t first_game, size_t n_games, int plies,
+                                    const Tables *__restrict__ tables, gn_board *__restrict__ out) {
+  __shared__ Tables T;
+  load_tables(T, tables);
+  const size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= n_games) return;
+  Xoshiro rng(seed + first_game + g);
+  Board B = start_position();
+  gn_board pb;
+  pack(B, pb);
+  gn_board *dst = out + g * (size_t)(plies + 1);
+  dst[0] = pb;
+  for (int k = 1; k <= plies; ++k) {
+    const int n = count_legal(B, T);
+    if (n && B.rule50 < 100) {
+      B = do_move(B, nth_legal(B, T, (int)rng.below((uint32_t)n)));
+      pack(B, pb);
+    }
+    dst[k] = pb;
+  }
+}
+
 __global__ void offsets_u32_kernel(const uint64_t *__restrict__ in, size_t n, uint32_t *__restrict__ out) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) out[i] = (uint32_t)in[i];
@@ -446,10 +695,11 @@ hipError_t launch_count_children(const gn_board *boards, size_t n, const Tables 
 }
 
 hipError_t launch_write_children(const gn_board *boards, size_t n, const Tables *tables, const uint64_t *offsets,
-                                 gn_board *children, uint16_t *moves, hipStream_t s) {
+                                 gn_board *children, uint16_t *moves, ChildDelta *deltas, unsigned long long *rows,
+                                 hipStream_t s) {
   if (!n) return hipSuccess;
   hipLaunchKernelGGL(write_children_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, boards, n, tables, offsets,
-                     children, moves);
+                     children, moves, deltas, rows);
   return hipGetLastError();
 }
 
@@ -465,6 +715,14 @@ hipError_t launch_random_positions(uint64_t seed, size_t first, size_t n, int ma
   if (!n) return hipSuccess;
   hipLaunchKernelGGL(random_positions_kernel, dim3(blocks_for(n, 128)), dim3(128), 0, s, seed, first, n, max_plies,
                      tables, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_random_games(uint64_t seed, size_t first_game, size_t n_games, int plies, const Tables *tables,
+                               gn_board *out, hipStream_t s) {
+  if (!n_games) return hipSuccess;
+  hipLaunchKernelGGL(random_games_kernel, dim3(blocks_for(n_games, 128)), dim3(128), 0, s, seed, first_game, n_games,
+                     plies, tables, out);
   return hipGetLastError();
 }
 

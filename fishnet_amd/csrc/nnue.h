@@ -50,6 +50,69 @@ GN_HD int feature_index(int persp, int sq, int pc, int ksq) {
   return (sq ^ orient) + 64 * plane + 704 * bucket;
 }
 
+// Feature-transformer delta of one child, written by the child generator
+// (write_children) from Dirty and read by expand_eval: for each ABSOLUTE
+// perspective either a refresh flag or up to 2 removed (idx[h][0..1]) and 2
+// added (idx[h][2..3]) HalfKAv2_hm rows.
+struct ChildDelta {
+  uint16_t idx[2][4];
+  uint32_t meta; // [1:0] nsub w, [3:2] nadd w, [5:4] nsub b, [7:6] nadd b, [8] refresh w, [9] refresh b,
+                 // [10] stm, [13:11] bucket
+  uint32_t pad;
+};
+static_assert(sizeof(ChildDelta) == 24, "ChildDelta is 24 bytes");
+
+GN_HD ChildDelta make_child_delta(const Board &parent, const Board &child, const Dirty &d) {
+  ChildDelta cd;
+  uint32_t meta = 0;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int ksq = king_square(child, h);
+    cd.idx[h][0] = cd.idx[h][1] = cd.idx[h][2] = cd.idx[h][3] = 0;
+    if (d.king_moved && h == parent.stm) {
+      meta |= 1u << (8 + h);
+    } else {
+      cd.idx[h][0] = (uint16_t)feature_index(h, d.rem_sq[0], d.rem_pc[0], ksq);
+      if (d.n_rem > 1) cd.idx[h][1] = (uint16_t)feature_index(h, d.rem_sq[1], d.rem_pc[1], ksq);
+      cd.idx[h][2] = (uint16_t)feature_index(h, d.add_sq[0], d.add_pc[0], ksq);
+      if (d.n_add > 1) cd.idx[h][3] = (uint16_t)feature_index(h, d.add_sq[1], d.add_pc[1], ksq);
+      meta |= (uint32_t)(d.n_rem | (d.n_add << 2)) << (4 * h);
+    }
+  }
+  meta |= (uint32_t)child.stm << 10;
+  meta |= (uint32_t)((popcnt(child.byType[0]) - 1) / 4) << 11;
+  cd.meta = meta;
+  cd.pad = 0;
+  return cd;
+}
+
+// Feature rows of both absolute perspectives straight from a packed board
+// (no Board needed).  Returns the piece count, or 0 for an invalid board
+// (bad nibble, not one king per side): nothing is then written, so no row
+// index can go out of range.
+GN_HD int packed_features(const gn_board &p, uint16_t *rows_white, uint16_t *rows_black) {
+  uint64_t wlo, whi;
+  piece_words(p, wlo, whi);
+  const int c = popcnt(p.occ);
+  int wk = -1, bk = -1;
+  bool ok = c >= 2 && c <= 32;
+  uint64_t o = p.occ;
+  for (int k = 0; ok && k < c; ++k) {
+    const int s = pop_lsb(o), pc = piece_nibble(wlo, whi, k), pt = pc & 7;
+    ok &= pt >= PAWN && pt <= KING;
+    if (pc == make_piece(WHITE, KING)) ok &= wk < 0, wk = s;
+    if (pc == make_piece(BLACK, KING)) ok &= bk < 0, bk = s;
+  }
+  if (!ok || wk < 0 || bk < 0) return 0;
+  o = p.occ;
+  for (int k = 0; k < c; ++k) {
+    const int s = pop_lsb(o), pc = piece_nibble(wlo, whi, k);
+    if (rows_white) rows_white[k] = (uint16_t)feature_index(WHITE, s, pc, wk);
+    if (rows_black) rows_black[k] = (uint16_t)feature_index(BLACK, s, pc, bk);
+  }
+  return c;
+}
+
 // 32-bit hashes stored in .nnue files
 inline uint32_t affine_hash(uint32_t prev, uint32_t outs) {
   uint32_t h = 0xCC03DAE4u + outs;

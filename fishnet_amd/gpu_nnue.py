@@ -33,7 +33,10 @@ EXPORTS = ["gn_load_net", "gn_load_net_memory", "gn_free", "gn_last_error", "gn_
            "gn_evaluate_batch_mode", "gn_expand_and_evaluate", "gn_perft", "gn_pack_fens",
            "gn_board_to_fen", "gn_random_positions", "gn_evaluate_device", "gn_expand_device",
            "gn_device_alloc", "gn_device_free", "gn_memcpy_h2d", "gn_memcpy_d2h", "gn_synchronize",
-           "gn_time_evaluate_device", "gn_random_positions_device"]
+           "gn_time_evaluate_device", "gn_random_positions_device", "gn_set_option", "gn_get_option",
+           "gn_time_expand_device", "gn_random_games_device"]
+OPT_INCREMENTAL_CHILDREN = 1
+EXPAND_STAGES = ["count_scan", "total_readback", "write_children", "classify", "small_net", "big_net", "finalize"]
 
 
 class GnError(RuntimeError):
@@ -86,6 +89,11 @@ def lib():
         "gn_synchronize": [vp, i32],
         "gn_time_evaluate_device": [vp, i32, vp, sz, i32, vp, i32, C.POINTER(C.c_float), vp],
         "gn_random_positions_device": [vp, i32, C.c_uint64, sz, sz, i32, vp, vp],
+        "gn_set_option": [vp, i32, C.c_int64],
+        "gn_get_option": [vp, i32, C.POINTER(C.c_int64)],
+        "gn_time_expand_device": [vp, i32, vp, sz, i32, i32, C.POINTER(C.c_float), C.POINTER(sz), vp,
+                                  C.POINTER(C.c_uint64)],
+        "gn_random_games_device": [vp, i32, C.c_uint64, sz, sz, i32, vp, vp],
     }
     for name, args in sig.items():
         f = getattr(L, name)
@@ -250,6 +258,24 @@ class GpuNnue:
 
     def random_positions_device(self, seed, first, n, max_plies, d_out: DeviceBuffer, stream=None, slot=0):
         _check(lib().gn_random_positions_device(self.h, slot, seed, first, n, max_plies, d_out.ptr, stream))
+
+    def set_option(self, option, value):
+        _check(lib().gn_set_option(self.h, option, value))
+
+    def get_option(self, option):
+        v = C.c_int64()
+        _check(lib().gn_get_option(self.h, option, C.byref(v)))
+        return v.value
+
+    def random_games_device(self, seed, first_game, n_games, plies, d_out: DeviceBuffer, stream=None, slot=0):
+        _check(lib().gn_random_games_device(self.h, slot, seed, first_game, n_games, plies, d_out.ptr, stream))
+
+    def time_expand_device(self, d_parents: DeviceBuffer, n, mode, iters, slot=0):
+        ms, total, rows = C.c_float(), C.c_size_t(), C.c_uint64()
+        st = (C.c_float * 7)()
+        _check(lib().gn_time_expand_device(self.h, slot, d_parents.ptr, n, mode, iters, C.byref(ms),
+                                           C.byref(total), st, C.byref(rows)))
+        return ms.value, total.value, list(st), rows.value
 
     def synchronize(self, slot=0):
         _check(lib().gn_synchronize(self.h, slot))

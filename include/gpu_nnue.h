@@ -54,6 +54,10 @@ extern "C" {
 #define GN_MODE_BIG 1   /* big net for every position (epilogue: smallNet=false) */
 #define GN_MODE_SMALL 2 /* small net for every position (epilogue: smallNet=true) */
 
+/* options (gn_set_option / gn_get_option) */
+#define GN_OPT_INCREMENTAL_CHILDREN 1 /* 1 (default): children from the parent accumulators
+                                         by add/sub deltas; 0: full refresh per child    */
+
 /* per-position flags */
 #define GN_FLAG_IN_CHECK 1u /* side to move in check: Stockfish has no static eval
                                (Eval::evaluate asserts !checkers); values are still
@@ -124,6 +128,8 @@ GN_API const char *gn_last_error(void); /* thread-local; valid until the next ca
 GN_API int gn_abi_version(void);
 GN_API int gn_get_eval_params(const gn_ctx *ctx, gn_eval_params *out);
 GN_API int gn_set_eval_params(gn_ctx *ctx, const gn_eval_params *params);
+GN_API int gn_set_option(gn_ctx *ctx, int option, int64_t value);
+GN_API int gn_get_option(const gn_ctx *ctx, int option, int64_t *value);
 /* network hashes / widths actually loaded (0 when absent) */
 GN_API int gn_net_info(const gn_ctx *ctx, int *big_l1, uint32_t *big_hash, int *small_l1, uint32_t *small_hash);
 
@@ -175,6 +181,20 @@ GN_API int gn_evaluate_device(gn_ctx *ctx, int device_slot, const gn_board *d_bo
 GN_API int gn_expand_device(gn_ctx *ctx, int device_slot, const gn_board *d_parents, size_t n, int mode,
                      gn_eval *d_parent_out, uint32_t *d_offsets, gn_board *d_children,
                      uint16_t *d_moves, gn_eval *d_child_out, size_t cap, size_t *total, void *stream);
+/* Time `iters` complete expansions of device-resident parents (child count +
+ * scan + child generation with deltas + evaluation of parents and children in
+ * `mode`), library-owned output buffers.  *total = children per expansion;
+ * stage_ms (optional, length 7) = average ms of [count+scan, total read-back,
+ * write children, classify, small net, big net, finalize]; ft_rows (optional)
+ * = feature-transformer rows one incremental expansion gathers (parent
+ * refreshes + child deltas / king-move refreshes; 0 when not incremental). */
+GN_API int gn_time_expand_device(gn_ctx *ctx, int device_slot, const gn_board *d_parents, size_t n, int mode,
+                                 int iters, float *ms_total, size_t *total, float *stage_ms, uint64_t *ft_rows);
+/* n_games random games of `plies` plies (xoshiro256**, seed + game index) on
+ * the GPU: d_out[g * (plies + 1) + k] = position after k plies of game g (a
+ * game that ends early repeats its final position).  Asynchronous. */
+GN_API int gn_random_games_device(gn_ctx *ctx, int device_slot, uint64_t seed, size_t first_game, size_t n_games,
+                                  int plies, gn_board *d_out, void *stream);
 /* Device memory helpers (so callers need no HIP headers). */
 GN_API int gn_device_alloc(gn_ctx *ctx, int device_slot, size_t bytes, void **ptr);
 GN_API int gn_device_free(gn_ctx *ctx, int device_slot, void *ptr);
