@@ -90,7 +90,7 @@ def cpu_baseline(G, boards_sample, mode, budget_s):
                       f"(AVX2 build class), {threads} POSIX threads on {cpu_model()}"}
 
 
-def run_children(args, ctx, wl, world, rank, dist, torch, net_label, big_p, small_p):
+def run_children(args, ctx, wl, world, rank, dist, torch, net_label, big_p, small_p, options):
     """configs[3] shape: games x 81 parents, every legal child, incremental."""
     from fishnet_amd import gpu_nnue as G
     games, plies, mode = (args.positions or wl["n"]), 80, wl["mode"]
@@ -130,7 +130,7 @@ def run_children(args, ctx, wl, world, rank, dist, torch, net_label, big_p, smal
         "config": {"workload": wl["config"], "games_per_gpu": games, "parents_per_gpu": n,
                    "children_per_gpu": children, "evals_per_step_per_gpu": evals,
                    "mode": ["full", "big", "small"][mode], "incremental": True,
-                   "parallelism": f"dp{world} (games sharded, no collective)"},
+                   "parallelism": f"dp{world} (games sharded, no collective)", "options": options},
         "roofline": {"bound": "hbm", "kernel": f"expand_eval<{l1}>", "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": None, "alg_bytes_per_launch": alg, "ft_rows_per_launch": rows,
@@ -173,6 +173,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true")
     ap.add_argument("--check", type=int, default=2048, help="positions re-checked against the oracle (rank 0)")
+    ap.add_argument("--swizzle", type=int, default=1, help="GN_OPT_XCD_SWIZZLE")
+    ap.add_argument("--king-sort", type=int, default=-1, help="GN_OPT_KING_SORT (-1: library default)")
     args = ap.parse_args()
 
     import torch  # first: torch's HIP runtime is the one libgpu_nnue then binds to
@@ -209,6 +211,10 @@ def main():
         dist.broadcast_object_list(lab, 0)
         net_label = lab[0]
     ctx = G.GpuNnue(big_bytes=blobs[0], small_bytes=blobs[1], devices=[local])
+    ctx.set_option(G.OPT_XCD_SWIZZLE, args.swizzle)
+    if args.king_sort >= 0:
+        ctx.set_option(G.OPT_KING_SORT, args.king_sort)
+    options = {"xcd_swizzle": ctx.get_option(G.OPT_XCD_SWIZZLE), "king_sort": ctx.get_option(G.OPT_KING_SORT)}
 
     def run_workload(mode, n, steps, warmup, measure_roofline):
         d_boards = ctx.alloc(n * 32)
@@ -241,7 +247,7 @@ def main():
         return res
 
     if args.workload == "children":
-        run_children(args, ctx, wl, world, rank, dist, torch, net_label, big_p, small_p)
+        run_children(args, ctx, wl, world, rank, dist, torch, net_label, big_p, small_p, options)
         return
 
     r = run_workload(mode, n, args.steps, args.warmup, True)
@@ -280,7 +286,8 @@ def main():
         "data": f"synthetic: seeded random-playout positions generated on the GPU; nets {net_label}",
         "config": {"workload": wl["config"], "positions_per_gpu": n, "global_batch": n * world,
                    "mode": ["full", "big", "small"][mode], "mean_pieces": round(float(pieces.mean()), 3),
-                   "max_plies": args.max_plies, "parallelism": f"dp{world} (positions sharded, no collective)"},
+                   "max_plies": args.max_plies, "parallelism": f"dp{world} (positions sharded, no collective)",
+                   "options": options},
         "roofline": {"bound": "hbm", "kernel": f"eval_net<{wl['l1']}> ({STAGES[stage]})",
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,

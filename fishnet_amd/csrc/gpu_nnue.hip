@@ -193,6 +193,10 @@ struct Dev {
   DevBuf<uint32_t> off32;
   DevBuf<uint16_t> moves;
   DevBuf<ChildDelta> deltas;
+  DevBuf<uint16_t> kkeys, kkeys2; // king-sort keys
+  DevBuf<uint32_t> kidx, kperm;   // king-sort permutation
+  void *sort_tmp = nullptr;
+  size_t sort_bytes = 0;
   DevBuf<int2> p_osm, p_obg;     // parent-side net outputs during expansion
   DevBuf<uint8_t> p_nsm, p_nbg;  // parent-side net selection during expansion
   DevBuf<unsigned long long> sum;
@@ -205,6 +209,8 @@ struct gn_ctx {
   std::vector<std::unique_ptr<Dev>> devs;
   gn_eval_params P;
   bool incremental = true; // GN_OPT_INCREMENTAL_CHILDREN
+  bool swizzle = true;      // GN_OPT_XCD_SWIZZLE
+  bool king_sort = false;   // GN_OPT_KING_SORT
   int l1[2] = {0, 0};
   uint32_t hash[2] = {0, 0};
 };
@@ -273,6 +279,8 @@ static void destroy(gn_ctx *ctx) {
     d.off32.release(), d.moves.release(), d.sum.release(), d.deltas.release();
     d.p_osm.release(), d.p_obg.release(), d.p_nsm.release(), d.p_nbg.release();
     if (d.scan_tmp) (void)hipFree(d.scan_tmp);
+    if (d.sort_tmp) (void)hipFree(d.sort_tmp);
+    d.kkeys.release(), d.kkeys2.release(), d.kidx.release(), d.kperm.release();
     if (d.stream) (void)hipStreamDestroy(d.stream);
   }
   delete ctx;
@@ -359,11 +367,24 @@ static int evaluate_on(gn_ctx *ctx, Dev &d, const gn_board *b, size_t n, int mod
   const gn_eval_params &P = ctx->P;
   HIP_TRY(mark(0));
   if (mode == GN_MODE_FULL) HIP_TRY(launch_classify(b, n, P, d.nsm.p, d.nbg.p, s));
+  const uint32_t *perm = nullptr;
+  if (ctx->king_sort) {
+    if (n > 0x7FFFFFFFull) return fail(GN_E_INVALID, "king sort supports < 2^31 positions per call");
+    HIP_TRY(d.kkeys.ensure(n));
+    HIP_TRY(d.kkeys2.ensure(n));
+    HIP_TRY(d.kidx.ensure(n));
+    HIP_TRY(d.kperm.ensure(n));
+    HIP_TRY(king_sort(b, n, d.kkeys.p, d.kidx.p, d.kkeys2.p, d.kperm.p, d.sort_tmp, d.sort_bytes, s));
+    perm = d.kperm.p;
+  }
+  const int swz = ctx->swizzle;
   HIP_TRY(mark(1));
-  if (mode != GN_MODE_BIG) HIP_TRY(launch_eval_net(d.net[SMALL], b, mode == GN_MODE_FULL ? d.nsm.p : nullptr, n, d.osm.p, s));
+  if (mode != GN_MODE_BIG)
+    HIP_TRY(launch_eval_net(d.net[SMALL], b, mode == GN_MODE_FULL ? d.nsm.p : nullptr, n, d.osm.p, perm, swz, s));
   if (mode == GN_MODE_FULL) HIP_TRY(launch_reeval(d.osm.p, d.nsm.p, n, P, d.nbg.p, s));
   HIP_TRY(mark(2));
-  if (mode != GN_MODE_SMALL) HIP_TRY(launch_eval_net(d.net[BIG], b, mode == GN_MODE_FULL ? d.nbg.p : nullptr, n, d.obg.p, s));
+  if (mode != GN_MODE_SMALL)
+    HIP_TRY(launch_eval_net(d.net[BIG], b, mode == GN_MODE_FULL ? d.nbg.p : nullptr, n, d.obg.p, perm, swz, s));
   HIP_TRY(mark(3));
   HIP_TRY(launch_finalize(b, n, mode, d.osm.p, d.obg.p, d.nsm.p, d.nbg.p, P, d.tables, out, s));
   HIP_TRY(mark(4));
@@ -469,7 +490,7 @@ static int expand_evaluate(gn_ctx *ctx, Dev &d, const gn_board *parents, size_t 
   if (mode != GN_MODE_BIG) {
     const bool f = mode == GN_MODE_FULL;
     HIP_TRY(launch_expand_net(d.net[SMALL], parents, n, off, children, dl, f ? d.p_nsm.p : nullptr,
-                              f ? d.nsm.p : nullptr, d.p_osm.p, d.osm.p, s));
+                              f ? d.nsm.p : nullptr, d.p_osm.p, d.osm.p, ctx->swizzle, s));
     if (f) {
       HIP_TRY(launch_reeval(d.p_osm.p, d.p_nsm.p, n, P, d.p_nbg.p, s));
       HIP_TRY(launch_reeval(d.osm.p, d.nsm.p, total, P, d.nbg.p, s));
@@ -479,7 +500,7 @@ static int expand_evaluate(gn_ctx *ctx, Dev &d, const gn_board *parents, size_t 
   if (mode != GN_MODE_SMALL) {
     const bool f = mode == GN_MODE_FULL;
     HIP_TRY(launch_expand_net(d.net[BIG], parents, n, off, children, dl, f ? d.p_nbg.p : nullptr,
-                              f ? d.nbg.p : nullptr, d.p_obg.p, d.obg.p, s));
+                              f ? d.nbg.p : nullptr, d.p_obg.p, d.obg.p, ctx->swizzle, s));
   }
   HIP_TRY(mark(2));
   HIP_TRY(launch_finalize(children, total, mode, d.osm.p, d.obg.p, d.nsm.p, d.nbg.p, P, d.tables, child_out, s));
@@ -849,6 +870,12 @@ int gn_set_option(gn_ctx *ctx, int option, int64_t value) {
   case GN_OPT_INCREMENTAL_CHILDREN:
     ctx->incremental = value != 0;
     return GN_OK;
+  case GN_OPT_XCD_SWIZZLE:
+    ctx->swizzle = value != 0;
+    return GN_OK;
+  case GN_OPT_KING_SORT:
+    ctx->king_sort = value != 0;
+    return GN_OK;
   default:
     return fail(GN_E_INVALID, "unknown option %d", option);
   }
@@ -859,6 +886,12 @@ int gn_get_option(const gn_ctx *ctx, int option, int64_t *value) {
   switch (option) {
   case GN_OPT_INCREMENTAL_CHILDREN:
     *value = ctx->incremental;
+    return GN_OK;
+  case GN_OPT_XCD_SWIZZLE:
+    *value = ctx->swizzle;
+    return GN_OK;
+  case GN_OPT_KING_SORT:
+    *value = ctx->king_sort;
     return GN_OK;
   default:
     return fail(GN_E_INVALID, "unknown option %d", option);

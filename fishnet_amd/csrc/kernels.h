@@ -10,14 +10,20 @@ namespace gn {
 
 // NetworkOutput {psqt / 16, positional / 16} for every position whose
 // need[i] != 0 (need == nullptr: all); other entries of out are untouched.
+// perm (optional): slot q evaluates boards[perm[q]] and writes out[perm[q]].
+// swz: XCD-aware tile order (each XCD gets a contiguous range of tiles).
 hipError_t launch_eval_net(const NetDevice &net, const gn_board *boards, const uint8_t *need, size_t n,
-                           int2 *out, hipStream_t s);
+                           int2 *out, const uint32_t *perm, int swz, hipStream_t s);
+// permutation of [0, n) ordering positions by (white king, black king) square
+hipError_t king_sort(const gn_board *boards, size_t n, uint16_t *keys, uint32_t *idx, uint16_t *keys_out,
+                     uint32_t *perm, void *&temp, size_t &temp_bytes, hipStream_t s);
 // Incremental evaluation of parents + all their children (children of parent
 // p are [offsets[p], offsets[p+1]) with moves[]); need_* select what this net
 // evaluates (nullptr: all).
 hipError_t launch_expand_net(const NetDevice &net, const gn_board *parents, size_t n, const uint64_t *offsets,
                              const gn_board *children, const ChildDelta *deltas, const uint8_t *need_parent,
-                             const uint8_t *need_child, int2 *out_parent, int2 *out_child, hipStream_t s);
+                             const uint8_t *need_child, int2 *out_parent, int2 *out_child, int swz,
+                             hipStream_t s);
 // GN_MODE_FULL preparation: need_small = valid && |simple_eval| > threshold,
 // need_big = valid && !need_small.
 hipError_t launch_classify(const gn_board *boards, size_t n, const gn_eval_params &P, uint8_t *need_small,

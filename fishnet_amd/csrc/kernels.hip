@@ -6,6 +6,8 @@
 //                     tile per workgroup.
 // classify / reeval / finalize   Eval::evaluate.
 // count / write children, count_sum   legal movegen for expansion and perft.
+#include <stdlib.h>
+
 #include <hipcub/hipcub.hpp>
 
 #include "kernels.h"
@@ -128,7 +130,7 @@ __device__ __forceinline__ void layer_stack_tile(const NetDevice &net, const uin
 template <int L1, int PAR>
 __global__ void __launch_bounds__(2 * (L1 / 16) * PAR)
     eval_net_kernel(NetDevice net, const gn_board *__restrict__ boards, const uint8_t *__restrict__ need,
-                    size_t n, int2 *__restrict__ out) {
+                    size_t n, int2 *__restrict__ out, const uint32_t *__restrict__ perm, unsigned tiles, int swz) {
   constexpr int G = L1 / 16;
   constexpr int NT = 2 * G * PAR;
   constexpr int NW = NT / 64;
@@ -148,20 +150,32 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR)
   __shared__ int nfeat[TILE];
   __shared__ int bkt[TILE];
   __shared__ uint32_t bmask;
+  __shared__ uint32_t gidx[TILE];
   uint16_t(*rows)[2][32] = reinterpret_cast<uint16_t(*)[2][32]>(scratch);
   uint8_t(*in1)[TILE][32] = reinterpret_cast<uint8_t(*)[TILE][32]>(scratch);
   int32_t(*fwd)[TILE] = reinterpret_cast<int32_t(*)[TILE]>(scratch + NW * TILE * 32);
 
   const int tid = threadIdx.x;
-  const size_t base = (size_t)blockIdx.x * TILE;
+  // XCD-aware tile order: blocks b, b+8, ... share an XCD (round-robin
+  // dispatch); give each XCD a contiguous range of tiles so its 4 MiB L2 sees
+  // positions of similar king squares (after an optional king sort).
+  unsigned tile = blockIdx.x;
+  if (swz) {
+    const unsigned t8 = (tiles + 7) / 8;
+    tile = (blockIdx.x & 7) * t8 + (blockIdx.x >> 3);
+    if (tile >= tiles) return;
+  }
+  const size_t base = (size_t)tile * TILE;
   if (tid == 0) bmask = 0;
   __syncthreads();
 
   // ---- phase 0: feature rows of both perspectives (slot 0 = side to move)
   if (tid < TILE) {
-    const size_t i = base + tid;
+    const size_t q = base + tid;
+    const size_t i = q < n ? (perm ? perm[q] : q) : 0;
+    gidx[tid] = (uint32_t)i;
     int cnt = 0;
-    if (i < n && (!need || need[i])) {
+    if (q < n && (!need || need[i])) {
       const gn_board p = boards[i];
       const int stm = p.stm_ep >> 7;
       cnt = packed_features(p, rows[tid][stm], rows[tid][stm ^ 1]);
@@ -233,7 +247,7 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR)
   // ---- phase 2: layer stack (MFMA), one wave per distinct bucket in the tile
   layer_stack_tile<L1, NW>(net, xt, in1, fwd, psq, bkt, bmask, [&](int pos, int b) {
     return base + pos < n && nfeat[pos] && bkt[pos] == b;
-  }, [&](int pos, int2 v) { out[base + pos] = v; });
+  }, [&](int pos, int2 v) { out[gidx[pos]] = v; });
 }
 
 // ---------------------------------------------------------- expand_eval --
@@ -253,7 +267,7 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR)
                        const gn_board *__restrict__ children, const ChildDelta *__restrict__ deltas,
                        const uint8_t *__restrict__ need_parent,
                        const uint8_t *__restrict__ need_child, int2 *__restrict__ out_parent,
-                       int2 *__restrict__ out_child) {
+                       int2 *__restrict__ out_child, size_t n_parents, int swz) {
   constexpr int G = L1 / 16;
   constexpr int NT = 2 * G * PAR;
   constexpr int NW = NT / 64;
@@ -278,7 +292,15 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR)
   int32_t(*fwd)[TILE] = reinterpret_cast<int32_t(*)[TILE]>(scratch + NW * TILE * 32);
 
   const int tid = threadIdx.x;
-  const size_t p = blockIdx.x;
+  // XCD-aware parent order: each XCD takes a contiguous range of parents, so
+  // the parents of one game (same kings, mostly the same pieces) and their
+  // children share that XCD's L2
+  size_t p = blockIdx.x;
+  if (swz) {
+    const size_t p8 = (n_parents + 7) / 8;
+    p = (blockIdx.x & 7) * p8 + (blockIdx.x >> 3);
+    if (p >= n_parents) return;
+  }
   const uint64_t off = offsets[p];
   const int nc = (int)(offsets[p + 1] - off);
   const int total = 1 + nc;
@@ -440,35 +462,18 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR)
   }
 }
 
-hipError_t launch_expand_net(const NetDevice &net, const gn_board *parents, size_t n, const uint64_t *offsets,
-                             const gn_board *children, const ChildDelta *deltas, const uint8_t *need_parent,
-                             const uint8_t *need_child, int2 *out_parent, int2 *out_child, hipStream_t s) {
-  if (!n) return hipSuccess;
-  if (net.L1 == 3072) {
-    hipLaunchKernelGGL((expand_eval_kernel<3072, 1>), dim3((unsigned)n), dim3(384), 0, s, net, parents, offsets, children,
-                       deltas, need_parent, need_child, out_parent, out_child);
-  } else if (net.L1 == 128) {
-    hipLaunchKernelGGL((expand_eval_kernel<128, 16>), dim3((unsigned)n), dim3(256), 0, s, net, parents, offsets, children,
-                       deltas, need_parent, need_child, out_parent, out_child);
-  } else if (net.L1 == 1024) {
-    hipLaunchKernelGGL((expand_eval_kernel<1024, 1>), dim3((unsigned)n), dim3(128), 0, s, net, parents, offsets, children,
-                       deltas, need_parent, need_child, out_parent, out_child);
-  } else {
-    return hipErrorInvalidValue;
-  }
-  return hipGetLastError();
-}
 
 hipError_t launch_eval_net(const NetDevice &net, const gn_board *boards, const uint8_t *need, size_t n, int2 *out,
-                           hipStream_t s) {
+                           const uint32_t *perm, int swz, hipStream_t s) {
   if (!n) return hipSuccess;
-  const size_t tiles = (n + 15) / 16;
+  const unsigned tiles = (unsigned)((n + 15) / 16);
+  const unsigned grid = swz ? 8 * ((tiles + 7) / 8) : tiles;
   if (net.L1 == 3072) {
-    hipLaunchKernelGGL((eval_net_kernel<3072, 1>), dim3((unsigned)tiles), dim3(384), 0, s, net, boards, need, n, out);
+    hipLaunchKernelGGL((eval_net_kernel<3072, 1>), dim3(grid), dim3(384), 0, s, net, boards, need, n, out, perm, tiles, swz);
   } else if (net.L1 == 128) {
-    hipLaunchKernelGGL((eval_net_kernel<128, 16>), dim3((unsigned)tiles), dim3(256), 0, s, net, boards, need, n, out);
+    hipLaunchKernelGGL((eval_net_kernel<128, 16>), dim3(grid), dim3(256), 0, s, net, boards, need, n, out, perm, tiles, swz);
   } else if (net.L1 == 1024) {
-    hipLaunchKernelGGL((eval_net_kernel<1024, 1>), dim3((unsigned)tiles), dim3(128), 0, s, net, boards, need, n, out);
+    hipLaunchKernelGGL((eval_net_kernel<1024, 1>), dim3(grid), dim3(128), 0, s, net, boards, need, n, out, perm, tiles, swz);
   } else {
     return hipErrorInvalidValue;
   }
@@ -682,6 +687,26 @@ __global__ void random_games_kernel(uint64_t seed, size_t first_game, size_t n_g
   }
 }
 
+// sort key of a position for L2 locality: both king squares (invalid last)
+__global__ void king_keys_kernel(const gn_board *__restrict__ boards, size_t n, uint16_t *__restrict__ keys,
+                                 uint32_t *__restrict__ idx) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const gn_board p = boards[i];
+  uint64_t wlo, whi;
+  piece_words(p, wlo, whi);
+  uint64_t o = p.occ;
+  int wk = 64, bk = 64;
+  const int c = popcnt(o) <= 32 ? popcnt(o) : 0;
+  for (int k = 0; k < c; ++k) {
+    const int s = pop_lsb(o), pc = piece_nibble(wlo, whi, k);
+    if (pc == make_piece(WHITE, KING)) wk = s;
+    if (pc == make_piece(BLACK, KING)) bk = s;
+  }
+  keys[i] = (uint16_t)(wk < 64 && bk < 64 ? (wk << 6 | bk) : 0xFFFF);
+  idx[i] = (uint32_t)i;
+}
+
 __global__ void offsets_u32_kernel(const uint64_t *__restrict__ in, size_t n, uint32_t *__restrict__ out) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) out[i] = (uint32_t)in[i];
@@ -732,6 +757,25 @@ hipError_t launch_offsets_u32(const uint64_t *in, size_t n, uint32_t *out, hipSt
   return hipGetLastError();
 }
 
+hipError_t king_sort(const gn_board *boards, size_t n, uint16_t *keys, uint32_t *idx, uint16_t *keys_out,
+                     uint32_t *perm, void *&temp, size_t &temp_bytes, hipStream_t s) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(king_keys_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, boards, n, keys, idx);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  size_t need = 0;
+  e = hipcub::DeviceRadixSort::SortPairs(nullptr, need, keys, keys_out, idx, perm, (int)n, 0, 16, s);
+  if (e != hipSuccess) return e;
+  if (need > temp_bytes) {
+    if (temp) (void)hipFree(temp);
+    temp = nullptr;
+    temp_bytes = 0;
+    if ((e = hipMalloc(&temp, need)) != hipSuccess) return e;
+    temp_bytes = need;
+  }
+  return hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, keys, keys_out, idx, perm, (int)n, 0, 16, s);
+}
+
 hipError_t exclusive_scan_u64(const uint64_t *counts, uint64_t *offsets, size_t n1, void *&temp, size_t &temp_bytes,
                               hipStream_t s) {
   size_t need = 0;
@@ -745,6 +789,25 @@ hipError_t exclusive_scan_u64(const uint64_t *counts, uint64_t *offsets, size_t 
     temp_bytes = need;
   }
   return hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, counts, offsets, n1, s);
+}
+
+hipError_t launch_expand_net(const NetDevice &net, const gn_board *parents, size_t n, const uint64_t *offsets,
+                             const gn_board *children, const ChildDelta *deltas, const uint8_t *need_parent,
+                             const uint8_t *need_child, int2 *out_parent, int2 *out_child, int swz, hipStream_t s) {
+  if (!n) return hipSuccess;
+  const unsigned g = (unsigned)(swz ? 8 * ((n + 7) / 8) : n);
+#define GN_EXPAND_ARGS net, parents, offsets, children, deltas, need_parent, need_child, out_parent, out_child, n, swz
+  if (net.L1 == 3072) {
+    hipLaunchKernelGGL((expand_eval_kernel<3072, 1>), dim3(g), dim3(384), 0, s, GN_EXPAND_ARGS);
+  } else if (net.L1 == 128) {
+    hipLaunchKernelGGL((expand_eval_kernel<128, 16>), dim3(g), dim3(256), 0, s, GN_EXPAND_ARGS);
+  } else if (net.L1 == 1024) {
+    hipLaunchKernelGGL((expand_eval_kernel<1024, 1>), dim3(g), dim3(128), 0, s, GN_EXPAND_ARGS);
+  } else {
+    return hipErrorInvalidValue;
+  }
+#undef GN_EXPAND_ARGS
+  return hipGetLastError();
 }
 
 } // namespace gn

@@ -35,7 +35,7 @@ EXPORTS = ["gn_load_net", "gn_load_net_memory", "gn_free", "gn_last_error", "gn_
            "gn_device_alloc", "gn_device_free", "gn_memcpy_h2d", "gn_memcpy_d2h", "gn_synchronize",
            "gn_time_evaluate_device", "gn_random_positions_device", "gn_set_option", "gn_get_option",
            "gn_time_expand_device", "gn_random_games_device"]
-OPT_INCREMENTAL_CHILDREN = 1
+OPT_INCREMENTAL_CHILDREN, OPT_XCD_SWIZZLE, OPT_KING_SORT = 1, 2, 3
 EXPAND_STAGES = ["count_scan", "total_readback", "write_children", "classify", "small_net", "big_net", "finalize"]
 
 

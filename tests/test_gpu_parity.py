@@ -205,3 +205,33 @@ def test_device_playouts_equal_host_playouts(gpu_ctx):
     gpu_ctx.random_positions_device(0x5EED0000, 12345, 500, 160, d)
     gpu_ctx.synchronize()
     assert d.download(G.BOARD_DTYPE, 500).tobytes() == host.tobytes()
+
+
+@pytest.mark.parametrize("swz,ksort", [(0, 0), (1, 0), (0, 1), (1, 1)])
+def test_locality_options_do_not_change_results(gpu_ctx, swz, ksort):
+    from fishnet_amd import gpu_nnue as G
+    boards = G.random_positions(3, 0, 5003, 160)
+    boards[17] = np.zeros(1, dtype=G.BOARD_DTYPE)  # an invalid board mixed in
+    d_b, d_o = gpu_ctx.alloc(boards.nbytes), gpu_ctx.alloc(len(boards) * 16)
+    d_b.upload(boards)
+    ref = {}
+    for mode in (0, 1, 2):
+        gpu_ctx.set_option(G.OPT_XCD_SWIZZLE, 0)
+        gpu_ctx.set_option(G.OPT_KING_SORT, 0)
+        gpu_ctx.evaluate_device(d_b, len(boards), mode, d_o)
+        ref[mode] = d_o.download(G.EVAL_DTYPE, len(boards))
+    try:
+        gpu_ctx.set_option(G.OPT_XCD_SWIZZLE, swz)
+        gpu_ctx.set_option(G.OPT_KING_SORT, ksort)
+        for mode in (0, 1, 2):
+            gpu_ctx.evaluate_device(d_b, len(boards), mode, d_o)
+            assert np.array_equal(d_o.download(G.EVAL_DTYPE, len(boards)), ref[mode])
+        assert ref[0][17]["flags"] & G.FLAG_BAD_FEN
+        fens = [G.board_to_fen(b) for b in boards[:200] if b["occ"]]
+        _, offs, moves, kids = gpu_ctx.expand_and_evaluate(fens, 1)
+        gpu_ctx.set_option(G.OPT_XCD_SWIZZLE, 1 - swz)
+        _, offs2, moves2, kids2 = gpu_ctx.expand_and_evaluate(fens, 1)
+        assert np.array_equal(kids, kids2) and np.array_equal(moves, moves2)
+    finally:
+        gpu_ctx.set_option(G.OPT_XCD_SWIZZLE, 1)
+        gpu_ctx.set_option(G.OPT_KING_SORT, 0)
