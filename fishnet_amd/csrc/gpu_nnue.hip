@@ -209,8 +209,8 @@ struct gn_ctx {
   std::vector<std::unique_ptr<Dev>> devs;
   gn_eval_params P;
   bool incremental = true; // GN_OPT_INCREMENTAL_CHILDREN
-  bool swizzle = true;      // GN_OPT_XCD_SWIZZLE
-  bool king_sort = false;   // GN_OPT_KING_SORT
+  int swizzle = 1;          // GN_OPT_XCD_SWIZZLE bit mask: 1 expansion, 2 batch evaluation
+  bool king_sort = true;    // GN_OPT_KING_SORT
   int l1[2] = {0, 0};
   uint32_t hash[2] = {0, 0};
 };
@@ -377,7 +377,7 @@ static int evaluate_on(gn_ctx *ctx, Dev &d, const gn_board *b, size_t n, int mod
     HIP_TRY(king_sort(b, n, d.kkeys.p, d.kidx.p, d.kkeys2.p, d.kperm.p, d.sort_tmp, d.sort_bytes, s));
     perm = d.kperm.p;
   }
-  const int swz = ctx->swizzle;
+  const int swz = (ctx->swizzle >> 1) & 1;
   HIP_TRY(mark(1));
   if (mode != GN_MODE_BIG)
     HIP_TRY(launch_eval_net(d.net[SMALL], b, mode == GN_MODE_FULL ? d.nsm.p : nullptr, n, d.osm.p, perm, swz, s));
@@ -490,7 +490,7 @@ static int expand_evaluate(gn_ctx *ctx, Dev &d, const gn_board *parents, size_t 
   if (mode != GN_MODE_BIG) {
     const bool f = mode == GN_MODE_FULL;
     HIP_TRY(launch_expand_net(d.net[SMALL], parents, n, off, children, dl, f ? d.p_nsm.p : nullptr,
-                              f ? d.nsm.p : nullptr, d.p_osm.p, d.osm.p, ctx->swizzle, s));
+                              f ? d.nsm.p : nullptr, d.p_osm.p, d.osm.p, ctx->swizzle & 1, s));
     if (f) {
       HIP_TRY(launch_reeval(d.p_osm.p, d.p_nsm.p, n, P, d.p_nbg.p, s));
       HIP_TRY(launch_reeval(d.osm.p, d.nsm.p, total, P, d.nbg.p, s));
@@ -500,7 +500,7 @@ static int expand_evaluate(gn_ctx *ctx, Dev &d, const gn_board *parents, size_t 
   if (mode != GN_MODE_SMALL) {
     const bool f = mode == GN_MODE_FULL;
     HIP_TRY(launch_expand_net(d.net[BIG], parents, n, off, children, dl, f ? d.p_nbg.p : nullptr,
-                              f ? d.nbg.p : nullptr, d.p_obg.p, d.obg.p, ctx->swizzle, s));
+                              f ? d.nbg.p : nullptr, d.p_obg.p, d.obg.p, ctx->swizzle & 1, s));
   }
   HIP_TRY(mark(2));
   HIP_TRY(launch_finalize(children, total, mode, d.osm.p, d.obg.p, d.nsm.p, d.nbg.p, P, d.tables, child_out, s));
@@ -871,7 +871,7 @@ int gn_set_option(gn_ctx *ctx, int option, int64_t value) {
     ctx->incremental = value != 0;
     return GN_OK;
   case GN_OPT_XCD_SWIZZLE:
-    ctx->swizzle = value != 0;
+    ctx->swizzle = (int)(value & 3);
     return GN_OK;
   case GN_OPT_KING_SORT:
     ctx->king_sort = value != 0;

@@ -1,0 +1,92 @@
+"""Multi-GPU plumbing for the evaluator: one process per GPU, positions sharded
+by rank, RCCL (torch.distributed backend "nccl") used only to broadcast the
+.nnue images and to gather per-rank results.  The same code runs
+on CPU with the "gloo" backend (tests/test_dist.py)."""
+from __future__ import annotations
+
+import os
+
+
+class ShardComm:
+    def __init__(self, backend: str | None = None):
+        import torch
+        import torch.distributed as dist
+        self.torch, self.dist = torch, dist
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.backend = backend or ("nccl" if torch.cuda.is_available() else "gloo")
+        self.device = torch.device("cuda", self.local) if self.backend == "nccl" else torch.device("cpu")
+        if self.backend == "nccl":
+            torch.cuda.set_device(self.local)
+        if self.world > 1 and not dist.is_initialized():
+            kw = {"device_id": self.device} if self.backend == "nccl" else {}
+            dist.init_process_group(self.backend, **kw)
+
+    # ---- sharding: contiguous, game-aligned ranges (weak scaling) ----------
+    def shard(self, per_rank: int) -> tuple[int, int]:
+        """[first, first + per_rank) of the global index space owned by this rank."""
+        return self.rank * per_rank, per_rank
+
+    # ---- collectives ---------------------------------------------------------
+    def broadcast_bytes(self, data: bytes, src: int = 0) -> bytes:
+        if self.world == 1:
+            return data
+        torch, dist = self.torch, self.dist
+        ln = torch.tensor([len(data)], dtype=torch.int64, device=self.device)
+        dist.broadcast(ln, src)
+        if self.rank == src:
+            t = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(self.device)
+        else:
+            t = torch.empty(int(ln.item()), dtype=torch.uint8, device=self.device)
+        dist.broadcast(t, src)
+        return t.cpu().numpy().tobytes()
+
+    def broadcast_obj(self, obj, src: int = 0):
+        if self.world == 1:
+            return obj
+        lst = [obj]
+        self.dist.broadcast_object_list(lst, src)
+        return lst[0]
+
+    def barrier(self):
+        if self.world > 1:
+            self.dist.barrier()
+
+    def max(self, x: float) -> float:
+        if self.world == 1:
+            return x
+        t = self.torch.tensor([x], dtype=self.torch.float64, device=self.device)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def gather_i64(self, x: int) -> list[int]:
+        if self.world == 1:
+            return [x]
+        t = self.torch.tensor([x & 0x7FFFFFFFFFFFFFFF], dtype=self.torch.int64, device=self.device)
+        lst = [self.torch.zeros_like(t) for _ in range(self.world)]
+        self.dist.all_gather(lst, t)
+        return [int(v.item()) for v in lst]
+
+    def gather_array(self, arr, dst: int = 0):
+        """Gathers equally sized numpy arrays (e.g. gn_eval records) to dst."""
+        import numpy as np
+        if self.world == 1:
+            return [arr]
+        torch, dist = self.torch, self.dist
+        raw = torch.frombuffer(bytearray(np.ascontiguousarray(arr).tobytes()), dtype=torch.uint8).to(self.device)
+        outs = [torch.empty_like(raw) for _ in range(self.world)] if self.rank == dst else None
+        if self.backend == "nccl":
+            lst = [torch.empty_like(raw) for _ in range(self.world)]
+            dist.all_gather(lst, raw)
+            outs = lst if self.rank == dst else None
+        else:
+            dist.gather(raw, outs, dst=dst)
+        if self.rank != dst:
+            return None
+        return [np.frombuffer(o.cpu().numpy().tobytes(), dtype=arr.dtype) for o in outs]
+
+    def close(self):
+        if self.world > 1 and self.dist.is_initialized():
+            self.dist.barrier()
+            self.dist.destroy_process_group()

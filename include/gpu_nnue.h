@@ -57,11 +57,12 @@ extern "C" {
 /* options (gn_set_option / gn_get_option) */
 #define GN_OPT_INCREMENTAL_CHILDREN 1 /* 1 (default): children from the parent accumulators
                                          by add/sub deltas; 0: full refresh per child    */
-#define GN_OPT_XCD_SWIZZLE 2          /* 1 (default): each XCD takes a contiguous range of
-                                         tiles / parents (L2 locality); 0: dispatch order */
-#define GN_OPT_KING_SORT 3            /* 1: evaluate a batch in (white king, black king)
-                                         square order (L2 locality), results in input
-                                         order; 0 (default): input order                 */
+#define GN_OPT_XCD_SWIZZLE 2          /* bit mask, default 1: each XCD takes a contiguous
+                                         range of parents (bit 0, expansion) / of 16-position
+                                         tiles (bit 1, batch evaluation); 0: dispatch order */
+#define GN_OPT_KING_SORT 3            /* 1 (default): evaluate a batch in (white king, black
+                                         king) square order for L2 / Infinity-Cache
+                                         locality, results in input order; 0: input order */
 
 /* per-position flags */
 #define GN_FLAG_IN_CHECK 1u /* side to move in check: Stockfish has no static eval
