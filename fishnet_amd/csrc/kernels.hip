@@ -223,11 +223,22 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR)
         lo += (a0 + a1) + (a2 + a3);
         hi += (b0 + b1) + (b2 + b3);
       }
-      for (; k < cnt; ++k) {
-        const uint32_t o0 = rr[k] * RS;
-        lo += *reinterpret_cast<const ushort8 *>(ftj + o0);
-        hi += *reinterpret_cast<const ushort8 *>(ftj + o0 + L1);
-        if (j == 0) ps += (uint32_t)(*reinterpret_cast<const int4v *>(net.ft + o0 + pso))[pse];
+      if (k < cnt) { // tail of 1-3 rows as one batch (no serialized round trips)
+        const int k1 = k + 1 < cnt ? k + 1 : k, k2 = k + 2 < cnt ? k + 2 : k;
+        const uint32_t o0 = rr[k] * RS, o1 = rr[k1] * RS, o2 = rr[k2] * RS;
+        const ushort8 a0 = *reinterpret_cast<const ushort8 *>(ftj + o0), a1 = *reinterpret_cast<const ushort8 *>(ftj + o1);
+        const ushort8 a2 = *reinterpret_cast<const ushort8 *>(ftj + o2);
+        const ushort8 b0 = *reinterpret_cast<const ushort8 *>(ftj + o0 + L1), b1 = *reinterpret_cast<const ushort8 *>(ftj + o1 + L1);
+        const ushort8 b2 = *reinterpret_cast<const ushort8 *>(ftj + o2 + L1);
+        uint32_t q0 = 0, q1 = 0, q2 = 0;
+        if (j == 0) {
+          q0 = (uint32_t)(*reinterpret_cast<const int4v *>(net.ft + o0 + pso))[pse];
+          q1 = (uint32_t)(*reinterpret_cast<const int4v *>(net.ft + o1 + pso))[pse];
+          q2 = (uint32_t)(*reinterpret_cast<const int4v *>(net.ft + o2 + pso))[pse];
+        }
+        lo += a0, hi += b0, ps += q0;
+        if (k + 1 < cnt) lo += a1, hi += b1, ps += q1;
+        if (k + 2 < cnt) lo += a2, hi += b2, ps += q2;
       }
       // transform: clamp to [0, 254] in the doubled domain, product / 512
       uint32_t w0 = 0, w1 = 0;
@@ -339,11 +350,21 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR)
       pacc_lo += (a0 + a1) + (a2 + a3);
       pacc_hi += (b0 + b1) + (b2 + b3);
     }
-    for (; k < cnt; ++k) {
-      const uint32_t o0 = prow[h][k] * RS;
-      pacc_lo += *reinterpret_cast<const ushort8 *>(ftj + o0);
-      pacc_hi += *reinterpret_cast<const ushort8 *>(ftj + o0 + L1);
-      if (j < 2) pps += *reinterpret_cast<const int4v *>(net.ft + o0 + pso);
+    if (k < cnt) { // tail of 1-3 rows as one batch
+      const int k1 = k + 1 < cnt ? k + 1 : k, k2 = k + 2 < cnt ? k + 2 : k;
+      const uint32_t o0 = prow[h][k] * RS, o1 = prow[h][k1] * RS, o2 = prow[h][k2] * RS;
+      const ushort8 a0 = *reinterpret_cast<const ushort8 *>(ftj + o0), a1 = *reinterpret_cast<const ushort8 *>(ftj + o1);
+      const ushort8 a2 = *reinterpret_cast<const ushort8 *>(ftj + o2);
+      const ushort8 b0 = *reinterpret_cast<const ushort8 *>(ftj + o0 + L1), b1 = *reinterpret_cast<const ushort8 *>(ftj + o1 + L1);
+      const ushort8 b2 = *reinterpret_cast<const ushort8 *>(ftj + o2 + L1);
+      int4v p0 = zero4, p1 = zero4, p2 = zero4;
+      if (j < 2) {
+        p0 = *reinterpret_cast<const int4v *>(net.ft + o0 + pso), p1 = *reinterpret_cast<const int4v *>(net.ft + o1 + pso);
+        p2 = *reinterpret_cast<const int4v *>(net.ft + o2 + pso);
+      }
+      pacc_lo += a0, pacc_hi += b0, pps += p0;
+      if (k + 1 < cnt) pacc_lo += a1, pacc_hi += b1, pps += p1;
+      if (k + 2 < cnt) pacc_lo += a2, pacc_hi += b2, pps += p2;
     }
     if (PAR > 1) {
       *reinterpret_cast<ushort8 *>(pacc_lds + h * L1 + 8 * j) = pacc_lo;
@@ -409,33 +430,45 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR)
       ushort8 lo = fromp ? pacc_lo : bias_lo, hi = fromp ? pacc_hi : bias_hi;
       int4v ps = fromp ? pps : zero4;
       const uint16_t *rr = rows[sl][h];
-      const int ns = nsub[sl][h], na = nadd[sl][h];
-      int k = 0;
-      for (; k < ns; ++k) {
-        const uint32_t o0 = rr[k] * RS;
-        lo -= *reinterpret_cast<const ushort8 *>(ftj + o0);
-        hi -= *reinterpret_cast<const ushort8 *>(ftj + o0 + L1);
-        if (j < 2) ps -= *reinterpret_cast<const int4v *>(net.ft + o0 + pso);
-      }
-      const int end = ns + na;
-      for (; k + 4 <= end; k += 4) {
-        const uint32_t o0 = rr[k] * RS, o1 = rr[k + 1] * RS, o2 = rr[k + 2] * RS, o3 = rr[k + 3] * RS;
+      const int ns = nsub[sl][h], end = ns + nadd[sl][h];
+      if (fromp) {
+        // delta child: <= 2 removed + <= 2 added rows, all four loads in flight at once
+        const uint32_t o0 = rr[0] * RS, o1 = rr[end > 1 ? 1 : 0] * RS;
+        const uint32_t o2 = rr[end > 2 ? 2 : 0] * RS, o3 = rr[end > 3 ? 3 : 0] * RS;
         const ushort8 a0 = *reinterpret_cast<const ushort8 *>(ftj + o0), a1 = *reinterpret_cast<const ushort8 *>(ftj + o1);
         const ushort8 a2 = *reinterpret_cast<const ushort8 *>(ftj + o2), a3 = *reinterpret_cast<const ushort8 *>(ftj + o3);
         const ushort8 b0 = *reinterpret_cast<const ushort8 *>(ftj + o0 + L1), b1 = *reinterpret_cast<const ushort8 *>(ftj + o1 + L1);
         const ushort8 b2 = *reinterpret_cast<const ushort8 *>(ftj + o2 + L1), b3 = *reinterpret_cast<const ushort8 *>(ftj + o3 + L1);
+        int4v p0 = zero4, p1 = zero4, p2 = zero4, p3 = zero4;
         if (j < 2) {
-          ps += *reinterpret_cast<const int4v *>(net.ft + o0 + pso) + *reinterpret_cast<const int4v *>(net.ft + o1 + pso);
-          ps += *reinterpret_cast<const int4v *>(net.ft + o2 + pso) + *reinterpret_cast<const int4v *>(net.ft + o3 + pso);
+          p0 = *reinterpret_cast<const int4v *>(net.ft + o0 + pso), p1 = *reinterpret_cast<const int4v *>(net.ft + o1 + pso);
+          p2 = *reinterpret_cast<const int4v *>(net.ft + o2 + pso), p3 = *reinterpret_cast<const int4v *>(net.ft + o3 + pso);
         }
-        lo += (a0 + a1) + (a2 + a3);
-        hi += (b0 + b1) + (b2 + b3);
-      }
-      for (; k < end; ++k) {
-        const uint32_t o0 = rr[k] * RS;
-        lo += *reinterpret_cast<const ushort8 *>(ftj + o0);
-        hi += *reinterpret_cast<const ushort8 *>(ftj + o0 + L1);
-        if (j < 2) ps += *reinterpret_cast<const int4v *>(net.ft + o0 + pso);
+        // entry e: subtract if e < ns, add if ns <= e < end, skip otherwise
+        lo = ns > 0 ? lo - a0 : lo + a0, hi = ns > 0 ? hi - b0 : hi + b0, ps = ns > 0 ? ps - p0 : ps + p0;
+        if (end > 1) lo = ns > 1 ? lo - a1 : lo + a1, hi = ns > 1 ? hi - b1 : hi + b1, ps = ns > 1 ? ps - p1 : ps + p1;
+        if (end > 2) lo = ns > 2 ? lo - a2 : lo + a2, hi = ns > 2 ? hi - b2 : hi + b2, ps = ns > 2 ? ps - p2 : ps + p2;
+        if (end > 3) lo += a3, hi += b3, ps += p3;
+      } else {
+        // refresh (own king moved) or parent slot: adds only, 4 rows in flight
+        int k = 0;
+        for (; k < end; k += 4) {
+          const int k1 = k + 1 < end ? k + 1 : k, k2 = k + 2 < end ? k + 2 : k, k3 = k + 3 < end ? k + 3 : k;
+          const uint32_t o0 = rr[k] * RS, o1 = rr[k1] * RS, o2 = rr[k2] * RS, o3 = rr[k3] * RS;
+          const ushort8 a0 = *reinterpret_cast<const ushort8 *>(ftj + o0), a1 = *reinterpret_cast<const ushort8 *>(ftj + o1);
+          const ushort8 a2 = *reinterpret_cast<const ushort8 *>(ftj + o2), a3 = *reinterpret_cast<const ushort8 *>(ftj + o3);
+          const ushort8 b0 = *reinterpret_cast<const ushort8 *>(ftj + o0 + L1), b1 = *reinterpret_cast<const ushort8 *>(ftj + o1 + L1);
+          const ushort8 b2 = *reinterpret_cast<const ushort8 *>(ftj + o2 + L1), b3 = *reinterpret_cast<const ushort8 *>(ftj + o3 + L1);
+          int4v p0 = zero4, p1 = zero4, p2 = zero4, p3 = zero4;
+          if (j < 2) {
+            p0 = *reinterpret_cast<const int4v *>(net.ft + o0 + pso), p1 = *reinterpret_cast<const int4v *>(net.ft + o1 + pso);
+            p2 = *reinterpret_cast<const int4v *>(net.ft + o2 + pso), p3 = *reinterpret_cast<const int4v *>(net.ft + o3 + pso);
+          }
+          lo += a0, hi += b0, ps += p0;
+          if (k + 1 < end) lo += a1, hi += b1, ps += p1;
+          if (k + 2 < end) lo += a2, hi += b2, ps += p2;
+          if (k + 3 < end) lo += a3, hi += b3, ps += p3;
+        }
       }
       const int side = h == sstm[sl] ? 0 : 1;
       uint32_t w0 = 0, w1 = 0;
