@@ -20,6 +20,10 @@ typedef int int4v __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ int32_t wmul(int32_t a, int32_t b) { return (int32_t)((uint32_t)a * (uint32_t)b); }
 __device__ __forceinline__ int32_t wadd(int32_t a, int32_t b) { return (int32_t)((uint32_t)a + (uint32_t)b); }
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : v > hi ? hi : v; }
+// feature row index as gathered: clamped into the table so that no stale or
+// corrupt index can ever address outside the weights (indices built by this
+// library are always < FT_INPUTS; the clamp is a single v_min per row)
+__device__ __forceinline__ uint32_t ft_row(uint32_t idx) { return idx < FT_INPUTS ? idx : FT_INPUTS - 1; }
 
 __device__ __forceinline__ void load_tables(Tables &dst, const Tables *src) {
   const uint4 *s = reinterpret_cast<const uint4 *>(src);
@@ -204,7 +208,7 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR)
       const uint16_t *rr = rows[p][h];
       int k = 0;
       for (; k + 4 <= cnt; k += 4) {
-        const uint32_t o0 = rr[k] * RS, o1 = rr[k + 1] * RS, o2 = rr[k + 2] * RS, o3 = rr[k + 3] * RS;
+        const uint32_t o0 = ft_row(rr[k]) * RS, o1 = ft_row(rr[k + 1]) * RS, o2 = ft_row(rr[k + 2]) * RS, o3 = ft_row(rr[k + 3]) * RS;
         const ushort8 a0 = *reinterpret_cast<const ushort8 *>(ftj + o0);
         const ushort8 a1 = *reinterpret_cast<const ushort8 *>(ftj + o1);
         const ushort8 a2 = *reinterpret_cast<const ushort8 *>(ftj + o2);
@@ -225,7 +229,7 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR)
       }
       if (k < cnt) { // tail of 1-3 rows as one batch (no serialized round trips)
         const int k1 = k + 1 < cnt ? k + 1 : k, k2 = k + 2 < cnt ? k + 2 : k;
-        const uint32_t o0 = rr[k] * RS, o1 = rr[k1] * RS, o2 = rr[k2] * RS;
+        const uint32_t o0 = ft_row(rr[k]) * RS, o1 = ft_row(rr[k1]) * RS, o2 = ft_row(rr[k2]) * RS;
         const ushort8 a0 = *reinterpret_cast<const ushort8 *>(ftj + o0), a1 = *reinterpret_cast<const ushort8 *>(ftj + o1);
         const ushort8 a2 = *reinterpret_cast<const ushort8 *>(ftj + o2);
         const ushort8 b0 = *reinterpret_cast<const ushort8 *>(ftj + o0 + L1), b1 = *reinterpret_cast<const ushort8 *>(ftj + o1 + L1);
@@ -338,7 +342,7 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR)
     const int cnt = pcount;
     int k = 0;
     for (; k + 4 <= cnt; k += 4) {
-      const uint32_t o0 = prow[h][k] * RS, o1 = prow[h][k + 1] * RS, o2 = prow[h][k + 2] * RS, o3 = prow[h][k + 3] * RS;
+      const uint32_t o0 = ft_row(prow[h][k]) * RS, o1 = ft_row(prow[h][k + 1]) * RS, o2 = ft_row(prow[h][k + 2]) * RS, o3 = ft_row(prow[h][k + 3]) * RS;
       const ushort8 a0 = *reinterpret_cast<const ushort8 *>(ftj + o0), a1 = *reinterpret_cast<const ushort8 *>(ftj + o1);
       const ushort8 a2 = *reinterpret_cast<const ushort8 *>(ftj + o2), a3 = *reinterpret_cast<const ushort8 *>(ftj + o3);
       const ushort8 b0 = *reinterpret_cast<const ushort8 *>(ftj + o0 + L1), b1 = *reinterpret_cast<const ushort8 *>(ftj + o1 + L1);
@@ -352,7 +356,7 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR)
     }
     if (k < cnt) { // tail of 1-3 rows as one batch
       const int k1 = k + 1 < cnt ? k + 1 : k, k2 = k + 2 < cnt ? k + 2 : k;
-      const uint32_t o0 = prow[h][k] * RS, o1 = prow[h][k1] * RS, o2 = prow[h][k2] * RS;
+      const uint32_t o0 = ft_row(prow[h][k]) * RS, o1 = ft_row(prow[h][k1]) * RS, o2 = ft_row(prow[h][k2]) * RS;
       const ushort8 a0 = *reinterpret_cast<const ushort8 *>(ftj + o0), a1 = *reinterpret_cast<const ushort8 *>(ftj + o1);
       const ushort8 a2 = *reinterpret_cast<const ushort8 *>(ftj + o2);
       const ushort8 b0 = *reinterpret_cast<const ushort8 *>(ftj + o0 + L1), b1 = *reinterpret_cast<const ushort8 *>(ftj + o1 + L1);
@@ -431,10 +435,10 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR)
       int4v ps = fromp ? pps : zero4;
       const uint16_t *rr = rows[sl][h];
       const int ns = nsub[sl][h], end = ns + nadd[sl][h];
-      if (fromp) {
+      if (fromp && end > 0) {
         // delta child: <= 2 removed + <= 2 added rows, all four loads in flight at once
-        const uint32_t o0 = rr[0] * RS, o1 = rr[end > 1 ? 1 : 0] * RS;
-        const uint32_t o2 = rr[end > 2 ? 2 : 0] * RS, o3 = rr[end > 3 ? 3 : 0] * RS;
+        const uint32_t o0 = ft_row(rr[0]) * RS, o1 = ft_row(rr[end > 1 ? 1 : 0]) * RS;
+        const uint32_t o2 = ft_row(rr[end > 2 ? 2 : 0]) * RS, o3 = ft_row(rr[end > 3 ? 3 : 0]) * RS;
         const ushort8 a0 = *reinterpret_cast<const ushort8 *>(ftj + o0), a1 = *reinterpret_cast<const ushort8 *>(ftj + o1);
         const ushort8 a2 = *reinterpret_cast<const ushort8 *>(ftj + o2), a3 = *reinterpret_cast<const ushort8 *>(ftj + o3);
         const ushort8 b0 = *reinterpret_cast<const ushort8 *>(ftj + o0 + L1), b1 = *reinterpret_cast<const ushort8 *>(ftj + o1 + L1);
@@ -449,12 +453,12 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR)
         if (end > 1) lo = ns > 1 ? lo - a1 : lo + a1, hi = ns > 1 ? hi - b1 : hi + b1, ps = ns > 1 ? ps - p1 : ps + p1;
         if (end > 2) lo = ns > 2 ? lo - a2 : lo + a2, hi = ns > 2 ? hi - b2 : hi + b2, ps = ns > 2 ? ps - p2 : ps + p2;
         if (end > 3) lo += a3, hi += b3, ps += p3;
-      } else {
-        // refresh (own king moved) or parent slot: adds only, 4 rows in flight
+      } else if (!fromp) {
+        // refresh (own king moved): adds only, 4 rows in flight
         int k = 0;
         for (; k < end; k += 4) {
           const int k1 = k + 1 < end ? k + 1 : k, k2 = k + 2 < end ? k + 2 : k, k3 = k + 3 < end ? k + 3 : k;
-          const uint32_t o0 = rr[k] * RS, o1 = rr[k1] * RS, o2 = rr[k2] * RS, o3 = rr[k3] * RS;
+          const uint32_t o0 = ft_row(rr[k]) * RS, o1 = ft_row(rr[k1]) * RS, o2 = ft_row(rr[k2]) * RS, o3 = ft_row(rr[k3]) * RS;
           const ushort8 a0 = *reinterpret_cast<const ushort8 *>(ftj + o0), a1 = *reinterpret_cast<const ushort8 *>(ftj + o1);
           const ushort8 a2 = *reinterpret_cast<const ushort8 *>(ftj + o2), a3 = *reinterpret_cast<const ushort8 *>(ftj + o3);
           const ushort8 b0 = *reinterpret_cast<const ushort8 *>(ftj + o0 + L1), b1 = *reinterpret_cast<const ushort8 *>(ftj + o1 + L1);
