@@ -34,63 +34,82 @@ __device__ __forceinline__ void load_tables(Tables &dst, const Tables *src) {
 
 // ------------------------------------------------------------ layer stack --
 // NetworkArchitecture::propagate for a 16-position tile held in LDS as
-// transformed features xt[16][L1 + 16] (u8), one wave per distinct bucket:
-//   fc_0  [16 x L1] . [L1 x 16]  -> int8 MFMA 16x16x64, K = L1 / 64 steps
-//   SqrClippedReLU / ClippedReLU -> in1[16][32] (LDS, per wave)
-//   fc_1  [16 x 32] . [32 x 32]  -> two int8 MFMAs (K padded to 64 with zeros)
-//   fc_2  32 -> 1 by a 16-lane shuffle reduction, + skip term from fc_0[15]
+// transformed features xt[16][L1 + 16] (u8).  Per distinct bucket b in the
+// tile (sequentially, all waves together):
+//   fc_0  [16 x L1] . [L1 x 16]: the L1/64 k-steps of int8 MFMA 16x16x64 are
+//         split across the NW waves (all weight loads of a wave in flight at
+//         once); partial 16x16 int32 tiles are summed with LDS integer atomics
+//         (exact and order-independent);
+//   wave 0: SqrClippedReLU / ClippedReLU -> in1[16][32], fc_1 [16 x 32] .
+//         [32 x 32] as two MFMAs (K zero-padded to 64), fc_2 by a 16-lane
+//         shuffle reduction, + the skip term from fc_0[15].
 // Lane layout of v_mfma_i32_16x16x64_i8: lane l holds A[row l&15][16(l>>4)..+16],
 // B[16(l>>4)..+16][col l&15]; C[4(l>>4)+i][l&15] in acc[i].  The K grouping
 // inside a lane is irrelevant to the result as long as A and B use the same.
-// valid(pos, b): slot pos holds a position of bucket b; emit(pos, {psqt/16, positional/16}).
+// ls: LDS scratch of LS_SCRATCH bytes.  valid(pos, b): slot pos holds a
+// position of bucket b; emit(pos, {psqt/16, positional/16}).
+constexpr int LS_SCRATCH = 16 * 16 * 4 + 16 * 32 + 16 * 4; // acc + in1 + fwd = 1600 B
+
 template <int L1, int NW, class Valid, class Emit>
-__device__ __forceinline__ void layer_stack_tile(const NetDevice &net, const uint8_t *xt, uint8_t (*in1)[16][32],
-                                                 int32_t (*fwd)[16], const int32_t (*psq)[2], const int *bkt,
-                                                 uint32_t bm, Valid &&valid, Emit &&emit) {
-  constexpr int XS = L1 + 16;
+__device__ __forceinline__ void layer_stack_tile(const NetDevice &net, const uint8_t *xt, uint8_t *ls,
+                                                 const int32_t (*psq)[2], const int *bkt, uint32_t bm,
+                                                 Valid &&valid, Emit &&emit) {
+  constexpr int XS = L1 + 16, KS = L1 / 64;
+  int32_t *acc0 = reinterpret_cast<int32_t *>(ls);                 // [16 pos][16 out]
+  uint8_t(*in1)[32] = reinterpret_cast<uint8_t(*)[32]>(ls + 1024); // [16][32]
+  int32_t *fwd = reinterpret_cast<int32_t *>(ls + 1536);           // [16]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int nb = popcnt(bm);
   const int row = lane & 15, kg = lane >> 4;
-  for (int round = 0; round * NW < nb; ++round) {
-    const int slot = round * NW + wave;
-    int b = -1;
-    if (slot < nb) {
-      uint32_t m = bm;
-      for (int t = 0; t < slot; ++t) m &= m - 1;
-      b = __builtin_ctz(m);
-    }
-    if (b >= 0) {
+  uint32_t m = bm;
+  while (m) {
+    const int b = __builtin_ctz(m);
+    m &= m - 1;
+    for (int i = tid; i < 256; i += NW * 64) acc0[i] = 0;
+    __syncthreads();
+    {
       int4v acc = {0, 0, 0, 0};
       const uint8_t *xa = xt + row * XS + kg * 16;
       const int8_t *wb = net.w0 + ((size_t)b * 16 + row) * L1 + kg * 16;
-#pragma unroll 4
-      for (int ks = 0; ks < L1; ks += 64) {
-        const int4v a = *reinterpret_cast<const int4v *>(xa + ks);
-        const int4v w = *reinterpret_cast<const int4v *>(wb + ks);
-        acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, w, acc, 0, 0, 0);
+      bool any = false;
+#pragma unroll
+      for (int t = 0; t < (KS + NW - 1) / NW; ++t) {
+        const int ks = wave + t * NW;
+        if (ks < KS) {
+          const int4v a = *reinterpret_cast<const int4v *>(xa + 64 * ks);
+          const int4v w = *reinterpret_cast<const int4v *>(wb + 64 * ks);
+          acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, w, acc, 0, 0, 0);
+          any = true;
+        }
       }
+      if (any) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) atomicAdd(&acc0[(4 * kg + i) * 16 + row], acc[i]);
+      }
+    }
+    __syncthreads();
+    if (wave == 0) {
       const int32_t bias0 = net.b0[b * 16 + row];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int pos = 4 * kg + i;
-        const int32_t v = wadd(acc[i], bias0);
+        const int32_t v = wadd(acc0[pos * 16 + row], bias0);
         if (row < 15) {
           const long long s2 = ((long long)v * v) >> 19;
-          in1[wave][pos][row] = (uint8_t)(s2 < 127 ? s2 : 127);
-          in1[wave][pos][15 + row] = (uint8_t)clampi(v >> 6, 0, 127);
+          in1[pos][row] = (uint8_t)(s2 < 127 ? s2 : 127);
+          in1[pos][15 + row] = (uint8_t)clampi(v >> 6, 0, 127);
         } else {
-          fwd[wave][pos] = wmul(v, 600 * 16) / (127 * 64);
-          in1[wave][pos][30] = 0;
-          in1[wave][pos][31] = 0;
+          fwd[pos] = wmul(v, 600 * 16) / (127 * 64);
+          in1[pos][30] = 0;
+          in1[pos][31] = 0;
         }
       }
     }
     __syncthreads();
-    if (b >= 0) {
+    if (wave == 0) {
       const int4v zero = {0, 0, 0, 0};
       int4v a = zero, wl = zero, wh = zero;
       if (kg < 2) {
-        a = *reinterpret_cast<const int4v *>(&in1[wave][row][kg * 16]);
+        a = *reinterpret_cast<const int4v *>(&in1[row][kg * 16]);
         wl = *reinterpret_cast<const int4v *>(net.w1 + ((size_t)b * 32 + row) * 32 + kg * 16);
         wh = *reinterpret_cast<const int4v *>(net.w1 + ((size_t)b * 32 + 16 + row) * 32 + kg * 16);
       }
@@ -113,7 +132,7 @@ __device__ __forceinline__ void layer_stack_tile(const NetDevice &net, const uin
         for (int i = 0; i < 4; ++i) {
           const int pos = 4 * kg + i;
           if (valid(pos, b)) {
-            const int32_t positional = wadd(wadd(net.b2[b], part[i]), fwd[wave][pos]);
+            const int32_t positional = wadd(wadd(net.b2[b], part[i]), fwd[pos]);
             const int32_t psqt = (int32_t)((uint32_t)psq[pos][0] - (uint32_t)psq[pos][1]) / 2;
             emit(pos, make_int2(psqt / 16, positional / 16));
           }
@@ -146,8 +165,7 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR)
   // LDS: big net 53.2 KB -> 3 workgroups (18 waves) per CU.  The feature list
   // (phase 0-1) and the layer-stack scratch (phase 2) share one region.
   constexpr int ROWS_BYTES = TILE * 2 * 32 * 2;
-  constexpr int LS_BYTES = NW * TILE * 32 + NW * TILE * 4;
-  constexpr int SCRATCH = ROWS_BYTES > LS_BYTES ? ROWS_BYTES : LS_BYTES;
+  constexpr int SCRATCH = ROWS_BYTES > LS_SCRATCH ? ROWS_BYTES : LS_SCRATCH;
   __shared__ __attribute__((aligned(16))) uint8_t xt[TILE * XS];
   __shared__ __attribute__((aligned(16))) uint8_t scratch[SCRATCH];
   __shared__ int32_t psq[TILE][2];
@@ -156,8 +174,6 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR)
   __shared__ uint32_t bmask;
   __shared__ uint32_t gidx[TILE];
   uint16_t(*rows)[2][32] = reinterpret_cast<uint16_t(*)[2][32]>(scratch);
-  uint8_t(*in1)[TILE][32] = reinterpret_cast<uint8_t(*)[TILE][32]>(scratch);
-  int32_t(*fwd)[TILE] = reinterpret_cast<int32_t(*)[TILE]>(scratch + NW * TILE * 32);
 
   const int tid = threadIdx.x;
   // XCD-aware tile order: blocks b, b+8, ... share an XCD (round-robin
@@ -260,7 +276,7 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR)
   __syncthreads();
 
   // ---- phase 2: layer stack (MFMA), one wave per distinct bucket in the tile
-  layer_stack_tile<L1, NW>(net, xt, in1, fwd, psq, bkt, bmask, [&](int pos, int b) {
+  layer_stack_tile<L1, NW>(net, xt, scratch, psq, bkt, bmask, [&](int pos, int b) {
     return base + pos < n && nfeat[pos] && bkt[pos] == b;
   }, [&](int pos, int2 v) { out[gidx[pos]] = v; });
 }
@@ -290,8 +306,7 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR)
   constexpr int XS = L1 + 16;
   constexpr uint32_t RS = 2 * L1 + 32;
   constexpr int ROWS_BYTES = TILE * 2 * 32 * 2;
-  constexpr int LS_BYTES = NW * TILE * 32 + NW * TILE * 4;
-  constexpr int SCRATCH = ROWS_BYTES > LS_BYTES ? ROWS_BYTES : LS_BYTES;
+  constexpr int SCRATCH = ROWS_BYTES > LS_SCRATCH ? ROWS_BYTES : LS_SCRATCH;
   constexpr int PACC = PAR > 1 ? 2 * L1 : 8; // shared parent accumulators (small net only)
   __shared__ __attribute__((aligned(16))) uint8_t xt[TILE * XS];
   __shared__ __attribute__((aligned(16))) uint8_t scratch[SCRATCH];
@@ -303,8 +318,6 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR)
   __shared__ int pcount;
   __shared__ uint32_t bmask;
   uint16_t(*rows)[2][32] = reinterpret_cast<uint16_t(*)[2][32]>(scratch);
-  uint8_t(*in1)[TILE][32] = reinterpret_cast<uint8_t(*)[TILE][32]>(scratch);
-  int32_t(*fwd)[TILE] = reinterpret_cast<int32_t(*)[TILE]>(scratch + NW * TILE * 32);
 
   const int tid = threadIdx.x;
   // XCD-aware parent order: each XCD takes a contiguous range of parents, so
@@ -490,7 +503,7 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR)
     __syncthreads();
 
     // ---- phase 2: layer stack
-    layer_stack_tile<L1, NW>(net, xt, in1, fwd, psq, bkt, bmask, [&](int pos, int b) {
+    layer_stack_tile<L1, NW>(net, xt, scratch, psq, bkt, bmask, [&](int pos, int b) {
       return t0 + pos < total && valid[pos] && bkt[pos] == b;
     }, [&](int pos, int2 v) {
       if (t0 + pos == 0) out_parent[p] = v;
