@@ -32,6 +32,32 @@ __device__ __forceinline__ void load_tables(Tables &dst, const Tables *src) {
   __syncthreads();
 }
 
+// --------------------------------------------------- feature extraction --
+// One wave turns a packed board into its HalfKAv2_hm rows, lane = square:
+// the lane's rank among occupied squares is a popcount, king squares and
+// validity come from ballots.  Writes rows_w[k] / rows_b[k] (k = square
+// order) for the non-null outputs; returns the piece count, or 0 (nothing
+// written) for an invalid board.  Must be called by all 64 lanes of a wave.
+__device__ __forceinline__ int wave_features(const gn_board &p, uint16_t *rows_w, uint16_t *rows_b, int lane) {
+  const uint64_t occ = p.occ;
+  const int c = popcnt(occ);
+  const bool has = (occ >> lane) & 1;
+  const int k = popcnt(occ & ((1ull << lane) - 1));
+  uint64_t wlo, whi;
+  piece_words(p, wlo, whi);
+  const int pc = has && k < 32 ? piece_nibble(wlo, whi, k) : 0;
+  const int pt = pc & 7;
+  const uint64_t bad = __ballot(has && (pt < PAWN || pt > KING));
+  const uint64_t wkb = __ballot(has && pc == make_piece(WHITE, KING));
+  const uint64_t bkb = __ballot(has && pc == make_piece(BLACK, KING));
+  if (c < 2 || c > 32 || bad || popcnt(wkb) != 1 || popcnt(bkb) != 1) return 0;
+  if (has) {
+    if (rows_w) rows_w[k] = (uint16_t)feature_index(WHITE, lane, pc, __builtin_ctzll(wkb));
+    if (rows_b) rows_b[k] = (uint16_t)feature_index(BLACK, lane, pc, __builtin_ctzll(bkb));
+  }
+  return c;
+}
+
 // ------------------------------------------------------------ layer stack --
 // NetworkArchitecture::propagate for a 16-position tile held in LDS as
 // transformed features xt[16][L1 + 16] (u8).  Per distinct bucket b in the
@@ -189,20 +215,25 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR)
   if (tid == 0) bmask = 0;
   __syncthreads();
 
-  // ---- phase 0: feature rows of both perspectives (slot 0 = side to move)
-  if (tid < TILE) {
-    const size_t q = base + tid;
-    const size_t i = q < n ? (perm ? perm[q] : q) : 0;
-    gidx[tid] = (uint32_t)i;
-    int cnt = 0;
-    if (q < n && (!need || need[i])) {
-      const gn_board p = boards[i];
-      const int stm = p.stm_ep >> 7;
-      cnt = packed_features(p, rows[tid][stm], rows[tid][stm ^ 1]);
+  // ---- phase 0: feature rows of both perspectives (h = 0: side to move), one wave per position
+  {
+    const int lane = tid & 63, wave = tid >> 6;
+    for (int sl = wave; sl < TILE; sl += NW) {
+      const size_t q = base + sl;
+      const size_t i = q < n ? (perm ? perm[q] : q) : 0;
+      int cnt = 0;
+      if (q < n && (!need || need[i])) {
+        const gn_board p = boards[i];
+        const int stm = p.stm_ep >> 7;
+        cnt = wave_features(p, rows[sl][stm], rows[sl][stm ^ 1], lane);
+      }
+      if (lane == 0) {
+        gidx[sl] = (uint32_t)i;
+        nfeat[sl] = cnt;
+        bkt[sl] = cnt ? (cnt - 1) / 4 : 0;
+        if (cnt) atomicOr(&bmask, 1u << ((cnt - 1) / 4));
+      }
     }
-    nfeat[tid] = cnt;
-    bkt[tid] = cnt ? (cnt - 1) / 4 : 0;
-    if (cnt) atomicOr(&bmask, 1u << ((cnt - 1) / 4));
   }
   __syncthreads();
 
@@ -298,7 +329,7 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR)
                        const gn_board *__restrict__ children, const ChildDelta *__restrict__ deltas,
                        const uint8_t *__restrict__ need_parent,
                        const uint8_t *__restrict__ need_child, int2 *__restrict__ out_parent,
-                       int2 *__restrict__ out_child, size_t n_parents, int swz) {
+                       int2 *__restrict__ out_child, size_t n_parents, int swz, int ablate) {
   constexpr int G = L1 / 16;
   constexpr int NT = 2 * G * PAR;
   constexpr int NW = NT / 64;
@@ -315,7 +346,8 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR)
   __shared__ uint16_t prow[2][32];
   __shared__ int32_t psq[TILE][2];
   __shared__ int nsub[TILE][2], nadd[TILE][2], usep[TILE][2], sstm[TILE], bkt[TILE], valid[TILE];
-  __shared__ int pcount;
+  __shared__ int pcount, njobs;
+  __shared__ uint8_t jobs[TILE * 2];
   __shared__ uint32_t bmask;
   uint16_t(*rows)[2][32] = reinterpret_cast<uint16_t(*)[2][32]>(scratch);
 
@@ -337,7 +369,10 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR)
   int want = 0;
   for (int q = tid; q < total; q += NT)
     want |= q == 0 ? (need_parent ? need_parent[p] : 1) : (need_child ? need_child[off + q - 1] : 1);
-  if (tid == 0) pcount = packed_features(parents[p], prow[0], prow[1]);
+  if (tid < 64) {
+    const int c = wave_features(parents[p], prow[0], prow[1], tid);
+    if (tid == 0) pcount = c;
+  }
   if (!__syncthreads_or(want)) return;
   if (!pcount) return;
 
@@ -351,7 +386,7 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR)
   // parent accumulators: bias + all rows (group q == 0), kept for every child
   ushort8 pacc_lo = bias_lo, pacc_hi = bias_hi;
   int4v pps = zero4;
-  if (q == 0) {
+  if (q == 0 && !(ablate & 1)) {
     const int cnt = pcount;
     int k = 0;
     for (; k + 4 <= cnt; k += 4) {
@@ -399,7 +434,10 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR)
   for (int t0 = 0; t0 < total; t0 += TILE) {
     if (tid == 0) bmask = 0;
     __syncthreads();
-    // ---- phase 0: slot descriptors (one thread per slot) from ChildDelta
+    // ---- phase 0: slot descriptors (one thread per slot) from ChildDelta; king-move
+    // refreshes are queued and extracted wave-parallel (lane = square)
+    if (tid == 0) njobs = 0;
+    __syncthreads();
     if (tid < TILE) {
       const int qq = t0 + tid;
       int v = 0, stm = 0, cnt = 2;
@@ -416,10 +454,8 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR)
 #pragma unroll
           for (int hh = 0; hh < 2; ++hh) {
             if (cd.meta & (1u << (8 + hh))) {
-              const gn_board cb = children[off + qq - 1];
-              const int c = packed_features(cb, hh == 0 ? rows[tid][0] : nullptr, hh == 1 ? rows[tid][1] : nullptr);
-              usep[tid][hh] = 0, nsub[tid][hh] = 0, nadd[tid][hh] = c;
-              if (!c) v = 0;
+              usep[tid][hh] = 0, nsub[tid][hh] = 0, nadd[tid][hh] = popcnt(children[off + qq - 1].occ);
+              jobs[atomicAdd(&njobs, 1)] = (uint8_t)(tid | (hh << 4));
             } else {
               const int ns = (cd.meta >> (4 * hh)) & 3, na = (cd.meta >> (4 * hh + 2)) & 3;
               rows[tid][hh][0] = cd.idx[hh][0];
@@ -437,6 +473,15 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR)
       if (v) atomicOr(&bmask, 1u << ((cnt - 1) / 4));
     }
     __syncthreads();
+    {
+      const int lane = tid & 63, wave = tid >> 6, nj = njobs;
+      for (int jb = wave; jb < nj; jb += NW) {
+        const int sl = jobs[jb] & 15, hh = jobs[jb] >> 4;
+        const gn_board cb = children[off + t0 + sl - 1];
+        wave_features(cb, hh == 0 ? rows[sl][0] : nullptr, hh == 1 ? rows[sl][1] : nullptr, lane);
+      }
+    }
+    __syncthreads();
 
     // ---- phase 1: accumulators + transform
 #pragma unroll 1
@@ -448,7 +493,8 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR)
       int4v ps = fromp ? pps : zero4;
       const uint16_t *rr = rows[sl][h];
       const int ns = nsub[sl][h], end = ns + nadd[sl][h];
-      if (fromp && end > 0) {
+      if (ablate & 2) {
+      } else if (fromp && end > 0) {
         // delta child: <= 2 removed + <= 2 added rows, all four loads in flight at once
         const uint32_t o0 = ft_row(rr[0]) * RS, o1 = ft_row(rr[end > 1 ? 1 : 0]) * RS;
         const uint32_t o2 = ft_row(rr[end > 2 ? 2 : 0]) * RS, o3 = ft_row(rr[end > 3 ? 3 : 0]) * RS;
@@ -503,7 +549,7 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR)
     __syncthreads();
 
     // ---- phase 2: layer stack
-    layer_stack_tile<L1, NW>(net, xt, scratch, psq, bkt, bmask, [&](int pos, int b) {
+    if (!(ablate & 4)) layer_stack_tile<L1, NW>(net, xt, scratch, psq, bkt, bmask, [&](int pos, int b) {
       return t0 + pos < total && valid[pos] && bkt[pos] == b;
     }, [&](int pos, int2 v) {
       if (t0 + pos == 0) out_parent[p] = v;
@@ -846,7 +892,8 @@ hipError_t launch_expand_net(const NetDevice &net, const gn_board *parents, size
                              const uint8_t *need_child, int2 *out_parent, int2 *out_child, int swz, hipStream_t s) {
   if (!n) return hipSuccess;
   const unsigned g = (unsigned)(swz ? 8 * ((n + 7) / 8) : n);
-#define GN_EXPAND_ARGS net, parents, offsets, children, deltas, need_parent, need_child, out_parent, out_child, n, swz
+  static const int ablate = getenv("GN_ABLATE") ? atoi(getenv("GN_ABLATE")) : 0; // timing diagnostics only
+#define GN_EXPAND_ARGS net, parents, offsets, children, deltas, need_parent, need_child, out_parent, out_child, n, swz, ablate
   if (net.L1 == 3072) {
     hipLaunchKernelGGL((expand_eval_kernel<3072, 1>), dim3(g), dim3(384), 0, s, GN_EXPAND_ARGS);
   } else if (net.L1 == 128) {
