@@ -32,6 +32,19 @@ __device__ __forceinline__ void load_tables(Tables &dst, const Tables *src) {
   __syncthreads();
 }
 
+// FT row loads as SGPR base + 32-bit VGPR offset (the table is < 4 GiB): one VGPR
+// per address instead of a 64-bit pointer, and the +L1 half folds into the
+// instruction's immediate offset
+__device__ __forceinline__ ushort8 ldft(const uint8_t *__restrict__ ft, uint32_t off) {
+  return *reinterpret_cast<const ushort8 *>(ft + off);
+}
+__device__ __forceinline__ uint32_t ldpd(const uint8_t *__restrict__ ft, uint32_t off) {
+  return *reinterpret_cast<const uint32_t *>(ft + off);
+}
+__device__ __forceinline__ int4v ldps(const uint8_t *__restrict__ ft, uint32_t off) {
+  return *reinterpret_cast<const int4v *>(ft + off);
+}
+
 // --------------------------------------------------- feature extraction --
 // One wave turns a packed board into its HalfKAv2_hm rows, lane = square:
 // the lane's rank among occupied squares is a popcount, king squares and
@@ -242,7 +255,7 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR)
     const int q = tid / (2 * G), h = (tid / G) & 1, j = tid % G;
     const ushort8 bias_lo = *reinterpret_cast<const ushort8 *>(net.bias + 8 * j);
     const ushort8 bias_hi = *reinterpret_cast<const ushort8 *>(net.bias + L1 / 2 + 8 * j);
-    const uint8_t *ftj = net.ft + 16 * j;
+    const uint32_t j16 = 16 * j; // byte offset of this thread's columns in a row
 #pragma unroll 1
     for (int r = 0; r < TILE / PAR; ++r) {
       const int p = r * PAR + q;
@@ -256,19 +269,19 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR)
       int k = 0;
       for (; k + 4 <= cnt; k += 4) {
         const uint32_t o0 = ft_row(rr[k]) * RS, o1 = ft_row(rr[k + 1]) * RS, o2 = ft_row(rr[k + 2]) * RS, o3 = ft_row(rr[k + 3]) * RS;
-        const ushort8 a0 = *reinterpret_cast<const ushort8 *>(ftj + o0);
-        const ushort8 a1 = *reinterpret_cast<const ushort8 *>(ftj + o1);
-        const ushort8 a2 = *reinterpret_cast<const ushort8 *>(ftj + o2);
-        const ushort8 a3 = *reinterpret_cast<const ushort8 *>(ftj + o3);
-        const ushort8 b0 = *reinterpret_cast<const ushort8 *>(ftj + o0 + L1);
-        const ushort8 b1 = *reinterpret_cast<const ushort8 *>(ftj + o1 + L1);
-        const ushort8 b2 = *reinterpret_cast<const ushort8 *>(ftj + o2 + L1);
-        const ushort8 b3 = *reinterpret_cast<const ushort8 *>(ftj + o3 + L1);
+        const ushort8 a0 = ldft(net.ft, j16 + o0);
+        const ushort8 a1 = ldft(net.ft, j16 + o1);
+        const ushort8 a2 = ldft(net.ft, j16 + o2);
+        const ushort8 a3 = ldft(net.ft, j16 + o3);
+        const ushort8 b0 = ldft(net.ft, j16 + o0 + L1);
+        const ushort8 b1 = ldft(net.ft, j16 + o1 + L1);
+        const ushort8 b2 = ldft(net.ft, j16 + o2 + L1);
+        const ushort8 b3 = ldft(net.ft, j16 + o3 + L1);
         if (j == 0) {
-          const int4v v0 = *reinterpret_cast<const int4v *>(net.ft + o0 + pso);
-          const int4v v1 = *reinterpret_cast<const int4v *>(net.ft + o1 + pso);
-          const int4v v2 = *reinterpret_cast<const int4v *>(net.ft + o2 + pso);
-          const int4v v3 = *reinterpret_cast<const int4v *>(net.ft + o3 + pso);
+          const int4v v0 = ldps(net.ft, o0 + pso);
+          const int4v v1 = ldps(net.ft, o1 + pso);
+          const int4v v2 = ldps(net.ft, o2 + pso);
+          const int4v v3 = ldps(net.ft, o3 + pso);
           ps += (uint32_t)v0[pse] + (uint32_t)v1[pse] + (uint32_t)v2[pse] + (uint32_t)v3[pse];
         }
         lo += (a0 + a1) + (a2 + a3);
@@ -277,15 +290,15 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR)
       if (k < cnt) { // tail of 1-3 rows as one batch (no serialized round trips)
         const int k1 = k + 1 < cnt ? k + 1 : k, k2 = k + 2 < cnt ? k + 2 : k;
         const uint32_t o0 = ft_row(rr[k]) * RS, o1 = ft_row(rr[k1]) * RS, o2 = ft_row(rr[k2]) * RS;
-        const ushort8 a0 = *reinterpret_cast<const ushort8 *>(ftj + o0), a1 = *reinterpret_cast<const ushort8 *>(ftj + o1);
-        const ushort8 a2 = *reinterpret_cast<const ushort8 *>(ftj + o2);
-        const ushort8 b0 = *reinterpret_cast<const ushort8 *>(ftj + o0 + L1), b1 = *reinterpret_cast<const ushort8 *>(ftj + o1 + L1);
-        const ushort8 b2 = *reinterpret_cast<const ushort8 *>(ftj + o2 + L1);
+        const ushort8 a0 = ldft(net.ft, j16 + o0), a1 = ldft(net.ft, j16 + o1);
+        const ushort8 a2 = ldft(net.ft, j16 + o2);
+        const ushort8 b0 = ldft(net.ft, j16 + o0 + L1), b1 = ldft(net.ft, j16 + o1 + L1);
+        const ushort8 b2 = ldft(net.ft, j16 + o2 + L1);
         uint32_t q0 = 0, q1 = 0, q2 = 0;
         if (j == 0) {
-          q0 = (uint32_t)(*reinterpret_cast<const int4v *>(net.ft + o0 + pso))[pse];
-          q1 = (uint32_t)(*reinterpret_cast<const int4v *>(net.ft + o1 + pso))[pse];
-          q2 = (uint32_t)(*reinterpret_cast<const int4v *>(net.ft + o2 + pso))[pse];
+          q0 = (uint32_t)(ldps(net.ft, o0 + pso))[pse];
+          q1 = (uint32_t)(ldps(net.ft, o1 + pso))[pse];
+          q2 = (uint32_t)(ldps(net.ft, o2 + pso))[pse];
         }
         lo += a0, hi += b0, ps += q0;
         if (k + 1 < cnt) lo += a1, hi += b1, ps += q1;
@@ -324,7 +337,7 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR)
 //   parent_acc - rows(removed) + rows(added)   (1-3 rows each, Dirty),
 // or a refresh from the bias when that perspective's own king moved.
 template <int L1, int PAR>
-__global__ void __launch_bounds__(2 * (L1 / 16) * PAR)
+__global__ void __launch_bounds__(2 * (L1 / 16) * PAR) __attribute__((amdgpu_waves_per_eu(3)))
     expand_eval_kernel(NetDevice net, const gn_board *__restrict__ parents, const uint64_t *__restrict__ offsets,
                        const gn_board *__restrict__ children, const ChildDelta *__restrict__ deltas,
                        const uint8_t *__restrict__ need_parent,
@@ -377,27 +390,27 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR)
   if (!pcount) return;
 
   const int q = tid / (2 * G), h = (tid / G) & 1, j = tid % G;
-  const ushort8 bias_lo = *reinterpret_cast<const ushort8 *>(net.bias + 8 * j);
-  const ushort8 bias_hi = *reinterpret_cast<const ushort8 *>(net.bias + L1 / 2 + 8 * j);
-  const uint8_t *ftj = net.ft + 16 * j;
+  const uint32_t j16 = 16 * j; // byte offset of this thread's columns in a row
   const uint32_t pso = 2 * L1 + 16 * (j & 1); // this thread's 4 PSQT buckets (j < 2 only)
   const int4v zero4 = {0, 0, 0, 0};
 
-  // parent accumulators: bias + all rows (group q == 0), kept for every child
-  ushort8 pacc_lo = bias_lo, pacc_hi = bias_hi;
-  int4v pps = zero4;
+  // parent accumulators: bias + all rows (group q == 0), kept for every child; the
+  // parent's 8 PSQT sums go to LDS (children read one bucket each)
+  ushort8 pacc_lo = *reinterpret_cast<const ushort8 *>(net.bias + 8 * j);
+  ushort8 pacc_hi = *reinterpret_cast<const ushort8 *>(net.bias + L1 / 2 + 8 * j);
   if (q == 0 && !(ablate & 1)) {
+    int4v pps = zero4;
     const int cnt = pcount;
     int k = 0;
     for (; k + 4 <= cnt; k += 4) {
       const uint32_t o0 = ft_row(prow[h][k]) * RS, o1 = ft_row(prow[h][k + 1]) * RS, o2 = ft_row(prow[h][k + 2]) * RS, o3 = ft_row(prow[h][k + 3]) * RS;
-      const ushort8 a0 = *reinterpret_cast<const ushort8 *>(ftj + o0), a1 = *reinterpret_cast<const ushort8 *>(ftj + o1);
-      const ushort8 a2 = *reinterpret_cast<const ushort8 *>(ftj + o2), a3 = *reinterpret_cast<const ushort8 *>(ftj + o3);
-      const ushort8 b0 = *reinterpret_cast<const ushort8 *>(ftj + o0 + L1), b1 = *reinterpret_cast<const ushort8 *>(ftj + o1 + L1);
-      const ushort8 b2 = *reinterpret_cast<const ushort8 *>(ftj + o2 + L1), b3 = *reinterpret_cast<const ushort8 *>(ftj + o3 + L1);
+      const ushort8 a0 = ldft(net.ft, j16 + o0), a1 = ldft(net.ft, j16 + o1);
+      const ushort8 a2 = ldft(net.ft, j16 + o2), a3 = ldft(net.ft, j16 + o3);
+      const ushort8 b0 = ldft(net.ft, j16 + o0 + L1), b1 = ldft(net.ft, j16 + o1 + L1);
+      const ushort8 b2 = ldft(net.ft, j16 + o2 + L1), b3 = ldft(net.ft, j16 + o3 + L1);
       if (j < 2) {
-        pps += *reinterpret_cast<const int4v *>(net.ft + o0 + pso) + *reinterpret_cast<const int4v *>(net.ft + o1 + pso);
-        pps += *reinterpret_cast<const int4v *>(net.ft + o2 + pso) + *reinterpret_cast<const int4v *>(net.ft + o3 + pso);
+        pps += ldps(net.ft, o0 + pso) + ldps(net.ft, o1 + pso);
+        pps += ldps(net.ft, o2 + pso) + ldps(net.ft, o3 + pso);
       }
       pacc_lo += (a0 + a1) + (a2 + a3);
       pacc_hi += (b0 + b1) + (b2 + b3);
@@ -405,14 +418,14 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR)
     if (k < cnt) { // tail of 1-3 rows as one batch
       const int k1 = k + 1 < cnt ? k + 1 : k, k2 = k + 2 < cnt ? k + 2 : k;
       const uint32_t o0 = ft_row(prow[h][k]) * RS, o1 = ft_row(prow[h][k1]) * RS, o2 = ft_row(prow[h][k2]) * RS;
-      const ushort8 a0 = *reinterpret_cast<const ushort8 *>(ftj + o0), a1 = *reinterpret_cast<const ushort8 *>(ftj + o1);
-      const ushort8 a2 = *reinterpret_cast<const ushort8 *>(ftj + o2);
-      const ushort8 b0 = *reinterpret_cast<const ushort8 *>(ftj + o0 + L1), b1 = *reinterpret_cast<const ushort8 *>(ftj + o1 + L1);
-      const ushort8 b2 = *reinterpret_cast<const ushort8 *>(ftj + o2 + L1);
+      const ushort8 a0 = ldft(net.ft, j16 + o0), a1 = ldft(net.ft, j16 + o1);
+      const ushort8 a2 = ldft(net.ft, j16 + o2);
+      const ushort8 b0 = ldft(net.ft, j16 + o0 + L1), b1 = ldft(net.ft, j16 + o1 + L1);
+      const ushort8 b2 = ldft(net.ft, j16 + o2 + L1);
       int4v p0 = zero4, p1 = zero4, p2 = zero4;
       if (j < 2) {
-        p0 = *reinterpret_cast<const int4v *>(net.ft + o0 + pso), p1 = *reinterpret_cast<const int4v *>(net.ft + o1 + pso);
-        p2 = *reinterpret_cast<const int4v *>(net.ft + o2 + pso);
+        p0 = ldps(net.ft, o0 + pso), p1 = ldps(net.ft, o1 + pso);
+        p2 = ldps(net.ft, o2 + pso);
       }
       pacc_lo += a0, pacc_hi += b0, pps += p0;
       if (k + 1 < cnt) pacc_lo += a1, pacc_hi += b1, pps += p1;
@@ -421,15 +434,17 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR)
     if (PAR > 1) {
       *reinterpret_cast<ushort8 *>(pacc_lds + h * L1 + 8 * j) = pacc_lo;
       *reinterpret_cast<ushort8 *>(pacc_lds + h * L1 + L1 / 2 + 8 * j) = pacc_hi;
-      if (j < 2) *reinterpret_cast<int4v *>(&pps_lds[h][4 * j]) = pps;
     }
+    if (j < 2) *reinterpret_cast<int4v *>(&pps_lds[h][4 * j]) = pps;
   }
   if (PAR > 1) {
     __syncthreads();
     pacc_lo = *reinterpret_cast<const ushort8 *>(pacc_lds + h * L1 + 8 * j);
     pacc_hi = *reinterpret_cast<const ushort8 *>(pacc_lds + h * L1 + L1 / 2 + 8 * j);
-    if (j < 2) pps = *reinterpret_cast<const int4v *>(&pps_lds[h][4 * j]);
   }
+
+  ushort8 base_lo = pacc_lo, base_hi = pacc_hi; // parent minus base_key's row (delta children)
+  int base_key = -1;
 
   for (int t0 = 0; t0 < total; t0 += TILE) {
     if (tid == 0) bmask = 0;
@@ -483,49 +498,64 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR)
     }
     __syncthreads();
 
-    // ---- phase 1: accumulators + transform
+    // ---- phase 1: accumulators + transform.  PSQT: thread j == 0 of each
+    // perspective sums the slot's own bucket (one dword per row).
 #pragma unroll 1
     for (int r = 0; r < TILE / PAR; ++r) {
       const int sl = r * PAR + q;
       if (!valid[sl]) continue;
       const bool fromp = usep[sl][h];
-      ushort8 lo = fromp ? pacc_lo : bias_lo, hi = fromp ? pacc_hi : bias_hi;
-      int4v ps = fromp ? pps : zero4;
+      const int b = bkt[sl];
+      const uint32_t psb = 2 * L1 + 4 * b;
+      ushort8 lo, hi;
+      uint32_t ps = fromp ? (uint32_t)pps_lds[h][b] : 0u;
       const uint16_t *rr = rows[sl][h];
       const int ns = nsub[sl][h], end = ns + nadd[sl][h];
+      if (fromp) lo = pacc_lo, hi = pacc_hi;
       if (ablate & 2) {
+        if (!fromp) lo = pacc_lo, hi = pacc_hi;
       } else if (fromp && end > 0) {
-        // delta child: <= 2 removed + <= 2 added rows, all four loads in flight at once
-        const uint32_t o0 = ft_row(rr[0]) * RS, o1 = ft_row(rr[end > 1 ? 1 : 0]) * RS;
-        const uint32_t o2 = ft_row(rr[end > 2 ? 2 : 0]) * RS, o3 = ft_row(rr[end > 3 ? 3 : 0]) * RS;
-        const ushort8 a0 = *reinterpret_cast<const ushort8 *>(ftj + o0), a1 = *reinterpret_cast<const ushort8 *>(ftj + o1);
-        const ushort8 a2 = *reinterpret_cast<const ushort8 *>(ftj + o2), a3 = *reinterpret_cast<const ushort8 *>(ftj + o3);
-        const ushort8 b0 = *reinterpret_cast<const ushort8 *>(ftj + o0 + L1), b1 = *reinterpret_cast<const ushort8 *>(ftj + o1 + L1);
-        const ushort8 b2 = *reinterpret_cast<const ushort8 *>(ftj + o2 + L1), b3 = *reinterpret_cast<const ushort8 *>(ftj + o3 + L1);
-        int4v p0 = zero4, p1 = zero4, p2 = zero4, p3 = zero4;
-        if (j < 2) {
-          p0 = *reinterpret_cast<const int4v *>(net.ft + o0 + pso), p1 = *reinterpret_cast<const int4v *>(net.ft + o1 + pso);
-          p2 = *reinterpret_cast<const int4v *>(net.ft + o2 + pso), p3 = *reinterpret_cast<const int4v *>(net.ft + o3 + pso);
+        // delta child: entry 0 is always the mover's from-row (subtracted).  Siblings are
+        // generated per from-square, so (parent - that row) is kept in registers and
+        // reused while consecutive children move the same piece; the remaining 1-3 entries
+        // are loaded together, without duplicate loads for short deltas.
+        const int key = rr[0];
+        const bool hit = key == base_key;
+        ushort8 a0, b0, a1, b1, a2, b2, a3, b3;
+        uint32_t p0 = 0, p1 = 0, p2 = 0, p3 = 0;
+        const uint32_t o0 = ft_row(rr[0]) * RS, o1 = ft_row(rr[1]) * RS;
+        const uint32_t o2 = ft_row(rr[end > 2 ? 2 : 1]) * RS, o3 = ft_row(rr[end > 3 ? 3 : 1]) * RS;
+        if (!hit) a0 = ldft(net.ft, j16 + o0), b0 = ldft(net.ft, j16 + o0 + L1);
+        if (end > 1) a1 = ldft(net.ft, j16 + o1), b1 = ldft(net.ft, j16 + o1 + L1);
+        if (end > 2) a2 = ldft(net.ft, j16 + o2), b2 = ldft(net.ft, j16 + o2 + L1);
+        if (end > 3) a3 = ldft(net.ft, j16 + o3), b3 = ldft(net.ft, j16 + o3 + L1);
+        if (j == 0) {
+          p0 = ldpd(net.ft, o0 + psb);
+          if (end > 1) p1 = ldpd(net.ft, o1 + psb);
+          if (end > 2) p2 = ldpd(net.ft, o2 + psb);
+          if (end > 3) p3 = ldpd(net.ft, o3 + psb);
         }
-        // entry e: subtract if e < ns, add if ns <= e < end, skip otherwise
-        lo = ns > 0 ? lo - a0 : lo + a0, hi = ns > 0 ? hi - b0 : hi + b0, ps = ns > 0 ? ps - p0 : ps + p0;
+        if (!hit) base_lo = pacc_lo - a0, base_hi = pacc_hi - b0, base_key = key;
+        lo = base_lo, hi = base_hi, ps -= p0;
+        // entry 1 is a removed row when ns == 2, else an added one; entries 2, 3 are added
         if (end > 1) lo = ns > 1 ? lo - a1 : lo + a1, hi = ns > 1 ? hi - b1 : hi + b1, ps = ns > 1 ? ps - p1 : ps + p1;
-        if (end > 2) lo = ns > 2 ? lo - a2 : lo + a2, hi = ns > 2 ? hi - b2 : hi + b2, ps = ns > 2 ? ps - p2 : ps + p2;
+        if (end > 2) lo += a2, hi += b2, ps += p2;
         if (end > 3) lo += a3, hi += b3, ps += p3;
       } else if (!fromp) {
-        // refresh (own king moved): adds only, 4 rows in flight
-        int k = 0;
-        for (; k < end; k += 4) {
+        // refresh (own king moved): bias + adds only, 4 rows in flight
+        lo = *reinterpret_cast<const ushort8 *>(net.bias + 8 * j);
+        hi = *reinterpret_cast<const ushort8 *>(net.bias + L1 / 2 + 8 * j);
+        for (int k = 0; k < end; k += 4) {
           const int k1 = k + 1 < end ? k + 1 : k, k2 = k + 2 < end ? k + 2 : k, k3 = k + 3 < end ? k + 3 : k;
           const uint32_t o0 = ft_row(rr[k]) * RS, o1 = ft_row(rr[k1]) * RS, o2 = ft_row(rr[k2]) * RS, o3 = ft_row(rr[k3]) * RS;
-          const ushort8 a0 = *reinterpret_cast<const ushort8 *>(ftj + o0), a1 = *reinterpret_cast<const ushort8 *>(ftj + o1);
-          const ushort8 a2 = *reinterpret_cast<const ushort8 *>(ftj + o2), a3 = *reinterpret_cast<const ushort8 *>(ftj + o3);
-          const ushort8 b0 = *reinterpret_cast<const ushort8 *>(ftj + o0 + L1), b1 = *reinterpret_cast<const ushort8 *>(ftj + o1 + L1);
-          const ushort8 b2 = *reinterpret_cast<const ushort8 *>(ftj + o2 + L1), b3 = *reinterpret_cast<const ushort8 *>(ftj + o3 + L1);
-          int4v p0 = zero4, p1 = zero4, p2 = zero4, p3 = zero4;
-          if (j < 2) {
-            p0 = *reinterpret_cast<const int4v *>(net.ft + o0 + pso), p1 = *reinterpret_cast<const int4v *>(net.ft + o1 + pso);
-            p2 = *reinterpret_cast<const int4v *>(net.ft + o2 + pso), p3 = *reinterpret_cast<const int4v *>(net.ft + o3 + pso);
+          const ushort8 a0 = ldft(net.ft, j16 + o0), a1 = ldft(net.ft, j16 + o1);
+          const ushort8 a2 = ldft(net.ft, j16 + o2), a3 = ldft(net.ft, j16 + o3);
+          const ushort8 b0 = ldft(net.ft, j16 + o0 + L1), b1 = ldft(net.ft, j16 + o1 + L1);
+          const ushort8 b2 = ldft(net.ft, j16 + o2 + L1), b3 = ldft(net.ft, j16 + o3 + L1);
+          uint32_t p0 = 0, p1 = 0, p2 = 0, p3 = 0;
+          if (j == 0) {
+            p0 = ldpd(net.ft, o0 + psb), p1 = ldpd(net.ft, o1 + psb);
+            p2 = ldpd(net.ft, o2 + psb), p3 = ldpd(net.ft, o3 + psb);
           }
           lo += a0, hi += b0, ps += p0;
           if (k + 1 < end) lo += a1, hi += b1, ps += p1;
@@ -537,14 +567,13 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR)
       uint32_t w0 = 0, w1 = 0;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        const int a = clampi((short)lo[e], 0, 254), b = clampi((short)hi[e], 0, 254);
-        const uint32_t v = (uint32_t)(a * b) >> 9;
+        const int a = clampi((short)lo[e], 0, 254), c = clampi((short)hi[e], 0, 254);
+        const uint32_t v = (uint32_t)(a * c) >> 9;
         if (e < 4) w0 |= v << (8 * e);
         else w1 |= v << (8 * (e - 4));
       }
       *reinterpret_cast<uint2 *>(xt + sl * XS + side * (L1 / 2) + 8 * j) = make_uint2(w0, w1);
-      const int b = bkt[sl];
-      if (j == (b >> 2)) psq[sl][side] = ps[b & 3];
+      if (j == 0) psq[sl][side] = (int32_t)ps;
     }
     __syncthreads();
 
