@@ -510,6 +510,104 @@ static int expand_evaluate(gn_ctx *ctx, Dev &d, const gn_board *parents, size_t 
   return GN_OK;
 }
 
+// Host boards -> device(s) -> gn_eval: contiguous shards, one host thread per device.
+static int evaluate_boards_host(gn_ctx *ctx, const gn_board *boards, size_t n, int mode, gn_eval *out) {
+  if (!n) return GN_OK;
+  try {
+    const size_t nd = ctx->devs.size(), per = (n + nd - 1) / nd;
+    std::vector<int> rcs(nd, GN_OK);
+    std::vector<std::string> errs(nd);
+    auto work = [&](size_t k) {
+      const size_t lo = k * per, hi = std::min(n, lo + per);
+      if (lo >= hi) return;
+      Dev &d = *ctx->devs[k];
+      std::lock_guard<std::mutex> lk(d.mu);
+      auto run = [&]() -> int {
+        HIP_TRY(hipSetDevice(d.id));
+        HIP_TRY(d.io_boards.ensure(hi - lo));
+        HIP_TRY(d.io_out.ensure(hi - lo));
+        HIP_TRY(hipMemcpyAsync(d.io_boards.p, boards + lo, (hi - lo) * sizeof(gn_board), hipMemcpyHostToDevice,
+                               d.stream));
+        int r = evaluate_on(ctx, d, d.io_boards.p, hi - lo, mode, d.io_out.p, d.stream, nullptr);
+        if (r) return r;
+        HIP_TRY(hipMemcpyAsync(out + lo, d.io_out.p, (hi - lo) * sizeof(gn_eval), hipMemcpyDeviceToHost, d.stream));
+        HIP_TRY(hipStreamSynchronize(d.stream));
+        return GN_OK;
+      };
+      rcs[k] = run();
+      if (rcs[k]) errs[k] = g_err;
+    };
+    if (nd == 1) work(0);
+    else {
+      std::vector<std::thread> th;
+      for (size_t k = 0; k < nd; ++k) th.emplace_back(work, k);
+      for (auto &t : th) t.join();
+    }
+    for (size_t k = 0; k < nd; ++k)
+      if (rcs[k]) {
+        g_err = errs[k];
+        return rcs[k];
+      }
+    return GN_OK;
+  } catch (const std::bad_alloc &) {
+    return fail(GN_E_NOMEM, "host allocation failed");
+  } catch (...) {
+    return fail(GN_E_INVALID, "unexpected exception");
+  }
+}
+
+// Host parent boards -> every legal child (device 0) -> parent/child gn_eval.
+static int expand_boards_host(gn_ctx *ctx, const gn_board *boards, size_t n, int mode, gn_eval *parent_out,
+                              uint32_t *child_offsets, uint16_t *child_moves, gn_eval *child_out, size_t cap) {
+  Dev *d = slot(ctx, 0);
+  if (!d) return fail(GN_E_INVALID, "bad context");
+  if (!n) {
+    child_offsets[0] = 0;
+    return GN_OK;
+  }
+  try {
+    int rc = GN_OK;
+    std::lock_guard<std::mutex> lk(d->mu);
+    HIP_TRY(hipSetDevice(d->id));
+    hipStream_t s = d->stream;
+    HIP_TRY(d->io_boards.ensure(n));
+    HIP_TRY(hipMemcpyAsync(d->io_boards.p, boards, n * sizeof(gn_board), hipMemcpyHostToDevice, s));
+    // size the move buffer from the counts first (generate_children syncs for the total)
+    HIP_TRY(d->counts.ensure(n + 1));
+    HIP_TRY(d->offsets.ensure(n + 1));
+    HIP_TRY(hipMemsetAsync(d->counts.p + n, 0, sizeof(uint64_t), s));
+    HIP_TRY(launch_count_children(d->io_boards.p, n, d->tables, d->counts.p, s));
+    HIP_TRY(exclusive_scan_u64(d->counts.p, d->offsets.p, n + 1, d->scan_tmp, d->scan_bytes, s));
+    std::vector<uint64_t> off(n + 1);
+    HIP_TRY(hipMemcpyAsync(off.data(), d->offsets.p, (n + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    const size_t total = (size_t)off[n];
+    if (total > 0xFFFFFFFFull) return fail(GN_E_CAPACITY, "children exceed 32-bit offsets");
+    for (size_t i = 0; i <= n; ++i) child_offsets[i] = (uint32_t)off[i];
+    if (total > cap) return fail(GN_E_CAPACITY, "%zu children exceed capacity %zu", total, cap);
+    if (total && (!child_moves || !child_out)) return fail(GN_E_INVALID, "NULL child buffer");
+    HIP_TRY(d->moves.ensure(std::max<size_t>(total, 1)));
+    size_t t = 0;
+    rc = generate_children(*d, d->io_boards.p, n, nullptr, 0, d->moves.p, ctx->incremental, &t, s, nullptr);
+    if (rc) return rc;
+    HIP_TRY(d->io_out.ensure(n));
+    HIP_TRY(d->io_out2.ensure(std::max<size_t>(t, 1)));
+    rc = expand_evaluate(ctx, *d, d->io_boards.p, n, d->frontier[1].p, t, mode, d->io_out.p, d->io_out2.p, s, nullptr);
+    if (rc) return rc;
+    if (t) {
+      HIP_TRY(hipMemcpyAsync(child_out, d->io_out2.p, t * sizeof(gn_eval), hipMemcpyDeviceToHost, s));
+      HIP_TRY(hipMemcpyAsync(child_moves, d->moves.p, t * sizeof(uint16_t), hipMemcpyDeviceToHost, s));
+    }
+    if (parent_out) HIP_TRY(hipMemcpyAsync(parent_out, d->io_out.p, n * sizeof(gn_eval), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return GN_OK;
+  } catch (const std::bad_alloc &) {
+    return fail(GN_E_NOMEM, "host allocation failed");
+  } catch (...) {
+    return fail(GN_E_INVALID, "unexpected exception");
+  }
+}
+
 // ============================================================ C-ABI ========
 extern "C" {
 
@@ -719,41 +817,7 @@ int gn_evaluate_batch_mode(gn_ctx *ctx, const char *const *fens, size_t n, int m
     std::vector<gn_board> boards(n);
     int rc = gn_pack_fens(fens, n, boards.data(), nullptr);
     if (rc) return rc;
-    const size_t nd = ctx->devs.size(), per = (n + nd - 1) / nd;
-    std::vector<int> rcs(nd, GN_OK);
-    std::vector<std::string> errs(nd);
-    auto work = [&](size_t k) {
-      const size_t lo = k * per, hi = std::min(n, lo + per);
-      if (lo >= hi) return;
-      Dev &d = *ctx->devs[k];
-      std::lock_guard<std::mutex> lk(d.mu);
-      auto run = [&]() -> int {
-        HIP_TRY(hipSetDevice(d.id));
-        HIP_TRY(d.io_boards.ensure(hi - lo));
-        HIP_TRY(d.io_out.ensure(hi - lo));
-        HIP_TRY(hipMemcpyAsync(d.io_boards.p, boards.data() + lo, (hi - lo) * sizeof(gn_board), hipMemcpyHostToDevice,
-                               d.stream));
-        int r = evaluate_on(ctx, d, d.io_boards.p, hi - lo, mode, d.io_out.p, d.stream, nullptr);
-        if (r) return r;
-        HIP_TRY(hipMemcpyAsync(out + lo, d.io_out.p, (hi - lo) * sizeof(gn_eval), hipMemcpyDeviceToHost, d.stream));
-        HIP_TRY(hipStreamSynchronize(d.stream));
-        return GN_OK;
-      };
-      rcs[k] = run();
-      if (rcs[k]) errs[k] = g_err;
-    };
-    if (nd == 1) work(0);
-    else {
-      std::vector<std::thread> th;
-      for (size_t k = 0; k < nd; ++k) th.emplace_back(work, k);
-      for (auto &t : th) t.join();
-    }
-    for (size_t k = 0; k < nd; ++k)
-      if (rcs[k]) {
-        g_err = errs[k];
-        return rcs[k];
-      }
-    return GN_OK;
+    return evaluate_boards_host(ctx, boards.data(), n, mode, out);
   } catch (const std::bad_alloc &) {
     return fail(GN_E_NOMEM, "host allocation failed");
   } catch (...) {
@@ -900,8 +964,7 @@ int gn_get_option(const gn_ctx *ctx, int option, int64_t *value) {
 
 int gn_expand_and_evaluate(gn_ctx *ctx, const char *const *parent_fens, size_t n, int mode, gn_eval *parent_out,
                            uint32_t *child_offsets, uint16_t *child_moves, gn_eval *child_out, size_t cap) {
-  Dev *d = slot(ctx, 0);
-  if (!d) return fail(GN_E_INVALID, "bad context");
+  if (!slot(ctx, 0)) return fail(GN_E_INVALID, "bad context");
   if (n && (!parent_fens || !child_offsets)) return fail(GN_E_INVALID, "NULL argument");
   if (!n) {
     if (child_offsets) child_offsets[0] = 0;
@@ -911,40 +974,7 @@ int gn_expand_and_evaluate(gn_ctx *ctx, const char *const *parent_fens, size_t n
     std::vector<gn_board> boards(n);
     int rc = gn_pack_fens(parent_fens, n, boards.data(), nullptr);
     if (rc) return rc;
-    std::lock_guard<std::mutex> lk(d->mu);
-    HIP_TRY(hipSetDevice(d->id));
-    hipStream_t s = d->stream;
-    HIP_TRY(d->io_boards.ensure(n));
-    HIP_TRY(hipMemcpyAsync(d->io_boards.p, boards.data(), n * sizeof(gn_board), hipMemcpyHostToDevice, s));
-    // size the move buffer from the counts first (generate_children syncs for the total)
-    HIP_TRY(d->counts.ensure(n + 1));
-    HIP_TRY(d->offsets.ensure(n + 1));
-    HIP_TRY(hipMemsetAsync(d->counts.p + n, 0, sizeof(uint64_t), s));
-    HIP_TRY(launch_count_children(d->io_boards.p, n, d->tables, d->counts.p, s));
-    HIP_TRY(exclusive_scan_u64(d->counts.p, d->offsets.p, n + 1, d->scan_tmp, d->scan_bytes, s));
-    std::vector<uint64_t> off(n + 1);
-    HIP_TRY(hipMemcpyAsync(off.data(), d->offsets.p, (n + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
-    const size_t total = (size_t)off[n];
-    if (total > 0xFFFFFFFFull) return fail(GN_E_CAPACITY, "children exceed 32-bit offsets");
-    for (size_t i = 0; i <= n; ++i) child_offsets[i] = (uint32_t)off[i];
-    if (total > cap) return fail(GN_E_CAPACITY, "%zu children exceed capacity %zu", total, cap);
-    if (total && (!child_moves || !child_out)) return fail(GN_E_INVALID, "NULL child buffer");
-    HIP_TRY(d->moves.ensure(std::max<size_t>(total, 1)));
-    size_t t = 0;
-    rc = generate_children(*d, d->io_boards.p, n, nullptr, 0, d->moves.p, ctx->incremental, &t, s, nullptr);
-    if (rc) return rc;
-    HIP_TRY(d->io_out.ensure(n));
-    HIP_TRY(d->io_out2.ensure(std::max<size_t>(t, 1)));
-    rc = expand_evaluate(ctx, *d, d->io_boards.p, n, d->frontier[1].p, t, mode, d->io_out.p, d->io_out2.p, s, nullptr);
-    if (rc) return rc;
-    if (t) {
-      HIP_TRY(hipMemcpyAsync(child_out, d->io_out2.p, t * sizeof(gn_eval), hipMemcpyDeviceToHost, s));
-      HIP_TRY(hipMemcpyAsync(child_moves, d->moves.p, t * sizeof(uint16_t), hipMemcpyDeviceToHost, s));
-    }
-    if (parent_out) HIP_TRY(hipMemcpyAsync(parent_out, d->io_out.p, n * sizeof(gn_eval), hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
-    return GN_OK;
+    return expand_boards_host(ctx, boards.data(), n, mode, parent_out, child_offsets, child_moves, child_out, cap);
   } catch (const std::bad_alloc &) {
     return fail(GN_E_NOMEM, "host allocation failed");
   } catch (...) {

@@ -8,9 +8,15 @@
 // count / write children, count_sum   legal movegen for expansion and perft.
 #include <stdlib.h>
 
+#include <algorithm>
+
 #include <hipcub/hipcub.hpp>
 
 #include "kernels.h"
+
+#ifndef GN_EXPAND_WPE
+#define GN_EXPAND_WPE 4
+#endif
 
 namespace gn {
 
@@ -91,13 +97,13 @@ constexpr int LS_SCRATCH = 16 * 16 * 4 + 16 * 32 + 16 * 4; // acc + in1 + fwd = 
 
 template <int L1, int NW, class Valid, class Emit>
 __device__ __forceinline__ void layer_stack_tile(const NetDevice &net, const uint8_t *xt, uint8_t *ls,
-                                                 const int32_t (*psq)[2], const int *bkt, uint32_t bm,
+                                                 const int32_t (*psq)[2], int tid, uint32_t bm,
                                                  Valid &&valid, Emit &&emit) {
   constexpr int XS = L1 + 16, KS = L1 / 64;
   int32_t *acc0 = reinterpret_cast<int32_t *>(ls);                 // [16 pos][16 out]
   uint8_t(*in1)[32] = reinterpret_cast<uint8_t(*)[32]>(ls + 1024); // [16][32]
   int32_t *fwd = reinterpret_cast<int32_t *>(ls + 1536);           // [16]
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lane = tid & 63, wave = tid >> 6;
   const int row = lane & 15, kg = lane >> 4;
   uint32_t m = bm;
   while (m) {
@@ -320,24 +326,80 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR)
   __syncthreads();
 
   // ---- phase 2: layer stack (MFMA), one wave per distinct bucket in the tile
-  layer_stack_tile<L1, NW>(net, xt, scratch, psq, bkt, bmask, [&](int pos, int b) {
+  layer_stack_tile<L1, NW>(net, xt, scratch, psq, (int)threadIdx.x, bmask, [&](int pos, int b) {
     return base + pos < n && nfeat[pos] && bkt[pos] == b;
   }, [&](int pos, int2 v) { out[gidx[pos]] = v; });
 }
 
 // ---------------------------------------------------------- expand_eval --
+// One row program of a slot perspective: lo/hi (and, on psq lanes, ps) -=
+// rows rr[k] for k < ns, += rows rr[k] for ns <= k < n; up to 4 rows in flight,
+// no loads for absent entries.  save: the batch holding entry 0 also stores
+// base = (accumulator before it) - row(rr[0]) (the sibling cache of expand_eval).
+template <int L1>
+__device__ __forceinline__ void run_rows(const uint8_t *__restrict__ ft, uint32_t j16, const uint16_t *rr, int k,
+                                         int ns, int n, bool psl, uint32_t psb, bool save, ushort8 &base_lo,
+                                         ushort8 &base_hi, ushort8 &lo, ushort8 &hi, uint32_t &ps) {
+  constexpr uint32_t RS = 2 * L1 + 32;
+#pragma unroll 1
+  for (; k < n; k += 4) {
+    ushort8 a0, a1, a2, a3, b0, b1, b2, b3;
+    uint32_t p0 = 0, p1 = 0, p2 = 0, p3 = 0;
+    const uint32_t o0 = ft_row(rr[k]) * RS;
+    a0 = ldft(ft, j16 + o0), b0 = ldft(ft, j16 + o0 + L1);
+    if (psl) p0 = ldpd(ft, o0 + psb);
+    if (k + 1 < n) {
+      const uint32_t o1 = ft_row(rr[k + 1]) * RS;
+      a1 = ldft(ft, j16 + o1), b1 = ldft(ft, j16 + o1 + L1);
+      if (psl) p1 = ldpd(ft, o1 + psb);
+    }
+    if (k + 2 < n) {
+      const uint32_t o2 = ft_row(rr[k + 2]) * RS;
+      a2 = ldft(ft, j16 + o2), b2 = ldft(ft, j16 + o2 + L1);
+      if (psl) p2 = ldpd(ft, o2 + psb);
+    }
+    if (k + 3 < n) {
+      const uint32_t o3 = ft_row(rr[k + 3]) * RS;
+      a3 = ldft(ft, j16 + o3), b3 = ldft(ft, j16 + o3 + L1);
+      if (psl) p3 = ldpd(ft, o3 + psb);
+    }
+    if (save && k == 0) base_lo = lo - a0, base_hi = hi - b0;
+    if (k < ns) lo -= a0, hi -= b0, ps -= p0;
+    else lo += a0, hi += b0, ps += p0;
+    if (k + 1 < n) {
+      if (k + 1 < ns) lo -= a1, hi -= b1, ps -= p1;
+      else lo += a1, hi += b1, ps += p1;
+    }
+    if (k + 2 < n) {
+      if (k + 2 < ns) lo -= a2, hi -= b2, ps -= p2;
+      else lo += a2, hi += b2, ps += p2;
+    }
+    if (k + 3 < n) {
+      if (k + 3 < ns) lo -= a3, hi -= b3, ps -= p3;
+      else lo += a3, hi += b3, ps += p3;
+    }
+  }
+}
+
 // Incremental evaluation of every legal child of a parent (SURVEY.md §8a row
 // a14, "children are derived from the parent accumulator by incremental
-// add/sub deltas").  One workgroup per parent; slot list = [parent, child_0 ..
-// child_{nc-1}] in tiles of 16.  Threads are split by ABSOLUTE perspective
-// (h = 0 white, 1 black) because the side to move alternates between parent
-// and children; h is mapped to the stm / ~stm half of the transformed
-// features per slot.  The parent accumulators (refreshed once) stay in
-// registers (big net) or LDS (small net, PAR > 1); a child perspective is
-//   parent_acc - rows(removed) + rows(added)   (1-3 rows each, Dirty),
-// or a refresh from the bias when that perspective's own king moved.
+// add/sub deltas").  One workgroup per parent (or, persistent, a strided walk
+// over parents); slot list = [parent, child_0 .. child_{nc-1}] in tiles of 16.
+// Threads are split by ABSOLUTE perspective (h = 0 white, 1 black) because the
+// side to move alternates between parent and children; h is mapped to the stm
+// / ~stm half of the transformed features per slot.  The parent accumulators
+// (refreshed once) stay in registers (big net) or LDS (small net, PAR > 1).
+// Each slot perspective runs one row program (run_rows):
+//   delta child:  parent - rows(removed) + rows(added)   (1-3 rows each, Dirty);
+//                 entry 0 is the mover's from-row, and (parent - that row) is
+//                 kept in registers while consecutive siblings move the same piece;
+//   king moved:   bias + all rows of that perspective (refresh);
+//   parent:       its accumulators as they are.
+// Register budget: <= 88 VGPRs so that three 384-thread workgroups (the LDS
+// limit) are resident per CU (tools/occupancy_probe.hip: 6-wave workgroups above
+// 128 VGPRs run one per CU).
 template <int L1, int PAR>
-__global__ void __launch_bounds__(2 * (L1 / 16) * PAR) __attribute__((amdgpu_waves_per_eu(3)))
+__global__ void __launch_bounds__(2 * (L1 / 16) * PAR) __attribute__((amdgpu_waves_per_eu(GN_EXPAND_WPE)))
     expand_eval_kernel(NetDevice net, const gn_board *__restrict__ parents, const uint64_t *__restrict__ offsets,
                        const gn_board *__restrict__ children, const ChildDelta *__restrict__ deltas,
                        const uint8_t *__restrict__ need_parent,
@@ -358,235 +420,198 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR) __attribute__((amdgpu_wav
   __shared__ __attribute__((aligned(16))) int32_t pps_lds[2][8];
   __shared__ uint16_t prow[2][32];
   __shared__ int32_t psq[TILE][2];
-  __shared__ int nsub[TILE][2], nadd[TILE][2], usep[TILE][2], sstm[TILE], bkt[TILE], valid[TILE];
+  __shared__ uint8_t nsub[TILE][2], ncnt[TILE][2], usep[TILE][2], sstm[TILE], bkt[TILE], valid[TILE];
   __shared__ int pcount, njobs;
   __shared__ uint8_t jobs[TILE * 2];
   __shared__ uint32_t bmask;
   uint16_t(*rows)[2][32] = reinterpret_cast<uint16_t(*)[2][32]>(scratch);
 
   const int tid = threadIdx.x;
-  // XCD-aware parent order: each XCD takes a contiguous range of parents, so
-  // the parents of one game (same kings, mostly the same pieces) and their
-  // children share that XCD's L2
-  size_t p = blockIdx.x;
-  if (swz) {
-    const size_t p8 = (n_parents + 7) / 8;
-    p = (blockIdx.x & 7) * p8 + (blockIdx.x >> 3);
-    if (p >= n_parents) return;
-  }
-  const uint64_t off = offsets[p];
-  const int nc = (int)(offsets[p + 1] - off);
-  const int total = 1 + nc;
-
-  // ---- pre-phase: is any slot needed?  parent feature rows (both perspectives)
-  int want = 0;
-  for (int q = tid; q < total; q += NT)
-    want |= q == 0 ? (need_parent ? need_parent[p] : 1) : (need_child ? need_child[off + q - 1] : 1);
-  if (tid < 64) {
-    const int c = wave_features(parents[p], prow[0], prow[1], tid);
-    if (tid == 0) pcount = c;
-  }
-  if (!__syncthreads_or(want)) return;
-  if (!pcount) return;
-
   const int q = tid / (2 * G), h = (tid / G) & 1, j = tid % G;
   const uint32_t j16 = 16 * j; // byte offset of this thread's columns in a row
-  const uint32_t pso = 2 * L1 + 16 * (j & 1); // this thread's 4 PSQT buckets (j < 2 only)
-  const int4v zero4 = {0, 0, 0, 0};
-
-  // parent accumulators: bias + all rows (group q == 0), kept for every child; the
-  // parent's 8 PSQT sums go to LDS (children read one bucket each)
-  ushort8 pacc_lo = *reinterpret_cast<const ushort8 *>(net.bias + 8 * j);
-  ushort8 pacc_hi = *reinterpret_cast<const ushort8 *>(net.bias + L1 / 2 + 8 * j);
-  if (q == 0 && !(ablate & 1)) {
-    int4v pps = zero4;
-    const int cnt = pcount;
-    int k = 0;
-    for (; k + 4 <= cnt; k += 4) {
-      const uint32_t o0 = ft_row(prow[h][k]) * RS, o1 = ft_row(prow[h][k + 1]) * RS, o2 = ft_row(prow[h][k + 2]) * RS, o3 = ft_row(prow[h][k + 3]) * RS;
-      const ushort8 a0 = ldft(net.ft, j16 + o0), a1 = ldft(net.ft, j16 + o1);
-      const ushort8 a2 = ldft(net.ft, j16 + o2), a3 = ldft(net.ft, j16 + o3);
-      const ushort8 b0 = ldft(net.ft, j16 + o0 + L1), b1 = ldft(net.ft, j16 + o1 + L1);
-      const ushort8 b2 = ldft(net.ft, j16 + o2 + L1), b3 = ldft(net.ft, j16 + o3 + L1);
-      if (j < 2) {
-        pps += ldps(net.ft, o0 + pso) + ldps(net.ft, o1 + pso);
-        pps += ldps(net.ft, o2 + pso) + ldps(net.ft, o3 + pso);
-      }
-      pacc_lo += (a0 + a1) + (a2 + a3);
-      pacc_hi += (b0 + b1) + (b2 + b3);
+  // Persistent when gridDim.x < the virtual grid: workgroup b walks virtual blocks
+  // b, b + gridDim.x, ... (gridDim.x is a multiple of 8, so every virtual block of a
+  // workgroup maps to the same XCD's parent range, in order)
+  const size_t vgrid = swz ? 8 * ((n_parents + 7) / 8) : n_parents;
+  for (size_t v = blockIdx.x; v < vgrid; v += gridDim.x) {
+    __syncthreads(); // LDS of the previous parent is dead
+    // XCD-aware parent order: each XCD takes a contiguous range of parents, so
+    // the parents of one game (same kings, mostly the same pieces) and their
+    // children share that XCD's L2
+    size_t p = v;
+    if (swz) {
+      const size_t p8 = (n_parents + 7) / 8;
+      p = (v & 7) * p8 + (v >> 3);
+      if (p >= n_parents) continue;
     }
-    if (k < cnt) { // tail of 1-3 rows as one batch
-      const int k1 = k + 1 < cnt ? k + 1 : k, k2 = k + 2 < cnt ? k + 2 : k;
-      const uint32_t o0 = ft_row(prow[h][k]) * RS, o1 = ft_row(prow[h][k1]) * RS, o2 = ft_row(prow[h][k2]) * RS;
-      const ushort8 a0 = ldft(net.ft, j16 + o0), a1 = ldft(net.ft, j16 + o1);
-      const ushort8 a2 = ldft(net.ft, j16 + o2);
-      const ushort8 b0 = ldft(net.ft, j16 + o0 + L1), b1 = ldft(net.ft, j16 + o1 + L1);
-      const ushort8 b2 = ldft(net.ft, j16 + o2 + L1);
-      int4v p0 = zero4, p1 = zero4, p2 = zero4;
-      if (j < 2) {
-        p0 = ldps(net.ft, o0 + pso), p1 = ldps(net.ft, o1 + pso);
-        p2 = ldps(net.ft, o2 + pso);
+    const uint64_t off = offsets[p];
+    const int total = 1 + (int)(offsets[p + 1] - off);
+
+    // ---- pre-phase: is any slot needed?  parent feature rows (both perspectives)
+    int want = 0;
+    for (int qq = tid; qq < total; qq += NT)
+      want |= qq == 0 ? (need_parent ? need_parent[p] : 1) : (need_child ? need_child[off + qq - 1] : 1);
+    if (tid < 64) {
+      const int c = wave_features(parents[p], prow[0], prow[1], tid);
+      if (tid == 0) pcount = c;
+    }
+    if (!__syncthreads_or(want)) continue;
+    if (!pcount) continue;
+
+    // parent accumulators: bias + all rows (group q == 0), kept for every child; the
+    // parent's 8 PSQT sums go to LDS (children read one bucket each)
+    ushort8 pacc_lo = *reinterpret_cast<const ushort8 *>(net.bias + 8 * j);
+    ushort8 pacc_hi = *reinterpret_cast<const ushort8 *>(net.bias + L1 / 2 + 8 * j);
+    if (q == 0 && !(ablate & 1)) {
+      const uint32_t pso = 2 * L1 + 16 * (j & 1); // this thread's 4 PSQT buckets (j < 2 only)
+      int4v pps = {0, 0, 0, 0};
+      const int cnt = pcount;
+#pragma unroll 1
+      for (int k = 0; k < cnt; k += 4) {
+        const int k1 = k + 1 < cnt ? k + 1 : k, k2 = k + 2 < cnt ? k + 2 : k, k3 = k + 3 < cnt ? k + 3 : k;
+        const uint32_t o0 = ft_row(prow[h][k]) * RS, o1 = ft_row(prow[h][k1]) * RS;
+        const uint32_t o2 = ft_row(prow[h][k2]) * RS, o3 = ft_row(prow[h][k3]) * RS;
+        const ushort8 a0 = ldft(net.ft, j16 + o0), a1 = ldft(net.ft, j16 + o1);
+        const ushort8 a2 = ldft(net.ft, j16 + o2), a3 = ldft(net.ft, j16 + o3);
+        const ushort8 b0 = ldft(net.ft, j16 + o0 + L1), b1 = ldft(net.ft, j16 + o1 + L1);
+        const ushort8 b2 = ldft(net.ft, j16 + o2 + L1), b3 = ldft(net.ft, j16 + o3 + L1);
+        if (j < 2) {
+          pps += ldps(net.ft, o0 + pso);
+          if (k + 1 < cnt) pps += ldps(net.ft, o1 + pso);
+          if (k + 2 < cnt) pps += ldps(net.ft, o2 + pso);
+          if (k + 3 < cnt) pps += ldps(net.ft, o3 + pso);
+        }
+        pacc_lo += a0, pacc_hi += b0;
+        if (k + 1 < cnt) pacc_lo += a1, pacc_hi += b1;
+        if (k + 2 < cnt) pacc_lo += a2, pacc_hi += b2;
+        if (k + 3 < cnt) pacc_lo += a3, pacc_hi += b3;
       }
-      pacc_lo += a0, pacc_hi += b0, pps += p0;
-      if (k + 1 < cnt) pacc_lo += a1, pacc_hi += b1, pps += p1;
-      if (k + 2 < cnt) pacc_lo += a2, pacc_hi += b2, pps += p2;
+      if (PAR > 1) {
+        *reinterpret_cast<ushort8 *>(pacc_lds + h * L1 + 8 * j) = pacc_lo;
+        *reinterpret_cast<ushort8 *>(pacc_lds + h * L1 + L1 / 2 + 8 * j) = pacc_hi;
+      }
+      if (j < 2) *reinterpret_cast<int4v *>(&pps_lds[h][4 * j]) = pps;
     }
     if (PAR > 1) {
-      *reinterpret_cast<ushort8 *>(pacc_lds + h * L1 + 8 * j) = pacc_lo;
-      *reinterpret_cast<ushort8 *>(pacc_lds + h * L1 + L1 / 2 + 8 * j) = pacc_hi;
+      __syncthreads();
+      pacc_lo = *reinterpret_cast<const ushort8 *>(pacc_lds + h * L1 + 8 * j);
+      pacc_hi = *reinterpret_cast<const ushort8 *>(pacc_lds + h * L1 + L1 / 2 + 8 * j);
     }
-    if (j < 2) *reinterpret_cast<int4v *>(&pps_lds[h][4 * j]) = pps;
-  }
-  if (PAR > 1) {
-    __syncthreads();
-    pacc_lo = *reinterpret_cast<const ushort8 *>(pacc_lds + h * L1 + 8 * j);
-    pacc_hi = *reinterpret_cast<const ushort8 *>(pacc_lds + h * L1 + L1 / 2 + 8 * j);
-  }
 
-  ushort8 base_lo = pacc_lo, base_hi = pacc_hi; // parent minus base_key's row (delta children)
-  int base_key = -1;
+    ushort8 base_lo = pacc_lo, base_hi = pacc_hi; // parent minus base_key's row (sibling cache)
+    int base_key = -1;
 
-  for (int t0 = 0; t0 < total; t0 += TILE) {
-    if (tid == 0) bmask = 0;
-    __syncthreads();
-    // ---- phase 0: slot descriptors (one thread per slot) from ChildDelta; king-move
-    // refreshes are queued and extracted wave-parallel (lane = square)
-    if (tid == 0) njobs = 0;
-    __syncthreads();
-    if (tid < TILE) {
-      const int qq = t0 + tid;
-      int v = 0, stm = 0, cnt = 2;
-      if (qq < total) {
-        if (qq == 0) {
-          v = need_parent ? need_parent[p] : 1;
-          stm = parents[p].stm_ep >> 7, cnt = pcount;
-          nsub[tid][0] = nsub[tid][1] = nadd[tid][0] = nadd[tid][1] = 0;
-          usep[tid][0] = usep[tid][1] = 1;
-        } else if ((v = need_child ? need_child[off + qq - 1] : 1)) {
-          const ChildDelta cd = deltas[off + qq - 1];
-          stm = (cd.meta >> 10) & 1;
-          cnt = 4 * ((cd.meta >> 11) & 7) + 1;
+#pragma unroll 1
+    for (int t0 = 0; t0 < total; t0 += TILE) {
+      // per-lane values are re-derived every tile from an opaque copy of the thread
+      // id instead of being hoisted and held live across the kernel (VGPR budget)
+      int tl = tid;
+      asm volatile("" : "+v"(tl));
+      const int qt = tl / (2 * G), ht = (tl / G) & 1, jt = tl % G;
+      if (tid == 0) bmask = 0, njobs = 0;
+      __syncthreads();
+      // ---- phase 0: slot descriptors (one thread per slot) from ChildDelta; king-move
+      // refreshes are queued and extracted wave-parallel (lane = square)
+      if (tid < TILE) {
+        const int qq = t0 + tid;
+        int vld = 0, stm = 0, cnt = 2;
+        if (qq < total) {
+          if (qq == 0) {
+            vld = need_parent ? need_parent[p] : 1;
+            stm = parents[p].stm_ep >> 7, cnt = pcount;
+            nsub[tid][0] = nsub[tid][1] = ncnt[tid][0] = ncnt[tid][1] = 0;
+            usep[tid][0] = usep[tid][1] = 1;
+          } else if ((vld = need_child ? need_child[off + qq - 1] : 1)) {
+            const ChildDelta cd = deltas[off + qq - 1];
+            stm = (cd.meta >> 10) & 1;
+            cnt = (cd.meta >> 14) & 63;
 #pragma unroll
-          for (int hh = 0; hh < 2; ++hh) {
-            if (cd.meta & (1u << (8 + hh))) {
-              usep[tid][hh] = 0, nsub[tid][hh] = 0, nadd[tid][hh] = popcnt(children[off + qq - 1].occ);
-              jobs[atomicAdd(&njobs, 1)] = (uint8_t)(tid | (hh << 4));
-            } else {
-              const int ns = (cd.meta >> (4 * hh)) & 3, na = (cd.meta >> (4 * hh + 2)) & 3;
-              rows[tid][hh][0] = cd.idx[hh][0];
-              rows[tid][hh][1] = cd.idx[hh][1];
-              rows[tid][hh][ns] = cd.idx[hh][2];
-              rows[tid][hh][ns + 1] = cd.idx[hh][3];
-              usep[tid][hh] = 1, nsub[tid][hh] = ns, nadd[tid][hh] = na;
+            for (int hh = 0; hh < 2; ++hh) {
+              if (cd.meta & (1u << (8 + hh))) {
+                usep[tid][hh] = 0, nsub[tid][hh] = 0, ncnt[tid][hh] = (uint8_t)cnt;
+                jobs[atomicAdd(&njobs, 1)] = (uint8_t)(tid | (hh << 4));
+              } else {
+                const int ns = (cd.meta >> (4 * hh)) & 3, na = (cd.meta >> (4 * hh + 2)) & 3;
+                rows[tid][hh][0] = cd.idx[hh][0];
+                rows[tid][hh][1] = cd.idx[hh][1];
+                rows[tid][hh][ns] = cd.idx[hh][2];
+                rows[tid][hh][ns + 1] = cd.idx[hh][3];
+                usep[tid][hh] = 1, nsub[tid][hh] = (uint8_t)ns, ncnt[tid][hh] = (uint8_t)(ns + na);
+              }
             }
           }
         }
+        valid[tid] = (uint8_t)vld;
+        sstm[tid] = (uint8_t)stm;
+        bkt[tid] = (uint8_t)((cnt - 1) / 4);
+        if (vld) atomicOr(&bmask, 1u << ((cnt - 1) / 4));
       }
-      valid[tid] = v;
-      sstm[tid] = stm;
-      bkt[tid] = (cnt - 1) / 4;
-      if (v) atomicOr(&bmask, 1u << ((cnt - 1) / 4));
-    }
-    __syncthreads();
-    {
-      const int lane = tid & 63, wave = tid >> 6, nj = njobs;
-      for (int jb = wave; jb < nj; jb += NW) {
-        const int sl = jobs[jb] & 15, hh = jobs[jb] >> 4;
-        const gn_board cb = children[off + t0 + sl - 1];
-        wave_features(cb, hh == 0 ? rows[sl][0] : nullptr, hh == 1 ? rows[sl][1] : nullptr, lane);
+      __syncthreads();
+      {
+        const int lane = tid & 63, wave = tid >> 6, nj = njobs;
+        for (int jb = wave; jb < nj; jb += NW) {
+          const int sl = jobs[jb] & 15, hh = jobs[jb] >> 4;
+          const gn_board cb = children[off + t0 + sl - 1];
+          wave_features(cb, hh == 0 ? rows[sl][0] : nullptr, hh == 1 ? rows[sl][1] : nullptr, lane);
+        }
       }
-    }
-    __syncthreads();
+      __syncthreads();
 
-    // ---- phase 1: accumulators + transform.  PSQT: thread j == 0 of each
-    // perspective sums the slot's own bucket (one dword per row).
+      // ---- phase 1: accumulators + transform.  PSQT: thread j == 0 of each
+      // perspective sums the slot's own bucket (one dword per row).
 #pragma unroll 1
-    for (int r = 0; r < TILE / PAR; ++r) {
-      const int sl = r * PAR + q;
-      if (!valid[sl]) continue;
-      const bool fromp = usep[sl][h];
-      const int b = bkt[sl];
-      const uint32_t psb = 2 * L1 + 4 * b;
-      ushort8 lo, hi;
-      uint32_t ps = fromp ? (uint32_t)pps_lds[h][b] : 0u;
-      const uint16_t *rr = rows[sl][h];
-      const int ns = nsub[sl][h], end = ns + nadd[sl][h];
-      if (fromp) lo = pacc_lo, hi = pacc_hi;
-      if (ablate & 2) {
-        if (!fromp) lo = pacc_lo, hi = pacc_hi;
-      } else if (fromp && end > 0) {
-        // delta child: entry 0 is always the mover's from-row (subtracted).  Siblings are
-        // generated per from-square, so (parent - that row) is kept in registers and
-        // reused while consecutive children move the same piece; the remaining 1-3 entries
-        // are loaded together, without duplicate loads for short deltas.
-        const int key = rr[0];
-        const bool hit = key == base_key;
-        ushort8 a0, b0, a1, b1, a2, b2, a3, b3;
-        uint32_t p0 = 0, p1 = 0, p2 = 0, p3 = 0;
-        const uint32_t o0 = ft_row(rr[0]) * RS, o1 = ft_row(rr[1]) * RS;
-        const uint32_t o2 = ft_row(rr[end > 2 ? 2 : 1]) * RS, o3 = ft_row(rr[end > 3 ? 3 : 1]) * RS;
-        if (!hit) a0 = ldft(net.ft, j16 + o0), b0 = ldft(net.ft, j16 + o0 + L1);
-        if (end > 1) a1 = ldft(net.ft, j16 + o1), b1 = ldft(net.ft, j16 + o1 + L1);
-        if (end > 2) a2 = ldft(net.ft, j16 + o2), b2 = ldft(net.ft, j16 + o2 + L1);
-        if (end > 3) a3 = ldft(net.ft, j16 + o3), b3 = ldft(net.ft, j16 + o3 + L1);
-        if (j == 0) {
-          p0 = ldpd(net.ft, o0 + psb);
-          if (end > 1) p1 = ldpd(net.ft, o1 + psb);
-          if (end > 2) p2 = ldpd(net.ft, o2 + psb);
-          if (end > 3) p3 = ldpd(net.ft, o3 + psb);
-        }
-        if (!hit) base_lo = pacc_lo - a0, base_hi = pacc_hi - b0, base_key = key;
-        lo = base_lo, hi = base_hi, ps -= p0;
-        // entry 1 is a removed row when ns == 2, else an added one; entries 2, 3 are added
-        if (end > 1) lo = ns > 1 ? lo - a1 : lo + a1, hi = ns > 1 ? hi - b1 : hi + b1, ps = ns > 1 ? ps - p1 : ps + p1;
-        if (end > 2) lo += a2, hi += b2, ps += p2;
-        if (end > 3) lo += a3, hi += b3, ps += p3;
-      } else if (!fromp) {
-        // refresh (own king moved): bias + adds only, 4 rows in flight
-        lo = *reinterpret_cast<const ushort8 *>(net.bias + 8 * j);
-        hi = *reinterpret_cast<const ushort8 *>(net.bias + L1 / 2 + 8 * j);
-        for (int k = 0; k < end; k += 4) {
-          const int k1 = k + 1 < end ? k + 1 : k, k2 = k + 2 < end ? k + 2 : k, k3 = k + 3 < end ? k + 3 : k;
-          const uint32_t o0 = ft_row(rr[k]) * RS, o1 = ft_row(rr[k1]) * RS, o2 = ft_row(rr[k2]) * RS, o3 = ft_row(rr[k3]) * RS;
-          const ushort8 a0 = ldft(net.ft, j16 + o0), a1 = ldft(net.ft, j16 + o1);
-          const ushort8 a2 = ldft(net.ft, j16 + o2), a3 = ldft(net.ft, j16 + o3);
-          const ushort8 b0 = ldft(net.ft, j16 + o0 + L1), b1 = ldft(net.ft, j16 + o1 + L1);
-          const ushort8 b2 = ldft(net.ft, j16 + o2 + L1), b3 = ldft(net.ft, j16 + o3 + L1);
-          uint32_t p0 = 0, p1 = 0, p2 = 0, p3 = 0;
-          if (j == 0) {
-            p0 = ldpd(net.ft, o0 + psb), p1 = ldpd(net.ft, o1 + psb);
-            p2 = ldpd(net.ft, o2 + psb), p3 = ldpd(net.ft, o3 + psb);
+      for (int r = 0; r < TILE / PAR; ++r) {
+        const int sl = r * PAR + qt;
+        if (!valid[sl]) continue;
+        const bool fromp = usep[sl][ht];
+        const int b = bkt[sl], ns = nsub[sl][ht], n = ncnt[sl][ht];
+        const uint16_t *rr = rows[sl][ht];
+        ushort8 lo, hi;
+        uint32_t ps = 0;
+        int k = 0;
+        bool save = false;
+        if (!fromp) {
+          lo = *reinterpret_cast<const ushort8 *>(net.bias + 8 * jt);
+          hi = *reinterpret_cast<const ushort8 *>(net.bias + L1 / 2 + 8 * jt);
+        } else {
+          ps = (uint32_t)pps_lds[ht][b];
+          if (n > 0 && rr[0] == base_key) {
+            lo = base_lo, hi = base_hi, k = 1;
+            if (jt == 0) ps -= ldpd(net.ft, ft_row(rr[0]) * RS + 2 * L1 + 4 * b);
+          } else {
+            lo = pacc_lo, hi = pacc_hi, save = n > 0;
           }
-          lo += a0, hi += b0, ps += p0;
-          if (k + 1 < end) lo += a1, hi += b1, ps += p1;
-          if (k + 2 < end) lo += a2, hi += b2, ps += p2;
-          if (k + 3 < end) lo += a3, hi += b3, ps += p3;
         }
-      }
-      const int side = h == sstm[sl] ? 0 : 1;
-      uint32_t w0 = 0, w1 = 0;
+        if (!(ablate & 2)) {
+          run_rows<L1>(net.ft, 16 * jt, rr, k, ns, n, jt == 0, 2 * L1 + 4 * b, save, base_lo, base_hi, lo, hi, ps);
+          if (save) base_key = rr[0];
+        }
+        const int side = ht == sstm[sl] ? 0 : 1;
+        uint32_t w0 = 0, w1 = 0;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int a = clampi((short)lo[e], 0, 254), c = clampi((short)hi[e], 0, 254);
-        const uint32_t v = (uint32_t)(a * c) >> 9;
-        if (e < 4) w0 |= v << (8 * e);
-        else w1 |= v << (8 * (e - 4));
+        for (int e = 0; e < 8; ++e) {
+          const int a = clampi((short)lo[e], 0, 254), c = clampi((short)hi[e], 0, 254);
+          const uint32_t vv = (uint32_t)(a * c) >> 9;
+          if (e < 4) w0 |= vv << (8 * e);
+          else w1 |= vv << (8 * (e - 4));
+        }
+        *reinterpret_cast<uint2 *>(xt + sl * XS + side * (L1 / 2) + 8 * jt) = make_uint2(w0, w1);
+        if (jt == 0) psq[sl][side] = (int32_t)ps;
       }
-      *reinterpret_cast<uint2 *>(xt + sl * XS + side * (L1 / 2) + 8 * j) = make_uint2(w0, w1);
-      if (j == 0) psq[sl][side] = (int32_t)ps;
-    }
-    __syncthreads();
+      __syncthreads();
 
-    // ---- phase 2: layer stack
-    if (!(ablate & 4)) layer_stack_tile<L1, NW>(net, xt, scratch, psq, bkt, bmask, [&](int pos, int b) {
-      return t0 + pos < total && valid[pos] && bkt[pos] == b;
-    }, [&](int pos, int2 v) {
-      if (t0 + pos == 0) out_parent[p] = v;
-      else out_child[off + t0 + pos - 1] = v;
-    });
+      // ---- phase 2: layer stack
+      if (!(ablate & 4)) {
+        layer_stack_tile<L1, NW>(net, xt, scratch, psq, tl, bmask, [&](int pos, int bb) {
+          return t0 + pos < total && valid[pos] && bkt[pos] == bb;
+        }, [&](int pos, int2 val) {
+          if (t0 + pos == 0) out_parent[p] = val;
+          else out_child[off + t0 + pos - 1] = val;
+        });
+      }
+    }
   }
 }
-
 
 hipError_t launch_eval_net(const NetDevice &net, const gn_board *boards, const uint8_t *need, size_t n, int2 *out,
                            const uint32_t *perm, int swz, hipStream_t s) {
@@ -920,8 +945,10 @@ hipError_t launch_expand_net(const NetDevice &net, const gn_board *parents, size
                              const gn_board *children, const ChildDelta *deltas, const uint8_t *need_parent,
                              const uint8_t *need_child, int2 *out_parent, int2 *out_child, int swz, hipStream_t s) {
   if (!n) return hipSuccess;
-  const unsigned g = (unsigned)(swz ? 8 * ((n + 7) / 8) : n);
+  unsigned g = (unsigned)(swz ? 8 * ((n + 7) / 8) : n);
   static const int ablate = getenv("GN_ABLATE") ? atoi(getenv("GN_ABLATE")) : 0; // timing diagnostics only
+  static const int persist = getenv("GN_PERSIST") ? atoi(getenv("GN_PERSIST")) : 0; // WGs per CU, 0: one per parent
+  if (persist > 0) g = std::min<unsigned>(g, 8u * ((256u * (unsigned)persist + 7) / 8));
 #define GN_EXPAND_ARGS net, parents, offsets, children, deltas, need_parent, need_child, out_parent, out_child, n, swz, ablate
   if (net.L1 == 3072) {
     hipLaunchKernelGGL((expand_eval_kernel<3072, 1>), dim3(g), dim3(384), 0, s, GN_EXPAND_ARGS);

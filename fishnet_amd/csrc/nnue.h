@@ -57,7 +57,7 @@ GN_HD int feature_index(int persp, int sq, int pc, int ksq) {
 struct ChildDelta {
   uint16_t idx[2][4];
   uint32_t meta; // [1:0] nsub w, [3:2] nadd w, [5:4] nsub b, [7:6] nadd b, [8] refresh w, [9] refresh b,
-                 // [10] stm, [13:11] bucket
+                 // [10] stm, [13:11] bucket, [19:14] child piece count
   uint32_t pad;
 };
 static_assert(sizeof(ChildDelta) == 24, "ChildDelta is 24 bytes");
@@ -81,6 +81,7 @@ GN_HD ChildDelta make_child_delta(const Board &parent, const Board &child, const
   }
   meta |= (uint32_t)child.stm << 10;
   meta |= (uint32_t)((popcnt(child.byType[0]) - 1) / 4) << 11;
+  meta |= (uint32_t)popcnt(child.byType[0]) << 14;
   cd.meta = meta;
   cd.pad = 0;
   return cd;
