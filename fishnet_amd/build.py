@@ -27,27 +27,33 @@ def _stale():
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and not _stale():
+def build(force: bool = False, verbose: bool = False, defines=(), out: str | None = None) -> str:
+    """defines/out: experiment variants (e.g. -DGN_EXPAND_WPE=5 into lib/libgpu_nnue_w5.so),
+    selected at run time with GPU_NNUE_LIB; the default build has neither."""
+    lib = out or LIB
+    if not force and not defines and not _stale():
         return LIB
     os.makedirs(LIBDIR, exist_ok=True)
     objs = []
     for src in SOURCES:
-        obj = os.path.join(LIBDIR, src.replace(".hip", ".o"))
+        obj = os.path.join(LIBDIR, src.replace(".hip", f".{os.getpid()}.o"))
         cmd = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden",
-               "-Wall", "-Wno-unused-function", "-c", os.path.join(CSRC, src), "-o", obj]
+               "-Wall", "-Wno-unused-function", *defines, "-c", os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)
         objs.append(obj)
-    tmp = LIB + f".tmp{os.getpid()}"
+    tmp = lib + f".tmp{os.getpid()}"
     cmd = ["hipcc", f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs + ["-lpthread"]
     subprocess.run(cmd, check=True)
-    os.replace(tmp, LIB)
+    os.replace(tmp, lib)
     for o in objs:
         os.remove(o)
-    return LIB
+    return lib
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True))
+    defs = [a for a in sys.argv[1:] if a.startswith("-D")]
+    outs = [a[len("--out="):] for a in sys.argv[1:] if a.startswith("--out=")]
+    print(build(force="--force" in sys.argv, verbose=True, defines=defs,
+                out=os.path.join(LIBDIR, outs[0]) if outs else None))

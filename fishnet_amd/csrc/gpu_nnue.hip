@@ -608,8 +608,196 @@ static int expand_boards_host(gn_ctx *ctx, const gn_board *boards, size_t n, int
   }
 }
 
+// ------------------------------------------------- lichess batch replay ----
+// IncomingBatch::from_acquired (/root/reference/src/queue.rs:548-700) for the
+// GPU path.  The root FEN is set up with Chess960 castling, ignoring an invalid
+// en-passant square or castling right (queue.rs:554-560).  Every UCI move of
+// AcquireResponseBody.moves (/root/reference/src/api.rs:306-321) is resolved as
+// shakmaty 0.27.3's UciMove::to_move resolves it (queue.rs:576) and played
+// (queue.rs:578).  That gives positions 0..=len, position i being the root after
+// i moves (queue.rs:605-637); skipPositions marks the ones not analysed
+// (queue.rs:617, 633).  A move that does not resolve to a legal move fails the
+// game, as `uci.to_move(&pos)?` fails the whole batch in the reference.
+
+static int uci_square(const char *s) {
+  if (s[0] < 'a' || s[0] > 'h' || s[1] < '1' || s[1] > '8') return -1;
+  return (s[1] - '1') * 8 + (s[0] - 'a');
+}
+
+// shakmaty 0.27.3 UciMove::to_move, standard chess:
+//   the king moving onto a square of the castling rights => castling with that rook
+//   (Chess960 notation, king takes rook);
+//   the king moving from e1/e8 to the c/g file of its back rank => castling with the
+//   a/h rook (standard notation);
+//   otherwise the move from `from` to `to` (en passant included) with the promotion
+//   piece of the 5th character;
+// and the candidate must be legal.
+static bool uci_to_move(const Board &B, const char *u, size_t len, uint16_t &out) {
+  if (len != 4 && len != 5) return false;
+  const int from = uci_square(u), to = uci_square(u + 2);
+  if (from < 0 || to < 0) return false;
+  int promo = 0;
+  if (len == 5) {
+    static const char P[] = "nbrq";
+    const char *c = (u[4] != '\0') ? strchr(P, u[4]) : nullptr;
+    if (!c) return false;
+    promo = KNIGHT + (int)(c - P);
+  }
+  const int pc = piece_on(B, from);
+  if (!pc || (promo && (pc & 7) != PAWN)) return false;
+  const int us = B.stm;
+  int rook = -1;
+  if ((pc & 7) == KING) {
+    for (int i = 0; i < 4; ++i)
+      if (B.castle_rook[i] == to) rook = to;
+    if (rook < 0 && from == (us ? 60 : 4) && (to >> 3) == (us ? 7 : 0) && ((to & 7) == 2 || (to & 7) == 6))
+      rook = (to & 56) | ((to & 7) == 2 ? 0 : 7);
+  }
+  uint16_t mv[256];
+  const int n = legal_moves(B, mv);
+  for (int i = 0; i < n; ++i) {
+    const uint16_t m = mv[i];
+    if (move_from(m) != from) continue;
+    const int t = move_type(m);
+    if (rook >= 0) {
+      if (t == MT_CASTLING && move_to(m) == rook) return out = m, true;
+      continue;
+    }
+    if (t == MT_CASTLING || move_to(m) != to) continue;
+    if (t == MT_PROMOTION ? move_promo(m) != promo : promo != 0) continue;
+    return out = m, true;
+  }
+  return false;
+}
+
+struct Replay {
+  std::vector<gn_board> boards; // positions 0..=len
+  std::vector<uint16_t> moves;  // len moves, Stockfish encoding (castling = king takes rook)
+  std::vector<uint8_t> skip;    // per position
+  int rc = GN_OK;
+  std::string err;
+};
+
+static void replay_game(const gn_game &g, Replay &r) {
+  Board B;
+  if (!g.root_fen || !parse_fen(g.root_fen, B)) {
+    r.rc = GN_E_INVALID, r.err = "bad root FEN";
+    return;
+  }
+  gn_board pb;
+  pack(B, pb);
+  r.boards.push_back(pb);
+  const char *s = g.uci_moves ? g.uci_moves : "";
+  while (*s) {
+    while (*s == ' ' || *s == '\t' || *s == '\n' || *s == '\r') ++s;
+    if (!*s) break;
+    const char *e = s;
+    while (*e && *e != ' ' && *e != '\t' && *e != '\n' && *e != '\r') ++e;
+    uint16_t m = 0;
+    if (!uci_to_move(B, s, (size_t)(e - s), m)) {
+      char buf[96];
+      snprintf(buf, sizeof(buf), "move %zu (%.*s) is not legal", r.moves.size() + 1, (int)std::min<ptrdiff_t>(e - s, 16), s);
+      r.rc = GN_E_ILLEGAL_MOVE, r.err = buf;
+      r.boards.clear(), r.moves.clear();
+      return;
+    }
+    B = do_move(B, m);
+    pack(B, pb);
+    r.boards.push_back(pb);
+    r.moves.push_back(m);
+    s = e;
+  }
+  r.skip.assign(r.boards.size(), 0);
+  for (size_t k = 0; k < g.n_skip; ++k)
+    if (g.skip_positions && g.skip_positions[k] < r.skip.size()) r.skip[g.skip_positions[k]] = 1;
+}
+
 // ============================================================ C-ABI ========
 extern "C" {
+
+int gn_replay_game(const gn_game *game, gn_board *positions, uint8_t *skipped, uint16_t *moves, size_t cap,
+                   size_t *n_positions) {
+  if (!game || !n_positions) return fail(GN_E_INVALID, "NULL argument");
+  try {
+    Replay r;
+    replay_game(*game, r);
+    *n_positions = r.boards.size();
+    if (r.rc) return fail(r.rc, "%s", r.err.c_str());
+    if (r.boards.size() > cap) return fail(GN_E_CAPACITY, "%zu positions exceed capacity %zu", r.boards.size(), cap);
+    if (positions) memcpy(positions, r.boards.data(), r.boards.size() * sizeof(gn_board));
+    if (skipped) memcpy(skipped, r.skip.data(), r.skip.size());
+    if (moves && !r.moves.empty()) memcpy(moves, r.moves.data(), r.moves.size() * sizeof(uint16_t));
+    return GN_OK;
+  } catch (const std::bad_alloc &) {
+    return fail(GN_E_NOMEM, "host allocation failed");
+  }
+}
+
+int gn_evaluate_games(gn_ctx *ctx, const gn_game *games, size_t n_games, int mode, int with_children,
+                      uint32_t *position_offsets, int32_t *game_status, gn_eval *position_out, size_t position_cap,
+                      uint32_t *child_offsets, uint16_t *child_moves, gn_eval *child_out, size_t child_cap) {
+  if (!slot(ctx, 0)) return fail(GN_E_INVALID, "bad context");
+  if (n_games && (!games || !position_offsets || !game_status)) return fail(GN_E_INVALID, "NULL argument");
+  if (with_children && !child_offsets) return fail(GN_E_INVALID, "child_offsets is NULL");
+  if (mode < GN_MODE_FULL || mode > GN_MODE_SMALL) return fail(GN_E_INVALID, "bad mode %d", mode);
+  try {
+    std::vector<Replay> rep(n_games);
+    parallel_for(n_games, 64, [&](size_t lo, size_t hi) {
+      for (size_t i = lo; i < hi; ++i) replay_game(games[i], rep[i]);
+    });
+    size_t total = 0;
+    std::string last_err;
+    for (size_t i = 0; i < n_games; ++i) {
+      position_offsets[i] = (uint32_t)total;
+      game_status[i] = rep[i].rc;
+      if (rep[i].rc) last_err = rep[i].err;
+      total += rep[i].boards.size();
+    }
+    if (total > 0xFFFFFFFFull) return fail(GN_E_CAPACITY, "positions exceed 32-bit offsets");
+    position_offsets[n_games] = (uint32_t)total;
+    if (total > position_cap) return fail(GN_E_CAPACITY, "%zu positions exceed capacity %zu", total, position_cap);
+    if (total && !position_out) return fail(GN_E_INVALID, "position_out is NULL");
+    // positions to evaluate: every non-skipped position of every replayed game
+    std::vector<gn_board> ev;
+    std::vector<uint32_t> where;
+    for (size_t i = 0; i < n_games; ++i)
+      for (size_t k = 0; k < rep[i].boards.size(); ++k) {
+        const size_t at = position_offsets[i] + k;
+        if (rep[i].skip[k]) {
+          position_out[at] = gn_eval{0, 0, 0, GN_FLAG_SKIPPED};
+        } else {
+          ev.push_back(rep[i].boards[k]);
+          where.push_back((uint32_t)at);
+        }
+      }
+    std::vector<gn_eval> res(ev.size());
+    int rc = GN_OK;
+    std::vector<uint32_t> coff;
+    if (!with_children) {
+      rc = evaluate_boards_host(ctx, ev.data(), ev.size(), mode, res.data());
+    } else {
+      coff.assign(ev.size() + 1, 0);
+      rc = expand_boards_host(ctx, ev.data(), ev.size(), mode, res.data(), coff.data(), child_moves, child_out,
+                              child_cap);
+      if (rc == GN_OK || rc == GN_E_CAPACITY) { // child offsets over all positions (skipped: no children)
+        size_t e = 0;
+        for (size_t at = 0; at < total; ++at) {
+          child_offsets[at] = coff[e];
+          if (e < where.size() && where[e] == at) ++e;
+        }
+        child_offsets[total] = coff[ev.size()];
+      }
+    }
+    if (rc) return rc;
+    for (size_t e = 0; e < ev.size(); ++e) position_out[where[e]] = res[e];
+    if (!last_err.empty()) g_err = last_err;
+    return GN_OK;
+  } catch (const std::bad_alloc &) {
+    return fail(GN_E_NOMEM, "host allocation failed");
+  } catch (...) {
+    return fail(GN_E_INVALID, "unexpected exception");
+  }
+}
 
 int gn_abi_version(void) { return GN_ABI_VERSION; }
 

@@ -6,7 +6,9 @@
 //                     tile per workgroup.
 // classify / reeval / finalize   Eval::evaluate.
 // count / write children, count_sum   legal movegen for expansion and perft.
+#include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include <algorithm>
 
@@ -14,8 +16,31 @@
 
 #include "kernels.h"
 
+// GN_PHASE_TIMING builds (diagnostics only): thread 0 of every expand_eval
+// workgroup adds the s_memtime cycles of each phase into gn_phase_cycles.
+#ifdef GN_PHASE_TIMING
+__device__ unsigned long long gn_phase_cycles[64][8];
+#define GN_STAMP_INIT()                                                          \
+  unsigned long long gn_t_ = __builtin_amdgcn_s_memtime(), gn_acc_[6] = {0, 0, 0, 0, 0, 0}
+#define GN_STAMP(k)                                                              \
+  do {                                                                           \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime();                  \
+    gn_acc_[k] += t_ - gn_t_;                                                    \
+    gn_t_ = t_;                                                                  \
+  } while (0)
+#define GN_STAMP_FLUSH()                                                         \
+  do {                                                                           \
+    if (threadIdx.x == 0)                                                        \
+      for (int k_ = 0; k_ < 6; ++k_) atomicAdd(&gn_phase_cycles[blockIdx.x & 63][k_], gn_acc_[k_]); \
+  } while (0)
+#else
+#define GN_STAMP_INIT() (void)0
+#define GN_STAMP(k) (void)0
+#define GN_STAMP_FLUSH() (void)0
+#endif
+
 #ifndef GN_EXPAND_WPE
-#define GN_EXPAND_WPE 4
+#define GN_EXPAND_WPE 5
 #endif
 
 namespace gn {
@@ -36,6 +61,16 @@ __device__ __forceinline__ void load_tables(Tables &dst, const Tables *src) {
   uint4 *d = reinterpret_cast<uint4 *>(&dst);
   for (int i = threadIdx.x; i < (int)(sizeof(Tables) / 16); i += blockDim.x) d[i] = s[i];
   __syncthreads();
+}
+
+// Wave-uniform value as an SGPR (readfirstlane) when U: descriptors and row
+// indices of a slot perspective are the same for every lane of a wave whenever a
+// perspective group is a whole number of waves (PAR == 1, L1 / 16 % 64 == 0), so
+// control flow on them is scalar and the row offsets fold into the load's SGPR base.
+template <bool U>
+__device__ __forceinline__ int uni(int x) {
+  if constexpr (U) return __builtin_amdgcn_readfirstlane(x);
+  else return x;
 }
 
 // FT row loads as SGPR base + 32-bit VGPR offset (the table is < 4 GiB): one VGPR
@@ -75,6 +110,25 @@ __device__ __forceinline__ int wave_features(const gn_board &p, uint16_t *rows_w
     if (rows_b) rows_b[k] = (uint16_t)feature_index(BLACK, lane, pc, __builtin_ctzll(bkb));
   }
   return c;
+}
+
+// Rows of perspective h of a child in which h's own king moved, straight from
+// the parent board (lane = square): the king goes kfrom -> kto (capturing
+// whatever stood there) and, for castling, the rook rfrom -> rto (64 = none).
+// The parent must be valid (its rows were extracted).  All 64 lanes.
+__device__ __forceinline__ void wave_features_king_move(const gn_board &p, int h, int kfrom, int kto, int rfrom,
+                                                        int rto, uint16_t *rows, int lane) {
+  const uint64_t occ = p.occ;
+  const bool has = (occ >> lane) & 1;
+  const int k = popcnt(occ & ((1ull << lane) - 1));
+  uint64_t wlo, whi;
+  piece_words(p, wlo, whi);
+  int pc = has && k < 32 ? piece_nibble(wlo, whi, k) : 0;
+  if (lane == kfrom || lane == rfrom) pc = 0;
+  if (lane == rto) pc = make_piece(h, ROOK);
+  if (lane == kto) pc = make_piece(h, KING);
+  const uint64_t cocc = __ballot(pc != 0);
+  if (pc) rows[popcnt(cocc & ((1ull << lane) - 1))] = (uint16_t)feature_index(h, lane, pc, kto);
 }
 
 // ------------------------------------------------------------ layer stack --
@@ -186,6 +240,26 @@ __device__ __forceinline__ void layer_stack_tile(const NetDevice &net, const uin
     }
     __syncthreads();
   }
+}
+
+// FeatureTransformer::transform for 8 columns pairs of one perspective, packed
+// 16-bit math: clamp both halves to [0, 254] (the doubled domain), multiply
+// (<= 64516, fits u16), >> 9, then v_perm the low bytes into 8 u8 outputs.
+typedef short short2v __attribute__((ext_vector_type(2)));
+typedef unsigned short ushort2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint2 transform8(ushort8 lo, ushort8 hi) {
+  uint32_t o[4];
+  const short2v z = {0, 0}, m = {254, 254};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    short2v a = {(short)lo[2 * i], (short)lo[2 * i + 1]}, b = {(short)hi[2 * i], (short)hi[2 * i + 1]};
+    a = __builtin_elementwise_min(__builtin_elementwise_max(a, z), m);
+    b = __builtin_elementwise_min(__builtin_elementwise_max(b, z), m);
+    ushort2v pr = __builtin_bit_cast(ushort2v, a) * __builtin_bit_cast(ushort2v, b);
+    pr = pr >> (ushort2v){9, 9};
+    o[i] = __builtin_bit_cast(uint32_t, pr);
+  }
+  return make_uint2(__builtin_amdgcn_perm(o[1], o[0], 0x06040200u), __builtin_amdgcn_perm(o[3], o[2], 0x06040200u));
 }
 
 // --------------------------------------------------------------- eval_net --
@@ -311,15 +385,7 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR)
         if (k + 2 < cnt) lo += a2, hi += b2, ps += q2;
       }
       // transform: clamp to [0, 254] in the doubled domain, product / 512
-      uint32_t w0 = 0, w1 = 0;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int a = clampi((short)lo[e], 0, 254), b = clampi((short)hi[e], 0, 254);
-        const uint32_t v = (uint32_t)(a * b) >> 9;
-        if (e < 4) w0 |= v << (8 * e);
-        else w1 |= v << (8 * (e - 4));
-      }
-      *reinterpret_cast<uint2 *>(xt + p * XS + h * (L1 / 2) + 8 * j) = make_uint2(w0, w1);
+      *reinterpret_cast<uint2 *>(xt + p * XS + h * (L1 / 2) + 8 * j) = transform8(lo, hi);
       if (j == 0) psq[p][h] = (int32_t)ps;
     }
   }
@@ -336,7 +402,7 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR)
 // rows rr[k] for k < ns, += rows rr[k] for ns <= k < n; up to 4 rows in flight,
 // no loads for absent entries.  save: the batch holding entry 0 also stores
 // base = (accumulator before it) - row(rr[0]) (the sibling cache of expand_eval).
-template <int L1>
+template <int L1, bool U>
 __device__ __forceinline__ void run_rows(const uint8_t *__restrict__ ft, uint32_t j16, const uint16_t *rr, int k,
                                          int ns, int n, bool psl, uint32_t psb, bool save, ushort8 &base_lo,
                                          ushort8 &base_hi, ushort8 &lo, ushort8 &hi, uint32_t &ps) {
@@ -345,21 +411,77 @@ __device__ __forceinline__ void run_rows(const uint8_t *__restrict__ ft, uint32_
   for (; k < n; k += 4) {
     ushort8 a0, a1, a2, a3, b0, b1, b2, b3;
     uint32_t p0 = 0, p1 = 0, p2 = 0, p3 = 0;
-    const uint32_t o0 = ft_row(rr[k]) * RS;
+    const uint32_t o0 = (uint32_t)uni<U>(ft_row(rr[k])) * RS;
     a0 = ldft(ft, j16 + o0), b0 = ldft(ft, j16 + o0 + L1);
     if (psl) p0 = ldpd(ft, o0 + psb);
     if (k + 1 < n) {
-      const uint32_t o1 = ft_row(rr[k + 1]) * RS;
+      const uint32_t o1 = (uint32_t)uni<U>(ft_row(rr[k + 1])) * RS;
       a1 = ldft(ft, j16 + o1), b1 = ldft(ft, j16 + o1 + L1);
       if (psl) p1 = ldpd(ft, o1 + psb);
     }
     if (k + 2 < n) {
-      const uint32_t o2 = ft_row(rr[k + 2]) * RS;
+      const uint32_t o2 = (uint32_t)uni<U>(ft_row(rr[k + 2])) * RS;
       a2 = ldft(ft, j16 + o2), b2 = ldft(ft, j16 + o2 + L1);
       if (psl) p2 = ldpd(ft, o2 + psb);
     }
     if (k + 3 < n) {
-      const uint32_t o3 = ft_row(rr[k + 3]) * RS;
+      const uint32_t o3 = (uint32_t)uni<U>(ft_row(rr[k + 3])) * RS;
+      a3 = ldft(ft, j16 + o3), b3 = ldft(ft, j16 + o3 + L1);
+      if (psl) p3 = ldpd(ft, o3 + psb);
+    }
+    if (save && k == 0) base_lo = lo - a0, base_hi = hi - b0;
+    if (k < ns) lo -= a0, hi -= b0, ps -= p0;
+    else lo += a0, hi += b0, ps += p0;
+    if (k + 1 < n) {
+      if (k + 1 < ns) lo -= a1, hi -= b1, ps -= p1;
+      else lo += a1, hi += b1, ps += p1;
+    }
+    if (k + 2 < n) {
+      if (k + 2 < ns) lo -= a2, hi -= b2, ps -= p2;
+      else lo += a2, hi += b2, ps += p2;
+    }
+    if (k + 3 < n) {
+      if (k + 3 < ns) lo -= a3, hi -= b3, ps -= p3;
+      else lo += a3, hi += b3, ps += p3;
+    }
+  }
+}
+
+// run_rows for wave-uniform descriptors (PAR == 1 perspective groups of whole
+// waves): entries 0..3 arrive as scalars (r01 = rows 0 | 1 << 16, r23 = rows
+// 2 | 3 << 16), later entries (refreshes only) come from the LDS row list rr by
+// one lane-indexed read, so no row offset waits on an LDS round trip.
+template <int L1>
+__device__ __forceinline__ void run_rows_u(const uint8_t *__restrict__ ft, uint32_t j16, const uint16_t *rr,
+                                           uint32_t r01, uint32_t r23, int k, int ns, int n, bool psl, uint32_t psb,
+                                           bool save, ushort8 &base_lo, ushort8 &base_hi, ushort8 &lo, ushort8 &hi,
+                                           uint32_t &ps, int lane) {
+  constexpr uint32_t RS = 2 * L1 + 32;
+  const uint32_t rl = n > 4 && lane < n ? rr[lane] : 0u;
+  auto off = [&](int e) -> uint32_t {
+    uint32_t v = e == 0 ? (r01 & 0xFFFF) : e == 1 ? (r01 >> 16) : e == 2 ? (r23 & 0xFFFF) : e == 3 ? (r23 >> 16) : 0u;
+    if (e >= 4) v = (uint32_t)__builtin_amdgcn_readlane((int)rl, e);
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)ft_row(v)) * RS;
+  };
+#pragma unroll 1
+  for (; k < n; k += 4) {
+    ushort8 a0, a1, a2, a3, b0, b1, b2, b3;
+    uint32_t p0 = 0, p1 = 0, p2 = 0, p3 = 0;
+    const uint32_t o0 = off(k);
+    a0 = ldft(ft, j16 + o0), b0 = ldft(ft, j16 + o0 + L1);
+    if (psl) p0 = ldpd(ft, o0 + psb);
+    if (k + 1 < n) {
+      const uint32_t o1 = off(k + 1);
+      a1 = ldft(ft, j16 + o1), b1 = ldft(ft, j16 + o1 + L1);
+      if (psl) p1 = ldpd(ft, o1 + psb);
+    }
+    if (k + 2 < n) {
+      const uint32_t o2 = off(k + 2);
+      a2 = ldft(ft, j16 + o2), b2 = ldft(ft, j16 + o2 + L1);
+      if (psl) p2 = ldpd(ft, o2 + psb);
+    }
+    if (k + 3 < n) {
+      const uint32_t o3 = off(k + 3);
       a3 = ldft(ft, j16 + o3), b3 = ldft(ft, j16 + o3 + L1);
       if (psl) p3 = ldpd(ft, o3 + psb);
     }
@@ -399,7 +521,7 @@ __device__ __forceinline__ void run_rows(const uint8_t *__restrict__ ft, uint32_
 // limit) are resident per CU (tools/occupancy_probe.hip: 6-wave workgroups above
 // 128 VGPRs run one per CU).
 template <int L1, int PAR>
-__global__ void __launch_bounds__(2 * (L1 / 16) * PAR) __attribute__((amdgpu_waves_per_eu(GN_EXPAND_WPE)))
+__global__ void __launch_bounds__(2 * (L1 / 16) * PAR) __attribute__((amdgpu_waves_per_eu(PAR == 1 ? GN_EXPAND_WPE : 4)))
     expand_eval_kernel(NetDevice net, const gn_board *__restrict__ parents, const uint64_t *__restrict__ offsets,
                        const gn_board *__restrict__ children, const ChildDelta *__restrict__ deltas,
                        const uint8_t *__restrict__ need_parent,
@@ -414,6 +536,7 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR) __attribute__((amdgpu_wav
   constexpr int ROWS_BYTES = TILE * 2 * 32 * 2;
   constexpr int SCRATCH = ROWS_BYTES > LS_SCRATCH ? ROWS_BYTES : LS_SCRATCH;
   constexpr int PACC = PAR > 1 ? 2 * L1 : 8; // shared parent accumulators (small net only)
+  constexpr bool U = PAR == 1 && G % 64 == 0; // a perspective group = whole waves
   __shared__ __attribute__((aligned(16))) uint8_t xt[TILE * XS];
   __shared__ __attribute__((aligned(16))) uint8_t scratch[SCRATCH];
   __shared__ __attribute__((aligned(16))) uint16_t pacc_lds[PACC];
@@ -421,9 +544,18 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR) __attribute__((amdgpu_wav
   __shared__ uint16_t prow[2][32];
   __shared__ int32_t psq[TILE][2];
   __shared__ uint8_t nsub[TILE][2], ncnt[TILE][2], usep[TILE][2], sstm[TILE], bkt[TILE], valid[TILE];
+  // packed slot descriptor per perspective (U path): [0] valid [1] from parent
+  // [2] side (0: h is the side to move) [5:3] bucket [7:6] nsub [13:8] rows
+  __shared__ uint32_t sdesc[TILE][2];
   __shared__ int pcount, njobs;
   __shared__ uint8_t jobs[TILE * 2];
   __shared__ uint32_t bmask;
+  // the parent board, and the first CDL children's deltas (idx + meta, 20 B each),
+  // loaded at parent start together with the parent's own rows so that no tile
+  // waits on an HBM round trip for its descriptors
+  constexpr int CDL = 64;
+  __shared__ gn_board pbd;
+  __shared__ uint32_t cdl[CDL][5];
   uint16_t(*rows)[2][32] = reinterpret_cast<uint16_t(*)[2][32]>(scratch);
 
   const int tid = threadIdx.x;
@@ -435,6 +567,7 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR) __attribute__((amdgpu_wav
   const size_t vgrid = swz ? 8 * ((n_parents + 7) / 8) : n_parents;
   for (size_t v = blockIdx.x; v < vgrid; v += gridDim.x) {
     __syncthreads(); // LDS of the previous parent is dead
+    GN_STAMP_INIT();
     // XCD-aware parent order: each XCD takes a contiguous range of parents, so
     // the parents of one game (same kings, mostly the same pieces) and their
     // children share that XCD's L2
@@ -447,16 +580,24 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR) __attribute__((amdgpu_wav
     const uint64_t off = offsets[p];
     const int total = 1 + (int)(offsets[p + 1] - off);
 
-    // ---- pre-phase: is any slot needed?  parent feature rows (both perspectives)
+    // ---- pre-phase: is any slot needed?  parent feature rows (both perspectives),
+    // parent board and the first CDL deltas into LDS
+    if (tid >= 64 && tid - 64 < (total - 1 < CDL ? total - 1 : CDL)) {
+      const uint32_t *src = reinterpret_cast<const uint32_t *>(deltas + off + (tid - 64));
+#pragma unroll
+      for (int w = 0; w < 5; ++w) cdl[tid - 64][w] = src[w];
+    }
     int want = 0;
     for (int qq = tid; qq < total; qq += NT)
       want |= qq == 0 ? (need_parent ? need_parent[p] : 1) : (need_child ? need_child[off + qq - 1] : 1);
     if (tid < 64) {
-      const int c = wave_features(parents[p], prow[0], prow[1], tid);
-      if (tid == 0) pcount = c;
+      const gn_board pb = parents[p];
+      const int c = wave_features(pb, prow[0], prow[1], tid);
+      if (tid == 0) pcount = c, pbd = pb;
     }
     if (!__syncthreads_or(want)) continue;
     if (!pcount) continue;
+    GN_STAMP(0);
 
     // parent accumulators: bias + all rows (group q == 0), kept for every child; the
     // parent's 8 PSQT sums go to LDS (children read one bucket each)
@@ -500,6 +641,7 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR) __attribute__((amdgpu_wav
 
     ushort8 base_lo = pacc_lo, base_hi = pacc_hi; // parent minus base_key's row (sibling cache)
     int base_key = -1;
+    GN_STAMP(1);
 
 #pragma unroll 1
     for (int t0 = 0; t0 < total; t0 += TILE) {
@@ -518,16 +660,28 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR) __attribute__((amdgpu_wav
         if (qq < total) {
           if (qq == 0) {
             vld = need_parent ? need_parent[p] : 1;
-            stm = parents[p].stm_ep >> 7, cnt = pcount;
+            stm = pbd.stm_ep >> 7, cnt = pcount;
             nsub[tid][0] = nsub[tid][1] = ncnt[tid][0] = ncnt[tid][1] = 0;
             usep[tid][0] = usep[tid][1] = 1;
           } else if ((vld = need_child ? need_child[off + qq - 1] : 1)) {
-            const ChildDelta cd = deltas[off + qq - 1];
+            ChildDelta cd;
+            if (qq - 1 < CDL) {
+              uint32_t *dst = reinterpret_cast<uint32_t *>(&cd);
+#pragma unroll
+              for (int w = 0; w < 5; ++w) dst[w] = cdl[qq - 1][w];
+            } else {
+              cd = deltas[off + qq - 1];
+            }
             stm = (cd.meta >> 10) & 1;
             cnt = (cd.meta >> 14) & 63;
 #pragma unroll
             for (int hh = 0; hh < 2; ++hh) {
               if (cd.meta & (1u << (8 + hh))) {
+                // king moved: the squares that change, for wave_features_king_move
+                rows[tid][hh][0] = cd.idx[hh][0];
+                rows[tid][hh][1] = cd.idx[hh][1];
+                rows[tid][hh][2] = cd.idx[hh][2];
+                rows[tid][hh][3] = cd.idx[hh][3];
                 usep[tid][hh] = 0, nsub[tid][hh] = 0, ncnt[tid][hh] = (uint8_t)cnt;
                 jobs[atomicAdd(&njobs, 1)] = (uint8_t)(tid | (hh << 4));
               } else {
@@ -545,26 +699,79 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR) __attribute__((amdgpu_wav
         sstm[tid] = (uint8_t)stm;
         bkt[tid] = (uint8_t)((cnt - 1) / 4);
         if (vld) atomicOr(&bmask, 1u << ((cnt - 1) / 4));
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh)
+          sdesc[tid][hh] = vld ? 1u | (uint32_t)usep[tid][hh] << 1 | (uint32_t)(hh != stm) << 2 |
+                                     (uint32_t)((cnt - 1) / 4) << 3 | (uint32_t)nsub[tid][hh] << 6 |
+                                     (uint32_t)ncnt[tid][hh] << 8
+                               : 0u;
       }
       __syncthreads();
+      GN_STAMP(2);
       {
         const int lane = tid & 63, wave = tid >> 6, nj = njobs;
         for (int jb = wave; jb < nj; jb += NW) {
           const int sl = jobs[jb] & 15, hh = jobs[jb] >> 4;
-          const gn_board cb = children[off + t0 + sl - 1];
-          wave_features(cb, hh == 0 ? rows[sl][0] : nullptr, hh == 1 ? rows[sl][1] : nullptr, lane);
+          uint16_t *rw = rows[sl][hh];
+          const int kf = rw[0], kt = rw[1], rf = rw[2], rt = rw[3]; // read by every lane before any writes
+          wave_features_king_move(pbd, hh, kf, kt, rf, rt, rw, lane);
         }
       }
       __syncthreads();
+      GN_STAMP(3);
 
       // ---- phase 1: accumulators + transform.  PSQT: thread j == 0 of each
       // perspective sums the slot's own bucket (one dword per row).
+      if constexpr (U) {
+        // descriptors and first rows of all 16 slots in one LDS read per lane, then
+        // scalar per slot (readlane)
+        const int lane = tl & 63, hu = __builtin_amdgcn_readfirstlane(ht);
+        uint32_t dv = 0, rv0 = 0, rv1 = 0;
+        if (lane < TILE) {
+          dv = sdesc[lane][hu];
+          const uint2 rw = *reinterpret_cast<const uint2 *>(rows[lane][hu]);
+          rv0 = rw.x, rv1 = rw.y;
+        }
+#pragma unroll 1
+        for (int sl = 0; sl < TILE; ++sl) {
+          const uint32_t d = (uint32_t)__builtin_amdgcn_readlane((int)dv, sl);
+          if (!(d & 1)) continue;
+          const bool fromp = (d >> 1) & 1;
+          const int side = (d >> 2) & 1, b = (d >> 3) & 7, ns = (d >> 6) & 3, n = (d >> 8) & 63;
+          const uint32_t r01 = (uint32_t)__builtin_amdgcn_readlane((int)rv0, sl);
+          const uint32_t r23 = (uint32_t)__builtin_amdgcn_readlane((int)rv1, sl);
+          const uint32_t psb = 2 * L1 + 4 * b;
+          ushort8 lo, hi;
+          uint32_t ps = 0;
+          int k = 0;
+          bool save = false;
+          if (!fromp) {
+            lo = *reinterpret_cast<const ushort8 *>(net.bias + 8 * jt);
+            hi = *reinterpret_cast<const ushort8 *>(net.bias + L1 / 2 + 8 * jt);
+          } else {
+            ps = (uint32_t)pps_lds[hu][b];
+            if (n > 0 && (int)(r01 & 0xFFFF) == base_key) {
+              lo = base_lo, hi = base_hi, k = 1;
+              if (jt == 0) ps -= ldpd(net.ft, ft_row(r01 & 0xFFFF) * RS + psb);
+            } else {
+              lo = pacc_lo, hi = pacc_hi, save = n > 0;
+            }
+          }
+          if (!(ablate & 2)) {
+            run_rows_u<L1>(net.ft, 16 * jt, rows[sl][hu], r01, r23, k, ns, n, jt == 0, psb, save, base_lo, base_hi,
+                           lo, hi, ps, lane);
+            if (save) base_key = (int)(r01 & 0xFFFF);
+          }
+          *reinterpret_cast<uint2 *>(xt + sl * XS + side * (L1 / 2) + 8 * jt) = transform8(lo, hi);
+          if (jt == 0) psq[sl][side] = (int32_t)ps;
+        }
+      } else {
 #pragma unroll 1
       for (int r = 0; r < TILE / PAR; ++r) {
         const int sl = r * PAR + qt;
         if (!valid[sl]) continue;
-        const bool fromp = usep[sl][ht];
-        const int b = bkt[sl], ns = nsub[sl][ht], n = ncnt[sl][ht];
+        const bool fromp = uni<U>(usep[sl][ht]);
+        const int b = uni<U>(bkt[sl]), ns = uni<U>(nsub[sl][ht]), n = uni<U>(ncnt[sl][ht]);
         const uint16_t *rr = rows[sl][ht];
         ushort8 lo, hi;
         uint32_t ps = 0;
@@ -575,30 +782,24 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR) __attribute__((amdgpu_wav
           hi = *reinterpret_cast<const ushort8 *>(net.bias + L1 / 2 + 8 * jt);
         } else {
           ps = (uint32_t)pps_lds[ht][b];
-          if (n > 0 && rr[0] == base_key) {
+          if (n > 0 && uni<U>(rr[0]) == base_key) {
             lo = base_lo, hi = base_hi, k = 1;
-            if (jt == 0) ps -= ldpd(net.ft, ft_row(rr[0]) * RS + 2 * L1 + 4 * b);
+            if (jt == 0) ps -= ldpd(net.ft, (uint32_t)uni<U>(ft_row(rr[0])) * RS + 2 * L1 + 4 * b);
           } else {
             lo = pacc_lo, hi = pacc_hi, save = n > 0;
           }
         }
         if (!(ablate & 2)) {
-          run_rows<L1>(net.ft, 16 * jt, rr, k, ns, n, jt == 0, 2 * L1 + 4 * b, save, base_lo, base_hi, lo, hi, ps);
-          if (save) base_key = rr[0];
+          run_rows<L1, U>(net.ft, 16 * jt, rr, k, ns, n, jt == 0, 2 * L1 + 4 * b, save, base_lo, base_hi, lo, hi, ps);
+          if (save) base_key = uni<U>(rr[0]);
         }
-        const int side = ht == sstm[sl] ? 0 : 1;
-        uint32_t w0 = 0, w1 = 0;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const int a = clampi((short)lo[e], 0, 254), c = clampi((short)hi[e], 0, 254);
-          const uint32_t vv = (uint32_t)(a * c) >> 9;
-          if (e < 4) w0 |= vv << (8 * e);
-          else w1 |= vv << (8 * (e - 4));
-        }
-        *reinterpret_cast<uint2 *>(xt + sl * XS + side * (L1 / 2) + 8 * jt) = make_uint2(w0, w1);
+        const int side = uni<U>(ht == sstm[sl] ? 0 : 1);
+        *reinterpret_cast<uint2 *>(xt + sl * XS + side * (L1 / 2) + 8 * jt) = transform8(lo, hi);
         if (jt == 0) psq[sl][side] = (int32_t)ps;
       }
+      }
       __syncthreads();
+      GN_STAMP(4);
 
       // ---- phase 2: layer stack
       if (!(ablate & 4)) {
@@ -609,7 +810,9 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR) __attribute__((amdgpu_wav
           else out_child[off + t0 + pos - 1] = val;
         });
       }
+      GN_STAMP(5);
     }
+    GN_STAMP_FLUSH();
   }
 }
 
@@ -960,6 +1163,19 @@ hipError_t launch_expand_net(const NetDevice &net, const gn_board *parents, size
     return hipErrorInvalidValue;
   }
 #undef GN_EXPAND_ARGS
+#ifdef GN_PHASE_TIMING
+  {
+    unsigned long long c[64][8], t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    (void)hipStreamSynchronize(s);
+    (void)hipMemcpyFromSymbol(c, HIP_SYMBOL(gn_phase_cycles), sizeof(c));
+    for (int i = 0; i < 64; ++i)
+      for (int k = 0; k < 8; ++k) t[k] += c[i][k];
+    fprintf(stderr, "phase cycles: parent_setup %llu parent_refresh %llu desc %llu jobs %llu gather %llu ls %llu\n",
+            t[0], t[1], t[2], t[3], t[4], t[5]);
+    memset(c, 0, sizeof(c));
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(gn_phase_cycles), c, sizeof(c));
+  }
+#endif
   return hipGetLastError();
 }
 

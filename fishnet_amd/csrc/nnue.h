@@ -70,7 +70,15 @@ GN_HD ChildDelta make_child_delta(const Board &parent, const Board &child, const
     const int ksq = king_square(child, h);
     cd.idx[h][0] = cd.idx[h][1] = cd.idx[h][2] = cd.idx[h][3] = 0;
     if (d.king_moved && h == parent.stm) {
+      // refresh of the mover's perspective: the squares that change instead of rows
+      // (king from, king to, and for castling rook from, rook to; 64 = none), so the
+      // evaluator derives the child's features from the parent board
       meta |= 1u << (8 + h);
+      const bool castle = d.n_add == 2; // castling: king + rook moved
+      cd.idx[h][0] = (uint16_t)d.rem_sq[0];
+      cd.idx[h][1] = (uint16_t)d.add_sq[0];
+      cd.idx[h][2] = (uint16_t)(castle ? d.rem_sq[1] : 64);
+      cd.idx[h][3] = (uint16_t)(castle ? d.add_sq[1] : 64);
     } else {
       cd.idx[h][0] = (uint16_t)feature_index(h, d.rem_sq[0], d.rem_pc[0], ksq);
       if (d.n_rem > 1) cd.idx[h][1] = (uint16_t)feature_index(h, d.rem_sq[1], d.rem_pc[1], ksq);

@@ -47,6 +47,7 @@ extern "C" {
 #define GN_E_CAPACITY (-6) /* caller's output buffer too small                */
 #define GN_E_NODEVICE (-7) /* no usable gfx950 device                         */
 #define GN_E_NONET (-8)    /* the requested mode needs a net that is not loaded */
+#define GN_E_ILLEGAL_MOVE (-9) /* a game's UCI move does not resolve to a legal move */
 
 /* evaluation modes */
 #define GN_MODE_FULL 0  /* Eval::evaluate: small net when |simple_eval| > 962,
@@ -71,6 +72,7 @@ extern "C" {
 #define GN_FLAG_SMALLNET 2u /* final_v came from the small net                    */
 #define GN_FLAG_BAD_FEN 4u  /* unparsable / unsupported position; values are 0     */
 #define GN_FLAG_REEVAL 8u   /* small net was run, then the big net re-evaluated   */
+#define GN_FLAG_SKIPPED 16u /* listed in skipPositions: not evaluated, values 0    */
 
 /* One result.  psqt/positional are Network::evaluate's NetworkOutput (already
  * divided by OutputScale = 16) of the net that produced final_v; final_v is
@@ -155,6 +157,45 @@ GN_API int gn_evaluate_batch_mode(gn_ctx *ctx, const char *const *fens, size_t n
 GN_API int gn_expand_and_evaluate(gn_ctx *ctx, const char *const *parent_fens, size_t n, int mode,
                            gn_eval *parent_out, uint32_t *child_offsets, uint16_t *child_moves,
                            gn_eval *child_out, size_t cap);
+
+/* ---- lichess analysis batches ------------------------------------------ */
+/* One acquired batch as the server sends it (AcquireResponseBody,
+ * /root/reference/src/api.rs:306-321): the root FEN, the game's UCI moves as
+ * one whitespace-separated string (the wire form; NULL or "" = no moves) and
+ * skipPositions (indices into positions 0..=moves). */
+typedef struct gn_game {
+  const char *root_fen;
+  const char *uci_moves;
+  const uint32_t *skip_positions;
+  size_t n_skip;
+} gn_game;
+
+/* Replaces IncomingBatch::from_acquired (/root/reference/src/queue.rs:548-700)
+ * for the evaluator: position i = root after i moves, i = 0..=moves.  Moves are
+ * resolved as shakmaty 0.27.3's UciMove::to_move does (queue.rs:576): king onto
+ * a castling rook = castling (Chess960 form), e1g1/e1c1-style king moves =
+ * castling with the h/a rook (standard form), promotion letter n/b/r/q.  moves[]
+ * receives them in Stockfish encoding (castling = king takes rook, i.e. the
+ * Chess960 UCI the reference forwards, queue.rs:577).  A bad root FEN fails with
+ * GN_E_INVALID, a move that is not legal with GN_E_ILLEGAL_MOVE (the reference
+ * fails the whole batch, `uci.to_move(&pos)?`).  *n_positions = moves + 1 is set
+ * on GN_E_CAPACITY too.  Host only, no context and no GPU needed. */
+GN_API int gn_replay_game(const gn_game *game, gn_board *positions, uint8_t *skipped, uint16_t *moves, size_t cap,
+                          size_t *n_positions);
+
+/* Replay + evaluate n_games batches at once.  position_offsets[n_games + 1]:
+ * positions of game g are [position_offsets[g], position_offsets[g + 1]);
+ * game_status[g] = GN_OK or that game's GN_E_* (a failed game has no positions;
+ * the other games are still evaluated and the call returns GN_OK).  Skipped
+ * positions get GN_FLAG_SKIPPED and no children.  with_children != 0: also every
+ * legal child of every evaluated position, child_offsets[total positions + 1]
+ * indexed by position (as gn_expand_and_evaluate).  GN_E_CAPACITY when the
+ * positions exceed position_cap or the children child_cap (the offsets are still
+ * filled so the caller can retry with the right sizes). */
+GN_API int gn_evaluate_games(gn_ctx *ctx, const gn_game *games, size_t n_games, int mode, int with_children,
+                             uint32_t *position_offsets, int32_t *game_status, gn_eval *position_out,
+                             size_t position_cap, uint32_t *child_offsets, uint16_t *child_moves,
+                             gn_eval *child_out, size_t child_cap);
 
 /* Legal-move-tree node count from fen to depth (GPU movegen, breadth-first). */
 GN_API int gn_perft(gn_ctx *ctx, const char *fen, int depth, uint64_t *nodes);
