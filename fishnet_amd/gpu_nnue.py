@@ -19,9 +19,10 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GPU_NNUE_LIB", os.path.join(HERE, "lib", "libgpu_nnue.so"))
 
 MODE_FULL, MODE_BIG, MODE_SMALL = 0, 1, 2
-FLAG_IN_CHECK, FLAG_SMALLNET, FLAG_BAD_FEN, FLAG_REEVAL = 1, 2, 4, 8
+FLAG_IN_CHECK, FLAG_SMALLNET, FLAG_BAD_FEN, FLAG_REEVAL, FLAG_SKIPPED = 1, 2, 4, 8, 16
 ERRORS = {-1: "INVALID", -2: "IO", -3: "FORMAT", -4: "HIP", -5: "NOMEM", -6: "CAPACITY",
-          -7: "NODEVICE", -8: "NONET"}
+          -7: "NODEVICE", -8: "NONET", -9: "ILLEGAL_MOVE"}
+E_INVALID, E_CAPACITY, E_ILLEGAL_MOVE = -1, -6, -9
 
 EVAL_DTYPE = np.dtype([("psqt", "<i4"), ("positional", "<i4"), ("final_v", "<i4"), ("flags", "<u4")])
 BOARD_DTYPE = np.dtype([("occ", "<u8"), ("pc", "u1", (16,)), ("stm_ep", "u1"), ("reserved", "u1"),
@@ -34,7 +35,7 @@ EXPORTS = ["gn_load_net", "gn_load_net_memory", "gn_free", "gn_last_error", "gn_
            "gn_board_to_fen", "gn_random_positions", "gn_evaluate_device", "gn_expand_device",
            "gn_device_alloc", "gn_device_free", "gn_memcpy_h2d", "gn_memcpy_d2h", "gn_synchronize",
            "gn_time_evaluate_device", "gn_random_positions_device", "gn_set_option", "gn_get_option",
-           "gn_time_expand_device", "gn_random_games_device"]
+           "gn_time_expand_device", "gn_random_games_device", "gn_replay_game", "gn_evaluate_games"]
 OPT_INCREMENTAL_CHILDREN, OPT_XCD_SWIZZLE, OPT_KING_SORT = 1, 2, 3
 EXPAND_STAGES = ["count_scan", "total_readback", "write_children", "classify", "small_net", "big_net", "finalize"]
 
@@ -50,6 +51,26 @@ class EvalParams(C.Structure):
         "small_net_threshold", "psqt_weight", "positional_weight", "reeval_threshold",
         "complexity_div_small", "complexity_div_big", "material_pawn_small", "material_pawn_big",
         "material_base", "rule50_div", "value_clamp")] + [("piece_value", C.c_int32 * 5)]
+
+
+class GnGame(C.Structure):
+    """gn_game: one acquired lichess batch (root FEN, UCI moves string, skipPositions)."""
+    _fields_ = [("root_fen", C.c_char_p), ("uci_moves", C.c_char_p),
+                ("skip_positions", C.POINTER(C.c_uint32)), ("n_skip", C.c_size_t)]
+
+
+def _games_array(games):
+    """[(root_fen, moves, skip)] -> (gn_game array, keep-alive list).  moves: str or list of UCI."""
+    keep, arr = [], (GnGame * max(len(games), 1))()
+    for i, g in enumerate(games):
+        root, moves, skip = (tuple(g) + ((),) * 3)[:3]
+        mv = moves if isinstance(moves, str) else " ".join(moves or ())
+        sk = (C.c_uint32 * max(len(skip), 1))(*skip)
+        keep += [root.encode(), mv.encode(), sk]
+        arr[i].root_fen, arr[i].uci_moves = keep[-3], keep[-2]
+        arr[i].skip_positions = C.cast(sk, C.POINTER(C.c_uint32))
+        arr[i].n_skip = len(skip)
+    return arr, keep
 
 
 _lib = None
@@ -94,6 +115,8 @@ def lib():
         "gn_time_expand_device": [vp, i32, vp, sz, i32, i32, C.POINTER(C.c_float), C.POINTER(sz), vp,
                                   C.POINTER(C.c_uint64)],
         "gn_random_games_device": [vp, i32, C.c_uint64, sz, sz, i32, vp, vp],
+        "gn_replay_game": [C.POINTER(GnGame), vp, vp, vp, sz, C.POINTER(sz)],
+        "gn_evaluate_games": [vp, vp, sz, i32, i32, vp, vp, vp, sz, vp, vp, vp, sz],
     }
     for name, args in sig.items():
         f = getattr(L, name)
@@ -137,6 +160,21 @@ def random_positions(seed: int, first: int, n: int, max_plies: int = 160):
     boards = np.zeros(n, dtype=BOARD_DTYPE)
     _check(lib().gn_random_positions(seed, first, n, max_plies, boards.ctypes.data))
     return boards
+
+
+def replay_game(root_fen: str, moves, skip=()):
+    """IncomingBatch::from_acquired replay (host only): (boards[n+1], skipped[n+1], moves[n] Stockfish encoding)."""
+    arr, _keep = _games_array([(root_fen, moves, tuple(skip))])
+    n = C.c_size_t()
+    rc = lib().gn_replay_game(arr, None, None, None, 0, C.byref(n))
+    if rc not in (0, E_CAPACITY):
+        _check(rc)
+    cap = n.value
+    boards = np.zeros(cap, dtype=BOARD_DTYPE)
+    skipped = np.zeros(cap, dtype=np.uint8)
+    mv = np.zeros(max(cap - 1, 1), dtype=np.uint16)
+    _check(lib().gn_replay_game(arr, boards.ctypes.data, skipped.ctypes.data, mv.ctypes.data, cap, C.byref(n)))
+    return boards, skipped.astype(bool), mv[:cap - 1]
 
 
 def default_eval_params() -> EvalParams:
@@ -243,6 +281,40 @@ class GpuNnue:
             t = int(offsets[-1])
             return parents, offsets, moves[:t], kids[:t]
         raise GnError(-6, "capacity retry failed")
+
+    def evaluate_games(self, games, mode=MODE_FULL, children=False):
+        """gn_evaluate_games over [(root_fen, moves, skip)]: per game a dict with status, evals of
+        positions 0..=moves (skipped ones flagged FLAG_SKIPPED) and, with children, per position
+        (child moves, child evals)."""
+        arr, _keep = _games_array(games)
+        ng = len(games)
+        offs = np.zeros(ng + 1, dtype=np.uint32)
+        status = np.zeros(max(ng, 1), dtype=np.int32)
+        pcap, ccap = 0, 0
+        for _ in range(3):
+            pos = np.zeros(max(pcap, 1), dtype=EVAL_DTYPE)
+            coffs = np.zeros(pcap + 1, dtype=np.uint32)
+            cmv = np.zeros(max(ccap, 1), dtype=np.uint16)
+            cev = np.zeros(max(ccap, 1), dtype=EVAL_DTYPE)
+            rc = lib().gn_evaluate_games(self.h, arr, ng, mode, int(children), offs.ctypes.data, status.ctypes.data,
+                                         pos.ctypes.data, pcap, coffs.ctypes.data if children else None,
+                                         cmv.ctypes.data, cev.ctypes.data, ccap)
+            if rc == E_CAPACITY:
+                need_p = int(offs[-1])
+                need_c = int(coffs[-1]) if children and need_p <= pcap else ccap
+                pcap, ccap = max(pcap, need_p), max(ccap, need_c)
+                continue
+            _check(rc)
+            out = []
+            for g in range(ng):
+                a, b = int(offs[g]), int(offs[g + 1])
+                d = {"status": int(status[g]), "evals": pos[a:b].copy()}
+                if children:
+                    d["children"] = [(cmv[coffs[i]:coffs[i + 1]].copy(), cev[coffs[i]:coffs[i + 1]].copy())
+                                     for i in range(a, b)]
+                out.append(d)
+            return out
+        raise GnError(E_CAPACITY, "capacity retry failed")
 
     def perft(self, fen: str, depth: int) -> int:
         v = C.c_uint64()

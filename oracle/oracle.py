@@ -191,3 +191,117 @@ def move_to_uci(m):
     if typ == 1:
         u += "nbrq"[(m >> 12) & 3]
     return u
+
+
+# ---- lichess batch replay (restatement for tests) --------------------------
+# IncomingBatch::from_acquired (/root/reference/src/queue.rs:548-700) replays
+# root_fen + the batch's UCI moves with shakmaty 0.27.3 (UciMove::to_move,
+# queue.rs:576; play_unchecked, queue.rs:578).  shakmaty is a Rust crate that is
+# not vendored in /root/reference (Cargo.lock pins 0.27.3); its published
+# to_move rule is restated here on top of this oracle's own movegen:
+#   king onto a square of the castling rights        -> castling with that rook;
+#   king e1/e8 -> c/g file of its back rank            -> castling with the a/h rook;
+#   otherwise from/to (+ promotion letter n/b/r/q)    -> must be a legal move.
+
+class IllegalMove(ValueError):
+    def __init__(self, index, uci):
+        super().__init__(f"move {index} ({uci}) is not legal")
+        self.index, self.uci = index, uci
+
+
+def _sq(s):
+    if len(s) != 2 or s[0] not in "abcdefgh" or s[1] not in "12345678":
+        return None
+    return (ord(s[1]) - ord("1")) * 8 + ord(s[0]) - ord("a")
+
+
+def _placement(fen):
+    board, rank, file = {}, 7, 0
+    for ch in fen.split()[0]:
+        if ch == "/":
+            rank, file = rank - 1, 0
+        elif ch.isdigit():
+            file += int(ch)
+        else:
+            board[rank * 8 + file] = ch
+            file += 1
+    return board
+
+
+def castling_rook_squares(fen):
+    """Rook squares carrying castling rights (X-FEN / Shredder, as normalize_fen prints them)."""
+    board, field, out = _placement(fen), fen.split()[2], set()
+    for ch in field:
+        if ch == "-":
+            continue
+        white = ch.isupper()
+        base = 0 if white else 56
+        rook, king = ("R", "K") if white else ("r", "k")
+        ksq = next((s for s in range(base, base + 8) if board.get(s) == king), None)
+        rooks = [s for s in range(base, base + 8) if board.get(s) == rook]
+        u = ch.upper()
+        if u == "K":
+            cand = [s for s in rooks if ksq is not None and s > ksq]
+            if cand:
+                out.add(max(cand))
+        elif u == "Q":
+            cand = [s for s in rooks if ksq is not None and s < ksq]
+            if cand:
+                out.add(min(cand))
+        else:
+            out.add(base + ord(u) - ord("A"))
+    return out
+
+
+def uci_to_move(fen, uci):
+    """shakmaty UciMove::to_move on this oracle's movegen; None when not legal."""
+    if len(uci) not in (4, 5):
+        return None
+    frm, to = _sq(uci[0:2]), _sq(uci[2:4])
+    if frm is None or to is None:
+        return None
+    promo = uci[4] if len(uci) == 5 else None
+    if promo is not None and promo not in "nbrq":
+        return None
+    board = _placement(fen)
+    pc = board.get(frm)
+    if pc is None or (promo and pc.upper() != "P"):
+        return None
+    white = fen.split()[1] == "w"
+    rook = None
+    if pc.upper() == "K":
+        if to in castling_rook_squares(fen):
+            rook = to
+        elif frm == (4 if white else 60) and to // 8 == (0 if white else 7) and to % 8 in (2, 6):
+            rook = (to & 56) | (0 if to % 8 == 2 else 7)
+    for m in legal_moves(fen):
+        mt, mf, typ = m & 63, (m >> 6) & 63, m >> 14
+        if mf != frm:
+            continue
+        if rook is not None:
+            if typ == 3 and mt == rook:
+                return m
+            continue
+        if typ == 3 or mt != to:
+            continue
+        if typ == 1:
+            if promo != "nbrq"[(m >> 12) & 3]:
+                continue
+        elif promo:
+            continue
+        return m
+    return None
+
+
+def replay_game(root_fen, moves):
+    """-> (fens of positions 0..=len, played moves in Stockfish encoding); raises IllegalMove."""
+    fen = normalize_fen(root_fen)
+    fens, played = [fen], []
+    for i, u in enumerate(moves.split() if isinstance(moves, str) else moves):
+        m = uci_to_move(fen, u)
+        if m is None:
+            raise IllegalMove(i + 1, u)
+        fen = child_fen(fen, m)
+        fens.append(fen)
+        played.append(m)
+    return fens, played

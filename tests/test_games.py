@@ -1,0 +1,172 @@
+"""Lichess analysis batches: root FEN + UCI moves + skipPositions -> positions
+(IncomingBatch::from_acquired, /root/reference/src/queue.rs:548-700) -> evaluations.
+
+CPU tests check the library's host replay (gn_replay_game needs no GPU) against
+public known answers and against the oracle's restatement of shakmaty 0.27.3's
+UciMove::to_move; the GPU tests check gn_evaluate_games against the oracle.
+The reference's own replay (shakmaty) is a Rust crate absent from the container,
+so the move-resolution rule is "parity unpinned" beyond the known answers below.
+"""
+import random
+
+import numpy as np
+import pytest
+
+START = "rnbqkbnr/pppppppp/8/8/8/8/PPPPPPPP/RNBQKBNR w KQkq - 0 1"
+# Morphy - Duke of Brunswick & Count Isouard, Paris 1858 ("Opera game"); the final
+# position is a public known answer.
+OPERA = ("e2e4 e7e5 g1f3 d7d6 d2d4 c8g4 d4e5 g4f3 d1f3 d6e5 f1c4 g8f6 f3b3 d8e7 b1c3 c7c6 c1g5 b7b5 "
+         "c3b5 c6b5 c4b5 b8d7 e1c1 a8d8 d1d7 d8d7 h1d1 e7e6 b5d7 f6d7 b3b8 d7b8 d1d8")
+OPERA_FINAL = "1n1Rkb1r/p4ppp/4q3/4p1B1/4P3/8/PPP2PPP/2K5 b k - 1 17"
+C960 = "bqnb1rkr/pp3ppp/3ppn2/2p5/5P2/P2P4/NPP1P1PP/BQ1BNRKR w HFhf - 2 9"
+# rooks on b and g: "e1g1" is castling (king onto a castling-rights rook), "e1c1" is not
+C960_CASTLE = "1r2k1r1/pppppppp/8/8/8/8/PPPPPPPP/1R2K1R1 w GBgb - 0 1"
+
+
+@pytest.fixture(scope="module")
+def G():
+    from fishnet_amd import build, gpu_nnue
+    build.build()
+    return gpu_nnue
+
+
+def fens_of(G, boards):
+    return [G.board_to_fen(b) for b in boards]
+
+
+def test_opera_game_known_answer(G, oracle_lib):
+    boards, skipped, moves = G.replay_game(START, OPERA, skip=[0, 3, 33])
+    assert len(boards) == 34 and len(moves) == 33
+    assert G.board_to_fen(boards[-1]) == OPERA_FINAL
+    assert G.board_to_fen(boards[1]) == "rnbqkbnr/pppppppp/8/8/4P3/8/PPPP1PPP/RNBQKBNR b KQkq - 0 1"
+    assert [int(i) for i in np.nonzero(skipped)[0]] == [0, 3, 33]
+    # the Chess960 UCI the reference forwards to the engine (queue.rs:577): O-O-O = king takes rook
+    assert G.move_to_uci(int(moves[22])) == "e1a1"
+    fens, played = oracle_lib.replay_game(START, OPERA)
+    assert fens_of(G, boards) == fens and [int(m) for m in moves] == played
+
+
+def test_castling_notations_agree(G):
+    pre = "e2e4 e7e5 g1f3 b8c6 f1c4 g8f6 "
+    a = G.replay_game(START, pre + "e1g1")
+    b = G.replay_game(START, pre + "e1h1")
+    assert fens_of(G, a[0]) == fens_of(G, b[0]) and list(a[2]) == list(b[2])
+    assert G.board_to_fen(a[0][-1]).startswith("r1bqkb1r/pppp1ppp/2n2n2/4p3/2B1P3/5N2/PPPP1PPP/RNBQ1RK1 b kq")
+
+
+@pytest.mark.parametrize("moves,bad", [
+    ("e2e4 e7e5 e1g1", 3),          # standard castling notation without the right to castle
+    ("e2e5", 1),                    # not a legal pawn move
+    ("e2e4 0000", 2),               # null move: UciMove::Null never resolves
+    ("e2e4 e7e5 d1h5 e8e7 h5e8", 5),  # a queen cannot take the king (not a legal move)
+    ("e2e4 e7e5 g1f3 k9a1", 4),     # malformed
+    ("e2e4 e7e5 e2e4", 3),          # empty from-square
+    ("e2e4 d7d5 e4d5 e7e5 d5e6q", 5),  # promotion letter on a non-promoting move
+    ("e2e4 e7e5 g1f3 g8f6 f1e2 f8e7 e1g1 e8g8 g1h1 g8h8 f1g1k", 11),  # promotion letter k
+    ("C960 e1c1", 1),               # standard O-O-O notation needs the a-rook
+])
+def test_illegal_moves_fail_the_game(G, moves, bad):
+    root = START
+    if moves.startswith("C960 "):
+        root, moves = C960_CASTLE, moves[5:]
+    with pytest.raises(G.GnError) as e:
+        G.replay_game(root, moves)
+    assert e.value.code == G.E_ILLEGAL_MOVE and f"move {bad} " in str(e.value)
+
+
+def test_bad_root_and_empty_game(G):
+    with pytest.raises(G.GnError) as e:
+        G.replay_game("8/8/8/8/8/8/8/8 w - - 0 1", "")
+    assert e.value.code == G.E_INVALID
+    boards, skipped, moves = G.replay_game(C960, "", skip=[5])  # out-of-range skip index is ignored
+    assert len(boards) == 1 and len(moves) == 0 and not skipped.any()
+
+
+def test_en_passant_promotion_and_chess960(G, oracle_lib):
+    games = [
+        (START, "e2e4 a7a6 e4e5 d7d5 e5d6 c7d6 g2g4 h7h5 g4h5 g7g5 h5g6 a6a5 g6g7 a5a4 g7h8n"),
+        (START, "b2b4 a7a5 b4a5 b7b5 a5b6 c7c5 b6b7 c5c4 b7a8r c4c3 a8b8 d8a5 b8c8 a5d8"),
+        (C960, "e2e4 e6e5 g2g3 f6e4"),
+        (C960_CASTLE, "e1g1 e8b8"),               # king takes its own rook: O-O then O-O-O
+        (C960_CASTLE, "e1b1 e8g8"),
+        ("r3k2r/8/8/8/8/8/8/R3K2R w KQkq - 0 1", "e1c1 e8g8"),
+        ("r3k2r/8/8/8/8/8/8/R3K2R w KQkq - 0 1", "e1a1 e8h8"),
+    ]
+    for root, moves in games:
+        boards, _, played = G.replay_game(root, moves)
+        fens, exp = oracle_lib.replay_game(root, moves)
+        assert fens_of(G, boards) == fens, (root, moves)
+        assert [int(m) for m in played] == exp
+
+
+def _random_game(oracle_lib, rng, root, plies):
+    """Random legal line from the oracle; castling written in either notation."""
+    fen, out = oracle_lib.normalize_fen(root), []
+    for _ in range(plies):
+        ms = oracle_lib.legal_moves(fen)
+        if not ms:
+            break
+        m = rng.choice(ms)
+        u = oracle_lib.move_to_uci(m)
+        frm, to = (m >> 6) & 63, m & 63
+        if m >> 14 == 3 and frm in (4, 60) and to % 8 in (0, 7) and rng.random() < 0.5:
+            u = u[:2] + ("c" if to % 8 == 0 else "g") + u[3]  # standard notation
+        out.append(u)
+        fen = oracle_lib.child_fen(fen, m)
+    return " ".join(out)
+
+
+def test_random_games_match_oracle(G, oracle_lib):
+    rng = random.Random(1234)
+    roots = [START, C960, "r3k2r/p1ppqpb1/bn2pnp1/3PN3/1p2P3/2N2Q1p/PPPBBPPP/R3K2R w KQkq - 0 1"]
+    for g in range(60):
+        root = roots[g % 3]
+        moves = _random_game(oracle_lib, rng, root, 60)
+        boards, _, played = G.replay_game(root, moves)
+        fens, exp = oracle_lib.replay_game(root, moves)
+        assert fens_of(G, boards) == fens and [int(m) for m in played] == exp
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_evaluate_games_vs_oracle(gpu_ctx, oracle_nets, oracle_lib, mode):
+    from fishnet_amd import gpu_nnue as G
+    big, small = oracle_nets
+    rng = random.Random(99 + mode)
+    games = [(START, OPERA, [0, 7]), (C960, _random_game(oracle_lib, rng, C960, 40), []),
+             (START, "e2e4 e7e5 e1g1", []),  # fails: illegal move
+             (START, "", [0]),                # everything skipped
+             (START, _random_game(oracle_lib, rng, START, 80), list(range(0, 81, 5)))]
+    out = gpu_ctx.evaluate_games(games, mode)
+    assert [o["status"] for o in out] == [0, 0, G.E_ILLEGAL_MOVE, 0, 0]
+    for (root, moves, skip), o in zip(games, out):
+        if o["status"]:
+            assert len(o["evals"]) == 0
+            continue
+        fens, _ = oracle_lib.replay_game(root, moves)
+        exp = oracle_lib.eval_fens(big, small, fens, mode)
+        got = o["evals"]
+        for i in range(len(fens)):
+            if i in skip:
+                assert tuple(got[i]) == (0, 0, 0, G.FLAG_SKIPPED)
+            else:
+                assert tuple(got[i]) == tuple(exp[i]), (fens[i], got[i], exp[i])
+
+
+@pytest.mark.gpu
+def test_evaluate_games_with_children_vs_oracle(gpu_ctx, oracle_nets, oracle_lib):
+    big, small = oracle_nets
+    rng = random.Random(5)
+    games = [(START, OPERA, [1, 2]), (C960, _random_game(oracle_lib, rng, C960, 30), [30])]
+    out = gpu_ctx.evaluate_games(games, 0, children=True)
+    for (root, moves, skip), o in zip(games, out):
+        assert o["status"] == 0
+        fens, _ = oracle_lib.replay_game(root, moves)
+        for i, fen in enumerate(fens):
+            cm, ce = o["children"][i]
+            if i in skip:
+                assert len(cm) == 0
+                continue
+            p_exp, m_exp, k_exp = oracle_lib.expand_eval(big, small, fen, 0)
+            assert tuple(o["evals"][i]) == tuple(p_exp)
+            assert dict(zip(cm.tolist(), map(tuple, ce.tolist()))) == dict(zip(m_exp, map(tuple, k_exp.tolist())))
