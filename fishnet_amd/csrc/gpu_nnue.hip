@@ -120,11 +120,12 @@ static int parse_net(const uint8_t *data, size_t len, HostNet &h) {
   h.L1 = l1;
   h.hash = hash;
   const size_t RS = 2 * (size_t)l1 + 32;
-  h.ft.assign((size_t)FT_INPUTS * RS, 0);
+  h.ft.assign((size_t)FT_ROWS * RS, 0);
   h.bias.resize(l1);
   uint8_t *ft = h.ft.data();
   if (!r.leb(16, l1, [&](size_t i, int32_t v) { h.bias[i] = (int16_t)(uint16_t)(v * 2); }))
     return fail(GN_E_FORMAT, "bad feature-transformer biases");
+  memcpy(ft + (size_t)FT_BIAS_ROW * RS, h.bias.data(), 2 * (size_t)l1);
   if (!r.leb(16, (size_t)l1 * FT_INPUTS, [&](size_t i, int32_t v) {
         const int16_t d = (int16_t)(uint16_t)(v * 2);
         memcpy(ft + (i / l1) * RS + 2 * (i % l1), &d, 2);
@@ -240,7 +241,7 @@ static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 static int upload_net(Dev &d, int which, const HostNet &h) {
   const size_t RS = 2 * (size_t)h.L1 + 32;
   size_t off[8], o = 0;
-  const size_t sz[8] = {(size_t)FT_INPUTS * RS, h.bias.size() * 2, h.w0.size(), h.b0.size() * 4,
+  const size_t sz[8] = {(size_t)FT_ROWS * RS, h.bias.size() * 2, h.w0.size(), h.b0.size() * 4,
                         h.w1.size(), h.b1.size() * 4, h.w2.size(), h.b2.size() * 4};
   const void *src[8] = {h.ft.data(), h.bias.data(), h.w0.data(), h.b0.data(),
                         h.w1.data(), h.b1.data(), h.w2.data(), h.b2.data()};

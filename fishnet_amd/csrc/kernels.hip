@@ -173,7 +173,7 @@ __device__ __forceinline__ void layer_stack_tile(const NetDevice &net, const uin
 #pragma unroll
       for (int t = 0; t < (KS + NW - 1) / NW; ++t) {
         const int ks = wave + t * NW;
-        if (ks < KS) {
+        if (KS % NW == 0 || ks < KS) { // static when the k-steps split evenly: all loads issue together
           const int4v a = *reinterpret_cast<const int4v *>(xa + 64 * ks);
           const int4v w = *reinterpret_cast<const int4v *>(wb + 64 * ks);
           acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, w, acc, 0, 0, 0);
@@ -816,6 +816,350 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR) __attribute__((amdgpu_wav
   }
 }
 
+// ------------------------------------------------------- expand_stream --
+// expand_eval for the big net with the gather as ONE row stream per perspective
+// and tile.  The slot programs of a tile (parent refresh, king-move refreshes,
+// child deltas) are flattened into a list of row entries in LDS; each wave walks
+// its perspective's list with a 4-deep register ring, so up to 4 rows stay in
+// flight across slot boundaries instead of one dependent round trip per slot.
+// A refresh is zero + the bias row (FT_BIAS_ROW) + the feature rows.
+// Entry (u32): [14:0] row, [15] subtract, [17:16] init before this entry
+// (0 none, 1 zero, 2 parent, 3 sibling base), [18] save base after it,
+// [19] last entry of its slot, [23:20] slot, [24] side (0: perspective to move),
+// [25] entry of the parent slot, [28:26] bucket, [29] PSQT only (sibling hit).
+namespace es {
+constexpr uint32_t SUB = 1u << 15, I_ZERO = 1u << 16, I_PACC = 2u << 16, I_BASE = 3u << 16, SAVEB = 1u << 18,
+                   LAST = 1u << 19, PAR_E = 1u << 25, PSQ_ONLY = 1u << 29;
+__device__ __forceinline__ uint32_t tmpl(int slot, int side, int bucket) {
+  return (uint32_t)slot << 20 | (uint32_t)side << 24 | (uint32_t)bucket << 26;
+}
+} // namespace es
+
+template <int L1>
+__global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_EXPAND_WPE)))
+    expand_stream_kernel(NetDevice net, const gn_board *__restrict__ parents, const uint64_t *__restrict__ offsets,
+                         const ChildDelta *__restrict__ deltas, const uint8_t *__restrict__ need_parent,
+                         const uint8_t *__restrict__ need_child, int2 *__restrict__ out_parent,
+                         int2 *__restrict__ out_child, size_t n_parents, int swz, int ablate) {
+  using namespace es;
+  constexpr int G = L1 / 16; // threads per perspective (whole waves)
+  constexpr int NT = 2 * G;
+  constexpr int NW = NT / 64;
+  constexpr int TILE = 16;
+  constexpr int XS = L1 + 16;
+  constexpr uint32_t RS = 2 * L1 + 32;
+  constexpr int CAP = 256; // row entries per perspective and tile
+  constexpr int SCRATCH = 2 * CAP * 4 > LS_SCRATCH ? 2 * CAP * 4 : LS_SCRATCH;
+  constexpr int CDL = 48;
+  static_assert(G % 64 == 0, "perspective groups must be whole waves");
+  __shared__ __attribute__((aligned(16))) uint8_t xt[TILE * XS];
+  __shared__ __attribute__((aligned(16))) uint8_t scratch[SCRATCH]; // entry lists, then layer-stack scratch
+  __shared__ uint16_t prow[2][32];
+  __shared__ int32_t psq[TILE][2];
+  __shared__ uint8_t bkt[TILE], valid[TILE];
+  __shared__ uint32_t cdl[CDL][5];
+  __shared__ gn_board pbd;
+  __shared__ int pcount;
+  __shared__ uint32_t tctl[3]; // slots in this tile, entries of perspective 0 / 1
+  __shared__ uint32_t bmask;
+  uint32_t(*ent)[CAP] = reinterpret_cast<uint32_t(*)[CAP]>(scratch);
+
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const size_t vgrid = swz ? 8 * ((n_parents + 7) / 8) : n_parents;
+  for (size_t v = blockIdx.x; v < vgrid; v += gridDim.x) {
+    __syncthreads(); // LDS of the previous parent is dead
+    size_t p = v;
+    if (swz) {
+      const size_t p8 = (n_parents + 7) / 8;
+      p = (v & 7) * p8 + (v >> 3);
+      if (p >= n_parents) continue;
+    }
+    const uint64_t off = offsets[p];
+    const int total = 1 + (int)(offsets[p + 1] - off);
+
+    // ---- pre-phase: parent rows + board (wave 0), first CDL deltas, any slot needed?
+    // (per-lane values are re-derived in every phase from an opaque copy of the thread
+    // id, so that nothing lane-dependent is hoisted and held across the kernel)
+    int tp = tid;
+    asm volatile("" : "+v"(tp));
+    if (tp >= 64 && tp - 64 < (total - 1 < CDL ? total - 1 : CDL)) {
+      const uint32_t *src = reinterpret_cast<const uint32_t *>(deltas + off + (tp - 64));
+#pragma unroll
+      for (int w = 0; w < 5; ++w) cdl[tp - 64][w] = src[w];
+    }
+    int want = 0;
+    for (int qq = tp; qq < total; qq += NT)
+      want |= qq == 0 ? (need_parent ? need_parent[p] : 1) : (need_child ? need_child[off + qq - 1] : 1);
+    if (wave == 0) {
+      const gn_board pb = parents[p];
+      const int c = wave_features(pb, prow[0], prow[1], tp & 63);
+      if (tp == 0) pcount = c, pbd = pb;
+    }
+    if (!__syncthreads_or(want)) continue;
+    if (!pcount) continue;
+
+    // per-thread state across the tiles of this parent
+    const int hu = __builtin_amdgcn_readfirstlane((tid / G) & 1);
+    const bool psqw = __builtin_amdgcn_readfirstlane((tid % G) >> 6) == 0; // the perspective's first wave sums PSQT
+    const int P = pcount, bp = (P - 1) / 4, b2 = P >= 2 ? (P - 2) / 4 : bp;
+    ushort8 pacc_lo = {}, pacc_hi = {}, base_lo = {}, base_hi = {};
+    uint32_t pps0 = 0, pps1 = 0; // parent PSQT at buckets bp / b2 (psq waves, scalar)
+    int ckey0 = -1, ckey1 = -1;  // sibling-cache keys carried across tiles (wave 0)
+    const __amdgpu_buffer_rsrc_t ftr =
+        __builtin_amdgcn_make_buffer_rsrc((void *)net.ft, 0, (int)((size_t)FT_ROWS * RS), 0x00020000);
+    const __amdgpu_buffer_rsrc_t nul = __builtin_amdgcn_make_buffer_rsrc((void *)net.ft, 0, 0, 0x00020000);
+
+#pragma unroll 1
+    for (int t0 = 0; t0 < total;) {
+      // ---- phase 0 (wave 0, lane = slot): descriptors -> entry counts -> prefix sums ->
+      // tile cut -> delta entries; refresh entries (parent, king moves) by the same wave
+      if (wave == 0) {
+        int lane = tid;
+        asm volatile("" : "+v"(lane));
+        lane &= 63;
+        const int qq = t0 + lane;
+        const bool inb = lane < TILE && qq < total;
+        // per slot: kinds (2 bits per perspective: 0 none, 1 delta, 2 king-move refresh,
+        // 3 parent), counts, the ChildDelta words
+        int vld = 0, stm = 0, cnt = 1, kinds = 0, n0 = 0, n1 = 0, s0 = 0, s1 = 0;
+        uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0; // idx[0][0..3], idx[1][0..3] as u16 pairs
+        if (inb) {
+          if (qq == 0) {
+            vld = need_parent ? need_parent[p] : 1;
+            stm = pbd.stm_ep >> 7, cnt = P, kinds = 3 | 3 << 2, n0 = n1 = P + 1;
+          } else if ((vld = need_child ? need_child[off + qq - 1] : 1)) {
+            uint32_t meta;
+            if (qq - 1 < CDL) {
+              w0 = cdl[qq - 1][0], w1 = cdl[qq - 1][1], w2 = cdl[qq - 1][2], w3 = cdl[qq - 1][3];
+              meta = cdl[qq - 1][4];
+            } else {
+              const uint32_t *src = reinterpret_cast<const uint32_t *>(deltas + off + qq - 1);
+              w0 = src[0], w1 = src[1], w2 = src[2], w3 = src[3], meta = src[4];
+            }
+            stm = (meta >> 10) & 1;
+            cnt = (meta >> 14) & 63;
+            if (meta & (1u << 8)) kinds |= 2, n0 = cnt + 1;
+            else kinds |= 1, s0 = meta & 3, n0 = s0 + ((meta >> 2) & 3);
+            if (meta & (1u << 9)) kinds |= 2 << 2, n1 = cnt + 1;
+            else kinds |= 1 << 2, s1 = (meta >> 4) & 3, n1 = s1 + ((meta >> 6) & 3);
+          }
+        }
+        const int key0 = (kinds & 3) == 1 ? (int)(w0 & 0xFFFF) : -1;
+        const int key1 = (kinds >> 2) == 1 ? (int)(w2 & 0xFFFF) : -1;
+        // sibling cache: the key before slot l is that of the nearest earlier delta slot
+        const uint64_t km0 = __ballot(key0 >= 0) & 0xFFFFull, km1 = __ballot(key1 >= 0) & 0xFFFFull;
+        const uint64_t lt = (1ull << lane) - 1;
+        const int pk0 = __shfl(key0, (km0 & lt) ? 63 - __builtin_clzll(km0 & lt) : 0);
+        const int pk1 = __shfl(key1, (km1 & lt) ? 63 - __builtin_clzll(km1 & lt) : 0);
+        const bool hit0 = key0 >= 0 && key0 == ((km0 & lt) ? pk0 : ckey0);
+        const bool hit1 = key1 >= 0 && key1 == ((km1 & lt) ? pk1 : ckey1);
+        // entry counts and their inclusive prefix sums (both perspectives packed)
+        const uint32_t c = (uint32_t)n0 | (uint32_t)n1 << 16;
+        uint32_t inc = c;
+#pragma unroll
+        for (int d = 1; d < TILE; d <<= 1) {
+          const uint32_t o = __shfl_up(inc, d);
+          if (lane >= d) inc += o;
+        }
+        const bool fits = inb && (inc & 0xFFFF) <= CAP && (inc >> 16) <= CAP;
+        const int m = __builtin_ctzll(~__ballot(fits)); // >= 1: one slot never exceeds CAP
+        const uint32_t exc = inc - c;
+        const bool mine = lane < m;
+        const uint32_t last_inc = __shfl(inc, m - 1);
+        {
+          const uint64_t k0 = __ballot(mine && key0 >= 0), k1 = __ballot(mine && key1 >= 0);
+          const int c0 = __shfl(key0, k0 ? 63 - __builtin_clzll(k0) : 0);
+          const int c1 = __shfl(key1, k1 ? 63 - __builtin_clzll(k1) : 0);
+          if (k0) ckey0 = __builtin_amdgcn_readfirstlane(c0);
+          if (k1) ckey1 = __builtin_amdgcn_readfirstlane(c1);
+        }
+        const int bk = (cnt - 1) / 4;
+        uint32_t bm = 0;
+#pragma unroll
+        for (int b = 0; b < 8; ++b)
+          if (__ballot(mine && vld && bk == b)) bm |= 1u << b;
+        if (lane < TILE) {
+          valid[lane] = (uint8_t)(mine && vld);
+          bkt[lane] = (uint8_t)bk;
+        }
+        if (lane == 0) {
+          bmask = bm;
+          tctl[0] = (uint32_t)m;
+          tctl[1] = last_inc & 0xFFFF;
+          tctl[2] = last_inc >> 16;
+        }
+        // pad both lists to a multiple of 4 with PSQT-only entries of row 0 (harmless:
+        // they follow the last slot of the list, no row is loaded)
+        if (lane < 3) {
+          const uint32_t l0 = last_inc & 0xFFFF, l1 = last_inc >> 16;
+          if (l0 + lane < ((l0 + 3) & ~3u)) ent[0][l0 + lane] = PSQ_ONLY;
+          if (l1 + lane < ((l1 + 3) & ~3u)) ent[1][l1 + lane] = PSQ_ONLY;
+        }
+        if (mine) {
+          const uint32_t t0w = tmpl(lane, stm != 0, bk), t1w = tmpl(lane, stm != 1, bk);
+          // delta rows: k < s removed (idx 0, 1), then added (idx 2, 3); s in {1, 2}
+          auto delta = [&](uint32_t *e, uint32_t lo2, uint32_t hi2, int s, int n, bool hit, uint32_t t) {
+            const uint32_t i0 = lo2 & 0xFFFF, i1 = lo2 >> 16, i2 = hi2 & 0xFFFF, i3 = hi2 >> 16;
+            const uint32_t r0 = i0, r1 = s >= 2 ? i1 : i2, r2 = s >= 2 ? i2 : i3, r3 = i3;
+            auto cl = [](uint32_t r) { return r < (uint32_t)FT_ROWS ? r : (uint32_t)FT_BIAS_ROW; };
+            e[0] = cl(r0) | t | SUB | (n == 1 ? LAST : 0u) | (hit ? (I_BASE | PSQ_ONLY) : (I_PACC | SAVEB));
+            if (n > 1) e[1] = cl(r1) | t | (s >= 2 ? SUB : 0u) | (n == 2 ? LAST : 0u);
+            if (n > 2) e[2] = cl(r2) | t | (n == 3 ? LAST : 0u);
+            if (n > 3) e[3] = cl(r3) | t | LAST;
+          };
+          uint32_t *e0 = ent[0] + (exc & 0xFFFF), *e1 = ent[1] + (exc >> 16);
+          if ((kinds & 3) == 1) delta(e0, w0, w1, s0, n0, hit0, t0w);
+          else if (kinds & 3) e0[0] = (uint32_t)FT_BIAS_ROW | t0w | I_ZERO | ((kinds & 3) == 3 ? PAR_E : 0u);
+          if ((kinds >> 2) == 1) delta(e1, w2, w3, s1, n1, hit1, t1w);
+          else if (kinds >> 2) e1[0] = (uint32_t)FT_BIAS_ROW | t1w | I_ZERO | ((kinds >> 2) == 3 ? PAR_E : 0u);
+        }
+        // refresh entries, lane = square: the parent (both perspectives) and king moves
+        uint64_t jm = __ballot(mine && (kinds & 10));
+        while (jm) {
+          const int l = __builtin_ctzll(jm);
+          jm &= jm - 1;
+          const int kl = __shfl(kinds, l), st = __shfl(stm, l), cn = __shfl(cnt, l);
+          const uint32_t ex = __shfl(exc, l);
+#pragma unroll
+          for (int hh = 0; hh < 2; ++hh) {
+            const int kd = (kl >> (2 * hh)) & 3;
+            if (kd < 2) continue;
+            const uint32_t t = tmpl(l, hh != st, (cn - 1) / 4) | (kd == 3 ? PAR_E : 0u);
+            uint32_t *e = ent[hh] + (hh ? ex >> 16 : ex & 0xFFFF) + 1;
+            if (kd == 3) {
+              if (lane < P) e[lane] = ft_row(prow[hh][lane]) | t | (lane == P - 1 ? LAST : 0u);
+            } else {
+              const uint32_t sq01 = __shfl(hh ? w2 : w0, l), sq23 = __shfl(hh ? w3 : w1, l);
+              const int kf = sq01 & 0xFFFF, kt = sq01 >> 16, rf = sq23 & 0xFFFF, rt = sq23 >> 16;
+              // wave_features_king_move, written as entries
+              const uint64_t occ = pbd.occ;
+              const bool has = (occ >> lane) & 1;
+              const int k = popcnt(occ & ((1ull << lane) - 1));
+              uint64_t wlo, whi;
+              piece_words(pbd, wlo, whi);
+              int pc = has && k < 32 ? piece_nibble(wlo, whi, k) : 0;
+              if (lane == kf || lane == rf) pc = 0;
+              if (lane == rt) pc = make_piece(hh, ROOK);
+              if (lane == kt) pc = make_piece(hh, KING);
+              const uint64_t cocc = __ballot(pc != 0);
+              const int pos = popcnt(cocc & ((1ull << lane) - 1));
+              if (pc && pos < cn)
+                e[pos] = (uint32_t)feature_index(hh, lane, pc, kt) | t | (pos == cn - 1 ? LAST : 0u);
+            }
+          }
+        }
+      }
+      __syncthreads();
+      const int m = (int)tctl[0];
+
+      // ---- phase 1: the row stream of this wave's perspective.  Every ring step issues
+      // exactly three buffer loads (row halves + PSQT dword) with the row offset as the
+      // scalar offset; loads that are not wanted (PSQT-only entries, PSQT on the other
+      // waves, steps past the list) go through a zero-size descriptor, which returns
+      // zeros without touching memory, so the outstanding-load count is the same on
+      // every path and the waits stay exact, at no vector-ALU cost.
+      {
+        int tl = tid;
+        asm volatile("" : "+v"(tl));
+        const int jt = tl % G;
+        const int lane = tl & 63;
+        const uint32_t j16 = 16 * jt;
+        const int n4 = ((int)tctl[1 + hu] + 3) & ~3; // padded with PSQT-only entries
+        const uint32_t *E = ent[hu];
+        // parent entries (bucket bp): lane 1 of the PSQT wave sums bucket b2 <= bp instead
+        // (scalar offset at b2, the other lanes add 4 * (bp - b2) in the vector offset)
+        const uint32_t dlt = psqw && jt == 1 ? 0u : 4u * (uint32_t)(bp - b2);
+        ushort8 rlo[4], rhi[4];
+        uint32_t rp[4];
+        uint32_t er[4];
+        ushort8 lo = {}, hi = {};
+        uint32_t ps = 0;
+        uint32_t ev = 0;
+        auto issue = [&](int r, int i) {
+          const bool live = i < n4;
+          uint32_t e = 0;
+          if (live) {
+            if ((i & 63) == 0) ev = E[i + lane];
+            e = (uint32_t)__builtin_amdgcn_readlane((int)ev, i & 63);
+          }
+          er[r] = e;
+          const uint32_t o = (e & 0x7FFF) * RS;
+          const __amdgpu_buffer_rsrc_t rs = live && !(e & PSQ_ONLY) && !(ablate & 2) ? ftr : nul;
+          rlo[r] = __builtin_bit_cast(ushort8, __builtin_amdgcn_raw_buffer_load_b128(rs, j16, o, 0));
+          rhi[r] = __builtin_bit_cast(ushort8, __builtin_amdgcn_raw_buffer_load_b128(rs, j16 + L1, o, 0));
+          const __amdgpu_buffer_rsrc_t rq = live && psqw ? ftr : nul;
+          const bool par = e & PAR_E;
+          rp[r] = __builtin_amdgcn_raw_buffer_load_b32(rq, par ? dlt : 0u,
+                                                       o + 2 * L1 + 4 * (par ? (uint32_t)b2 : (e >> 26) & 7), 0);
+        };
+        auto consume = [&](int r) {
+          const uint32_t e = er[r];
+          const uint32_t init = e & (3u << 16);
+          const bool sub = e & SUB;
+          const uint32_t pp = ((e >> 26) & 7) == (uint32_t)bp ? pps0 : pps1;
+          // scalar branches; the empty asm keeps the compiler from if-converting them into
+          // selects over every alternative (vector work on all paths)
+          if (init == I_ZERO) { // the bias row
+            asm volatile("");
+            lo = rlo[r], hi = rhi[r], ps = rp[r];
+          } else if (init == I_PACC) { // a miss: parent - from-row
+            asm volatile("");
+            lo = pacc_lo - rlo[r], hi = pacc_hi - rhi[r], ps = pp - rp[r];
+          } else if (init == I_BASE) { // a hit: the cached parent - from-row
+            asm volatile("");
+            lo = base_lo, hi = base_hi, ps = pp - rp[r];
+          } else if (sub) {
+            asm volatile("");
+            lo -= rlo[r], hi -= rhi[r], ps -= rp[r];
+          } else {
+            asm volatile("");
+            lo += rlo[r], hi += rhi[r], ps += rp[r];
+          }
+          if (e & SAVEB) {
+            asm volatile("");
+            base_lo = lo, base_hi = hi;
+          }
+          if (e & LAST) {
+            const int sl = (e >> 20) & 15, side = (e >> 24) & 1;
+            *reinterpret_cast<uint2 *>(xt + sl * XS + side * (L1 / 2) + 8 * jt) = transform8(lo, hi);
+            if (psqw && jt == 0) psq[sl][side] = (int32_t)ps;
+            if (e & PAR_E) {
+              pacc_lo = lo, pacc_hi = hi;
+              pps0 = (uint32_t)__builtin_amdgcn_readlane((int)ps, 0);
+              pps1 = (uint32_t)__builtin_amdgcn_readlane((int)ps, 1);
+            }
+          }
+        };
+#pragma unroll
+        for (int r = 0; r < 4; ++r) issue(r, r);
+#pragma unroll 1
+        for (int i = 0; i < n4; i += 4) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            consume(r);
+            issue(r, i + r + 4);
+          }
+        }
+      }
+      __syncthreads();
+      // ---- phase 2: layer stack
+      if (!(ablate & 4)) {
+        int tl = tid;
+        asm volatile("" : "+v"(tl));
+        layer_stack_tile<L1, NW>(net, xt, scratch, psq, tl, bmask, [&](int pos, int bb) {
+          return pos < m && valid[pos] && bkt[pos] == bb;
+        }, [&](int pos, int2 val) {
+          if (t0 + pos == 0) out_parent[p] = val;
+          else out_child[off + t0 + pos - 1] = val;
+        });
+      }
+      t0 += m;
+      __syncthreads(); // entry lists / layer-stack scratch / xt reused by the next tile
+    }
+  }
+}
+
 hipError_t launch_eval_net(const NetDevice &net, const gn_board *boards, const uint8_t *need, size_t n, int2 *out,
                            const uint32_t *perm, int swz, hipStream_t s) {
   if (!n) return hipSuccess;
@@ -1153,7 +1497,14 @@ hipError_t launch_expand_net(const NetDevice &net, const gn_board *parents, size
   static const int persist = getenv("GN_PERSIST") ? atoi(getenv("GN_PERSIST")) : 0; // WGs per CU, 0: one per parent
   if (persist > 0) g = std::min<unsigned>(g, 8u * ((256u * (unsigned)persist + 7) / 8));
 #define GN_EXPAND_ARGS net, parents, offsets, children, deltas, need_parent, need_child, out_parent, out_child, n, swz, ablate
-  if (net.L1 == 3072) {
+  // GN_EXPAND_LEGACY=1: the per-slot row programs (expand_eval) for the big nets, for A/B timing
+  static const int legacy = getenv("GN_EXPAND_LEGACY") ? atoi(getenv("GN_EXPAND_LEGACY")) : 0;
+#define GN_STREAM_ARGS net, parents, offsets, deltas, need_parent, need_child, out_parent, out_child, n, swz, ablate
+  if (net.L1 == 3072 && !legacy) {
+    hipLaunchKernelGGL((expand_stream_kernel<3072>), dim3(g), dim3(384), 0, s, GN_STREAM_ARGS);
+  } else if (net.L1 == 1024 && !legacy) {
+    hipLaunchKernelGGL((expand_stream_kernel<1024>), dim3(g), dim3(128), 0, s, GN_STREAM_ARGS);
+  } else if (net.L1 == 3072) {
     hipLaunchKernelGGL((expand_eval_kernel<3072, 1>), dim3(g), dim3(384), 0, s, GN_EXPAND_ARGS);
   } else if (net.L1 == 128) {
     hipLaunchKernelGGL((expand_eval_kernel<128, 16>), dim3(g), dim3(256), 0, s, GN_EXPAND_ARGS);
@@ -1163,6 +1514,7 @@ hipError_t launch_expand_net(const NetDevice &net, const gn_board *parents, size
     return hipErrorInvalidValue;
   }
 #undef GN_EXPAND_ARGS
+#undef GN_STREAM_ARGS
 #ifdef GN_PHASE_TIMING
   {
     unsigned long long c[64][8], t[8] = {0, 0, 0, 0, 0, 0, 0, 0};

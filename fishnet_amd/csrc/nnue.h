@@ -2,10 +2,12 @@
 // libgpu_nnue, shared between the host loader and the kernels.
 //
 // HBM layout of one network (all arrays 256-B aligned):
-//   ft      [22528][RS] bytes, RS = 2*L1 + 32: one feature's row is the L1
+//   ft      [22528 + 1][RS] bytes, RS = 2*L1 + 32: one feature's row is the L1
 //           int16 feature-transformer weights (doubled at load, as Stockfish
 //           scale_weights does) followed by its 8 int32 PSQT weights, so one
-//           gathered feature = one contiguous row (6,176 B big / 288 B small)
+//           gathered feature = one contiguous row (6,176 B big / 288 B small).
+//           Row FT_BIAS_ROW (the extra last row) is the bias with zero PSQT, so
+//           a refresh is "zero + bias row + feature rows" in one row stream.
 //   bias    [L1] int16 (doubled)
 //   w0      [8 buckets][16][L1] int8     b0 [8][16] int32    (fc_0)
 //   w1      [8][32][32] int8             b1 [8][32] int32    (fc_1, cols 30,31 pad)
@@ -18,6 +20,8 @@
 namespace gn {
 
 constexpr int FT_INPUTS = 22528;
+constexpr int FT_BIAS_ROW = FT_INPUTS; // see the layout above
+constexpr int FT_ROWS = FT_INPUTS + 1;
 constexpr int PSQT_BUCKETS = 8;
 constexpr int LAYER_STACKS = 8;
 constexpr uint32_t NNUE_VERSION = 0x7AF32F20u;
