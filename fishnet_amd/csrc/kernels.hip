@@ -869,6 +869,7 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
   const size_t vgrid = swz ? 8 * ((n_parents + 7) / 8) : n_parents;
   for (size_t v = blockIdx.x; v < vgrid; v += gridDim.x) {
     __syncthreads(); // LDS of the previous parent is dead
+    GN_STAMP_INIT();
     size_t p = v;
     if (swz) {
       const size_t p8 = (n_parents + 7) / 8;
@@ -898,6 +899,7 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
     }
     if (!__syncthreads_or(want)) continue;
     if (!pcount) continue;
+    GN_STAMP(0);
 
     // per-thread state across the tiles of this parent
     const int hu = __builtin_amdgcn_readfirstlane((tid / G) & 1);
@@ -954,15 +956,21 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
         const int pk1 = __shfl(key1, (km1 & lt) ? 63 - __builtin_clzll(km1 & lt) : 0);
         const bool hit0 = key0 >= 0 && key0 == ((km0 & lt) ? pk0 : ckey0);
         const bool hit1 = key1 >= 0 && key1 == ((km1 & lt) ? pk1 : ckey1);
-        // entry counts and their inclusive prefix sums (both perspectives packed)
-        const uint32_t c = (uint32_t)n0 | (uint32_t)n1 << 16;
+        // Entry counts.  Delta and parent entries stay in their own perspective's list
+        // (they start from that perspective's parent accumulator); a king-move refresh
+        // (zero + bias + all rows) needs no accumulator, so it goes to whichever list is
+        // shorter: the two wave groups finish the stream together.
+        const bool ref0 = (kinds & 3) == 2, ref1 = (kinds >> 2) == 2;
+        const int nr = ref0 ? n0 : ref1 ? n1 : 0;
+        const uint32_t c = (uint32_t)(ref0 ? 0 : n0) | (uint32_t)(ref1 ? 0 : n1) << 10 | (uint32_t)nr << 20;
         uint32_t inc = c;
 #pragma unroll
         for (int d = 1; d < TILE; d <<= 1) {
           const uint32_t o = __shfl_up(inc, d);
           if (lane >= d) inc += o;
         }
-        const bool fits = inb && (inc & 0xFFFF) <= CAP && (inc >> 16) <= CAP;
+        // fits even if every refresh landed in the same list
+        const bool fits = inb && (inc & 1023) + (inc >> 20) <= CAP && ((inc >> 10) & 1023) + (inc >> 20) <= CAP;
         const int m = __builtin_ctzll(~__ballot(fits)); // >= 1: one slot never exceeds CAP
         const uint32_t exc = inc - c;
         const bool mine = lane < m;
@@ -983,19 +991,6 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
           valid[lane] = (uint8_t)(mine && vld);
           bkt[lane] = (uint8_t)bk;
         }
-        if (lane == 0) {
-          bmask = bm;
-          tctl[0] = (uint32_t)m;
-          tctl[1] = last_inc & 0xFFFF;
-          tctl[2] = last_inc >> 16;
-        }
-        // pad both lists to a multiple of 4 with PSQT-only entries of row 0 (harmless:
-        // they follow the last slot of the list, no row is loaded)
-        if (lane < 3) {
-          const uint32_t l0 = last_inc & 0xFFFF, l1 = last_inc >> 16;
-          if (l0 + lane < ((l0 + 3) & ~3u)) ent[0][l0 + lane] = PSQ_ONLY;
-          if (l1 + lane < ((l1 + 3) & ~3u)) ent[1][l1 + lane] = PSQ_ONLY;
-        }
         if (mine) {
           const uint32_t t0w = tmpl(lane, stm != 0, bk), t1w = tmpl(lane, stm != 1, bk);
           // delta rows: k < s removed (idx 0, 1), then added (idx 2, 3); s in {1, 2}
@@ -1008,49 +1003,67 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
             if (n > 2) e[2] = cl(r2) | t | (n == 3 ? LAST : 0u);
             if (n > 3) e[3] = cl(r3) | t | LAST;
           };
-          uint32_t *e0 = ent[0] + (exc & 0xFFFF), *e1 = ent[1] + (exc >> 16);
+          uint32_t *e0 = ent[0] + (exc & 1023), *e1 = ent[1] + ((exc >> 10) & 1023);
           if ((kinds & 3) == 1) delta(e0, w0, w1, s0, n0, hit0, t0w);
-          else if (kinds & 3) e0[0] = (uint32_t)FT_BIAS_ROW | t0w | I_ZERO | ((kinds & 3) == 3 ? PAR_E : 0u);
           if ((kinds >> 2) == 1) delta(e1, w2, w3, s1, n1, hit1, t1w);
-          else if (kinds >> 2) e1[0] = (uint32_t)FT_BIAS_ROW | t1w | I_ZERO | ((kinds >> 2) == 3 ? PAR_E : 0u);
+          if (kinds == 15) { // the parent: bias entry, its rows follow (below)
+            e0[0] = (uint32_t)FT_BIAS_ROW | t0w | I_ZERO | PAR_E;
+            e1[0] = (uint32_t)FT_BIAS_ROW | t1w | I_ZERO | PAR_E;
+          }
         }
-        // refresh entries, lane = square: the parent (both perspectives) and king moves
-        uint64_t jm = __ballot(mine && (kinds & 10));
+        // the parent's rows (lane = row), in its own lists after the bias entry
+        if (__builtin_amdgcn_readfirstlane(t0) == 0) {
+          const int st = __shfl(stm, 0);
+#pragma unroll
+          for (int hh = 0; hh < 2; ++hh)
+            if (lane < P)
+              ent[hh][1 + lane] = ft_row(prow[hh][lane]) | tmpl(0, hh != st, bp) | PAR_E | (lane == P - 1 ? LAST : 0u);
+        }
+        // king-move refreshes (lane = square), each appended to the shorter list
+        int len0 = (int)(last_inc & 1023), len1 = (int)((last_inc >> 10) & 1023);
+        uint64_t jm = __ballot(mine && (ref0 || ref1));
         while (jm) {
           const int l = __builtin_ctzll(jm);
           jm &= jm - 1;
-          const int kl = __shfl(kinds, l), st = __shfl(stm, l), cn = __shfl(cnt, l);
-          const uint32_t ex = __shfl(exc, l);
-#pragma unroll
-          for (int hh = 0; hh < 2; ++hh) {
-            const int kd = (kl >> (2 * hh)) & 3;
-            if (kd < 2) continue;
-            const uint32_t t = tmpl(l, hh != st, (cn - 1) / 4) | (kd == 3 ? PAR_E : 0u);
-            uint32_t *e = ent[hh] + (hh ? ex >> 16 : ex & 0xFFFF) + 1;
-            if (kd == 3) {
-              if (lane < P) e[lane] = ft_row(prow[hh][lane]) | t | (lane == P - 1 ? LAST : 0u);
-            } else {
-              const uint32_t sq01 = __shfl(hh ? w2 : w0, l), sq23 = __shfl(hh ? w3 : w1, l);
-              const int kf = sq01 & 0xFFFF, kt = sq01 >> 16, rf = sq23 & 0xFFFF, rt = sq23 >> 16;
-              // wave_features_king_move, written as entries
-              const uint64_t occ = pbd.occ;
-              const bool has = (occ >> lane) & 1;
-              const int k = popcnt(occ & ((1ull << lane) - 1));
-              uint64_t wlo, whi;
-              piece_words(pbd, wlo, whi);
-              int pc = has && k < 32 ? piece_nibble(wlo, whi, k) : 0;
-              if (lane == kf || lane == rf) pc = 0;
-              if (lane == rt) pc = make_piece(hh, ROOK);
-              if (lane == kt) pc = make_piece(hh, KING);
-              const uint64_t cocc = __ballot(pc != 0);
-              const int pos = popcnt(cocc & ((1ull << lane) - 1));
-              if (pc && pos < cn)
-                e[pos] = (uint32_t)feature_index(hh, lane, pc, kt) | t | (pos == cn - 1 ? LAST : 0u);
-            }
-          }
+          const int hh = __shfl((int)ref1, l), st = __shfl(stm, l), cn = __shfl(cnt, l);
+          const int g = len0 <= len1 ? 0 : 1;
+          uint32_t *e = ent[g] + (g ? len1 : len0);
+          if (g) len1 += cn + 1;
+          else len0 += cn + 1;
+          const uint32_t t = tmpl(l, hh != st, (cn - 1) / 4);
+          if (lane == 0) e[0] = (uint32_t)FT_BIAS_ROW | t | I_ZERO;
+          const uint32_t sq01 = __shfl(hh ? w2 : w0, l), sq23 = __shfl(hh ? w3 : w1, l);
+          const int kf = sq01 & 0xFFFF, kt = sq01 >> 16, rf = sq23 & 0xFFFF, rt = sq23 >> 16;
+          // wave_features_king_move, written as entries
+          const uint64_t occ = pbd.occ;
+          const bool has = (occ >> lane) & 1;
+          const int k = popcnt(occ & ((1ull << lane) - 1));
+          uint64_t wlo, whi;
+          piece_words(pbd, wlo, whi);
+          int pc = has && k < 32 ? piece_nibble(wlo, whi, k) : 0;
+          if (lane == kf || lane == rf) pc = 0;
+          if (lane == rt) pc = make_piece(hh, ROOK);
+          if (lane == kt) pc = make_piece(hh, KING);
+          const uint64_t cocc = __ballot(pc != 0);
+          const int pos = popcnt(cocc & ((1ull << lane) - 1));
+          if (pc && pos < cn)
+            e[1 + pos] = (uint32_t)feature_index(hh, lane, pc, kt) | t | (pos == cn - 1 ? LAST : 0u);
+        }
+        if (lane == 0) {
+          bmask = bm;
+          tctl[0] = (uint32_t)m;
+          tctl[1] = (uint32_t)len0;
+          tctl[2] = (uint32_t)len1;
+        }
+        // pad both lists to a multiple of 4 with PSQT-only entries of row 0 (harmless:
+        // they follow the last slot of the list, no row is loaded)
+        if (lane < 3) {
+          if (len0 + lane < ((len0 + 3) & ~3)) ent[0][len0 + lane] = PSQ_ONLY;
+          if (len1 + lane < ((len1 + 3) & ~3)) ent[1][len1 + lane] = PSQ_ONLY;
         }
       }
       __syncthreads();
+      GN_STAMP(2);
       const int m = (int)tctl[0];
 
       // ---- phase 1: the row stream of this wave's perspective.  Every ring step issues
@@ -1143,6 +1156,7 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
         }
       }
       __syncthreads();
+      GN_STAMP(4);
       // ---- phase 2: layer stack
       if (!(ablate & 4)) {
         int tl = tid;
@@ -1156,7 +1170,9 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
       }
       t0 += m;
       __syncthreads(); // entry lists / layer-stack scratch / xt reused by the next tile
+      GN_STAMP(5);
     }
+    GN_STAMP_FLUSH();
   }
 }
 
