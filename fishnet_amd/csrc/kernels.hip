@@ -817,23 +817,47 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR) __attribute__((amdgpu_wav
 }
 
 // ------------------------------------------------------- expand_stream --
-// expand_eval for the big net with the gather as ONE row stream per perspective
-// and tile.  The slot programs of a tile (parent refresh, king-move refreshes,
-// child deltas) are flattened into a list of row entries in LDS; each wave walks
-// its perspective's list with a 4-deep register ring, so up to 4 rows stay in
-// flight across slot boundaries instead of one dependent round trip per slot.
-// A refresh is zero + the bias row (FT_BIAS_ROW) + the feature rows.
+// expand_eval for the big nets with the gather as ONE row stream per perspective
+// list and tile.  The slot programs of a tile (parent refresh, king-move refreshes,
+// child deltas) are flattened into lists of row entries in LDS; each wave walks its
+// list with a 4-deep register ring, so up to 4 rows stay in flight across slot
+// boundaries instead of one dependent round trip per slot.  A refresh is the bias
+// row (FT_BIAS_ROW) + the feature rows.  PSQT is not in the stream: the waves that
+// are idle while wave 0 builds the lists sum it lane-parallel (one round trip).
 // Entry (u32): [14:0] row, [15] subtract, [17:16] init before this entry
 // (0 none, 1 zero, 2 parent, 3 sibling base), [18] save base after it,
 // [19] last entry of its slot, [23:20] slot, [24] side (0: perspective to move),
-// [25] entry of the parent slot, [28:26] bucket, [29] PSQT only (sibling hit).
+// [25] entry of the parent slot.
 namespace es {
 constexpr uint32_t SUB = 1u << 15, I_ZERO = 1u << 16, I_PACC = 2u << 16, I_BASE = 3u << 16, SAVEB = 1u << 18,
-                   LAST = 1u << 19, PAR_E = 1u << 25, PSQ_ONLY = 1u << 29;
-__device__ __forceinline__ uint32_t tmpl(int slot, int side, int bucket) {
-  return (uint32_t)slot << 20 | (uint32_t)side << 24 | (uint32_t)bucket << 26;
-}
+                   LAST = 1u << 19, PAR_E = 1u << 25;
+__device__ __forceinline__ uint32_t tmpl(int slot, int side) { return (uint32_t)slot << 20 | (uint32_t)side << 24; }
 } // namespace es
+
+// rows of perspective h of a child whose h-king moved kf -> kt (castling: rook rf -> rt,
+// 64 = none), from the parent board, lane = square: the row of this lane's piece in
+// the child (or -1) and its rank among the child's pieces.  All 64 lanes.
+__device__ __forceinline__ int king_move_row(const gn_board &pb, int h, int kf, int kt, int rf, int rt, int lane,
+                                             int &pos) {
+  const uint64_t occ = pb.occ;
+  const bool has = (occ >> lane) & 1;
+  const int k = popcnt(occ & ((1ull << lane) - 1));
+  uint64_t wlo, whi;
+  piece_words(pb, wlo, whi);
+  int pc = has && k < 32 ? piece_nibble(wlo, whi, k) : 0;
+  if (lane == kf || lane == rf) pc = 0;
+  if (lane == rt) pc = make_piece(h, ROOK);
+  if (lane == kt) pc = make_piece(h, KING);
+  const uint64_t cocc = __ballot(pc != 0);
+  pos = popcnt(cocc & ((1ull << lane) - 1));
+  return pc ? feature_index(h, lane, pc, kt) : -1;
+}
+
+__device__ __forceinline__ int32_t wave_sum(int32_t v) {
+#pragma unroll
+  for (int off = 32; off; off >>= 1) v = wadd(v, __shfl_xor(v, off));
+  return v;
+}
 
 template <int L1>
 __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_EXPAND_WPE)))
@@ -848,24 +872,29 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
   constexpr int TILE = 16;
   constexpr int XS = L1 + 16;
   constexpr uint32_t RS = 2 * L1 + 32;
-  constexpr int CAP = 256; // row entries per perspective and tile
+  constexpr int CAP = 256;         // row entries per list and tile
+  constexpr int FILL = CAP - 8;    // content limit: padding to 4 + 4 run-ahead entries
   constexpr int SCRATCH = 2 * CAP * 4 > LS_SCRATCH ? 2 * CAP * 4 : LS_SCRATCH;
   constexpr int CDL = 48;
-  static_assert(G % 64 == 0, "perspective groups must be whole waves");
+  static_assert(G % 64 == 0 && NW >= 2, "perspective groups must be whole waves");
   __shared__ __attribute__((aligned(16))) uint8_t xt[TILE * XS];
   __shared__ __attribute__((aligned(16))) uint8_t scratch[SCRATCH]; // entry lists, then layer-stack scratch
   __shared__ uint16_t prow[2][32];
-  __shared__ int32_t psq[TILE][2];
-  __shared__ uint8_t bkt[TILE], valid[TILE];
+  __shared__ int32_t psa[TILE][2];  // PSQT partial sums by absolute perspective
+  __shared__ int32_t psqf[TILE][2]; // final PSQT accumulators by side (layer-stack input)
+  __shared__ int32_t pps[2][2];     // parent PSQT per perspective at buckets bp, b2
+  __shared__ uint8_t bkt[TILE], valid[TILE], sstm[TILE], pinit[TILE][2];
   __shared__ uint32_t cdl[CDL][5];
   __shared__ gn_board pbd;
   __shared__ int pcount;
-  __shared__ uint32_t tctl[3]; // slots in this tile, entries of perspective 0 / 1
+  __shared__ uint32_t tctl[3]; // slots in this tile, entries of list 0 / 1
   __shared__ uint32_t bmask;
   uint32_t(*ent)[CAP] = reinterpret_cast<uint32_t(*)[CAP]>(scratch);
 
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const __amdgpu_buffer_rsrc_t ftr =
+      __builtin_amdgcn_make_buffer_rsrc((void *)net.ft, 0, (int)((size_t)FT_ROWS * RS), 0x00020000);
   const size_t vgrid = swz ? 8 * ((n_parents + 7) / 8) : n_parents;
   for (size_t v = blockIdx.x; v < vgrid; v += gridDim.x) {
     __syncthreads(); // LDS of the previous parent is dead
@@ -903,53 +932,54 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
 
     // per-thread state across the tiles of this parent
     const int hu = __builtin_amdgcn_readfirstlane((tid / G) & 1);
-    const bool psqw = __builtin_amdgcn_readfirstlane((tid % G) >> 6) == 0; // the perspective's first wave sums PSQT
     const int P = pcount, bp = (P - 1) / 4, b2 = P >= 2 ? (P - 2) / 4 : bp;
     ushort8 pacc_lo = {}, pacc_hi = {}, base_lo = {}, base_hi = {};
-    uint32_t pps0 = 0, pps1 = 0; // parent PSQT at buckets bp / b2 (psq waves, scalar)
-    int ckey0 = -1, ckey1 = -1;  // sibling-cache keys carried across tiles (wave 0)
-    const __amdgpu_buffer_rsrc_t ftr =
-        __builtin_amdgcn_make_buffer_rsrc((void *)net.ft, 0, (int)((size_t)FT_ROWS * RS), 0x00020000);
-    const __amdgpu_buffer_rsrc_t nul = __builtin_amdgcn_make_buffer_rsrc((void *)net.ft, 0, 0, 0x00020000);
+    int ckey0 = -1, ckey1 = -1; // sibling-cache keys carried across tiles (wave 0)
 
 #pragma unroll 1
     for (int t0 = 0; t0 < total;) {
-      // ---- phase 0 (wave 0, lane = slot): descriptors -> entry counts -> prefix sums ->
-      // tile cut -> delta entries; refresh entries (parent, king moves) by the same wave
-      if (wave == 0) {
-        int lane = tid;
-        asm volatile("" : "+v"(lane));
-        lane &= 63;
-        const int qq = t0 + lane;
-        const bool inb = lane < TILE && qq < total;
-        // per slot: kinds (2 bits per perspective: 0 none, 1 delta, 2 king-move refresh,
-        // 3 parent), counts, the ChildDelta words
-        int vld = 0, stm = 0, cnt = 1, kinds = 0, n0 = 0, n1 = 0, s0 = 0, s1 = 0;
-        uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0; // idx[0][0..3], idx[1][0..3] as u16 pairs
-        if (inb) {
-          if (qq == 0) {
-            vld = need_parent ? need_parent[p] : 1;
-            stm = pbd.stm_ep >> 7, cnt = P, kinds = 3 | 3 << 2, n0 = n1 = P + 1;
-          } else if ((vld = need_child ? need_child[off + qq - 1] : 1)) {
-            uint32_t meta;
-            if (qq - 1 < CDL) {
-              w0 = cdl[qq - 1][0], w1 = cdl[qq - 1][1], w2 = cdl[qq - 1][2], w3 = cdl[qq - 1][3];
-              meta = cdl[qq - 1][4];
-            } else {
-              const uint32_t *src = reinterpret_cast<const uint32_t *>(deltas + off + qq - 1);
-              w0 = src[0], w1 = src[1], w2 = src[2], w3 = src[3], meta = src[4];
-            }
-            stm = (meta >> 10) & 1;
-            cnt = (meta >> 14) & 63;
-            if (meta & (1u << 8)) kinds |= 2, n0 = cnt + 1;
-            else kinds |= 1, s0 = meta & 3, n0 = s0 + ((meta >> 2) & 3);
-            if (meta & (1u << 9)) kinds |= 2 << 2, n1 = cnt + 1;
-            else kinds |= 1 << 2, s1 = (meta >> 4) & 3, n1 = s1 + ((meta >> 6) & 3);
+      int lane = tid;
+      asm volatile("" : "+v"(lane));
+      lane &= 63;
+      // slot descriptor of lane & 15 (both the list builder and the PSQT waves)
+      auto desc = [&](int sl, int &vld, int &stm, int &cnt, int &kinds, int &n0, int &n1, int &s0, int &s1,
+                      uint32_t &w0, uint32_t &w1, uint32_t &w2, uint32_t &w3) {
+        const int qq = t0 + sl;
+        vld = 0, stm = 0, cnt = 1, kinds = 0, n0 = n1 = s0 = s1 = 0, w0 = w1 = w2 = w3 = 0;
+        if (sl >= TILE || qq >= total) return;
+        if (qq == 0) {
+          vld = need_parent ? need_parent[p] : 1;
+          stm = pbd.stm_ep >> 7, cnt = P, kinds = 3 | 3 << 2, n0 = n1 = P + 1;
+        } else if ((vld = need_child ? need_child[off + qq - 1] : 1)) {
+          uint32_t meta;
+          if (qq - 1 < CDL) {
+            w0 = cdl[qq - 1][0], w1 = cdl[qq - 1][1], w2 = cdl[qq - 1][2], w3 = cdl[qq - 1][3];
+            meta = cdl[qq - 1][4];
+          } else {
+            const uint32_t *src = reinterpret_cast<const uint32_t *>(deltas + off + qq - 1);
+            w0 = src[0], w1 = src[1], w2 = src[2], w3 = src[3], meta = src[4];
           }
+          stm = (meta >> 10) & 1;
+          cnt = (meta >> 14) & 63;
+          if (meta & (1u << 8)) kinds |= 2, n0 = cnt + 1;
+          else kinds |= 1, s0 = meta & 3, n0 = s0 + ((meta >> 2) & 3);
+          if (meta & (1u << 9)) kinds |= 2 << 2, n1 = cnt + 1;
+          else kinds |= 1 << 2, s1 = (meta >> 4) & 3, n1 = s1 + ((meta >> 6) & 3);
         }
+      };
+
+      // ---- phase 0.  Wave 0 (lane = slot): descriptors -> sibling hits -> entry counts ->
+      // prefix sums -> tile cut -> entries.  The other waves: PSQT sums of the same
+      // slots (deltas lane-parallel, refreshes wave-parallel), one round trip.
+      if (wave == 0) {
+        int vld, stm, cnt, kinds, n0, n1, s0, s1;
+        uint32_t w0, w1, w2, w3;
+        desc(lane, vld, stm, cnt, kinds, n0, n1, s0, s1, w0, w1, w2, w3);
+        const bool inb = lane < TILE && t0 + lane < total;
         const int key0 = (kinds & 3) == 1 ? (int)(w0 & 0xFFFF) : -1;
         const int key1 = (kinds >> 2) == 1 ? (int)(w2 & 0xFFFF) : -1;
-        // sibling cache: the key before slot l is that of the nearest earlier delta slot
+        // sibling cache: the key before slot l is that of the nearest earlier delta slot;
+        // a hit starts from the cached (parent - from-row) and drops the from-row entry
         const uint64_t km0 = __ballot(key0 >= 0) & 0xFFFFull, km1 = __ballot(key1 >= 0) & 0xFFFFull;
         const uint64_t lt = (1ull << lane) - 1;
         const int pk0 = __shfl(key0, (km0 & lt) ? 63 - __builtin_clzll(km0 & lt) : 0);
@@ -957,12 +987,13 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
         const bool hit0 = key0 >= 0 && key0 == ((km0 & lt) ? pk0 : ckey0);
         const bool hit1 = key1 >= 0 && key1 == ((km1 & lt) ? pk1 : ckey1);
         // Entry counts.  Delta and parent entries stay in their own perspective's list
-        // (they start from that perspective's parent accumulator); a king-move refresh
-        // (zero + bias + all rows) needs no accumulator, so it goes to whichever list is
-        // shorter: the two wave groups finish the stream together.
+        // (they start from that perspective's accumulators); a king-move refresh needs
+        // no accumulator, so it goes to whichever list is shorter and the two wave
+        // groups finish the stream together.
         const bool ref0 = (kinds & 3) == 2, ref1 = (kinds >> 2) == 2;
         const int nr = ref0 ? n0 : ref1 ? n1 : 0;
-        const uint32_t c = (uint32_t)(ref0 ? 0 : n0) | (uint32_t)(ref1 ? 0 : n1) << 10 | (uint32_t)nr << 20;
+        const int d0 = ref0 ? 0 : n0 - (hit0 ? 1 : 0), d1 = ref1 ? 0 : n1 - (hit1 ? 1 : 0);
+        const uint32_t c = (uint32_t)d0 | (uint32_t)d1 << 10 | (uint32_t)nr << 20;
         uint32_t inc = c;
 #pragma unroll
         for (int d = 1; d < TILE; d <<= 1) {
@@ -970,8 +1001,9 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
           if (lane >= d) inc += o;
         }
         // fits even if every refresh landed in the same list
-        const bool fits = inb && (inc & 1023) + (inc >> 20) <= CAP && ((inc >> 10) & 1023) + (inc >> 20) <= CAP;
-        const int m = __builtin_ctzll(~__ballot(fits)); // >= 1: one slot never exceeds CAP
+        const bool fits =
+            inb && (int)((inc & 1023) + (inc >> 20)) <= FILL && (int)(((inc >> 10) & 1023) + (inc >> 20)) <= FILL;
+        const int m = __builtin_ctzll(~__ballot(fits)); // >= 1: one slot never exceeds FILL
         const uint32_t exc = inc - c;
         const bool mine = lane < m;
         const uint32_t last_inc = __shfl(inc, m - 1);
@@ -990,18 +1022,26 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
         if (lane < TILE) {
           valid[lane] = (uint8_t)(mine && vld);
           bkt[lane] = (uint8_t)bk;
+          sstm[lane] = (uint8_t)stm;
         }
         if (mine) {
-          const uint32_t t0w = tmpl(lane, stm != 0, bk), t1w = tmpl(lane, stm != 1, bk);
+          const uint32_t t0w = tmpl(lane, stm != 0), t1w = tmpl(lane, stm != 1);
           // delta rows: k < s removed (idx 0, 1), then added (idx 2, 3); s in {1, 2}
           auto delta = [&](uint32_t *e, uint32_t lo2, uint32_t hi2, int s, int n, bool hit, uint32_t t) {
             const uint32_t i0 = lo2 & 0xFFFF, i1 = lo2 >> 16, i2 = hi2 & 0xFFFF, i3 = hi2 >> 16;
-            const uint32_t r0 = i0, r1 = s >= 2 ? i1 : i2, r2 = s >= 2 ? i2 : i3, r3 = i3;
-            auto cl = [](uint32_t r) { return r < (uint32_t)FT_ROWS ? r : (uint32_t)FT_BIAS_ROW; };
-            e[0] = cl(r0) | t | SUB | (n == 1 ? LAST : 0u) | (hit ? (I_BASE | PSQ_ONLY) : (I_PACC | SAVEB));
-            if (n > 1) e[1] = cl(r1) | t | (s >= 2 ? SUB : 0u) | (n == 2 ? LAST : 0u);
-            if (n > 2) e[2] = cl(r2) | t | (n == 3 ? LAST : 0u);
-            if (n > 3) e[3] = cl(r3) | t | LAST;
+            auto cl = [](uint32_t r) { return r < (uint32_t)FT_INPUTS ? r : (uint32_t)FT_BIAS_ROW; };
+            uint32_t r[4] = {cl(i0), cl(s >= 2 ? i1 : i2), cl(s >= 2 ? i2 : i3), cl(i3)};
+            uint32_t f[4] = {SUB, s >= 2 ? SUB : 0u, 0u, 0u};
+            if (!hit) {
+              e[0] = r[0] | t | SUB | I_PACC | SAVEB;
+              if (n > 1) e[1] = r[1] | t | f[1] | (n == 2 ? LAST : 0u);
+              if (n > 2) e[2] = r[2] | t | (n == 3 ? LAST : 0u);
+              if (n > 3) e[3] = r[3] | t | LAST;
+            } else { // the from-row is in the cached base
+              e[0] = r[1] | t | f[1] | I_BASE | (n == 2 ? LAST : 0u);
+              if (n > 2) e[1] = r[2] | t | (n == 3 ? LAST : 0u);
+              if (n > 3) e[2] = r[3] | t | LAST;
+            }
           };
           uint32_t *e0 = ent[0] + (exc & 1023), *e1 = ent[1] + ((exc >> 10) & 1023);
           if ((kinds & 3) == 1) delta(e0, w0, w1, s0, n0, hit0, t0w);
@@ -1012,12 +1052,12 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
           }
         }
         // the parent's rows (lane = row), in its own lists after the bias entry
-        if (__builtin_amdgcn_readfirstlane(t0) == 0) {
+        if (t0 == 0) {
           const int st = __shfl(stm, 0);
 #pragma unroll
           for (int hh = 0; hh < 2; ++hh)
             if (lane < P)
-              ent[hh][1 + lane] = ft_row(prow[hh][lane]) | tmpl(0, hh != st, bp) | PAR_E | (lane == P - 1 ? LAST : 0u);
+              ent[hh][1 + lane] = ft_row(prow[hh][lane]) | tmpl(0, hh != st) | PAR_E | (lane == P - 1 ? LAST : 0u);
         }
         // king-move refreshes (lane = square), each appended to the shorter list
         int len0 = (int)(last_inc & 1023), len1 = (int)((last_inc >> 10) & 1023);
@@ -1030,24 +1070,12 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
           uint32_t *e = ent[g] + (g ? len1 : len0);
           if (g) len1 += cn + 1;
           else len0 += cn + 1;
-          const uint32_t t = tmpl(l, hh != st, (cn - 1) / 4);
+          const uint32_t t = tmpl(l, hh != st);
           if (lane == 0) e[0] = (uint32_t)FT_BIAS_ROW | t | I_ZERO;
           const uint32_t sq01 = __shfl(hh ? w2 : w0, l), sq23 = __shfl(hh ? w3 : w1, l);
-          const int kf = sq01 & 0xFFFF, kt = sq01 >> 16, rf = sq23 & 0xFFFF, rt = sq23 >> 16;
-          // wave_features_king_move, written as entries
-          const uint64_t occ = pbd.occ;
-          const bool has = (occ >> lane) & 1;
-          const int k = popcnt(occ & ((1ull << lane) - 1));
-          uint64_t wlo, whi;
-          piece_words(pbd, wlo, whi);
-          int pc = has && k < 32 ? piece_nibble(wlo, whi, k) : 0;
-          if (lane == kf || lane == rf) pc = 0;
-          if (lane == rt) pc = make_piece(hh, ROOK);
-          if (lane == kt) pc = make_piece(hh, KING);
-          const uint64_t cocc = __ballot(pc != 0);
-          const int pos = popcnt(cocc & ((1ull << lane) - 1));
-          if (pc && pos < cn)
-            e[1 + pos] = (uint32_t)feature_index(hh, lane, pc, kt) | t | (pos == cn - 1 ? LAST : 0u);
+          int pos;
+          const int row = king_move_row(pbd, hh, sq01 & 0xFFFF, sq01 >> 16, sq23 & 0xFFFF, sq23 >> 16, lane, pos);
+          if (row >= 0 && pos < cn) e[1 + pos] = (uint32_t)row | t | (pos == cn - 1 ? LAST : 0u);
         }
         if (lane == 0) {
           bmask = bm;
@@ -1055,79 +1083,141 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
           tctl[1] = (uint32_t)len0;
           tctl[2] = (uint32_t)len1;
         }
-        // pad both lists to a multiple of 4 with PSQT-only entries of row 0 (harmless:
-        // they follow the last slot of the list, no row is loaded)
-        if (lane < 3) {
-          if (len0 + lane < ((len0 + 3) & ~3)) ent[0][len0 + lane] = PSQ_ONLY;
-          if (len1 + lane < ((len1 + 3) & ~3)) ent[1][len1 + lane] = PSQ_ONLY;
+        // pad both lists with bias-row entries to a multiple of 4 plus the ring's 4
+        // run-ahead entries (harmless: they follow the last slot of the list)
+        if (lane < 7) {
+          const uint32_t pad = (uint32_t)FT_BIAS_ROW;
+          if (len0 + lane < ((len0 + 3) & ~3) + 4) ent[0][len0 + lane] = pad;
+          if (len1 + lane < ((len1 + 3) & ~3) + 4) ent[1][len1 + lane] = pad;
+        }
+      } else {
+        // PSQT.  Deltas (wave 1, lane = (perspective, slot)): +- the slot's rows at its
+        // bucket, the parent's sum at that bucket is added when the tile is finalised.
+        // Parent (tile 0, wave 1 second pass): both buckets the children can have.
+        // King-move refreshes: one wave per job, lane = square.
+        const int wk = wave - 1, nwk = NW - 1;
+        if (wk == 0) {
+          const int sl = lane & 15, h = (lane >> 4) & 1;
+          int vld, stm, cnt, kinds, n0, n1, s0, s1;
+          uint32_t w0, w1, w2, w3;
+          desc(sl, vld, stm, cnt, kinds, n0, n1, s0, s1, w0, w1, w2, w3);
+          const int kd = h ? kinds >> 2 : kinds & 3, s = h ? s1 : s0, n = h ? n1 : n0;
+          const uint32_t lo2 = h ? w2 : w0, hi2 = h ? w3 : w1;
+          const uint32_t pso = 2 * L1 + 4 * ((cnt - 1) / 4);
+          int32_t sum = 0;
+          if (lane < 32 && vld && kd == 1) {
+            const uint32_t i0 = lo2 & 0xFFFF, i1 = lo2 >> 16, i2 = hi2 & 0xFFFF, i3 = hi2 >> 16;
+            const uint32_t r1 = s >= 2 ? i1 : i2, r2 = s >= 2 ? i2 : i3;
+            const int32_t v0 = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(ftr, ft_row(i0) * RS + pso, 0, 0);
+            const int32_t v1 = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(ftr, ft_row(r1) * RS + pso, 0, 0);
+            const int32_t v2 = n > 2 ? (int32_t)__builtin_amdgcn_raw_buffer_load_b32(ftr, ft_row(r2) * RS + pso, 0, 0) : 0;
+            const int32_t v3 = n > 3 ? (int32_t)__builtin_amdgcn_raw_buffer_load_b32(ftr, ft_row(i3) * RS + pso, 0, 0) : 0;
+            sum = wadd(wadd(-v0, s >= 2 ? -v1 : v1), wadd(v2, v3));
+          }
+          if (lane < 32 && sl + t0 < total && kd != 2) { // refreshes: their job's wave writes
+            psa[sl][h] = sum;
+            pinit[sl][h] = (uint8_t)(kd == 1);
+          }
+          if (t0 == 0) { // the parent: lane = (perspective, row)
+            const int hh = lane >> 5, k = lane & 31;
+            int32_t a = 0, b = 0;
+            if (k < P) {
+              const uint32_t o = ft_row(prow[hh][k]) * RS + 2 * L1;
+              a = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(ftr, o + 4 * bp, 0, 0);
+              b = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(ftr, o + 4 * b2, 0, 0);
+            }
+#pragma unroll
+            for (int o2 = 16; o2; o2 >>= 1) a = wadd(a, __shfl_xor(a, o2)), b = wadd(b, __shfl_xor(b, o2));
+            if (k == 0) {
+              pps[hh][0] = a, pps[hh][1] = b;
+              psa[0][hh] = a;
+              pinit[0][hh] = 0;
+            }
+          }
+        }
+        // king-move refresh jobs, round robin over the PSQT waves
+        int jn = 0;
+        for (int sl = 0; sl < TILE && t0 + sl < total; ++sl) {
+          if (t0 + sl == 0) continue;
+          const int qq = t0 + sl;
+          if (need_child && !need_child[off + qq - 1]) continue;
+          const uint32_t meta = qq - 1 < CDL ? cdl[qq - 1][4] : deltas[off + qq - 1].meta;
+          if (!(meta & (3u << 8))) continue;
+          if (jn++ % nwk != wk) continue;
+          const int hh = (meta >> 9) & 1, cn = (meta >> 14) & 63;
+          const uint32_t sq01 = qq - 1 < CDL ? cdl[qq - 1][2 * hh] : deltas[off + qq - 1].idx[hh][0] |
+                                                                           (uint32_t)deltas[off + qq - 1].idx[hh][1] << 16;
+          const uint32_t sq23 = qq - 1 < CDL ? cdl[qq - 1][2 * hh + 1] : deltas[off + qq - 1].idx[hh][2] |
+                                                                               (uint32_t)deltas[off + qq - 1].idx[hh][3] << 16;
+          int pos;
+          const int row = king_move_row(pbd, hh, sq01 & 0xFFFF, sq01 >> 16, sq23 & 0xFFFF, sq23 >> 16, lane, pos);
+          const int32_t a = row >= 0 ? (int32_t)__builtin_amdgcn_raw_buffer_load_b32(
+                                           ftr, (uint32_t)row * RS + 2 * L1 + 4 * ((cn - 1) / 4), 0, 0)
+                                     : 0;
+          const int32_t sum = wave_sum(a);
+          if (lane == 0) psa[sl][hh] = sum, pinit[sl][hh] = 0;
         }
       }
       __syncthreads();
       GN_STAMP(2);
       const int m = (int)tctl[0];
 
-      // ---- phase 1: the row stream of this wave's perspective.  Every ring step issues
-      // exactly three buffer loads (row halves + PSQT dword) with the row offset as the
-      // scalar offset; loads that are not wanted (PSQT-only entries, PSQT on the other
-      // waves, steps past the list) go through a zero-size descriptor, which returns
-      // zeros without touching memory, so the outstanding-load count is the same on
-      // every path and the waits stay exact, at no vector-ALU cost.
+      // ---- phase 1: the row stream of this wave's list.  Every ring step issues the two
+      // row-half loads with the row offset as the scalar offset (lists are padded, so no
+      // step needs a guard and the outstanding-load count is the same on every path).
       {
         int tl = tid;
         asm volatile("" : "+v"(tl));
         const int jt = tl % G;
-        const int lane = tl & 63;
+        const int ln = tl & 63;
+        // PSQT of the tile's slots by side (wave 0): partial + the parent's at the bucket
+        if (wave == 0 && ln < TILE && ln < m && valid[ln]) {
+          const int st = sstm[ln], useb2 = bkt[ln] != bp;
+          int32_t vv[2];
+#pragma unroll
+          for (int hh = 0; hh < 2; ++hh) vv[hh] = wadd(psa[ln][hh], pinit[ln][hh] ? pps[hh][useb2] : 0);
+          psqf[ln][0] = vv[st];
+          psqf[ln][1] = vv[st ^ 1];
+        }
         const uint32_t j16 = 16 * jt;
-        const int n4 = ((int)tctl[1 + hu] + 3) & ~3; // padded with PSQT-only entries
+        const int n4 = ((int)tctl[1 + hu] + 3) & ~3;
         const uint32_t *E = ent[hu];
-        // parent entries (bucket bp): lane 1 of the PSQT wave sums bucket b2 <= bp instead
-        // (scalar offset at b2, the other lanes add 4 * (bp - b2) in the vector offset)
-        const uint32_t dlt = psqw && jt == 1 ? 0u : 4u * (uint32_t)(bp - b2);
         ushort8 rlo[4], rhi[4];
-        uint32_t rp[4];
         uint32_t er[4];
         ushort8 lo = {}, hi = {};
-        uint32_t ps = 0;
         uint32_t ev = 0;
         auto issue = [&](int r, int i) {
-          const bool live = i < n4;
-          uint32_t e = 0;
-          if (live) {
-            if ((i & 63) == 0) ev = E[i + lane];
-            e = (uint32_t)__builtin_amdgcn_readlane((int)ev, i & 63);
-          }
-          er[r] = e;
-          const uint32_t o = (e & 0x7FFF) * RS;
-          const __amdgpu_buffer_rsrc_t rs = live && !(e & PSQ_ONLY) && !(ablate & 2) ? ftr : nul;
-          rlo[r] = __builtin_bit_cast(ushort8, __builtin_amdgcn_raw_buffer_load_b128(rs, j16, o, 0));
-          rhi[r] = __builtin_bit_cast(ushort8, __builtin_amdgcn_raw_buffer_load_b128(rs, j16 + L1, o, 0));
-          const __amdgpu_buffer_rsrc_t rq = live && psqw ? ftr : nul;
-          const bool par = e & PAR_E;
-          rp[r] = __builtin_amdgcn_raw_buffer_load_b32(rq, par ? dlt : 0u,
-                                                       o + 2 * L1 + 4 * (par ? (uint32_t)b2 : (e >> 26) & 7), 0);
+          if ((i & 63) == 0) ev = E[i + ln];
+          const uint32_t e = er[r] = (uint32_t)__builtin_amdgcn_readlane((int)ev, i & 63);
+          const uint32_t o = (ablate & 2) ? (uint32_t)FT_BIAS_ROW * RS : (e & 0x7FFF) * RS;
+          rlo[r] = __builtin_bit_cast(ushort8, __builtin_amdgcn_raw_buffer_load_b128(ftr, j16, o, 0));
+          rhi[r] = __builtin_bit_cast(ushort8, __builtin_amdgcn_raw_buffer_load_b128(ftr, j16 + L1, o, 0));
         };
         auto consume = [&](int r) {
           const uint32_t e = er[r];
           const uint32_t init = e & (3u << 16);
-          const bool sub = e & SUB;
-          const uint32_t pp = ((e >> 26) & 7) == (uint32_t)bp ? pps0 : pps1;
           // scalar branches; the empty asm keeps the compiler from if-converting them into
           // selects over every alternative (vector work on all paths)
           if (init == I_ZERO) { // the bias row
             asm volatile("");
-            lo = rlo[r], hi = rhi[r], ps = rp[r];
+            lo = rlo[r], hi = rhi[r];
           } else if (init == I_PACC) { // a miss: parent - from-row
             asm volatile("");
-            lo = pacc_lo - rlo[r], hi = pacc_hi - rhi[r], ps = pp - rp[r];
-          } else if (init == I_BASE) { // a hit: the cached parent - from-row
+            lo = pacc_lo - rlo[r], hi = pacc_hi - rhi[r];
+          } else if (init == I_BASE) { // a hit: the cached (parent - from-row) +- the next row
+            if (e & SUB) {
+              asm volatile("");
+              lo = base_lo - rlo[r], hi = base_hi - rhi[r];
+            } else {
+              asm volatile("");
+              lo = base_lo + rlo[r], hi = base_hi + rhi[r];
+            }
+          } else if (e & SUB) {
             asm volatile("");
-            lo = base_lo, hi = base_hi, ps = pp - rp[r];
-          } else if (sub) {
-            asm volatile("");
-            lo -= rlo[r], hi -= rhi[r], ps -= rp[r];
+            lo -= rlo[r], hi -= rhi[r];
           } else {
             asm volatile("");
-            lo += rlo[r], hi += rhi[r], ps += rp[r];
+            lo += rlo[r], hi += rhi[r];
           }
           if (e & SAVEB) {
             asm volatile("");
@@ -1136,12 +1226,7 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
           if (e & LAST) {
             const int sl = (e >> 20) & 15, side = (e >> 24) & 1;
             *reinterpret_cast<uint2 *>(xt + sl * XS + side * (L1 / 2) + 8 * jt) = transform8(lo, hi);
-            if (psqw && jt == 0) psq[sl][side] = (int32_t)ps;
-            if (e & PAR_E) {
-              pacc_lo = lo, pacc_hi = hi;
-              pps0 = (uint32_t)__builtin_amdgcn_readlane((int)ps, 0);
-              pps1 = (uint32_t)__builtin_amdgcn_readlane((int)ps, 1);
-            }
+            if (e & PAR_E) pacc_lo = lo, pacc_hi = hi;
           }
         };
 #pragma unroll
@@ -1161,7 +1246,7 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
       if (!(ablate & 4)) {
         int tl = tid;
         asm volatile("" : "+v"(tl));
-        layer_stack_tile<L1, NW>(net, xt, scratch, psq, tl, bmask, [&](int pos, int bb) {
+        layer_stack_tile<L1, NW>(net, xt, scratch, psqf, tl, bmask, [&](int pos, int bb) {
           return pos < m && valid[pos] && bkt[pos] == bb;
         }, [&](int pos, int2 val) {
           if (t0 + pos == 0) out_parent[p] = val;
