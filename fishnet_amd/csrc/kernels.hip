@@ -262,6 +262,87 @@ __device__ __forceinline__ uint2 transform8(ushort8 lo, ushort8 hi) {
   return make_uint2(__builtin_amdgcn_perm(o[1], o[0], 0x06040200u), __builtin_amdgcn_perm(o[3], o[2], 0x06040200u));
 }
 
+// Layer stack of one bucket by ONE wave (expand_stream): fc_0 accumulates all L1/64
+// k-steps in registers (no partial sums through LDS, no workgroup barrier), so the
+// wave can run it while the rest of the workgroup builds the next tile.  The fc_0
+// result is in the lane layout of the MFMA accumulator, which is exactly what the
+// epilogue of layer_stack_tile reads back from LDS, so the math below is the same.
+// in1: this wave's 16 x 32 B, fwd: its 16 ints (LDS, private to the wave).
+template <int L1, class Valid, class Emit>
+__device__ __forceinline__ void layer_stack_wave(const NetDevice &net, const uint8_t *xt, uint8_t (*in1)[32],
+                                                 int32_t *fwd, const int32_t (*psq)[2], int b, int lane,
+                                                 Valid &&valid, Emit &&emit) {
+  constexpr int XS = L1 + 16, KS = L1 / 64, BATCH = KS % 6 == 0 ? 6 : 4;
+  static_assert(KS % BATCH == 0, "k-steps per batch");
+  const int row = lane & 15, kg = lane >> 4;
+  // fc_1 / fc_2 parameters first: their latency hides behind fc_0
+  const int4v zero = {0, 0, 0, 0};
+  int4v wl = zero, wh = zero;
+  if (kg < 2) {
+    wl = *reinterpret_cast<const int4v *>(net.w1 + ((size_t)b * 32 + row) * 32 + kg * 16);
+    wh = *reinterpret_cast<const int4v *>(net.w1 + ((size_t)b * 32 + 16 + row) * 32 + kg * 16);
+  }
+  const int32_t bias0 = net.b0[b * 16 + row];
+  const int32_t b1l = net.b1[b * 32 + row], b1h = net.b1[b * 32 + 16 + row];
+  const int32_t w2l = net.w2[b * 32 + row], w2h = net.w2[b * 32 + 16 + row];
+  const int32_t b2v = net.b2[b];
+  const int8_t *wb = net.w0 + ((size_t)b * 16 + row) * L1 + kg * 16;
+  const uint8_t *xa = xt + row * XS + kg * 16;
+  int4v acc = zero;
+#pragma unroll 1
+  for (int k0 = 0; k0 < KS; k0 += BATCH) {
+    int4v w[BATCH], a[BATCH];
+#pragma unroll
+    for (int j = 0; j < BATCH; ++j) w[j] = *reinterpret_cast<const int4v *>(wb + 64 * (k0 + j));
+#pragma unroll
+    for (int j = 0; j < BATCH; ++j) a[j] = *reinterpret_cast<const int4v *>(xa + 64 * (k0 + j));
+#pragma unroll
+    for (int j = 0; j < BATCH; ++j) acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[j], w[j], acc, 0, 0, 0);
+  }
+  // SqrClippedReLU / ClippedReLU of fc_0 outputs 0..14, skip term from output 15
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int pos = 4 * kg + i;
+    const int32_t v = wadd(acc[i], bias0);
+    if (row < 15) {
+      const long long s2 = ((long long)v * v) >> 19;
+      in1[pos][row] = (uint8_t)(s2 < 127 ? s2 : 127);
+      in1[pos][15 + row] = (uint8_t)clampi(v >> 6, 0, 127);
+    } else {
+      fwd[pos] = wmul(v, 600 * 16) / (127 * 64);
+      in1[pos][30] = 0;
+      in1[pos][31] = 0;
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const int4v a1 = kg < 2 ? *reinterpret_cast<const int4v *>(&in1[row][kg * 16]) : zero;
+  const int4v cl = __builtin_amdgcn_mfma_i32_16x16x64_i8(a1, wl, zero, 0, 0, 0);
+  const int4v ch = __builtin_amdgcn_mfma_i32_16x16x64_i8(a1, wh, zero, 0, 0, 0);
+  int32_t part[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int32_t l = clampi(wadd(cl[i], b1l) >> 6, 0, 127), hh = clampi(wadd(ch[i], b1h) >> 6, 0, 127);
+    part[i] = w2l * l + w2h * hh;
+  }
+#pragma unroll
+  for (int off = 8; off; off >>= 1)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) part[i] = wadd(part[i], __shfl_xor(part[i], off, 16));
+  if (row == 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int pos = 4 * kg + i;
+      if (valid(pos, b)) {
+        const int32_t positional = wadd(wadd(b2v, part[i]), fwd[pos]);
+        const int32_t psqt = (int32_t)((uint32_t)psq[pos][0] - (uint32_t)psq[pos][1]) / 2;
+        emit(pos, make_int2(psqt / 16, positional / 16));
+      }
+    }
+  }
+}
+
 // --------------------------------------------------------------- eval_net --
 // Workgroup = 2 * G * PAR threads, G = L1 / 16 threads per (position,
 // perspective): thread j of a perspective group owns accumulator columns
@@ -874,30 +955,35 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
   constexpr uint32_t RS = 2 * L1 + 32;
   constexpr int CAP = 256;         // row entries per list and tile
   constexpr int FILL = CAP - 8;    // content limit: padding to 4 + 4 run-ahead entries
-  constexpr int SCRATCH = 2 * CAP * 4 > LS_SCRATCH ? 2 * CAP * 4 : LS_SCRATCH;
+  constexpr int NLS = NW >= 4 ? 2 : 1; // layer-stack waves: the last NLS waves
+  constexpr int NPJ = NW >= 4 ? NW - 1 - NLS : NW - 1; // PSQT refresh-job waves: 1 .. NPJ
   constexpr int CDL = 48;
   static_assert(G % 64 == 0 && NW >= 2, "perspective groups must be whole waves");
   __shared__ __attribute__((aligned(16))) uint8_t xt[TILE * XS];
-  __shared__ __attribute__((aligned(16))) uint8_t scratch[SCRATCH]; // entry lists, then layer-stack scratch
+  __shared__ __attribute__((aligned(16))) uint32_t ent[2][CAP]; // the row-entry lists
+  __shared__ __attribute__((aligned(16))) uint8_t ls_in1[NLS][TILE][32]; // layer-stack waves' scratch
+  __shared__ int32_t ls_fwd[NLS][TILE];
   __shared__ uint16_t prow[2][32];
   __shared__ int32_t psa[TILE][2];  // PSQT partial sums by absolute perspective
-  __shared__ int32_t psqf[TILE][2]; // final PSQT accumulators by side (layer-stack input)
+  __shared__ int32_t psqf[2][TILE][2]; // final PSQT accumulators by side, per tile parity
   __shared__ int32_t pps[2][2];     // parent PSQT per perspective at buckets bp, b2
-  __shared__ uint8_t bkt[TILE], valid[TILE], sstm[TILE], pinit[TILE][2];
+  __shared__ uint8_t tmeta[2][TILE]; // per tile parity: valid | bucket << 1 (read by the layer stack)
+  __shared__ uint8_t sstm[TILE], pinit[TILE][2];
   __shared__ uint32_t cdl[CDL][5];
   __shared__ gn_board pbd;
   __shared__ int pcount;
   __shared__ uint32_t tctl[3]; // slots in this tile, entries of list 0 / 1
   __shared__ uint32_t bmask;
-  uint32_t(*ent)[CAP] = reinterpret_cast<uint32_t(*)[CAP]>(scratch);
 
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const __amdgpu_buffer_rsrc_t ftr =
       __builtin_amdgcn_make_buffer_rsrc((void *)net.ft, 0, (int)((size_t)FT_ROWS * RS), 0x00020000);
   const size_t vgrid = swz ? 8 * ((n_parents + 7) / 8) : n_parents;
+  int tpar = 0; // tile parity: the layer stack of tile k runs beside phase 0 of tile k + 1
+  // (no barrier at the top: the previous parent's last stream barrier already ordered
+  // every use of the LDS written below)
   for (size_t v = blockIdx.x; v < vgrid; v += gridDim.x) {
-    __syncthreads(); // LDS of the previous parent is dead
     GN_STAMP_INIT();
     size_t p = v;
     if (swz) {
@@ -1020,8 +1106,7 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
         for (int b = 0; b < 8; ++b)
           if (__ballot(mine && vld && bk == b)) bm |= 1u << b;
         if (lane < TILE) {
-          valid[lane] = (uint8_t)(mine && vld);
-          bkt[lane] = (uint8_t)bk;
+          tmeta[tpar][lane] = (uint8_t)((mine && vld) | bk << 1);
           sstm[lane] = (uint8_t)stm;
         }
         if (mine) {
@@ -1095,7 +1180,7 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
         // bucket, the parent's sum at that bucket is added when the tile is finalised.
         // Parent (tile 0, wave 1 second pass): both buckets the children can have.
         // King-move refreshes: one wave per job, lane = square.
-        const int wk = wave - 1, nwk = NW - 1;
+        const int wk = wave - 1, nwk = NPJ;
         if (wk == 0) {
           const int sl = lane & 15, h = (lane >> 4) & 1;
           int vld, stm, cnt, kinds, n0, n1, s0, s1;
@@ -1143,7 +1228,7 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
           if (need_child && !need_child[off + qq - 1]) continue;
           const uint32_t meta = qq - 1 < CDL ? cdl[qq - 1][4] : deltas[off + qq - 1].meta;
           if (!(meta & (3u << 8))) continue;
-          if (jn++ % nwk != wk) continue;
+          if (wk >= nwk || jn++ % nwk != wk) continue;
           const int hh = (meta >> 9) & 1, cn = (meta >> 14) & 63;
           const uint32_t sq01 = qq - 1 < CDL ? cdl[qq - 1][2 * hh] : deltas[off + qq - 1].idx[hh][0] |
                                                                            (uint32_t)deltas[off + qq - 1].idx[hh][1] << 16;
@@ -1161,6 +1246,7 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
       __syncthreads();
       GN_STAMP(2);
       const int m = (int)tctl[0];
+      const uint32_t bm_tile = bmask;
 
       // ---- phase 1: the row stream of this wave's list.  Every ring step issues the two
       // row-half loads with the row offset as the scalar offset (lists are padded, so no
@@ -1171,13 +1257,13 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
         const int jt = tl % G;
         const int ln = tl & 63;
         // PSQT of the tile's slots by side (wave 0): partial + the parent's at the bucket
-        if (wave == 0 && ln < TILE && ln < m && valid[ln]) {
-          const int st = sstm[ln], useb2 = bkt[ln] != bp;
+        if (wave == 0 && ln < TILE && ln < m && (tmeta[tpar][ln] & 1)) {
+          const int st = sstm[ln], useb2 = (tmeta[tpar][ln] >> 1) != bp;
           int32_t vv[2];
 #pragma unroll
           for (int hh = 0; hh < 2; ++hh) vv[hh] = wadd(psa[ln][hh], pinit[ln][hh] ? pps[hh][useb2] : 0);
-          psqf[ln][0] = vv[st];
-          psqf[ln][1] = vv[st ^ 1];
+          psqf[tpar][ln][0] = vv[st];
+          psqf[tpar][ln][1] = vv[st ^ 1];
         }
         const uint32_t j16 = 16 * jt;
         const int n4 = ((int)tctl[1 + hu] + 3) & ~3;
@@ -1242,19 +1328,30 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
       }
       __syncthreads();
       GN_STAMP(4);
-      // ---- phase 2: layer stack
-      if (!(ablate & 4)) {
+      // ---- phase 2: layer stack of this tile by the last NLS waves, one bucket per wave at a
+      // time; the other waves go on to the next tile (or parent), which touches none of
+      // what the layer stack reads (xt until the next stream barrier, which these waves
+      // join only when done; tile metadata and PSQT double-buffered by tile parity)
+      if (wave >= NW - NLS && !(ablate & 4)) {
         int tl = tid;
         asm volatile("" : "+v"(tl));
-        layer_stack_tile<L1, NW>(net, xt, scratch, psqf, tl, bmask, [&](int pos, int bb) {
-          return pos < m && valid[pos] && bkt[pos] == bb;
-        }, [&](int pos, int2 val) {
-          if (t0 + pos == 0) out_parent[p] = val;
-          else out_child[off + t0 + pos - 1] = val;
-        });
+        const int lw = wave - (NW - NLS), ln = tl & 63;
+        const uint8_t *meta = tmeta[tpar];
+        const int tp0 = t0;
+        int idx = 0;
+        for (uint32_t mm = bm_tile; mm; mm &= mm - 1, ++idx) {
+          if (idx % NLS != lw) continue;
+          const int b = __builtin_ctz(mm);
+          layer_stack_wave<L1>(net, xt, ls_in1[lw], ls_fwd[lw], psqf[tpar], b, ln, [&](int pos, int bb) {
+            return pos < m && meta[pos] == (1 | bb << 1);
+          }, [&](int pos, int2 val) {
+            if (tp0 + pos == 0) out_parent[p] = val;
+            else out_child[off + tp0 + pos - 1] = val;
+          });
+        }
       }
       t0 += m;
-      __syncthreads(); // entry lists / layer-stack scratch / xt reused by the next tile
+      tpar ^= 1;
       GN_STAMP(5);
     }
     GN_STAMP_FLUSH();
