@@ -174,7 +174,7 @@ def run_expand(c: Ctx, wl: dict, games: int, steps: int, warmup: int):
     alg = rows * (2 * l1 + 4) + n * 32 + children * (24 + 8)
     k = 5 if mode != 2 else 4
     return dict(value=c.world * (n + children) * steps / wall, wall=wall, stage=stage, kern_ms=stage[k], alg=alg,
-                rows=rows, parents=parents, n=n, children=children, gen_s=gen_s, kernel=f"expand_eval<{l1}>")
+                rows=rows, parents=parents, n=n, children=children, gen_s=gen_s, kernel=f"expand_stream<{l1}>" if l1 != 128 else f"expand_eval<{l1}>")
 
 
 def oracle_threads():

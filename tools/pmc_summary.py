@@ -26,7 +26,7 @@ import sys
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-DOMINANT = {"expand": "expand_eval_kernel<3072", "big16m": "eval_net_kernel<3072", "small1m": "eval_net_kernel<128"}
+DOMINANT = {"expand": "expand_stream_kernel<3072", "big16m": "eval_net_kernel<3072", "small1m": "eval_net_kernel<128"}
 N_SIMD = 256 * 4  # CUs x SIMDs
 
 
