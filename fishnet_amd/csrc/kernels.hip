@@ -1199,11 +1199,13 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
             const int32_t v3 = n > 3 ? (int32_t)__builtin_amdgcn_raw_buffer_load_b32(ftr, ft_row(i3) * RS + pso, 0, 0) : 0;
             sum = wadd(wadd(-v0, s >= 2 ? -v1 : v1), wadd(v2, v3));
           }
-          if (lane < 32 && sl + t0 < total && kd != 2) { // refreshes: their job's wave writes
+          if (lane < 32 && sl + t0 < total && kd < 2) { // refreshes, parent: other waves write
             psa[sl][h] = sum;
             pinit[sl][h] = (uint8_t)(kd == 1);
           }
-          if (t0 == 0) { // the parent: lane = (perspective, row)
+        }
+        if (wk == nwk - 1 && t0 == 0) { // the parent (last PSQT wave): lane = (perspective, row)
+          {
             const int hh = lane >> 5, k = lane & 31;
             int32_t a = 0, b = 0;
             if (k < P) {
