@@ -92,6 +92,21 @@ def test_big_stress_net(oracle_lib):
     _cmp(ctx.evaluate_batch(fens, 1), oracle_lib.eval_fens(on, None, fens, 1, threads=8), fens)
 
 
+def test_big_stress_net_expansion(oracle_lib):
+    """Big-net incremental children (expand_stream) under constant int16 wrapping."""
+    from fishnet_amd import gpu_nnue as G, synthnet
+    p = synthnet.cached_synth_net(3072, 11, stress=True)
+    ctx = G.GpuNnue(p, None)
+    on = oracle_lib.Net(p)
+    fens = special_fens() + random_fens(60, 4343)
+    parents, offs, moves, kids = ctx.expand_and_evaluate(fens, 1)
+    for i, fen in enumerate(fens):
+        p_exp, m_exp, k_exp = oracle_lib.expand_eval(on, None, fen, 1)
+        assert tuple(parents[i]) == p_exp, fen
+        got = {int(m): tuple(k) for m, k in zip(moves[offs[i]:offs[i + 1]], kids[offs[i]:offs[i + 1]])}
+        assert got == {int(m): tuple(k) for m, k in zip(m_exp, k_exp)}, fen
+
+
 def test_device_api_matches_host_api(gpu_ctx):
     from fishnet_amd import gpu_nnue as G
     boards = G.random_positions(42, 1000, 4099, 160)
