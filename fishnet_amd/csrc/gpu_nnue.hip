@@ -18,6 +18,7 @@
 
 #include "host_board.h"
 #include "kernels.h"
+#include "sha256.h"
 
 using namespace gn;
 
@@ -804,11 +805,40 @@ int gn_abi_version(void) { return GN_ABI_VERSION; }
 
 const char *gn_last_error(void) { return g_err.c_str(); }
 
+// Stockfish names nets "nn-" + the first 12 hex digits of the file's SHA-256 + ".nnue"
+// (checked after download by Stockfish's `make net`, which fishnet's build runs,
+// /root/reference/build.rs:318-333).  A file named that way must hash to its name.
+static int check_net_name(const char *path, const std::vector<uint8_t> &data) {
+  const char *base = strrchr(path, '/');
+  base = base ? base + 1 : path;
+  if (strlen(base) != 20 || strncmp(base, "nn-", 3) != 0 || strcmp(base + 15, ".nnue") != 0) return GN_OK;
+  for (int i = 3; i < 15; ++i)
+    if (!((base[i] >= '0' && base[i] <= '9') || (base[i] >= 'a' && base[i] <= 'f'))) return GN_OK;
+  Sha256 h;
+  h.update(data.data(), data.size());
+  char hex[65];
+  h.hex(hex);
+  if (strncmp(hex, base + 3, 12) != 0)
+    return fail(GN_E_FORMAT, "%s: content hashes to nn-%.12s.nnue (corrupt or renamed net)", path, hex);
+  return GN_OK;
+}
+
+int gn_net_sha256(const uint8_t *data, size_t len, char *hex65) {
+  if ((!data && len) || !hex65) return fail(GN_E_INVALID, "NULL argument");
+  Sha256 h;
+  h.update(data, len);
+  h.hex(hex65);
+  return GN_OK;
+}
+
 int gn_load_net(const char *big_path, const char *small_path, const int *devices, int n_devices, gn_ctx **out) {
   try {
     std::vector<uint8_t> b, s;
     if (big_path && !read_file(big_path, b)) return fail(GN_E_IO, "cannot read %s", big_path);
     if (small_path && !read_file(small_path, s)) return fail(GN_E_IO, "cannot read %s", small_path);
+    int rc;
+    if (big_path && (rc = check_net_name(big_path, b)) != GN_OK) return rc;
+    if (small_path && (rc = check_net_name(small_path, s)) != GN_OK) return rc;
     return create(big_path ? b.data() : nullptr, b.size(), small_path ? s.data() : nullptr, s.size(), devices,
                   n_devices, out);
   } catch (const std::bad_alloc &) {

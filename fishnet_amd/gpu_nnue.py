@@ -35,7 +35,8 @@ EXPORTS = ["gn_load_net", "gn_load_net_memory", "gn_free", "gn_last_error", "gn_
            "gn_board_to_fen", "gn_random_positions", "gn_evaluate_device", "gn_expand_device",
            "gn_device_alloc", "gn_device_free", "gn_memcpy_h2d", "gn_memcpy_d2h", "gn_synchronize",
            "gn_time_evaluate_device", "gn_random_positions_device", "gn_set_option", "gn_get_option",
-           "gn_time_expand_device", "gn_random_games_device", "gn_replay_game", "gn_evaluate_games"]
+           "gn_time_expand_device", "gn_random_games_device", "gn_replay_game", "gn_evaluate_games",
+           "gn_net_sha256"]
 OPT_INCREMENTAL_CHILDREN, OPT_XCD_SWIZZLE, OPT_KING_SORT = 1, 2, 3
 EXPAND_STAGES = ["count_scan", "total_readback", "write_children", "classify", "small_net", "big_net", "finalize"]
 
@@ -116,6 +117,7 @@ def lib():
                                   C.POINTER(C.c_uint64)],
         "gn_random_games_device": [vp, i32, C.c_uint64, sz, sz, i32, vp, vp],
         "gn_replay_game": [C.POINTER(GnGame), vp, vp, vp, sz, C.POINTER(sz)],
+        "gn_net_sha256": [vp, sz, C.c_char_p],
         "gn_evaluate_games": [vp, vp, sz, i32, i32, vp, vp, vp, sz, vp, vp, vp, sz],
     }
     for name, args in sig.items():
@@ -175,6 +177,14 @@ def replay_game(root_fen: str, moves, skip=()):
     mv = np.zeros(max(cap - 1, 1), dtype=np.uint16)
     _check(lib().gn_replay_game(arr, boards.ctypes.data, skipped.ctypes.data, mv.ctypes.data, cap, C.byref(n)))
     return boards, skipped.astype(bool), mv[:cap - 1]
+
+
+def net_sha256(data: bytes) -> str:
+    """gn_net_sha256: hex SHA-256 (Stockfish net names are nn-<first 12 digits>.nnue)."""
+    out = C.create_string_buffer(65)
+    buf = (C.c_uint8 * max(len(data), 1)).from_buffer_copy(data or b"\0")
+    _check(lib().gn_net_sha256(buf, len(data), out))
+    return out.value.decode()
 
 
 def default_eval_params() -> EvalParams:

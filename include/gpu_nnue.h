@@ -128,6 +128,10 @@ typedef struct gn_ctx gn_ctx;
  * (then only GN_MODE_SMALL works). */
 GN_API int gn_load_net(const char *big_path, const char *small_path, const int *devices, int n_devices,
                 gn_ctx **out);
+/* A file named like Stockfish's nets, "nn-" + 12 lowercase hex digits + ".nnue"
+ * (build.rs:8-9), must hash to its name: the first 12 hex digits of its SHA-256
+ * (the check Stockfish's `make net` does after download, build.rs:318-333);
+ * otherwise gn_load_net fails with GN_E_FORMAT.  Other file names are not checked. */
 /* Same from in-memory .nnue images (e.g. after an RCCL broadcast). */
 GN_API int gn_load_net_memory(const uint8_t *big, size_t big_len, const uint8_t *small, size_t small_len,
                        const int *devices, int n_devices, gn_ctx **out);
@@ -138,6 +142,8 @@ GN_API int gn_get_eval_params(const gn_ctx *ctx, gn_eval_params *out);
 GN_API int gn_set_eval_params(gn_ctx *ctx, const gn_eval_params *params);
 GN_API int gn_set_option(gn_ctx *ctx, int option, int64_t value);
 GN_API int gn_get_option(const gn_ctx *ctx, int option, int64_t *value);
+/* SHA-256 of a buffer as 64 lowercase hex digits + NUL (net provenance; host only). */
+GN_API int gn_net_sha256(const uint8_t *data, size_t len, char *hex65);
 /* network hashes / widths actually loaded (0 when absent) */
 GN_API int gn_net_info(const gn_ctx *ctx, int *big_l1, uint32_t *big_hash, int *small_l1, uint32_t *small_hash);
 

@@ -109,3 +109,31 @@ def test_net_format_errors_reported(G, tmp_path):
     with pytest.raises(G.GnError) as e:
         G.GpuNnue(None, str(tmp_path / "missing.nnue"))
     assert e.value.code == -2
+
+
+def test_net_sha256_matches_hashlib(G):
+    import hashlib
+    rng = np.random.default_rng(3)
+    for n in (0, 1, 55, 56, 63, 64, 65, 119, 1000, 1 << 20):
+        data = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        assert G.net_sha256(data) == hashlib.sha256(data).hexdigest(), n
+
+
+def test_net_named_by_hash_is_checked(G, synth_small_path, tmp_path):
+    """nn-<first 12 hex of SHA-256>.nnue (Stockfish's naming, verified by `make net`,
+    /root/reference/build.rs:318-333): a renamed or corrupted net is rejected before
+    any device work; a correctly named one gets past the check (GN_E_NODEVICE here)."""
+    import hashlib
+    import shutil
+    data = open(synth_small_path, "rb").read()
+    good = tmp_path / f"nn-{hashlib.sha256(data).hexdigest()[:12]}.nnue"
+    bad = tmp_path / "nn-1c0000000000.nnue"
+    shutil.copy(synth_small_path, good)
+    shutil.copy(synth_small_path, bad)
+    with pytest.raises(G.GnError) as e:
+        G.GpuNnue(None, str(bad))
+    assert e.value.code == -3 and "hashes to" in str(e.value)
+    try:
+        G.GpuNnue(None, str(good)).close()
+    except G.GnError as e2:  # no GPU in this container
+        assert e2.code == -7, e2
