@@ -96,9 +96,18 @@ class Ctx:
             self.nn.set_option(G.OPT_XCD_SWIZZLE, args.swizzle)
         if args.king_sort >= 0:
             self.nn.set_option(G.OPT_KING_SORT, args.king_sort)
+        if args.chain is not None:
+            self.nn.set_option(G.OPT_CHAIN, args.chain)
         self.options = {"xcd_swizzle": self.nn.get_option(G.OPT_XCD_SWIZZLE),
                         "king_sort": self.nn.get_option(G.OPT_KING_SORT),
-                        "incremental_children": self.nn.get_option(G.OPT_INCREMENTAL_CHILDREN)}
+                        "incremental_children": self.nn.get_option(G.OPT_INCREMENTAL_CHILDREN),
+                        "chain": self._opt(G.OPT_CHAIN)}
+
+    def _opt(self, option):
+        try:
+            return self.nn.get_option(option)
+        except self.G.GnError:  # an older library (A/B runs through GPU_NNUE_LIB)
+            return None
 
     def barrier_sync(self):
         self.comm.barrier()
@@ -234,6 +243,7 @@ def main():
     ap.add_argument("--check", type=int, default=1024, help="positions / parents re-checked against the oracle")
     ap.add_argument("--swizzle", type=int, default=-1, help="GN_OPT_XCD_SWIZZLE mask (-1: library default)")
     ap.add_argument("--king-sort", type=int, default=-1, help="GN_OPT_KING_SORT (-1: library default)")
+    ap.add_argument("--chain", type=int, default=None, help="GN_OPT_CHAIN (None: library default; -k: exactly k)")
     args = ap.parse_args()
 
     c = Ctx(args)

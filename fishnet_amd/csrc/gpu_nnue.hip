@@ -202,6 +202,9 @@ struct Dev {
   DevBuf<int2> p_osm, p_obg;     // parent-side net outputs during expansion
   DevBuf<uint8_t> p_nsm, p_nbg;  // parent-side net selection during expansion
   DevBuf<unsigned long long> sum;
+  DevBuf<uint8_t> nslot; // chained walk: child of parent i that is parent i + 1 (255: none)
+  DevBuf<uint32_t> tickets; // chained walk: per carry slot, how many workgroups are done with it
+  int chain_k = 1;          // block length of the current expansion (1: no chaining)
   void *scan_tmp = nullptr;
   size_t scan_bytes = 0;
   std::mutex mu;
@@ -213,6 +216,7 @@ struct gn_ctx {
   bool incremental = true; // GN_OPT_INCREMENTAL_CHILDREN
   int swizzle = 1;          // GN_OPT_XCD_SWIZZLE bit mask: 1 expansion, 2 batch evaluation
   bool king_sort = true;    // GN_OPT_KING_SORT
+  int chain = 81;           // GN_OPT_CHAIN (blocks of consecutive parents per workgroup)
   int l1[2] = {0, 0};
   uint32_t hash[2] = {0, 0};
 };
@@ -242,7 +246,8 @@ static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 static int upload_net(Dev &d, int which, const HostNet &h) {
   const size_t RS = 2 * (size_t)h.L1 + 32;
   size_t off[8], o = 0;
-  const size_t sz[8] = {(size_t)FT_ROWS * RS, h.bias.size() * 2, h.w0.size(), h.b0.size() * 4,
+  const int carry = h.L1 == 128 ? 0 : CARRY_SLOTS; // the chained walk's scratch rows
+  const size_t sz[8] = {((size_t)FT_ROWS + 4 * (size_t)carry) * RS, h.bias.size() * 2, h.w0.size(), h.b0.size() * 4,
                         h.w1.size(), h.b1.size() * 4, h.w2.size(), h.b2.size() * 4};
   const void *src[8] = {h.ft.data(), h.bias.data(), h.w0.data(), h.b0.data(),
                         h.w1.data(), h.b1.data(), h.w2.data(), h.b2.data()};
@@ -250,10 +255,13 @@ static int upload_net(Dev &d, int which, const HostNet &h) {
   uint8_t *m = nullptr;
   if (hipMalloc(&m, o) != hipSuccess) return fail(GN_E_NOMEM, "device allocation of %zu bytes failed", o);
   d.net_mem[which] = m;
-  for (int i = 0; i < 8; ++i) HIP_TRY(hipMemcpy(m + off[i], src[i], sz[i], hipMemcpyHostToDevice));
+  for (int i = 0; i < 8; ++i)
+    HIP_TRY(hipMemcpy(m + off[i], src[i], i == 0 ? (size_t)FT_ROWS * RS : sz[i], hipMemcpyHostToDevice));
+  if (carry) HIP_TRY(hipMemset(m + off[0] + (size_t)FT_ROWS * RS, 0, 4 * (size_t)carry * RS));
   NetDevice &n = d.net[which];
   n.L1 = h.L1;
   n.row_stride = (uint32_t)RS;
+  n.carry_slots = carry;
   n.ft = m + off[0];
   n.bias = reinterpret_cast<const int16_t *>(m + off[1]);
   n.w0 = reinterpret_cast<const int8_t *>(m + off[2]);
@@ -419,9 +427,26 @@ static void parallel_for(size_t n, size_t grain, F &&f) {
 // boards (+ moves, + ChildDelta when deltas is non-null).  *total = children.
 // ev (optional) gets 3 events: after count+scan, after the host read of the
 // total, after write_children.
+// Block length of the chained walk for an n-parent expansion: GN_OPT_CHAIN, shortened
+// (to >= 2) when the blocks would not fill the resident workgroups; 1 = off.
+static int chain_len(const gn_ctx *ctx, Dev &d, size_t n) {
+  if (!ctx->incremental || (ctx->chain >= -1 && ctx->chain <= 1) || !d.has[BIG] || !d.net[BIG].carry_slots)
+    return 1;
+  if (ctx->chain < 0) return -ctx->chain; // exact (tests)
+  // keep >= 2048 blocks (8 per resident workgroup) when the batch allows
+  size_t k = (size_t)ctx->chain;
+  if ((n + k - 1) / k < 2048) k = std::max<size_t>(2, std::min(k, n / 2048));
+  return (int)k;
+}
+
 static int generate_children(Dev &d, const gn_board *parents, size_t n, gn_board *children_or_null, size_t cap,
                              uint16_t *moves, bool want_deltas, size_t *total, hipStream_t s, hipEvent_t *ev,
-                             unsigned long long *rows = nullptr) {
+                             unsigned long long *rows = nullptr, int chain_k = 1) {
+  d.chain_k = want_deltas ? chain_k : 1;
+  if (d.chain_k > 1) {
+    HIP_TRY(d.nslot.ensure(n));
+    HIP_TRY(d.tickets.ensure(CARRY_SLOTS));
+  }
   HIP_TRY(d.counts.ensure(n + 1));
   HIP_TRY(d.offsets.ensure(n + 1));
   HIP_TRY(hipMemsetAsync(d.counts.p + n, 0, sizeof(uint64_t), s));
@@ -442,7 +467,8 @@ static int generate_children(Dev &d, const gn_board *parents, size_t n, gn_board
   }
   if (want_deltas) HIP_TRY(d.deltas.ensure(std::max<size_t>(t, 1)));
   if (t) HIP_TRY(launch_write_children(parents, n, d.tables, d.offsets.p, children, moves,
-                                        want_deltas ? d.deltas.p : nullptr, rows, s));
+                                        want_deltas ? d.deltas.p : nullptr, d.chain_k > 1 ? d.nslot.p : nullptr,
+                                        d.chain_k, rows, s));
   if (ev) HIP_TRY(hipEventRecord(ev[2], s));
   return GN_OK;
 }
@@ -492,7 +518,8 @@ static int expand_evaluate(gn_ctx *ctx, Dev &d, const gn_board *parents, size_t 
   if (mode != GN_MODE_BIG) {
     const bool f = mode == GN_MODE_FULL;
     HIP_TRY(launch_expand_net(d.net[SMALL], parents, n, off, children, dl, f ? d.p_nsm.p : nullptr,
-                              f ? d.nsm.p : nullptr, d.p_osm.p, d.osm.p, ctx->swizzle & 1, s));
+                              f ? d.nsm.p : nullptr, d.p_osm.p, d.osm.p, ctx->swizzle & 1, nullptr, nullptr, 1,
+                              s));
     if (f) {
       HIP_TRY(launch_reeval(d.p_osm.p, d.p_nsm.p, n, P, d.p_nbg.p, s));
       HIP_TRY(launch_reeval(d.osm.p, d.nsm.p, total, P, d.nbg.p, s));
@@ -502,7 +529,8 @@ static int expand_evaluate(gn_ctx *ctx, Dev &d, const gn_board *parents, size_t 
   if (mode != GN_MODE_SMALL) {
     const bool f = mode == GN_MODE_FULL;
     HIP_TRY(launch_expand_net(d.net[BIG], parents, n, off, children, dl, f ? d.p_nbg.p : nullptr,
-                              f ? d.nbg.p : nullptr, d.p_obg.p, d.obg.p, ctx->swizzle & 1, s));
+                              f ? d.nbg.p : nullptr, d.p_obg.p, d.obg.p, ctx->swizzle & 1,
+                              d.chain_k > 1 ? d.nslot.p : nullptr, d.tickets.p, d.chain_k, s));
   }
   HIP_TRY(mark(2));
   HIP_TRY(launch_finalize(children, total, mode, d.osm.p, d.obg.p, d.nsm.p, d.nbg.p, P, d.tables, child_out, s));
@@ -590,7 +618,8 @@ static int expand_boards_host(gn_ctx *ctx, const gn_board *boards, size_t n, int
     if (total && (!child_moves || !child_out)) return fail(GN_E_INVALID, "NULL child buffer");
     HIP_TRY(d->moves.ensure(std::max<size_t>(total, 1)));
     size_t t = 0;
-    rc = generate_children(*d, d->io_boards.p, n, nullptr, 0, d->moves.p, ctx->incremental, &t, s, nullptr);
+    rc = generate_children(*d, d->io_boards.p, n, nullptr, 0, d->moves.p, ctx->incremental, &t, s, nullptr, nullptr,
+                           chain_len(ctx, *d, n));
     if (rc) return rc;
     HIP_TRY(d->io_out.ensure(n));
     HIP_TRY(d->io_out2.ensure(std::max<size_t>(t, 1)));
@@ -1061,7 +1090,8 @@ int gn_expand_device(gn_ctx *ctx, int device_slot, const gn_board *d_parents, si
   if (!n) return GN_OK;
   if (!d_children || !d_moves || !d_child_out) return fail(GN_E_INVALID, "NULL child buffer");
   size_t t = 0;
-  int rc = generate_children(*d, d_parents, n, d_children, cap, d_moves, ctx->incremental, &t, s, nullptr);
+  int rc = generate_children(*d, d_parents, n, d_children, cap, d_moves, ctx->incremental, &t, s, nullptr, nullptr,
+                             chain_len(ctx, *d, n));
   *total = t;
   if (t > 0xFFFFFFFFull) return fail(GN_E_CAPACITY, "%zu children exceed 32-bit offsets", t);
   HIP_TRY(launch_offsets_u32(d->offsets.p, n + 1, d_offsets, s));
@@ -1103,7 +1133,7 @@ int gn_time_expand_device(gn_ctx *ctx, int device_slot, const gn_board *d_parent
     he = hipEventRecord(e[0], s);
     if (he != hipSuccess) break;
     rc = generate_children(*d, d_parents, n, nullptr, 0, nullptr, ctx->incremental, &t, s, e + 1,
-                           it == 0 ? d->sum.p : nullptr);
+                           it == 0 ? d->sum.p : nullptr, chain_len(ctx, *d, n));
     if (rc) break;
     HIP_TRY(d->io_out.ensure(n));
     HIP_TRY(d->io_out2.ensure(std::max<size_t>(t, 1)));
@@ -1159,6 +1189,10 @@ int gn_set_option(gn_ctx *ctx, int option, int64_t value) {
   case GN_OPT_KING_SORT:
     ctx->king_sort = value != 0;
     return GN_OK;
+  case GN_OPT_CHAIN:
+    if (value < -(1 << 20) || value > (1 << 20)) return fail(GN_E_INVALID, "chain length out of range");
+    ctx->chain = (int)value;
+    return GN_OK;
   default:
     return fail(GN_E_INVALID, "unknown option %d", option);
   }
@@ -1175,6 +1209,9 @@ int gn_get_option(const gn_ctx *ctx, int option, int64_t *value) {
     return GN_OK;
   case GN_OPT_KING_SORT:
     *value = ctx->king_sort;
+    return GN_OK;
+  case GN_OPT_CHAIN:
+    *value = ctx->chain;
     return GN_OK;
   default:
     return fail(GN_E_INVALID, "unknown option %d", option);

@@ -23,7 +23,10 @@ hipError_t king_sort(const gn_board *boards, size_t n, uint16_t *keys, uint32_t 
 hipError_t launch_expand_net(const NetDevice &net, const gn_board *parents, size_t n, const uint64_t *offsets,
                              const gn_board *children, const ChildDelta *deltas, const uint8_t *need_parent,
                              const uint8_t *need_child, int2 *out_parent, int2 *out_child, int swz,
-                             hipStream_t s);
+                             const uint8_t *next_slot, uint32_t *tickets, int chain_k, hipStream_t s);
+// Chained walk (big nets with carry rows): one workgroup per block of chain_k
+// consecutive parents; parent p + 1 starts from child next_slot[p] of parent p when
+// that child has its placement.  tickets: CARRY_SLOTS words (zeroed by the launcher).
 // GN_MODE_FULL preparation: need_small = valid && |simple_eval| > threshold,
 // need_big = valid && !need_small.
 hipError_t launch_classify(const gn_board *boards, size_t n, const gn_eval_params &P, uint8_t *need_small,
@@ -41,7 +44,7 @@ hipError_t launch_count_children(const gn_board *boards, size_t n, const Tables 
 // children of every board at offsets[i] (exclusive prefix sums of counts)
 hipError_t launch_write_children(const gn_board *boards, size_t n, const Tables *tables,
                                  const uint64_t *offsets, gn_board *children, uint16_t *moves, ChildDelta *deltas,
-                                 unsigned long long *rows, hipStream_t s);
+                                 uint8_t *next_slot, int chain_k, unsigned long long *rows, hipStream_t s);
 // sum of legal-move counts over all boards into *total (added; caller zeroes)
 hipError_t launch_count_sum(const gn_board *boards, size_t n, const Tables *tables,
                             unsigned long long *total, hipStream_t s);

@@ -908,10 +908,11 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR) __attribute__((amdgpu_wav
 // Entry (u32): [14:0] row, [15] subtract, [17:16] init before this entry
 // (0 none, 1 zero, 2 parent, 3 sibling base), [18] save base after it,
 // [19] last entry of its slot, [23:20] slot, [24] side (0: perspective to move),
-// [25] entry of the parent slot.
+// [25] entry of the parent slot, [26] store the slot's accumulator as the next
+// parent's (chained walk), [27] its absolute perspective.
 namespace es {
 constexpr uint32_t SUB = 1u << 15, I_ZERO = 1u << 16, I_PACC = 2u << 16, I_BASE = 3u << 16, SAVEB = 1u << 18,
-                   LAST = 1u << 19, PAR_E = 1u << 25;
+                   LAST = 1u << 19, PAR_E = 1u << 25, NXT = 1u << 26;
 __device__ __forceinline__ uint32_t tmpl(int slot, int side) { return (uint32_t)slot << 20 | (uint32_t)side << 24; }
 } // namespace es
 
@@ -945,7 +946,8 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
     expand_stream_kernel(NetDevice net, const gn_board *__restrict__ parents, const uint64_t *__restrict__ offsets,
                          const ChildDelta *__restrict__ deltas, const uint8_t *__restrict__ need_parent,
                          const uint8_t *__restrict__ need_child, int2 *__restrict__ out_parent,
-                         int2 *__restrict__ out_child, size_t n_parents, int swz, int ablate) {
+                         int2 *__restrict__ out_child, size_t n_parents, int swz, int ablate,
+                         const uint8_t *__restrict__ next_slot, uint32_t *__restrict__ tickets, int chain_k) {
   using namespace es;
   constexpr int G = L1 / 16; // threads per perspective (whole waves)
   constexpr int NT = 2 * G;
@@ -978,19 +980,42 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const __amdgpu_buffer_rsrc_t ftr =
-      __builtin_amdgcn_make_buffer_rsrc((void *)net.ft, 0, (int)((size_t)FT_ROWS * RS), 0x00020000);
-  const size_t vgrid = swz ? 8 * ((n_parents + 7) / 8) : n_parents;
+      __builtin_amdgcn_make_buffer_rsrc((void *)net.ft, 0, (int)(((size_t)FT_ROWS + 4 * (size_t)net.carry_slots) * RS), 0x00020000);
+  // Chained walk: a workgroup takes a block of chain_k consecutive parents.  When parent
+  // p + 1 is a child of parent p (next_slot[p], a game's next position), that child's
+  // accumulators are stored to this workgroup's carry rows (4: parity of p x
+  // perspective, FT rows CARRY_ROW0 + 4 * slot ..) and parent p + 1 starts from them
+  // instead of a bias + P-row refresh.  slot = dispatch index mod CARRY_SLOTS; a
+  // workgroup first waits for the one CARRY_SLOTS dispatches before it to release the
+  // slot (dispatched earlier, so resident or done: the wait always ends).
+  // (32-bit parent indices: the launcher rejects n_parents >= 2^31)
+  const uint32_t np = (uint32_t)n_parents;
+  const uint32_t K = chain_k > 1 && tickets && next_slot && net.carry_slots ? (uint32_t)chain_k : 1;
+  const uint32_t nblk = (np + K - 1) / K;
+  const uint32_t vgrid = swz ? 8 * ((nblk + 7) / 8) : nblk;
   int tpar = 0; // tile parity: the layer stack of tile k runs beside phase 0 of tile k + 1
   // (no barrier at the top: the previous parent's last stream barrier already ordered
   // every use of the LDS written below)
-  for (size_t v = blockIdx.x; v < vgrid; v += gridDim.x) {
+  for (uint32_t v = blockIdx.x; v < vgrid; v += gridDim.x) {
+   uint32_t blk = v;
+   if (swz) {
+     const uint32_t b8 = (nblk + 7) / 8;
+     blk = (v & 7) * b8 + (v >> 3);
+     if (blk >= nblk) continue;
+   }
+   const uint32_t pend = blk * K + K < np ? blk * K + K : np;
+   const uint32_t cslot = v % CARRY_SLOTS;
+   if (K > 1) {
+     if (tid == 0)
+       while (__hip_atomic_load(tickets + cslot, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != v / CARRY_SLOTS)
+         __builtin_amdgcn_s_sleep(8);
+     __syncthreads();
+   }
+   int carry_ok = 0; // the previous parent stored its next-parent accumulators
+   for (uint32_t p = blk * K; p < pend; ++p) {
     GN_STAMP_INIT();
-    size_t p = v;
-    if (swz) {
-      const size_t p8 = (n_parents + 7) / 8;
-      p = (v & 7) * p8 + (v >> 3);
-      if (p >= n_parents) continue;
-    }
+    const int have = carry_ok;
+    carry_ok = 0;
     const uint64_t off = offsets[p];
     const int total = 1 + (int)(offsets[p + 1] - off);
 
@@ -1015,6 +1040,15 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
     if (!__syncthreads_or(want)) continue;
     if (!pcount) continue;
     GN_STAMP(0);
+    // slot of the child that is the next parent (-1: none)
+    int nxq = -1;
+    if (K > 1 && p + 1 < pend) {
+      const int ns = next_slot[p];
+      if (ns != 255 && ns < total - 1 && (!need_child || need_child[off + ns])) nxq = ns + 1;
+    }
+    carry_ok = nxq > 0;
+    // carry rows of this parent: load (written by the previous parent) / store
+    const uint32_t cb = (uint32_t)CARRY_ROW0 + 4 * (v % CARRY_SLOTS), st2 = cb + (p & 1) * 2, ld2 = cb + (~p & 1) * 2;
 
     // per-thread state across the tiles of this parent
     const int hu = __builtin_amdgcn_readfirstlane((tid / G) & 1);
@@ -1035,7 +1069,7 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
         if (sl >= TILE || qq >= total) return;
         if (qq == 0) {
           vld = need_parent ? need_parent[p] : 1;
-          stm = pbd.stm_ep >> 7, cnt = P, kinds = 3 | 3 << 2, n0 = n1 = P + 1;
+          stm = pbd.stm_ep >> 7, cnt = P, kinds = 3 | 3 << 2, n0 = n1 = have ? 1 : P + 1;
         } else if ((vld = need_child ? need_child[off + qq - 1] : 1)) {
           uint32_t meta;
           if (qq - 1 < CDL) {
@@ -1112,32 +1146,36 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
         if (mine) {
           const uint32_t t0w = tmpl(lane, stm != 0), t1w = tmpl(lane, stm != 1);
           // delta rows: k < s removed (idx 0, 1), then added (idx 2, 3); s in {1, 2}
-          auto delta = [&](uint32_t *e, uint32_t lo2, uint32_t hi2, int s, int n, bool hit, uint32_t t) {
+          const bool nx = t0 + lane == nxq; // this slot is the next parent: store its accumulators
+          auto delta = [&](uint32_t *e, uint32_t lo2, uint32_t hi2, int s, int n, bool hit, uint32_t t, uint32_t L) {
             const uint32_t i0 = lo2 & 0xFFFF, i1 = lo2 >> 16, i2 = hi2 & 0xFFFF, i3 = hi2 >> 16;
             auto cl = [](uint32_t r) { return r < (uint32_t)FT_INPUTS ? r : (uint32_t)FT_BIAS_ROW; };
             uint32_t r[4] = {cl(i0), cl(s >= 2 ? i1 : i2), cl(s >= 2 ? i2 : i3), cl(i3)};
             uint32_t f[4] = {SUB, s >= 2 ? SUB : 0u, 0u, 0u};
             if (!hit) {
               e[0] = r[0] | t | SUB | I_PACC | SAVEB;
-              if (n > 1) e[1] = r[1] | t | f[1] | (n == 2 ? LAST : 0u);
-              if (n > 2) e[2] = r[2] | t | (n == 3 ? LAST : 0u);
-              if (n > 3) e[3] = r[3] | t | LAST;
+              if (n > 1) e[1] = r[1] | t | f[1] | (n == 2 ? L : 0u);
+              if (n > 2) e[2] = r[2] | t | (n == 3 ? L : 0u);
+              if (n > 3) e[3] = r[3] | t | L;
             } else { // the from-row is in the cached base
-              e[0] = r[1] | t | f[1] | I_BASE | (n == 2 ? LAST : 0u);
-              if (n > 2) e[1] = r[2] | t | (n == 3 ? LAST : 0u);
-              if (n > 3) e[2] = r[3] | t | LAST;
+              e[0] = r[1] | t | f[1] | I_BASE | (n == 2 ? L : 0u);
+              if (n > 2) e[1] = r[2] | t | (n == 3 ? L : 0u);
+              if (n > 3) e[2] = r[3] | t | L;
             }
           };
           uint32_t *e0 = ent[0] + (exc & 1023), *e1 = ent[1] + ((exc >> 10) & 1023);
-          if ((kinds & 3) == 1) delta(e0, w0, w1, s0, n0, hit0, t0w);
-          if ((kinds >> 2) == 1) delta(e1, w2, w3, s1, n1, hit1, t1w);
-          if (kinds == 15) { // the parent: bias entry, its rows follow (below)
+          if ((kinds & 3) == 1) delta(e0, w0, w1, s0, n0, hit0, t0w, LAST | (nx ? NXT : 0u));
+          if ((kinds >> 2) == 1) delta(e1, w2, w3, s1, n1, hit1, t1w, LAST | (nx ? NXT | 1u << 27 : 0u));
+          if (kinds == 15 && have) { // the parent from the carry rows (one entry per list)
+            e0[0] = ld2 | t0w | I_ZERO | PAR_E | LAST;
+            e1[0] = (ld2 + 1) | t1w | I_ZERO | PAR_E | LAST;
+          } else if (kinds == 15) { // the parent: bias entry, its rows follow (below)
             e0[0] = (uint32_t)FT_BIAS_ROW | t0w | I_ZERO | PAR_E;
             e1[0] = (uint32_t)FT_BIAS_ROW | t1w | I_ZERO | PAR_E;
           }
         }
         // the parent's rows (lane = row), in its own lists after the bias entry
-        if (t0 == 0) {
+        if (t0 == 0 && !have) {
           const int st = __shfl(stm, 0);
 #pragma unroll
           for (int hh = 0; hh < 2; ++hh)
@@ -1156,11 +1194,12 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
           if (g) len1 += cn + 1;
           else len0 += cn + 1;
           const uint32_t t = tmpl(l, hh != st);
+          const uint32_t L = LAST | (t0 + l == nxq ? NXT | (uint32_t)hh << 27 : 0u);
           if (lane == 0) e[0] = (uint32_t)FT_BIAS_ROW | t | I_ZERO;
           const uint32_t sq01 = __shfl(hh ? w2 : w0, l), sq23 = __shfl(hh ? w3 : w1, l);
           int pos;
           const int row = king_move_row(pbd, hh, sq01 & 0xFFFF, sq01 >> 16, sq23 & 0xFFFF, sq23 >> 16, lane, pos);
-          if (row >= 0 && pos < cn) e[1 + pos] = (uint32_t)row | t | (pos == cn - 1 ? LAST : 0u);
+          if (row >= 0 && pos < cn) e[1 + pos] = (uint32_t)row | t | (pos == cn - 1 ? L : 0u);
         }
         if (lane == 0) {
           bmask = bm;
@@ -1268,7 +1307,7 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
           psqf[tpar][ln][1] = vv[st ^ 1];
         }
         const uint32_t j16 = 16 * jt;
-        const int n4 = ((int)tctl[1 + hu] + 3) & ~3;
+        const int n4 = (ablate & 8) ? 0 : ((int)tctl[1 + hu] + 3) & ~3;
         const uint32_t *E = ent[hu];
         ushort8 rlo[4], rhi[4];
         uint32_t er[4];
@@ -1289,9 +1328,10 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
           if (init == I_ZERO) { // the bias row
             asm volatile("");
             lo = rlo[r], hi = rhi[r];
-          } else if (init == I_PACC) { // a miss: parent - from-row
+          } else if (init == I_PACC) { // a miss: parent - from-row, saved as the sibling base
             asm volatile("");
             lo = pacc_lo - rlo[r], hi = pacc_hi - rhi[r];
+            base_lo = lo, base_hi = hi;
           } else if (init == I_BASE) { // a hit: the cached (parent - from-row) +- the next row
             if (e & SUB) {
               asm volatile("");
@@ -1307,14 +1347,18 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
             asm volatile("");
             lo += rlo[r], hi += rhi[r];
           }
-          if (e & SAVEB) {
-            asm volatile("");
-            base_lo = lo, base_hi = hi;
-          }
           if (e & LAST) {
             const int sl = (e >> 20) & 15, side = (e >> 24) & 1;
             *reinterpret_cast<uint2 *>(xt + sl * XS + side * (L1 / 2) + 8 * jt) = transform8(lo, hi);
-            if (e & PAR_E) pacc_lo = lo, pacc_hi = hi;
+            if (e & PAR_E) { // (kept a branch: a select would cost 8 VALU on every LAST entry)
+              asm volatile("");
+              pacc_lo = lo, pacc_hi = hi;
+            }
+            if (e & NXT) { // the next parent's accumulators -> carry row st2 + perspective
+              const uint32_t so = (st2 + ((e >> 27) & 1)) * RS;
+              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(int4v, lo), ftr, j16, so, 0);
+              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(int4v, hi), ftr, j16 + L1, so, 0);
+            }
           }
         };
 #pragma unroll
@@ -1327,6 +1371,9 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
             issue(r, i + r + 4);
           }
         }
+        // the carry-row stores must be complete before the barrier (which waits only
+        // for LDS): the next parent's loads may come from the other wave group
+        if (nxq >= t0 && nxq < t0 + m) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
       __syncthreads();
       GN_STAMP(4);
@@ -1357,6 +1404,11 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
       GN_STAMP(5);
     }
     GN_STAMP_FLUSH();
+   }
+   if (K > 1) { // release the carry slot to the workgroup CARRY_SLOTS dispatches later
+     __syncthreads();
+     if (tid == 0) __hip_atomic_store(tickets + cslot, v / CARRY_SLOTS + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+   }
   }
 }
 
@@ -1501,9 +1553,17 @@ __global__ void count_children_kernel(const gn_board *__restrict__ boards, size_
   counts[i] = c;
 }
 
+__device__ __forceinline__ bool same_placement(const gn_board &a, const gn_board &b) {
+  uint64_t x[2], y[2];
+  __builtin_memcpy(x, a.pc, 16);
+  __builtin_memcpy(y, b.pc, 16);
+  return a.occ == b.occ && x[0] == y[0] && x[1] == y[1];
+}
+
 __global__ void write_children_kernel(const gn_board *__restrict__ boards, size_t n, const Tables *__restrict__ tables,
                                       const uint64_t *__restrict__ offsets, gn_board *__restrict__ children,
                                       uint16_t *__restrict__ moves, ChildDelta *__restrict__ deltas,
+                                      uint8_t *__restrict__ next_slot, int chain_k,
                                       unsigned long long *__restrict__ rows) {
   __shared__ Tables T;
   load_tables(T, tables);
@@ -1516,17 +1576,28 @@ __global__ void write_children_kernel(const gn_board *__restrict__ boards, size_
   // parent's refresh (both perspectives) + per child either the delta rows or
   // a refresh of the perspective whose king moved
   unsigned long long nrows = 2ull * popcnt(B.byType[0]);
+  // next_slot[i]: the child whose placement is boards[i + 1]'s (a game's next position),
+  // 255 if none; the chained walk then starts parent i + 1 from that child's accumulators
+  gn_board nb = {};
+  const bool look = next_slot && i + 1 < n;
+  if (look) nb = boards[i + 1];
+  const uint64_t k0 = k;
+  uint32_t ns = 255;
   gen_legal(B, T, [&](uint16_t m) {
     gn_board pb;
     Dirty d;
     const Board C = do_move(B, m, &d);
     pack(C, pb);
+    if (look && ns == 255 && same_placement(pb, nb)) ns = (uint32_t)(k - k0);
     children[k] = pb;
     if (moves) moves[k] = m;
     if (deltas) deltas[k] = make_child_delta(B, C, d);
     nrows += d.king_moved ? popcnt(C.byType[0]) + d.n_rem + d.n_add : 2 * (d.n_rem + d.n_add);
     ++k;
   });
+  if (next_slot) next_slot[i] = (uint8_t)ns;
+  // a chained next parent gathers one carry row per perspective instead of its refresh
+  if (ns != 255 && chain_k > 1 && (i + 1) % (size_t)chain_k != 0) nrows -= 2ull * popcnt(nb.occ) - 2;
   if (rows) atomicAdd(rows, nrows);
 }
 
@@ -1617,11 +1688,11 @@ hipError_t launch_count_children(const gn_board *boards, size_t n, const Tables 
 }
 
 hipError_t launch_write_children(const gn_board *boards, size_t n, const Tables *tables, const uint64_t *offsets,
-                                 gn_board *children, uint16_t *moves, ChildDelta *deltas, unsigned long long *rows,
-                                 hipStream_t s) {
+                                 gn_board *children, uint16_t *moves, ChildDelta *deltas, uint8_t *next_slot,
+                                 int chain_k, unsigned long long *rows, hipStream_t s) {
   if (!n) return hipSuccess;
   hipLaunchKernelGGL(write_children_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, boards, n, tables, offsets,
-                     children, moves, deltas, rows);
+                     children, moves, deltas, next_slot, chain_k, rows);
   return hipGetLastError();
 }
 
@@ -1690,16 +1761,28 @@ hipError_t exclusive_scan_u64(const uint64_t *counts, uint64_t *offsets, size_t 
 
 hipError_t launch_expand_net(const NetDevice &net, const gn_board *parents, size_t n, const uint64_t *offsets,
                              const gn_board *children, const ChildDelta *deltas, const uint8_t *need_parent,
-                             const uint8_t *need_child, int2 *out_parent, int2 *out_child, int swz, hipStream_t s) {
+                             const uint8_t *need_child, int2 *out_parent, int2 *out_child, int swz,
+                             const uint8_t *next_slot, uint32_t *tickets, int chain_k, hipStream_t s) {
   if (!n) return hipSuccess;
   unsigned g = (unsigned)(swz ? 8 * ((n + 7) / 8) : n);
-  static const int ablate = getenv("GN_ABLATE") ? atoi(getenv("GN_ABLATE")) : 0; // timing diagnostics only
-  static const int persist = getenv("GN_PERSIST") ? atoi(getenv("GN_PERSIST")) : 0; // WGs per CU, 0: one per parent
-  if (persist > 0) g = std::min<unsigned>(g, 8u * ((256u * (unsigned)persist + 7) / 8));
-#define GN_EXPAND_ARGS net, parents, offsets, children, deltas, need_parent, need_child, out_parent, out_child, n, swz, ablate
   // GN_EXPAND_LEGACY=1: the per-slot row programs (expand_eval) for the big nets, for A/B timing
   static const int legacy = getenv("GN_EXPAND_LEGACY") ? atoi(getenv("GN_EXPAND_LEGACY")) : 0;
-#define GN_STREAM_ARGS net, parents, offsets, deltas, need_parent, need_child, out_parent, out_child, n, swz, ablate
+  if (n >= 0x80000000ull) return hipErrorInvalidValue; // 32-bit parent indices in the kernels
+  const bool chained =
+      !legacy && chain_k > 1 && next_slot && tickets && net.carry_slots && (net.L1 == 3072 || net.L1 == 1024);
+  if (!chained) chain_k = 1;
+  if (chained) { // one workgroup per block (never persistent: the slot tickets assume dispatch order)
+    const size_t nblk = (n + chain_k - 1) / chain_k;
+    g = (unsigned)(swz ? 8 * ((nblk + 7) / 8) : nblk);
+    hipError_t e = hipMemsetAsync(tickets, 0, CARRY_SLOTS * sizeof(uint32_t), s);
+    if (e != hipSuccess) return e;
+  }
+  static const int ablate = getenv("GN_ABLATE") ? atoi(getenv("GN_ABLATE")) : 0; // timing diagnostics only
+  static const int persist = getenv("GN_PERSIST") ? atoi(getenv("GN_PERSIST")) : 0; // WGs per CU, 0: one per parent
+  if (persist > 0 && !chained) g = std::min<unsigned>(g, 8u * ((256u * (unsigned)persist + 7) / 8));
+#define GN_EXPAND_ARGS net, parents, offsets, children, deltas, need_parent, need_child, out_parent, out_child, n, swz, ablate
+#define GN_STREAM_ARGS net, parents, offsets, deltas, need_parent, need_child, out_parent, out_child, n, swz, ablate, \
+                       chained ? next_slot : nullptr, chained ? tickets : nullptr, chain_k
   if (net.L1 == 3072 && !legacy) {
     hipLaunchKernelGGL((expand_stream_kernel<3072>), dim3(g), dim3(384), 0, s, GN_STREAM_ARGS);
   } else if (net.L1 == 1024 && !legacy) {

@@ -64,6 +64,14 @@ extern "C" {
 #define GN_OPT_KING_SORT 3            /* 1 (default): evaluate a batch in (white king, black
                                          king) square order for L2 / Infinity-Cache
                                          locality, results in input order; 0: input order */
+#define GN_OPT_CHAIN 4                /* expansion (big net): a workgroup walks blocks of up to
+                                         this many consecutive parents (default 81: one
+                                         80-ply game); a parent that is a child of the
+                                         previous one (same placement) starts from that
+                                         child's accumulators instead of a refresh.
+                                         Shortened when the blocks would not fill the GPU;
+                                         -k: exactly k.  0, 1 or -1: every parent
+                                         refreshes.  Results are identical either way.    */
 
 /* per-position flags */
 #define GN_FLAG_IN_CHECK 1u /* side to move in check: Stockfish has no static eval
@@ -240,7 +248,9 @@ GN_API int gn_expand_device(gn_ctx *ctx, int device_slot, const gn_board *d_pare
  * stage_ms (optional, length 7) = average ms of [count+scan, total read-back,
  * write children, classify, small net, big net, finalize]; ft_rows (optional)
  * = feature-transformer rows one incremental expansion gathers (parent
- * refreshes + child deltas / king-move refreshes; 0 when not incremental). */
+ * refreshes, or one carried accumulator row per perspective for a parent that
+ * is a child of the previous one (GN_OPT_CHAIN), + child deltas / king-move
+ * refreshes; 0 when not incremental). */
 GN_API int gn_time_expand_device(gn_ctx *ctx, int device_slot, const gn_board *d_parents, size_t n, int mode,
                                  int iters, float *ms_total, size_t *total, float *stage_ms, uint64_t *ft_rows);
 /* n_games random games of `plies` plies (xoshiro256**, seed + game index) on

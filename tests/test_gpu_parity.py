@@ -250,3 +250,44 @@ def test_locality_options_do_not_change_results(gpu_ctx, swz, ksort):
     finally:
         gpu_ctx.set_option(G.OPT_XCD_SWIZZLE, 1)
         gpu_ctx.set_option(G.OPT_KING_SORT, 1)
+
+
+@pytest.mark.parametrize("mode", [1, 0])
+def test_chained_walk_matches_refresh_and_oracle(gpu_ctx, oracle_nets, oracle_lib, mode):
+    """Chained walk (GN_OPT_CHAIN): consecutive game positions start from the previous
+    parent's child accumulators.  Every block length gives the refresh results, and the
+    first games agree with the oracle."""
+    from fishnet_amd import gpu_nnue as G
+    games, plies = 40, 80
+    n = games * (plies + 1)
+    d_b = gpu_ctx.alloc(n * 32)
+    gpu_ctx.random_games_device(0x5EED0000, 0, games, plies, d_b)
+    gpu_ctx.synchronize()
+    boards = d_b.download(G.BOARD_DTYPE, n)
+    cap = 60 * n
+    bufs = {k: gpu_ctx.alloc(sz) for k, sz in (("po", n * 16), ("off", (n + 1) * 4), ("ch", cap * 32),
+                                                  ("mv", cap * 2), ("co", cap * 16))}
+
+    def run(k):
+        gpu_ctx.set_option(G.OPT_CHAIN, k)
+        t = gpu_ctx.expand_device(d_b, n, mode, bufs["po"], bufs["off"], bufs["ch"], bufs["mv"], bufs["co"], cap)
+        return (bufs["po"].download(G.EVAL_DTYPE, n), bufs["off"].download(np.uint32, n + 1),
+                bufs["mv"].download(np.uint16, t), bufs["co"].download(G.EVAL_DTYPE, t))
+
+    try:
+        ref = run(1)
+        for k in (-81, -7, -2, 81):
+            got = run(k)
+            for a, b in zip(ref, got):
+                assert np.array_equal(a, b), k
+    finally:
+        gpu_ctx.set_option(G.OPT_CHAIN, 81)
+    big, small = oracle_nets
+    parents, offs, moves, kids = ref
+    for i in range(2 * (plies + 1)):
+        fen = G.board_to_fen(boards[i])
+        p_exp, m_exp, k_exp = oracle_lib.expand_eval(big, small, fen, mode)
+        assert tuple(parents[i]) == p_exp, fen
+        lo, hi = int(offs[i]), int(offs[i + 1])
+        got = {int(m): tuple(x) for m, x in zip(moves[lo:hi], kids[lo:hi])}
+        assert got == {int(m): tuple(x) for m, x in zip(m_exp, k_exp)}, fen

@@ -1,5 +1,6 @@
 #!/bin/bash
-# expand_eval ablations (GN_ABLATE bits: 2 = no FT row traffic, 4 = no layer stack)
+# expand ablations (GN_ABLATE bits: 2 = every row load hits the bias row, 4 = no layer stack,
+# 8 = no row stream: lists, PSQT and barriers only)
 # for a kernel variant (GN_EXPAND_LEGACY=$LEG), 16,384 games.
 OUT=gpurun_out/abl2
 mkdir -p $OUT
