@@ -98,10 +98,12 @@ class Ctx:
             self.nn.set_option(G.OPT_KING_SORT, args.king_sort)
         if args.chain is not None:
             self.nn.set_option(G.OPT_CHAIN, args.chain)
+        if args.king_cache is not None:
+            self.nn.set_option(G.OPT_KING_CACHE, args.king_cache)
         self.options = {"xcd_swizzle": self.nn.get_option(G.OPT_XCD_SWIZZLE),
                         "king_sort": self.nn.get_option(G.OPT_KING_SORT),
                         "incremental_children": self.nn.get_option(G.OPT_INCREMENTAL_CHILDREN),
-                        "chain": self._opt(G.OPT_CHAIN)}
+                        "chain": self._opt(G.OPT_CHAIN), "king_cache": self._opt(G.OPT_KING_CACHE)}
 
     def _opt(self, option):
         try:
@@ -244,6 +246,7 @@ def main():
     ap.add_argument("--swizzle", type=int, default=-1, help="GN_OPT_XCD_SWIZZLE mask (-1: library default)")
     ap.add_argument("--king-sort", type=int, default=-1, help="GN_OPT_KING_SORT (-1: library default)")
     ap.add_argument("--chain", type=int, default=None, help="GN_OPT_CHAIN (None: library default; -k: exactly k)")
+    ap.add_argument("--king-cache", type=int, default=None, help="GN_OPT_KING_CACHE (None: library default)")
     args = ap.parse_args()
 
     c = Ctx(args)

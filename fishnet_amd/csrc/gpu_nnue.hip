@@ -204,6 +204,7 @@ struct Dev {
   DevBuf<unsigned long long> sum;
   DevBuf<uint8_t> nslot; // chained walk: child of parent i that is parent i + 1 (255: none)
   DevBuf<uint32_t> tickets; // chained walk: per carry slot, how many workgroups are done with it
+  DevBuf<uint32_t> ksnap;   // king cache: per slot x (perspective, king square) a 32-B placement snapshot
   int chain_k = 1;          // block length of the current expansion (1: no chaining)
   void *scan_tmp = nullptr;
   size_t scan_bytes = 0;
@@ -217,6 +218,7 @@ struct gn_ctx {
   int swizzle = 1;          // GN_OPT_XCD_SWIZZLE bit mask: 1 expansion, 2 batch evaluation
   bool king_sort = true;    // GN_OPT_KING_SORT
   int chain = 81;           // GN_OPT_CHAIN (blocks of consecutive parents per workgroup)
+  bool king_cache = true;   // GN_OPT_KING_CACHE
   int l1[2] = {0, 0};
   uint32_t hash[2] = {0, 0};
 };
@@ -247,7 +249,7 @@ static int upload_net(Dev &d, int which, const HostNet &h) {
   const size_t RS = 2 * (size_t)h.L1 + 32;
   size_t off[8], o = 0;
   const int carry = h.L1 == 128 ? 0 : CARRY_SLOTS; // the chained walk's scratch rows
-  const size_t sz[8] = {((size_t)FT_ROWS + 4 * (size_t)carry) * RS, h.bias.size() * 2, h.w0.size(), h.b0.size() * 4,
+  const size_t sz[8] = {((size_t)FT_ROWS + 4 * (size_t)carry + 128 * (size_t)carry) * RS, h.bias.size() * 2, h.w0.size(), h.b0.size() * 4,
                         h.w1.size(), h.b1.size() * 4, h.w2.size(), h.b2.size() * 4};
   const void *src[8] = {h.ft.data(), h.bias.data(), h.w0.data(), h.b0.data(),
                         h.w1.data(), h.b1.data(), h.w2.data(), h.b2.data()};
@@ -262,6 +264,7 @@ static int upload_net(Dev &d, int which, const HostNet &h) {
   n.L1 = h.L1;
   n.row_stride = (uint32_t)RS;
   n.carry_slots = carry;
+  n.kc_slots = carry;
   n.ft = m + off[0];
   n.bias = reinterpret_cast<const int16_t *>(m + off[1]);
   n.w0 = reinterpret_cast<const int8_t *>(m + off[2]);
@@ -446,6 +449,7 @@ static int generate_children(Dev &d, const gn_board *parents, size_t n, gn_board
   if (d.chain_k > 1) {
     HIP_TRY(d.nslot.ensure(n));
     HIP_TRY(d.tickets.ensure(CARRY_SLOTS));
+    HIP_TRY(d.ksnap.ensure((size_t)CARRY_SLOTS * 128 * 8));
   }
   HIP_TRY(d.counts.ensure(n + 1));
   HIP_TRY(d.offsets.ensure(n + 1));
@@ -480,7 +484,7 @@ static int generate_children(Dev &d, const gn_board *parents, size_t n, gn_board
 // after the big net, after finalize.
 static int expand_evaluate(gn_ctx *ctx, Dev &d, const gn_board *parents, size_t n, const gn_board *children,
                            size_t total, int mode, gn_eval *parent_out, gn_eval *child_out, hipStream_t s,
-                           hipEvent_t *ev) {
+                           hipEvent_t *ev, unsigned long long *rows_out = nullptr) {
   if (mode < GN_MODE_FULL || mode > GN_MODE_SMALL) return fail(GN_E_INVALID, "bad mode %d", mode);
   if ((mode != GN_MODE_SMALL && !d.has[BIG]) || (mode != GN_MODE_BIG && !d.has[SMALL]))
     return fail(GN_E_NONET, "mode %d needs a network that is not loaded", mode);
@@ -518,7 +522,7 @@ static int expand_evaluate(gn_ctx *ctx, Dev &d, const gn_board *parents, size_t 
   if (mode != GN_MODE_BIG) {
     const bool f = mode == GN_MODE_FULL;
     HIP_TRY(launch_expand_net(d.net[SMALL], parents, n, off, children, dl, f ? d.p_nsm.p : nullptr,
-                              f ? d.nsm.p : nullptr, d.p_osm.p, d.osm.p, ctx->swizzle & 1, nullptr, nullptr, 1,
+                              f ? d.nsm.p : nullptr, d.p_osm.p, d.osm.p, ctx->swizzle & 1, nullptr, nullptr, 1, nullptr, nullptr,
                               s));
     if (f) {
       HIP_TRY(launch_reeval(d.p_osm.p, d.p_nsm.p, n, P, d.p_nbg.p, s));
@@ -530,7 +534,8 @@ static int expand_evaluate(gn_ctx *ctx, Dev &d, const gn_board *parents, size_t 
     const bool f = mode == GN_MODE_FULL;
     HIP_TRY(launch_expand_net(d.net[BIG], parents, n, off, children, dl, f ? d.p_nbg.p : nullptr,
                               f ? d.nbg.p : nullptr, d.p_obg.p, d.obg.p, ctx->swizzle & 1,
-                              d.chain_k > 1 ? d.nslot.p : nullptr, d.tickets.p, d.chain_k, s));
+                              d.chain_k > 1 ? d.nslot.p : nullptr, d.tickets.p, d.chain_k,
+                              ctx->king_cache ? d.ksnap.p : nullptr, rows_out, s));
   }
   HIP_TRY(mark(2));
   HIP_TRY(launch_finalize(children, total, mode, d.osm.p, d.obg.p, d.nsm.p, d.nbg.p, P, d.tables, child_out, s));
@@ -1125,8 +1130,8 @@ int gn_time_expand_device(gn_ctx *ctx, int device_slot, const gn_board *d_parent
     }
   int rc = GN_OK;
   size_t t = 0;
-  HIP_TRY(d->sum.ensure(1));
-  HIP_TRY(hipMemsetAsync(d->sum.p, 0, sizeof(unsigned long long), s));
+  HIP_TRY(d->sum.ensure(2)); // [0] rows by write_children's formula, [1] rows the row stream gathered
+  HIP_TRY(hipMemsetAsync(d->sum.p, 0, 2 * sizeof(unsigned long long), s));
   hipError_t he = hipEventRecord(ev[0], s);
   for (int it = 0; it < iters && rc == GN_OK && he == hipSuccess; ++it) {
     hipEvent_t *e = &ev[2 + (size_t)NE * it];
@@ -1137,7 +1142,8 @@ int gn_time_expand_device(gn_ctx *ctx, int device_slot, const gn_board *d_parent
     if (rc) break;
     HIP_TRY(d->io_out.ensure(n));
     HIP_TRY(d->io_out2.ensure(std::max<size_t>(t, 1)));
-    rc = expand_evaluate(ctx, *d, d_parents, n, d->frontier[1].p, t, mode, d->io_out.p, d->io_out2.p, s, e + 4);
+    rc = expand_evaluate(ctx, *d, d_parents, n, d->frontier[1].p, t, mode, d->io_out.p, d->io_out2.p, s, e + 4,
+                         it == 0 ? d->sum.p + 1 : nullptr);
   }
   if (rc == GN_OK && he == hipSuccess) he = hipEventRecord(ev[1], s);
   if (rc == GN_OK && he == hipSuccess) he = hipEventSynchronize(ev[1]);
@@ -1156,9 +1162,9 @@ int gn_time_expand_device(gn_ctx *ctx, int device_slot, const gn_board *d_parent
   *total = t;
   if (rc) return rc;
   if (ft_rows && he == hipSuccess) {
-    unsigned long long r = 0;
-    he = hipMemcpy(&r, d->sum.p, sizeof(r), hipMemcpyDeviceToHost);
-    *ft_rows = ctx->incremental ? r : 0;
+    unsigned long long r[2] = {0, 0};
+    he = hipMemcpy(r, d->sum.p, sizeof(r), hipMemcpyDeviceToHost);
+    *ft_rows = ctx->incremental ? (r[1] ? r[1] : r[0]) : 0; // the row stream's own count when it ran
   }
   if (he != hipSuccess) return fail(GN_E_HIP, "timing failed: %s", hipGetErrorString(he));
   return GN_OK;
@@ -1189,6 +1195,9 @@ int gn_set_option(gn_ctx *ctx, int option, int64_t value) {
   case GN_OPT_KING_SORT:
     ctx->king_sort = value != 0;
     return GN_OK;
+  case GN_OPT_KING_CACHE:
+    ctx->king_cache = value != 0;
+    return GN_OK;
   case GN_OPT_CHAIN:
     if (value < -(1 << 20) || value > (1 << 20)) return fail(GN_E_INVALID, "chain length out of range");
     ctx->chain = (int)value;
@@ -1209,6 +1218,9 @@ int gn_get_option(const gn_ctx *ctx, int option, int64_t *value) {
     return GN_OK;
   case GN_OPT_KING_SORT:
     *value = ctx->king_sort;
+    return GN_OK;
+  case GN_OPT_KING_CACHE:
+    *value = ctx->king_cache;
     return GN_OK;
   case GN_OPT_CHAIN:
     *value = ctx->chain;

@@ -23,10 +23,16 @@ hipError_t king_sort(const gn_board *boards, size_t n, uint16_t *keys, uint32_t 
 hipError_t launch_expand_net(const NetDevice &net, const gn_board *parents, size_t n, const uint64_t *offsets,
                              const gn_board *children, const ChildDelta *deltas, const uint8_t *need_parent,
                              const uint8_t *need_child, int2 *out_parent, int2 *out_child, int swz,
-                             const uint8_t *next_slot, uint32_t *tickets, int chain_k, hipStream_t s);
+                             const uint8_t *next_slot, uint32_t *tickets, int chain_k, uint32_t *ksnap,
+                             unsigned long long *rows_out, hipStream_t s);
 // Chained walk (big nets with carry rows): one workgroup per block of chain_k
 // consecutive parents; parent p + 1 starts from child next_slot[p] of parent p when
 // that child has its placement.  tickets: CARRY_SLOTS words (zeroed by the launcher).
+// ksnap (optional, chained walk only): CARRY_SLOTS x 128 x 32 B of king-cache
+// placement snapshots; king-move refreshes then start from the block's cached
+// accumulator for (perspective, king square) when the placement difference is shorter.
+// rows_out (optional, big-net row stream only): += FT rows gathered (bias, carry and
+// king-cache rows included).
 // GN_MODE_FULL preparation: need_small = valid && |simple_eval| > threshold,
 // need_big = valid && !need_small.
 hipError_t launch_classify(const gn_board *boards, size_t n, const gn_eval_params &P, uint8_t *need_small,

@@ -905,22 +905,26 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR) __attribute__((amdgpu_wav
 // boundaries instead of one dependent round trip per slot.  A refresh is the bias
 // row (FT_BIAS_ROW) + the feature rows.  PSQT is not in the stream: the waves that
 // are idle while wave 0 builds the lists sum it lane-parallel (one round trip).
-// Entry (u32): [14:0] row, [15] subtract, [17:16] init before this entry
-// (0 none, 1 zero, 2 parent, 3 sibling base), [18] save base after it,
-// [19] last entry of its slot, [23:20] slot, [24] side (0: perspective to move),
-// [25] entry of the parent slot, [26] store the slot's accumulator as the next
-// parent's (chained walk), [27] its absolute perspective.
+// Entry (u32): [18:0] row (FT rows, then the carry and king-cache rows), [19]
+// subtract, [21:20] init before this entry (0 none, 1 zero, 2 parent - row, saved
+// as the sibling base, 3 sibling base), [22] last entry of its slot, [26:23] slot,
+// [27] side (0: perspective to move), [28] entry of the parent slot, [29] store the
+// slot's accumulator as the next parent's (chained walk), [30] its absolute
+// perspective, [31] store it to the slot's king-cache row (kcrow in LDS).
 namespace es {
-constexpr uint32_t SUB = 1u << 15, I_ZERO = 1u << 16, I_PACC = 2u << 16, I_BASE = 3u << 16, SAVEB = 1u << 18,
-                   LAST = 1u << 19, PAR_E = 1u << 25, NXT = 1u << 26;
-__device__ __forceinline__ uint32_t tmpl(int slot, int side) { return (uint32_t)slot << 20 | (uint32_t)side << 24; }
+constexpr uint32_t ROW = (1u << 19) - 1, SUB = 1u << 19, I_ZERO = 1u << 20, I_PACC = 2u << 20, I_BASE = 3u << 20,
+                   INIT = 3u << 20, LAST = 1u << 22, SLOT_SH = 23, SIDE_SH = 27, PAR_E = 1u << 28, NXT = 1u << 29,
+                   NXT_SH = 30, KST = 1u << 31;
+__device__ __forceinline__ uint32_t tmpl(int slot, int side) {
+  return (uint32_t)slot << SLOT_SH | (uint32_t)side << SIDE_SH;
+}
 } // namespace es
 
 // rows of perspective h of a child whose h-king moved kf -> kt (castling: rook rf -> rt,
 // 64 = none), from the parent board, lane = square: the row of this lane's piece in
 // the child (or -1) and its rank among the child's pieces.  All 64 lanes.
 __device__ __forceinline__ int king_move_row(const gn_board &pb, int h, int kf, int kt, int rf, int rt, int lane,
-                                             int &pos) {
+                                             int &pos, int *piece = nullptr) {
   const uint64_t occ = pb.occ;
   const bool has = (occ >> lane) & 1;
   const int k = popcnt(occ & ((1ull << lane) - 1));
@@ -932,6 +936,7 @@ __device__ __forceinline__ int king_move_row(const gn_board &pb, int h, int kf, 
   if (lane == kt) pc = make_piece(h, KING);
   const uint64_t cocc = __ballot(pc != 0);
   pos = popcnt(cocc & ((1ull << lane) - 1));
+  if (piece) *piece = pc;
   return pc ? feature_index(h, lane, pc, kt) : -1;
 }
 
@@ -947,7 +952,8 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
                          const ChildDelta *__restrict__ deltas, const uint8_t *__restrict__ need_parent,
                          const uint8_t *__restrict__ need_child, int2 *__restrict__ out_parent,
                          int2 *__restrict__ out_child, size_t n_parents, int swz, int ablate,
-                         const uint8_t *__restrict__ next_slot, uint32_t *__restrict__ tickets, int chain_k) {
+                         const uint8_t *__restrict__ next_slot, uint32_t *__restrict__ tickets, int chain_k,
+                         uint32_t *__restrict__ ksnap, unsigned long long *__restrict__ rows_out) {
   using namespace es;
   constexpr int G = L1 / 16; // threads per perspective (whole waves)
   constexpr int NT = 2 * G;
@@ -974,13 +980,15 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
   __shared__ uint32_t cdl[CDL][5];
   __shared__ gn_board pbd;
   __shared__ int pcount;
-  __shared__ uint32_t tctl[3]; // slots in this tile, entries of list 0 / 1
+  __shared__ uint32_t tctl[4]; // slots in this tile, entries of list 0 / 1, carry/king-cache stores
   __shared__ uint32_t bmask;
 
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const __amdgpu_buffer_rsrc_t ftr =
-      __builtin_amdgcn_make_buffer_rsrc((void *)net.ft, 0, (int)(((size_t)FT_ROWS + 4 * (size_t)net.carry_slots) * RS), 0x00020000);
+      __builtin_amdgcn_make_buffer_rsrc(
+          (void *)net.ft, 0, (int)(((size_t)FT_ROWS + 4 * (size_t)net.carry_slots + 128 * (size_t)net.kc_slots) * RS),
+          0x00020000);
   // Chained walk: a workgroup takes a block of chain_k consecutive parents.  When parent
   // p + 1 is a child of parent p (next_slot[p], a game's next position), that child's
   // accumulators are stored to this workgroup's carry rows (4: parity of p x
@@ -991,6 +999,7 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
   // (32-bit parent indices: the launcher rejects n_parents >= 2^31)
   const uint32_t np = (uint32_t)n_parents;
   const uint32_t K = chain_k > 1 && tickets && next_slot && net.carry_slots ? (uint32_t)chain_k : 1;
+  const bool kc = K > 1 && ksnap && net.kc_slots; // king cache (Finny-table analog) for king-move refreshes
   const uint32_t nblk = (np + K - 1) / K;
   const uint32_t vgrid = swz ? 8 * ((nblk + 7) / 8) : nblk;
   int tpar = 0; // tile parity: the layer stack of tile k runs beside phase 0 of tile k + 1
@@ -1010,6 +1019,13 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
        while (__hip_atomic_load(tickets + cslot, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != v / CARRY_SLOTS)
          __builtin_amdgcn_s_sleep(8);
      __syncthreads();
+     // King cache (per block: written and read by this workgroup only): one accumulator
+     // row + one placement snapshot per (perspective, king square); empty at block start.
+     if (kc) {
+       for (int i = tid; i < 256; i += NT)
+         *reinterpret_cast<uint4 *>(ksnap + (size_t)cslot * 1024 + 4 * i) = make_uint4(0, 0, 0, 0);
+       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+     }
    }
    int carry_ok = 0; // the previous parent stored its next-parent accumulators
    for (uint32_t p = blk * K; p < pend; ++p) {
@@ -1111,7 +1127,7 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
         // no accumulator, so it goes to whichever list is shorter and the two wave
         // groups finish the stream together.
         const bool ref0 = (kinds & 3) == 2, ref1 = (kinds >> 2) == 2;
-        const int nr = ref0 ? n0 : ref1 ? n1 : 0;
+        const int nr = (ref0 ? n0 : ref1 ? n1 : 0) + (kc && (ref0 || ref1) ? 1 : 0); // + a king-cache store entry
         const int d0 = ref0 ? 0 : n0 - (hit0 ? 1 : 0), d1 = ref1 ? 0 : n1 - (hit1 ? 1 : 0);
         const uint32_t c = (uint32_t)d0 | (uint32_t)d1 << 10 | (uint32_t)nr << 20;
         uint32_t inc = c;
@@ -1153,7 +1169,7 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
             uint32_t r[4] = {cl(i0), cl(s >= 2 ? i1 : i2), cl(s >= 2 ? i2 : i3), cl(i3)};
             uint32_t f[4] = {SUB, s >= 2 ? SUB : 0u, 0u, 0u};
             if (!hit) {
-              e[0] = r[0] | t | SUB | I_PACC | SAVEB;
+              e[0] = r[0] | t | SUB | I_PACC;
               if (n > 1) e[1] = r[1] | t | f[1] | (n == 2 ? L : 0u);
               if (n > 2) e[2] = r[2] | t | (n == 3 ? L : 0u);
               if (n > 3) e[3] = r[3] | t | L;
@@ -1165,7 +1181,7 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
           };
           uint32_t *e0 = ent[0] + (exc & 1023), *e1 = ent[1] + ((exc >> 10) & 1023);
           if ((kinds & 3) == 1) delta(e0, w0, w1, s0, n0, hit0, t0w, LAST | (nx ? NXT : 0u));
-          if ((kinds >> 2) == 1) delta(e1, w2, w3, s1, n1, hit1, t1w, LAST | (nx ? NXT | 1u << 27 : 0u));
+          if ((kinds >> 2) == 1) delta(e1, w2, w3, s1, n1, hit1, t1w, LAST | (nx ? NXT | 1u << NXT_SH : 0u));
           if (kinds == 15 && have) { // the parent from the carry rows (one entry per list)
             e0[0] = ld2 | t0w | I_ZERO | PAR_E | LAST;
             e1[0] = (ld2 + 1) | t1w | I_ZERO | PAR_E | LAST;
@@ -1185,27 +1201,75 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
         // king-move refreshes (lane = square), each appended to the shorter list
         int len0 = (int)(last_inc & 1023), len1 = (int)((last_inc >> 10) & 1023);
         uint64_t jm = __ballot(mine && (ref0 || ref1));
+        uint32_t kst_any = 0;
         while (jm) {
           const int l = __builtin_ctzll(jm);
           jm &= jm - 1;
-          const int hh = __shfl((int)ref1, l), st = __shfl(stm, l), cn = __shfl(cnt, l);
+          // (readlane: job values are wave-uniform and stay in SGPRs)
+          const int hh = __builtin_amdgcn_readlane((int)ref1, l), st = __builtin_amdgcn_readlane(stm, l),
+                    cn = __builtin_amdgcn_readlane(cnt, l);
+          const uint32_t t = tmpl(l, hh != st);
+          const uint32_t sq01 = (uint32_t)__builtin_amdgcn_readlane((int)(hh ? w2 : w0), l),
+                         sq23 = (uint32_t)__builtin_amdgcn_readlane((int)(hh ? w3 : w1), l);
+          const int kt = (int)(sq01 >> 16);
+          int pos, cpc;
+          const int row =
+              king_move_row(pbd, hh, sq01 & 0xFFFF, kt, sq23 & 0xFFFF, sq23 >> 16, lane, pos, &cpc);
+          // King cache (not for castling): start from the accumulator this block last
+          // stored for (hh, kt) and apply the placement difference, when that is shorter.
+          const bool kuse = kc && (sq23 & 0xFFFF) == 64;
+          const uint32_t kcr = (uint32_t)KC_ROW0 + 128 * cslot + 64 * hh + kt;
+          int ne = cn + 1 + (kuse ? 1 : 0), spc = 0;
+          bool kh = false;
+          uint64_t bs = 0, ba = 0;
+          if (kuse) {
+            // snapshot: the placement as 64 square-indexed nibbles (8 dwords, dword = rank)
+            uint32_t *rec = ksnap + ((size_t)cslot * 128 + 64 * hh + kt) * 8;
+            const uint32_t wv = lane < 8 ? rec[lane] : 0u; // lane-indexed: a vector load
+            spc = (int)((__shfl(wv, lane >> 3) >> (4 * (lane & 7))) & 15);
+            if (__ballot(spc != 0)) { // empty record: nothing cached for (hh, kt) yet
+              bs = __ballot(spc != cpc && spc != 0);
+              ba = __ballot(spc != cpc && cpc != 0);
+              const int nd = popcnt(bs) + popcnt(ba);
+              if (nd < cn) kh = true, ne = 2 + nd;
+            }
+            // the snapshot becomes the child's placement (its row is stored at LAST)
+            uint32_t x = (uint32_t)cpc << (4 * (lane & 7));
+            x |= __shfl_xor(x, 1);
+            x |= __shfl_xor(x, 2);
+            x |= __shfl_xor(x, 4);
+            if ((lane & 7) == 0) rec[lane >> 3] = x;
+            kst_any += 1; // one store-only entry
+          }
           const int g = len0 <= len1 ? 0 : 1;
           uint32_t *e = ent[g] + (g ? len1 : len0);
-          if (g) len1 += cn + 1;
-          else len0 += cn + 1;
-          const uint32_t t = tmpl(l, hh != st);
-          const uint32_t L = LAST | (t0 + l == nxq ? NXT | (uint32_t)hh << 27 : 0u);
-          if (lane == 0) e[0] = (uint32_t)FT_BIAS_ROW | t | I_ZERO;
-          const uint32_t sq01 = __shfl(hh ? w2 : w0, l), sq23 = __shfl(hh ? w3 : w1, l);
-          int pos;
-          const int row = king_move_row(pbd, hh, sq01 & 0xFFFF, sq01 >> 16, sq23 & 0xFFFF, sq23 >> 16, lane, pos);
-          if (row >= 0 && pos < cn) e[1 + pos] = (uint32_t)row | t | (pos == cn - 1 ? L : 0u);
+          if (g) len1 += ne;
+          else len0 += ne;
+          // the slot's last entry: with the cache, a store-only entry for the cache row
+          // (I_ZERO | SUB = keep the accumulator; KST: store it to this entry's row)
+          const uint32_t L = LAST | (t0 + l == nxq ? NXT | (uint32_t)hh << NXT_SH : 0u);
+          const int el = kuse ? ne - 2 : ne - 1; // index of the last accumulating entry
+          if (kuse && lane == 0) e[ne - 1] = kcr | t | I_ZERO | SUB | KST | L;
+          const uint32_t La = kuse ? 0u : L;
+          if (!kh) {
+            if (lane == 0) e[0] = (uint32_t)FT_BIAS_ROW | t | I_ZERO;
+            if (row >= 0 && pos < cn) e[1 + pos] = (uint32_t)row | t | (1 + pos == el ? La : 0u);
+          } else {
+            const uint64_t lt2 = (1ull << lane) - 1;
+            const int ps = 1 + popcnt(bs & lt2), pa = 1 + popcnt(bs) + popcnt(ba & lt2);
+            if (lane == 0) e[0] = kcr | t | I_ZERO;
+            if ((bs >> lane) & 1) e[ps] = (uint32_t)feature_index(hh, lane, spc, kt) | t | SUB;
+            if ((ba >> lane) & 1) e[pa] = (uint32_t)row | t;
+          }
         }
         if (lane == 0) {
           bmask = bm;
           tctl[0] = (uint32_t)m;
           tctl[1] = (uint32_t)len0;
           tctl[2] = (uint32_t)len1;
+          tctl[3] = kst_any | (uint32_t)(nxq >= t0 && nxq < t0 + m);
+          // FT rows this tile gathers (every streamed entry but the store-only ones)
+          if (rows_out) atomicAdd(rows_out, (unsigned long long)(len0 + len1 - (int)kst_any));
         }
         // pad both lists with bias-row entries to a multiple of 4 plus the ring's 4
         // run-ahead entries (harmless: they follow the last slot of the list)
@@ -1316,18 +1380,18 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
         auto issue = [&](int r, int i) {
           if ((i & 63) == 0) ev = E[i + ln];
           const uint32_t e = er[r] = (uint32_t)__builtin_amdgcn_readlane((int)ev, i & 63);
-          const uint32_t o = (ablate & 2) ? (uint32_t)FT_BIAS_ROW * RS : (e & 0x7FFF) * RS;
+          const uint32_t o = (ablate & 2) ? (uint32_t)FT_BIAS_ROW * RS : (e & ROW) * RS;
           rlo[r] = __builtin_bit_cast(ushort8, __builtin_amdgcn_raw_buffer_load_b128(ftr, j16, o, 0));
           rhi[r] = __builtin_bit_cast(ushort8, __builtin_amdgcn_raw_buffer_load_b128(ftr, j16 + L1, o, 0));
         };
         auto consume = [&](int r) {
           const uint32_t e = er[r];
-          const uint32_t init = e & (3u << 16);
+          const uint32_t init = e & INIT;
           // scalar branches; the empty asm keeps the compiler from if-converting them into
           // selects over every alternative (vector work on all paths)
-          if (init == I_ZERO) { // the bias row
+          if (init == I_ZERO) { // the bias row (or a king-cache row); with SUB: keep (store-only)
             asm volatile("");
-            lo = rlo[r], hi = rhi[r];
+            if (!(e & SUB)) lo = rlo[r], hi = rhi[r];
           } else if (init == I_PACC) { // a miss: parent - from-row, saved as the sibling base
             asm volatile("");
             lo = pacc_lo - rlo[r], hi = pacc_hi - rhi[r];
@@ -1348,16 +1412,21 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
             lo += rlo[r], hi += rhi[r];
           }
           if (e & LAST) {
-            const int sl = (e >> 20) & 15, side = (e >> 24) & 1;
+            const int sl = (e >> SLOT_SH) & 15, side = (e >> SIDE_SH) & 1;
             *reinterpret_cast<uint2 *>(xt + sl * XS + side * (L1 / 2) + 8 * jt) = transform8(lo, hi);
             if (e & PAR_E) { // (kept a branch: a select would cost 8 VALU on every LAST entry)
               asm volatile("");
               pacc_lo = lo, pacc_hi = hi;
             }
-            if (e & NXT) { // the next parent's accumulators -> carry row st2 + perspective
-              const uint32_t so = (st2 + ((e >> 27) & 1)) * RS;
-              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(int4v, lo), ftr, j16, so, 0);
-              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(int4v, hi), ftr, j16 + L1, so, 0);
+            if (e & (KST | NXT)) { // accumulator stores: king-cache row and / or next-parent carry row
+              asm volatile("");
+              uint32_t so = (st2 + ((e >> NXT_SH) & 1)) * RS;
+              if (e & KST) so = (e & ROW) * RS;
+              for (int rep = (e & KST) && (e & NXT) ? 2 : 1; rep; --rep) {
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(int4v, lo), ftr, j16, so, 0);
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(int4v, hi), ftr, j16 + L1, so, 0);
+                so = (st2 + ((e >> NXT_SH) & 1)) * RS;
+              }
             }
           }
         };
@@ -1373,7 +1442,7 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
         }
         // the carry-row stores must be complete before the barrier (which waits only
         // for LDS): the next parent's loads may come from the other wave group
-        if (nxq >= t0 && nxq < t0 + m) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (tctl[3]) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
       __syncthreads();
       GN_STAMP(4);
@@ -1762,7 +1831,8 @@ hipError_t exclusive_scan_u64(const uint64_t *counts, uint64_t *offsets, size_t 
 hipError_t launch_expand_net(const NetDevice &net, const gn_board *parents, size_t n, const uint64_t *offsets,
                              const gn_board *children, const ChildDelta *deltas, const uint8_t *need_parent,
                              const uint8_t *need_child, int2 *out_parent, int2 *out_child, int swz,
-                             const uint8_t *next_slot, uint32_t *tickets, int chain_k, hipStream_t s) {
+                             const uint8_t *next_slot, uint32_t *tickets, int chain_k, uint32_t *ksnap,
+                             unsigned long long *rows_out, hipStream_t s) {
   if (!n) return hipSuccess;
   unsigned g = (unsigned)(swz ? 8 * ((n + 7) / 8) : n);
   // GN_EXPAND_LEGACY=1: the per-slot row programs (expand_eval) for the big nets, for A/B timing
@@ -1782,7 +1852,8 @@ hipError_t launch_expand_net(const NetDevice &net, const gn_board *parents, size
   if (persist > 0 && !chained) g = std::min<unsigned>(g, 8u * ((256u * (unsigned)persist + 7) / 8));
 #define GN_EXPAND_ARGS net, parents, offsets, children, deltas, need_parent, need_child, out_parent, out_child, n, swz, ablate
 #define GN_STREAM_ARGS net, parents, offsets, deltas, need_parent, need_child, out_parent, out_child, n, swz, ablate, \
-                       chained ? next_slot : nullptr, chained ? tickets : nullptr, chain_k
+                       chained ? next_slot : nullptr, chained ? tickets : nullptr, chain_k, chained ? ksnap : nullptr, \
+                       rows_out
   if (net.L1 == 3072 && !legacy) {
     hipLaunchKernelGGL((expand_stream_kernel<3072>), dim3(g), dim3(384), 0, s, GN_STREAM_ARGS);
   } else if (net.L1 == 1024 && !legacy) {

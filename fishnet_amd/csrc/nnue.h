@@ -25,10 +25,12 @@ constexpr int FT_ROWS = FT_INPUTS + 1;
 // Big nets: CARRY_SLOTS x 4 scratch rows follow the FT rows in the same allocation
 // (the expansion's chained walk, kernels.hip expand_stream): slot = dispatch index
 // mod CARRY_SLOTS, rows = parity of the parent x perspective.  Row indices stay
-// below 2^15 (the row field of a stream entry).
+// below 2^19 (the row field of a stream entry).
 constexpr int CARRY_SLOTS = 2048;
 constexpr int CARRY_ROW0 = FT_ROWS;
-static_assert(CARRY_ROW0 + 4 * CARRY_SLOTS <= 32768, "carry rows must fit the 15-bit row field");
+// Then the king cache: per slot, one accumulator row per (perspective, king square).
+constexpr int KC_ROW0 = CARRY_ROW0 + 4 * CARRY_SLOTS;
+static_assert(KC_ROW0 + 128 * CARRY_SLOTS <= (1 << 19), "carry and king-cache rows must fit the 19-bit row field");
 constexpr int PSQT_BUCKETS = 8;
 constexpr int LAYER_STACKS = 8;
 constexpr uint32_t NNUE_VERSION = 0x7AF32F20u;
@@ -37,6 +39,7 @@ struct NetDevice {
   int L1;
   uint32_t row_stride;
   int carry_slots; // CARRY_SLOTS when the carry rows exist (big nets), else 0
+  int kc_slots;    // CARRY_SLOTS when the king-cache rows exist (big nets), else 0
   const uint8_t *ft;
   const int16_t *bias;
   const int8_t *w0;

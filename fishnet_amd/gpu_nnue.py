@@ -37,7 +37,7 @@ EXPORTS = ["gn_load_net", "gn_load_net_memory", "gn_free", "gn_last_error", "gn_
            "gn_time_evaluate_device", "gn_random_positions_device", "gn_set_option", "gn_get_option",
            "gn_time_expand_device", "gn_random_games_device", "gn_replay_game", "gn_evaluate_games",
            "gn_net_sha256"]
-OPT_INCREMENTAL_CHILDREN, OPT_XCD_SWIZZLE, OPT_KING_SORT, OPT_CHAIN = 1, 2, 3, 4
+OPT_INCREMENTAL_CHILDREN, OPT_XCD_SWIZZLE, OPT_KING_SORT, OPT_CHAIN, OPT_KING_CACHE = 1, 2, 3, 4, 5
 EXPAND_STAGES = ["count_scan", "total_readback", "write_children", "classify", "small_net", "big_net", "finalize"]
 
 

@@ -64,6 +64,13 @@ extern "C" {
 #define GN_OPT_KING_SORT 3            /* 1 (default): evaluate a batch in (white king, black
                                          king) square order for L2 / Infinity-Cache
                                          locality, results in input order; 0: input order */
+#define GN_OPT_KING_CACHE 5           /* 1 (default): with the chained walk, a king-move
+                                         child's refresh starts from the accumulator the
+                                         workgroup last computed for that (perspective,
+                                         king square) in the same block, plus the placement
+                                         difference, when that is shorter (Stockfish's
+                                         AccumulatorCaches analog); 0: full refresh.
+                                         Results are identical either way.               */
 #define GN_OPT_CHAIN 4                /* expansion (big net): a workgroup walks blocks of up to
                                          this many consecutive parents (default 81: one
                                          80-ply game); a parent that is a child of the
@@ -247,10 +254,10 @@ GN_API int gn_expand_device(gn_ctx *ctx, int device_slot, const gn_board *d_pare
  * `mode`), library-owned output buffers.  *total = children per expansion;
  * stage_ms (optional, length 7) = average ms of [count+scan, total read-back,
  * write children, classify, small net, big net, finalize]; ft_rows (optional)
- * = feature-transformer rows one incremental expansion gathers (parent
- * refreshes, or one carried accumulator row per perspective for a parent that
- * is a child of the previous one (GN_OPT_CHAIN), + child deltas / king-move
- * refreshes; 0 when not incremental). */
+ * = feature-transformer rows one incremental expansion gathers: for the big
+ * nets the row stream's own count (bias, carry and king-cache rows included:
+ * GN_OPT_CHAIN, GN_OPT_KING_CACHE), else parent refreshes + child deltas /
+ * king-move refreshes; 0 when not incremental. */
 GN_API int gn_time_expand_device(gn_ctx *ctx, int device_slot, const gn_board *d_parents, size_t n, int mode,
                                  int iters, float *ms_total, size_t *total, float *stage_ms, uint64_t *ft_rows);
 /* n_games random games of `plies` plies (xoshiro256**, seed + game index) on

@@ -107,6 +107,33 @@ def test_big_stress_net_expansion(oracle_lib):
         assert got == {int(m): tuple(k) for m, k in zip(m_exp, k_exp)}, fen
 
 
+def test_big_stress_net_chained_king_cache():
+    """Chained walk + king cache under constant int16 wrapping: identical to one
+    refresh-started workgroup per parent on whole random games."""
+    from fishnet_amd import gpu_nnue as G, synthnet
+    ctx = G.GpuNnue(synthnet.cached_synth_net(3072, 11, stress=True), None)
+    games, plies = 24, 80
+    n = games * (plies + 1)
+    d_b = ctx.alloc(n * 32)
+    ctx.random_games_device(0x5EED0000 + 99, 0, games, plies, d_b)
+    ctx.synchronize()
+    cap = 60 * n
+    bufs = {k: ctx.alloc(sz) for k, sz in (("po", n * 16), ("off", (n + 1) * 4), ("ch", cap * 32),
+                                              ("mv", cap * 2), ("co", cap * 16))}
+
+    def run(k, kc):
+        ctx.set_option(G.OPT_CHAIN, k)
+        ctx.set_option(G.OPT_KING_CACHE, kc)
+        t = ctx.expand_device(d_b, n, 1, bufs["po"], bufs["off"], bufs["ch"], bufs["mv"], bufs["co"], cap)
+        return bufs["po"].download(G.EVAL_DTYPE, n), bufs["co"].download(G.EVAL_DTYPE, t)
+
+    ref = run(1, 0)
+    for k, kc in ((-81, 1), (-81, 0), (-5, 1)):
+        got = run(k, kc)
+        assert np.array_equal(ref[0], got[0]) and np.array_equal(ref[1], got[1]), (k, kc)
+    ctx.close()
+
+
 def test_device_api_matches_host_api(gpu_ctx):
     from fishnet_amd import gpu_nnue as G
     boards = G.random_positions(42, 1000, 4099, 160)
@@ -255,8 +282,9 @@ def test_locality_options_do_not_change_results(gpu_ctx, swz, ksort):
 @pytest.mark.parametrize("mode", [1, 0])
 def test_chained_walk_matches_refresh_and_oracle(gpu_ctx, oracle_nets, oracle_lib, mode):
     """Chained walk (GN_OPT_CHAIN): consecutive game positions start from the previous
-    parent's child accumulators.  Every block length gives the refresh results, and the
-    first games agree with the oracle."""
+    parent's child accumulators, king-move children from the block's king cache
+    (GN_OPT_KING_CACHE).  Every block length, with and without the cache, gives the
+    refresh results, and the first games agree with the oracle."""
     from fishnet_amd import gpu_nnue as G
     games, plies = 40, 80
     n = games * (plies + 1)
@@ -276,12 +304,15 @@ def test_chained_walk_matches_refresh_and_oracle(gpu_ctx, oracle_nets, oracle_li
 
     try:
         ref = run(1)
-        for k in (-81, -7, -2, 81):
-            got = run(k)
-            for a, b in zip(ref, got):
-                assert np.array_equal(a, b), k
+        for kc in (1, 0):
+            gpu_ctx.set_option(G.OPT_KING_CACHE, kc)
+            for k in (-81, -7, -2, 81):
+                got = run(k)
+                for a, b in zip(ref, got):
+                    assert np.array_equal(a, b), (k, kc)
     finally:
         gpu_ctx.set_option(G.OPT_CHAIN, 81)
+        gpu_ctx.set_option(G.OPT_KING_CACHE, 1)
     big, small = oracle_nets
     parents, offs, moves, kids = ref
     for i in range(2 * (plies + 1)):

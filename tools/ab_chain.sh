@@ -11,7 +11,8 @@ if [ -n "$HEADLIB" ]; then
   GPU_NNUE_LIB=$HEADLIB timeout -k 10 200 $B > $OUT/head.json 2> $OUT/head.err || { tail -20 $OUT/head.err; exit 1; }
   python -c "import json;d=json.load(open('$OUT/head.json'));print('head kernel_ms', round(d['roofline']['kernel_ms_per_launch'],2), 'evals/s %.4g'%d['value'])"
 fi
-for v in ${VARIANTS:-1 -4 -8 -16 -81}; do
-  timeout -k 10 200 $B --chain=$v > $OUT/chain$v.json 2> $OUT/chain$v.err || { tail -20 $OUT/chain$v.err; exit 1; }
-  python -c "import json;d=json.load(open('$OUT/chain$v.json'));print('chain=$v kernel_ms', round(d['roofline']['kernel_ms_per_launch'],2), 'evals/s %.4g'%d['value'], 'rows', d['config']['ft_rows_per_step_per_gpu'], d.get('oracle_check'))"
+for v in ${VARIANTS:-1 -81:0 -81:1}; do
+  ch=${v%%:*}; kc=${v#*:}; [ "$kc" = "$v" ] && kc=1
+  timeout -k 10 200 $B --chain=$ch --king-cache=$kc > $OUT/chain$v.json 2> $OUT/chain$v.err || { tail -20 $OUT/chain$v.err; exit 1; }
+  python -c "import json;d=json.load(open('$OUT/chain$v.json'));print('chain:kc=$v kernel_ms', round(d['roofline']['kernel_ms_per_launch'],2), 'evals/s %.4g'%d['value'], 'rows', d['config']['ft_rows_per_step_per_gpu'], d.get('oracle_check'))"
 done
