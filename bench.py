@@ -217,11 +217,11 @@ def cpu_baseline_expand(c: Ctx, parents, mode, budget_s):
     big = O.Net(c.big_p) if mode != 2 else None
     small = O.Net(c.small_p) if mode != 1 else None
     th = oracle_threads()
-    fens = [c.G.board_to_fen(b) for b in parents]
     done, t = 0, time.perf_counter()
     with cf.ThreadPoolExecutor(th) as ex:  # ctypes releases the GIL inside the C call
-        for k in range(0, len(fens), th * 8):
-            done += sum(1 + len(r[1]) for r in ex.map(lambda f: O.expand_eval(big, small, f, mode), fens[k:k + th * 8]))
+        for k in range(0, len(parents), th * 8):  # FEN text per chunk (the oracle's input), timed with it
+            fens = [c.G.board_to_fen(b) for b in parents[k:k + th * 8]]
+            done += sum(1 + len(r[1]) for r in ex.map(lambda f: O.expand_eval(big, small, f, mode), fens))
             if time.perf_counter() - t >= budget_s:
                 break
     dt = time.perf_counter() - t
@@ -312,7 +312,7 @@ def main():
 
     if c.rank == 0 and not args.no_cpu_baseline:
         if args.workload == "expand":
-            line["cpu_baseline"] = cpu_baseline_expand(c, r["parents"][:20000], mode, args.cpu_seconds)
+            line["cpu_baseline"] = cpu_baseline_expand(c, r["parents"][:400_000], mode, args.cpu_seconds)
         else:
             line["cpu_baseline"] = cpu_baseline_eval(c, r["boards"][:200_000], mode, args.cpu_seconds)
 
