@@ -195,7 +195,7 @@ struct Dev {
   DevBuf<uint32_t> off32;
   DevBuf<uint16_t> moves;
   DevBuf<ChildDelta> deltas;
-  DevBuf<uint16_t> kkeys, kkeys2; // king-sort keys
+  DevBuf<uint64_t> kkeys, kkeys2; // king-sort keys
   DevBuf<uint32_t> kidx, kperm;   // king-sort permutation
   void *sort_tmp = nullptr;
   size_t sort_bytes = 0;
@@ -387,7 +387,8 @@ static int evaluate_on(gn_ctx *ctx, Dev &d, const gn_board *b, size_t n, int mod
     HIP_TRY(d.kkeys2.ensure(n));
     HIP_TRY(d.kidx.ensure(n));
     HIP_TRY(d.kperm.ensure(n));
-    HIP_TRY(king_sort(b, n, d.kkeys.p, d.kidx.p, d.kkeys2.p, d.kperm.p, d.sort_tmp, d.sort_bytes, s));
+    HIP_TRY(king_sort(b, n, d.kkeys.p, d.kidx.p, d.kkeys2.p, d.kperm.p, mode != GN_MODE_SMALL, d.sort_tmp,
+                      d.sort_bytes, s));
     perm = d.kperm.p;
   }
   const int swz = (ctx->swizzle >> 1) & 1;

@@ -14,9 +14,11 @@ namespace gn {
 // swz: XCD-aware tile order (each XCD gets a contiguous range of tiles).
 hipError_t launch_eval_net(const NetDevice &net, const gn_board *boards, const uint8_t *need, size_t n,
                            int2 *out, const uint32_t *perm, int swz, hipStream_t s);
-// permutation of [0, n) ordering positions by (white king, black king) square
-hipError_t king_sort(const gn_board *boards, size_t n, uint16_t *keys, uint32_t *idx, uint16_t *keys_out,
-                     uint32_t *perm, void *&temp, size_t &temp_bytes, hipStream_t s);
+// permutation of [0, n) ordering positions by (white king, black king) square, then
+// (placement) by the pieces of the first two ranks (king_keys_kernel), which serve
+// the big net's common-row base; kings only (16-bit keys) otherwise
+hipError_t king_sort(const gn_board *boards, size_t n, uint64_t *keys, uint32_t *idx, uint64_t *keys_out,
+                     uint32_t *perm, bool placement, void *&temp, size_t &temp_bytes, hipStream_t s);
 // Incremental evaluation of parents + all their children (children of parent
 // p are [offsets[p], offsets[p+1]) with moves[]); need_* select what this net
 // evaluates (nullptr: all).

@@ -112,6 +112,37 @@ __device__ __forceinline__ int wave_features(const gn_board &p, uint16_t *rows_w
   return c;
 }
 
+// piece nibble on this lane's square (0: empty); lane = square.
+__device__ __forceinline__ int lane_piece(const gn_board &p, int lane) {
+  const uint64_t occ = p.occ;
+  const bool has = (occ >> lane) & 1;
+  const int k = popcnt(occ & ((1ull << lane) - 1));
+  uint64_t wlo, whi;
+  piece_words(p, wlo, whi);
+  return has && k < 32 ? piece_nibble(wlo, whi, k) : 0;
+}
+
+// wave_features without the squares of excl (the tile's common rows, eval_net):
+// rows in square order among occ & ~excl; returns the full piece count (bucket) or 0.
+__device__ __forceinline__ int wave_features_excl(const gn_board &p, uint16_t *rows_w, uint16_t *rows_b, int lane,
+                                                  uint64_t excl) {
+  const uint64_t occ = p.occ;
+  const int c = popcnt(occ);
+  const bool has = (occ >> lane) & 1;
+  const int pc = lane_piece(p, lane);
+  const int pt = pc & 7;
+  const uint64_t bad = __ballot(has && (pt < PAWN || pt > KING));
+  const uint64_t wkb = __ballot(has && pc == make_piece(WHITE, KING));
+  const uint64_t bkb = __ballot(has && pc == make_piece(BLACK, KING));
+  if (c < 2 || c > 32 || bad || popcnt(wkb) != 1 || popcnt(bkb) != 1) return 0;
+  if (has && !((excl >> lane) & 1)) {
+    const int k = popcnt(occ & ~excl & ((1ull << lane) - 1));
+    rows_w[k] = (uint16_t)feature_index(WHITE, lane, pc, __builtin_ctzll(wkb));
+    rows_b[k] = (uint16_t)feature_index(BLACK, lane, pc, __builtin_ctzll(bkb));
+  }
+  return c;
+}
+
 // Rows of perspective h of a child in which h's own king moved, straight from
 // the parent board (lane = square): the king goes kfrom -> kto (capturing
 // whatever stood there) and, for castling, the rook rfrom -> rto (64 = none).
@@ -351,7 +382,7 @@ __device__ __forceinline__ void layer_stack_wave(const NetDevice &net, const uin
 // 16 positions of the tile one after another); small net: G = 8, PAR = 16
 // (256 threads, all 16 positions at once).
 template <int L1, int PAR>
-__global__ void __launch_bounds__(2 * (L1 / 16) * PAR)
+__global__ void __launch_bounds__(2 * (L1 / 16) * PAR) __attribute__((amdgpu_waves_per_eu(PAR == 1 ? 1 : 6)))
     eval_net_kernel(NetDevice net, const gn_board *__restrict__ boards, const uint8_t *__restrict__ need,
                     size_t n, int2 *__restrict__ out, const uint32_t *__restrict__ perm, unsigned tiles, int swz) {
   constexpr int G = L1 / 16;
@@ -373,6 +404,11 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR)
   __shared__ int bkt[TILE];
   __shared__ uint32_t bmask;
   __shared__ uint32_t gidx[TILE];
+  __shared__ uint8_t sstm[TILE];
+  __shared__ uint8_t refpc[64];     // piece per square of the tile's first position (0xFF: none)
+  __shared__ uint32_t cmask[2];     // squares holding the same piece in every valid position
+  __shared__ uint16_t crow[2][32];  // the tile's common rows by ABSOLUTE perspective
+  __shared__ int ccnt;
   uint16_t(*rows)[2][32] = reinterpret_cast<uint16_t(*)[2][32]>(scratch);
 
   const int tid = threadIdx.x;
@@ -386,47 +422,98 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR)
     if (tile >= tiles) return;
   }
   const size_t base = (size_t)tile * TILE;
-  if (tid == 0) bmask = 0;
-  __syncthreads();
+  auto pos_index = [&](int sl) -> size_t {
+    const size_t q = base + sl;
+    return q < n ? (perm ? perm[q] : q) : 0;
+  };
+  auto pos_live = [&](int sl, size_t i) { return base + sl < n && (!need || need[i]); };
 
-  // ---- phase 0: feature rows of both perspectives (h = 0: side to move), one wave per position
+  // ---- phase 0: feature rows of both ABSOLUTE perspectives, one wave per position.
+  // Common-row base: the rows of the pieces that stand on the same square in every
+  // valid position of the tile (both kings included, so their feature indices agree)
+  // are gathered once per tile into the accumulator's starting value instead of once
+  // per position.  With the batch sorted by (kings, first squares' pieces) tiles share
+  // their kings and a few unmoved pieces.  Wrapping int16 adds are order-independent,
+  // so the results are those of a plain refresh.
+  // Big net only (PAR == 1): the small net's table is L2-resident and its rows cheap, so
+  // the two extra barriers cost more than the rows they save.
+  constexpr bool CB = PAR == 1;
   {
     const int lane = tid & 63, wave = tid >> 6;
-    for (int sl = wave; sl < TILE; sl += NW) {
-      const size_t q = base + sl;
-      const size_t i = q < n ? (perm ? perm[q] : q) : 0;
-      int cnt = 0;
-      if (q < n && (!need || need[i])) {
+    if (!CB) {
+      if (tid == 0) bmask = 0;
+    } else {
+      if (wave == 0) { // A: the first position's placement is the reference
+        const size_t i = pos_index(0);
+        int pc = 0xFF;
+        if (pos_live(0, i)) {
+          const gn_board p = boards[i];
+          if (wave_features(p, nullptr, nullptr, lane)) pc = lane_piece(p, lane);
+        }
+        refpc[lane] = (uint8_t)pc;
+        if (lane == 0) bmask = 0, cmask[0] = ~0u, cmask[1] = ~0u;
+      }
+      __syncthreads();
+      for (int sl = wave; sl < TILE; sl += NW) { // B: AND of the per-position agreement masks
+        const size_t i = pos_index(sl);
+        if (!pos_live(sl, i)) continue;
         const gn_board p = boards[i];
-        const int stm = p.stm_ep >> 7;
-        cnt = wave_features(p, rows[sl][stm], rows[sl][stm ^ 1], lane);
+        const int pc = lane_piece(p, lane);
+        const uint64_t eq = __ballot(pc == refpc[lane]);
+        if (wave_features(p, nullptr, nullptr, lane) && lane == 0) {
+          atomicAnd(&cmask[0], (uint32_t)eq);
+          atomicAnd(&cmask[1], (uint32_t)(eq >> 32));
+        }
+      }
+    }
+    __syncthreads();
+    // C: the common squares (occupied in the reference, both kings among them, else none)
+    const int rp = CB ? refpc[lane] : 0;
+    const bool cm = CB && ((((uint64_t)cmask[1] << 32 | cmask[0]) >> lane) & 1) && rp != 0 && rp != 0xFF;
+    const uint64_t wkb = __ballot(cm && rp == make_piece(WHITE, KING));
+    const uint64_t bkb = __ballot(cm && rp == make_piece(BLACK, KING));
+    const uint64_t excl = wkb && bkb ? __ballot(cm) : 0;
+    if (wave == 0) {
+      if ((excl >> lane) & 1) {
+        const int k = popcnt(excl & ((1ull << lane) - 1));
+        crow[WHITE][k] = (uint16_t)feature_index(WHITE, lane, rp, __builtin_ctzll(wkb));
+        crow[BLACK][k] = (uint16_t)feature_index(BLACK, lane, rp, __builtin_ctzll(bkb));
+      }
+      if (lane == 0) ccnt = popcnt(excl);
+    }
+    for (int sl = wave; sl < TILE; sl += NW) {
+      const size_t i = pos_index(sl);
+      int cnt = 0, stm = 0;
+      if (pos_live(sl, i)) {
+        const gn_board p = boards[i];
+        stm = p.stm_ep >> 7;
+        // big net: rows by absolute perspective (the base is per colour); small net: by
+        // relative perspective (h = 0: side to move), as the transform consumes them
+        if constexpr (CB) cnt = wave_features_excl(p, rows[sl][WHITE], rows[sl][BLACK], lane, excl);
+        else cnt = wave_features(p, rows[sl][stm], rows[sl][stm ^ 1], lane);
       }
       if (lane == 0) {
         gidx[sl] = (uint32_t)i;
         nfeat[sl] = cnt;
         bkt[sl] = cnt ? (cnt - 1) / 4 : 0;
+        sstm[sl] = (uint8_t)stm;
         if (cnt) atomicOr(&bmask, 1u << ((cnt - 1) / 4));
       }
     }
   }
   __syncthreads();
 
-  // ---- phase 1: gather-accumulate + transform into the LDS tile
+  // ---- phase 1: gather-accumulate + transform into the LDS tile (h: absolute perspective
+  // for the big net, relative for the small net)
   {
     const int q = tid / (2 * G), h = (tid / G) & 1, j = tid % G;
-    const ushort8 bias_lo = *reinterpret_cast<const ushort8 *>(net.bias + 8 * j);
-    const ushort8 bias_hi = *reinterpret_cast<const ushort8 *>(net.bias + L1 / 2 + 8 * j);
     const uint32_t j16 = 16 * j; // byte offset of this thread's columns in a row
-#pragma unroll 1
-    for (int r = 0; r < TILE / PAR; ++r) {
-      const int p = r * PAR + q;
-      const int cnt = nfeat[p];
-      if (!cnt) continue;
-      ushort8 lo = bias_lo, hi = bias_hi;
-      uint32_t ps = 0;
-      const uint32_t pso = 2 * L1 + ((bkt[p] >> 2) << 4);
-      const int pse = bkt[p] & 3;
-      const uint16_t *rr = rows[p][h];
+    const int nc = ccnt;
+    const uint16_t *cr = crow[h];
+    // rows rr[0..cnt) added to lo/hi and, on lane j == 0 when wps, their PSQT dword
+    // (16-B half at pso, element pse) to ps; 4 rows in flight, tail as one batch
+    auto gather = [&](const uint16_t *rr, int cnt, ushort8 &lo, ushort8 &hi, uint32_t &ps, uint32_t pso, int pse,
+                      bool wps) {
       int k = 0;
       for (; k + 4 <= cnt; k += 4) {
         const uint32_t o0 = ft_row(rr[k]) * RS, o1 = ft_row(rr[k + 1]) * RS, o2 = ft_row(rr[k + 2]) * RS, o3 = ft_row(rr[k + 3]) * RS;
@@ -438,7 +525,7 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR)
         const ushort8 b1 = ldft(net.ft, j16 + o1 + L1);
         const ushort8 b2 = ldft(net.ft, j16 + o2 + L1);
         const ushort8 b3 = ldft(net.ft, j16 + o3 + L1);
-        if (j == 0) {
+        if (wps && j == 0) {
           const int4v v0 = ldps(net.ft, o0 + pso);
           const int4v v1 = ldps(net.ft, o1 + pso);
           const int4v v2 = ldps(net.ft, o2 + pso);
@@ -456,7 +543,7 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR)
         const ushort8 b0 = ldft(net.ft, j16 + o0 + L1), b1 = ldft(net.ft, j16 + o1 + L1);
         const ushort8 b2 = ldft(net.ft, j16 + o2 + L1);
         uint32_t q0 = 0, q1 = 0, q2 = 0;
-        if (j == 0) {
+        if (wps && j == 0) {
           q0 = (uint32_t)(ldps(net.ft, o0 + pso))[pse];
           q1 = (uint32_t)(ldps(net.ft, o1 + pso))[pse];
           q2 = (uint32_t)(ldps(net.ft, o2 + pso))[pse];
@@ -465,9 +552,31 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR)
         if (k + 1 < cnt) lo += a1, hi += b1, ps += q1;
         if (k + 2 < cnt) lo += a2, hi += b2, ps += q2;
       }
+    };
+    // the tile's starting accumulator: bias + common rows (PSQT per position below)
+    ushort8 base_lo = *reinterpret_cast<const ushort8 *>(net.bias + 8 * j);
+    ushort8 base_hi = *reinterpret_cast<const ushort8 *>(net.bias + L1 / 2 + 8 * j);
+    {
+      uint32_t unused = 0;
+      gather(cr, nc, base_lo, base_hi, unused, 0, 0, false);
+    }
+#pragma unroll 1
+    for (int r = 0; r < TILE / PAR; ++r) {
+      const int p = r * PAR + q;
+      const int cnt = nfeat[p];
+      if (!cnt) continue;
+      ushort8 lo = base_lo, hi = base_hi;
+      uint32_t ps = 0;
+      const uint32_t pso = 2 * L1 + ((bkt[p] >> 2) << 4);
+      const int pse = bkt[p] & 3;
+      if (j == 0) { // PSQT of the common rows at this position's bucket (one lane)
+        for (int k = 0; k < nc; ++k) ps += (uint32_t)(ldps(net.ft, ft_row(cr[k]) * RS + pso))[pse];
+      }
+      gather(rows[p][h], cnt - nc, lo, hi, ps, pso, pse, true);
       // transform: clamp to [0, 254] in the doubled domain, product / 512
-      *reinterpret_cast<uint2 *>(xt + p * XS + h * (L1 / 2) + 8 * j) = transform8(lo, hi);
-      if (j == 0) psq[p][h] = (int32_t)ps;
+      const int rel = CB ? h ^ sstm[p] : h; // 0: side to move
+      *reinterpret_cast<uint2 *>(xt + p * XS + rel * (L1 / 2) + 8 * j) = transform8(lo, hi);
+      if (j == 0) psq[p][rel] = (int32_t)ps;
     }
   }
   __syncthreads();
@@ -1724,8 +1833,12 @@ __global__ void random_games_kernel(uint64_t seed, size_t first_game, size_t n_g
   }
 }
 
-// sort key of a position for L2 locality: both king squares (invalid last)
-__global__ void king_keys_kernel(const gn_board *__restrict__ boards, size_t n, uint16_t *__restrict__ keys,
+// sort key of a position: both king squares (L2 locality of the king-bucket slices),
+// then the pieces on a1-d1, f1-h1, a2-f2 (4 bits each) so that a tile of 16 positions
+// shares kings and unmoved pieces (eval_net's common-row base); invalid last.
+// Key = uint16_t: kings only (wk << 6 | bk), for small-net-only batches.
+template <class Key>
+__global__ void king_keys_kernel(const gn_board *__restrict__ boards, size_t n, Key *__restrict__ keys,
                                  uint32_t *__restrict__ idx) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -1734,13 +1847,29 @@ __global__ void king_keys_kernel(const gn_board *__restrict__ boards, size_t n, 
   piece_words(p, wlo, whi);
   uint64_t o = p.occ;
   int wk = 64, bk = 64;
+  uint64_t low = 0; // piece nibble per square of the first two ranks
   const int c = popcnt(o) <= 32 ? popcnt(o) : 0;
   for (int k = 0; k < c; ++k) {
     const int s = pop_lsb(o), pc = piece_nibble(wlo, whi, k);
     if (pc == make_piece(WHITE, KING)) wk = s;
     if (pc == make_piece(BLACK, KING)) bk = s;
+    if (s < 16) low |= (uint64_t)pc << (4 * s);
   }
-  keys[i] = (uint16_t)(wk < 64 && bk < 64 ? (wk << 6 | bk) : 0xFFFF);
+  if constexpr (sizeof(Key) == 2) {
+    keys[i] = (Key)(wk < 64 && bk < 64 ? (wk << 6 | bk) : 0xFFFF);
+    idx[i] = (uint32_t)i;
+    return;
+  }
+  uint64_t key = ~0ull;
+  if (wk < 64 && bk < 64) {
+    // squares 0-3, 5-13 (e1 is usually the white king, already in the key)
+    const uint64_t sq = (low & 0xFFFF) | ((low >> 4) & ~0xFFFFull);
+    // most significant squares first: reverse the 13 nibbles
+    uint64_t r = 0, t = sq;
+    for (int k = 0; k < 13; ++k, t >>= 4) r = r << 4 | (t & 15);
+    key = (uint64_t)wk << 58 | (uint64_t)bk << 52 | r;
+  }
+  keys[i] = (Key)key;
   idx[i] = (uint32_t)i;
 }
 
@@ -1794,14 +1923,15 @@ hipError_t launch_offsets_u32(const uint64_t *in, size_t n, uint32_t *out, hipSt
   return hipGetLastError();
 }
 
-hipError_t king_sort(const gn_board *boards, size_t n, uint16_t *keys, uint32_t *idx, uint16_t *keys_out,
-                     uint32_t *perm, void *&temp, size_t &temp_bytes, hipStream_t s) {
-  if (!n) return hipSuccess;
-  hipLaunchKernelGGL(king_keys_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, boards, n, keys, idx);
+template <class Key>
+static hipError_t king_sort_t(const gn_board *boards, size_t n, Key *keys, uint32_t *idx, Key *keys_out,
+                              uint32_t *perm, void *&temp, size_t &temp_bytes, hipStream_t s) {
+  hipLaunchKernelGGL(king_keys_kernel<Key>, dim3(blocks_for(n, 256)), dim3(256), 0, s, boards, n, keys, idx);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
+  constexpr int BITS = 8 * sizeof(Key);
   size_t need = 0;
-  e = hipcub::DeviceRadixSort::SortPairs(nullptr, need, keys, keys_out, idx, perm, (int)n, 0, 16, s);
+  e = hipcub::DeviceRadixSort::SortPairs(nullptr, need, keys, keys_out, idx, perm, (int)n, 0, BITS, s);
   if (e != hipSuccess) return e;
   if (need > temp_bytes) {
     if (temp) (void)hipFree(temp);
@@ -1810,7 +1940,15 @@ hipError_t king_sort(const gn_board *boards, size_t n, uint16_t *keys, uint32_t 
     if ((e = hipMalloc(&temp, need)) != hipSuccess) return e;
     temp_bytes = need;
   }
-  return hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, keys, keys_out, idx, perm, (int)n, 0, 16, s);
+  return hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, keys, keys_out, idx, perm, (int)n, 0, BITS, s);
+}
+
+hipError_t king_sort(const gn_board *boards, size_t n, uint64_t *keys, uint32_t *idx, uint64_t *keys_out,
+                     uint32_t *perm, bool placement, void *&temp, size_t &temp_bytes, hipStream_t s) {
+  if (!n) return hipSuccess;
+  if (placement) return king_sort_t(boards, n, keys, idx, keys_out, perm, temp, temp_bytes, s);
+  return king_sort_t(boards, n, reinterpret_cast<uint16_t *>(keys), idx, reinterpret_cast<uint16_t *>(keys_out), perm,
+                     temp, temp_bytes, s);
 }
 
 hipError_t exclusive_scan_u64(const uint64_t *counts, uint64_t *offsets, size_t n1, void *&temp, size_t &temp_bytes,

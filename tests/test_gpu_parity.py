@@ -322,3 +322,35 @@ def test_chained_walk_matches_refresh_and_oracle(gpu_ctx, oracle_nets, oracle_li
         lo, hi = int(offs[i]), int(offs[i + 1])
         got = {int(m): tuple(x) for m, x in zip(moves[lo:hi], kids[lo:hi])}
         assert got == {int(m): tuple(x) for m, x in zip(m_exp, k_exp)}, fen
+
+
+@pytest.mark.parametrize("ksort", [1, 0])
+def test_common_row_base_tiles(gpu_ctx, oracle_nets, oracle_lib, ksort):
+    """eval_net's common-row base (pieces on the same square in every position of a
+    16-position tile are gathered once per tile): consecutive positions of games share
+    most pieces and alternate the side to move; runs of one repeated position make the
+    whole placement common (zero per-position rows); invalid boards and a tile whose
+    first position is invalid must not constrain the base.  Bit-exact vs the oracle,
+    with the batch king/placement-sorted and in input order."""
+    from fishnet_amd import gpu_nnue as G
+    games, plies = 12, 60
+    n = games * (plies + 1)
+    d_b = gpu_ctx.alloc(n * 32)
+    gpu_ctx.random_games_device(0x5EED0077, 0, games, plies, d_b)
+    gpu_ctx.synchronize()
+    boards = d_b.download(G.BOARD_DTYPE, n)
+    boards = np.concatenate([boards, np.repeat(boards[5:6], 40), np.repeat(boards[70:71], 17)])
+    boards[32] = np.zeros(1, dtype=G.BOARD_DTYPE)  # first slot of a tile in input order
+    boards[100] = np.zeros(1, dtype=G.BOARD_DTYPE)
+    fens = [G.board_to_fen(b) if b["occ"] else "8/8/8/8/8/8/8/8 w - - 0 1" for b in boards]
+    big, small = oracle_nets
+    try:
+        gpu_ctx.set_option(G.OPT_KING_SORT, ksort)
+        for mode in (1, 0):
+            got = gpu_ctx.evaluate_batch(fens, mode)
+            ok = boards["occ"] != 0
+            vf = [f for f, v in zip(fens, ok) if v]
+            _cmp(got[ok], oracle_lib.eval_fens(big, small, vf, mode, threads=8), vf)
+            assert got[32]["flags"] & G.FLAG_BAD_FEN and got[100]["flags"] & G.FLAG_BAD_FEN
+    finally:
+        gpu_ctx.set_option(G.OPT_KING_SORT, 1)
