@@ -63,7 +63,10 @@ extern "C" {
                                          tiles (bit 1, batch evaluation); 0: dispatch order */
 #define GN_OPT_KING_SORT 3            /* 1 (default): evaluate a batch in (white king, black
                                          king) square order for L2 / Infinity-Cache
-                                         locality, results in input order; 0: input order */
+                                         locality, then (big net) by the pieces of the
+                                         first two ranks so that 16-position tiles share
+                                         rows gathered once per tile; results in input
+                                         order; 0: input order                            */
 #define GN_OPT_KING_CACHE 5           /* 1 (default): with the chained walk, a king-move
                                          child's refresh starts from the accumulator the
                                          workgroup last computed for that (perspective,
