@@ -1834,8 +1834,9 @@ __global__ void random_games_kernel(uint64_t seed, size_t first_game, size_t n_g
 }
 
 // sort key of a position: both king squares (L2 locality of the king-bucket slices),
-// then the pieces on a1-d1, f1-h1, a2-f2 (4 bits each) so that a tile of 16 positions
-// shares kings and unmoved pieces (eval_net's common-row base); invalid last.
+// then one bit per home square (ranks 1, 2, 7, 8 without e1 / e8, in square order):
+// the start position's piece still stands there.  A tile of 16 positions then shares
+// its kings and unmoved pieces (eval_net's common-row base); invalid last.
 // Key = uint16_t: kings only (wk << 6 | bk), for small-net-only batches.
 template <class Key>
 __global__ void king_keys_kernel(const gn_board *__restrict__ boards, size_t n, Key *__restrict__ keys,
@@ -1847,13 +1848,17 @@ __global__ void king_keys_kernel(const gn_board *__restrict__ boards, size_t n, 
   piece_words(p, wlo, whi);
   uint64_t o = p.occ;
   int wk = 64, bk = 64;
-  uint64_t low = 0; // piece nibble per square of the first two ranks
+  uint64_t home = 0; // bit s: square s holds its start-position piece
   const int c = popcnt(o) <= 32 ? popcnt(o) : 0;
   for (int k = 0; k < c; ++k) {
     const int s = pop_lsb(o), pc = piece_nibble(wlo, whi, k);
     if (pc == make_piece(WHITE, KING)) wk = s;
     if (pc == make_piece(BLACK, KING)) bk = s;
-    if (s < 16) low |= (uint64_t)pc << (4 * s);
+    const int r = s >> 3, f = s & 7;
+    constexpr int BACK[8] = {ROOK, KNIGHT, BISHOP, QUEEN, KING, BISHOP, KNIGHT, ROOK};
+    const int want = r == 0 ? make_piece(WHITE, BACK[f]) : r == 1 ? make_piece(WHITE, PAWN)
+                   : r == 6 ? make_piece(BLACK, PAWN) : r == 7 ? make_piece(BLACK, BACK[f]) : -1;
+    if (pc == want) home |= 1ull << s;
   }
   if constexpr (sizeof(Key) == 2) {
     keys[i] = (Key)(wk < 64 && bk < 64 ? (wk << 6 | bk) : 0xFFFF);
@@ -1862,12 +1867,13 @@ __global__ void king_keys_kernel(const gn_board *__restrict__ boards, size_t n, 
   }
   uint64_t key = ~0ull;
   if (wk < 64 && bk < 64) {
-    // squares 0-3, 5-13 (e1 is usually the white king, already in the key)
-    const uint64_t sq = (low & 0xFFFF) | ((low >> 4) & ~0xFFFFull);
-    // most significant squares first: reverse the 13 nibbles
-    uint64_t r = 0, t = sq;
-    for (int k = 0; k < 13; ++k, t >>= 4) r = r << 4 | (t & 15);
-    key = (uint64_t)wk << 58 | (uint64_t)bk << 52 | r;
+    // 30 home squares: a1-d1, f1-h1, rank 2, rank 7, a8-d8, f8-h8 -> bits 51..22
+    const uint64_t lo16 = home & 0xFFFF, hi16 = home >> 48;
+    const uint64_t h30 = (lo16 & 0xF) | ((lo16 >> 1) & ~0xFull) // 15 bits: squares 0-3, 5-15
+                         | ((hi16 & 0xFFF) | ((hi16 >> 1) & ~0xFFFull)) << 15; // 15 bits: 48-59, 61-63
+    uint64_t r = 0, t = h30; // square order, lowest square most significant
+    for (int k = 0; k < 30; ++k, t >>= 1) r = r << 1 | (t & 1);
+    key = (uint64_t)wk << 58 | (uint64_t)bk << 52 | r << 22;
   }
   keys[i] = (Key)key;
   idx[i] = (uint32_t)i;
