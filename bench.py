@@ -9,18 +9,25 @@ configuration; configs[3]'s batch shape): every GPU holds 49,152 random 80-ply
 games = 3,981,312 parent positions (81 per game), and one step is
   legal-child generation (GPU bitboard movegen, count + scan + write with
   per-child FT deltas) + big-net evaluation of every parent and every legal
-  child (parents refreshed once, children incremental from the parent
-  accumulators) + the Eval::evaluate epilogue,
+  child (children incremental from the parent accumulators, consecutive game
+  positions chained, king-move refreshes from the block's king cache) + the
+  Eval::evaluate epilogue with to_cp,
 ~127 M evaluated positions per GPU per step, i.e. >= 1e9 per step on 8 GPUs.
+The timed step's own outputs are verified: a device checksum of every parent and
+child result against the same expansion run the plain way (one workgroup per
+parent, every parent refreshed, no king cache), and sampled parents with all
+their children against the CPU oracle.
 Secondary results (same JSON object, not `value`):
   big16m  configs[2]: big-net full refresh of 16,777,216 positions per GPU;
-  small1m configs[1]: small-net evaluation of 1,048,576 positions per GPU.
+  small1m configs[1]: small-net evaluation of 1,048,576 positions per GPU;
+each with an oracle check of 4,096 of the timed outputs.
 
 All inputs are generated on the GPU by the same seeded playout code the host
 uses (`value` never includes host transfers), per-GPU work is fixed as N grows
 ("scaling": "weak"), and there is no data-path collective: RCCL
 (torch.distributed "nccl") only broadcasts the .nnue images from rank 0 and
-gathers per-rank checksums / the max wall time.  Nets: GPU_NNUE_BIG /
+gathers per-rank checksums, check results and the max wall time.  Ranks shard
+games by the library's partitioner (gn_partition).  Nets: GPU_NNUE_BIG /
 GPU_NNUE_SMALL if set (real Stockfish nets), else seeded synthetic nets of
 identical shape (fishnet_amd/synthnet.py).
 """
@@ -40,7 +47,12 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "NNUE evals/sec (node) at 1/2/4/8 MI355X + FT gather HBM GB/s as % of peak"
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (/opt/skills/guides/MI355X_MICROARCH.md, chip table)
+# /opt/skills/guides/MI355X_MICROARCH.md: HBM3E 8 TB/s peak; L2 34.5 TB/s aggregate (§L2);
+# gathered rows served by the Infinity Cache 8.6 TB/s (§Indexed rows, 38 MB table: the
+# guide's fastest past-L2 gather figure)
+HBM_PEAK_GBS = 8000.0
+L2_PEAK_GBS = 34500.0
+IC_GATHER_GBS = 8600.0
 SEED = 0x5EED0000
 PLIES = 80
 WORKLOADS = {
@@ -64,14 +76,74 @@ def popcounts(occ: np.ndarray) -> np.ndarray:
     return table[b].sum(axis=1, dtype=np.int64)
 
 
-def cpu_model():
+def cpuinfo():
+    info = {"model": platform.processor() or "unknown", "flags": set(), "vendor": "", "family": 0}
     try:
         for line in open("/proc/cpuinfo"):
-            if line.startswith("model name"):
-                return line.split(":", 1)[1].strip()
+            k, _, v = line.partition(":")
+            k, v = k.strip(), v.strip()
+            if k == "model name":
+                info["model"] = v
+            elif k == "flags":
+                info["flags"] = set(v.split())
+            elif k == "vendor_id":
+                info["vendor"] = v
+            elif k == "cpu family":
+                info["family"] = int(v)
+            if info["flags"] and info["vendor"] and info["family"] and k == "flags":
+                break
     except OSError:
         pass
-    return platform.processor() or "unknown"
+    return info
+
+
+def fishnet_cpu_class(info) -> str:
+    """The Stockfish build fishnet would pick on this CPU: Cpu::detect + Cpu::requirements
+    (/root/reference/src/assets.rs:52-121), best first."""
+    f = info["flags"]
+    sse41 = "sse4_1" in f and "popcnt" in f
+    avx2 = sse41 and "avx2" in f
+    bmi2 = avx2 and "bmi2" in f and (info["vendor"] != "AuthenticAMD" or info["family"] >= 0x19)
+    avx512 = bmi2 and "avx512f" in f and "avx512bw" in f
+    vnni = avx512 and {"avx512dq", "avx512vl", "avx512_vnni"} <= f
+    for ok, name in ((vnni, "x86-64-vnni256"), (avx512, "x86-64-avx512"), (bmi2, "x86-64-bmi2"),
+                     (avx2, "x86-64-avx2"), (sse41, "x86-64-sse41-popcnt")):
+        if ok:
+            return name
+    return "x86-64"
+
+
+def host_threads():
+    """This GPU's share of host cores: the affinity mask, capped by OMP_NUM_THREADS (the
+    GPU pool sets it to its per-GPU CPU share)."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    return max(1, min(aff, int(omp))) if omp.isdigit() and int(omp) > 0 else aff
+
+
+def roofline(alg_bytes, kern_ms, kernel, pmc):
+    """Hierarchical memory ceiling of the FT row gather: every gathered row byte passes
+    the L2 (34.5 TB/s), the bytes past L2 (PMC traffic) come from the Infinity Cache /
+    HBM (8.6 TB/s for gathered rows); the kernel cannot beat the slower of the two.
+    Without PMC data only the L2 term is known (frac then a lower bound)."""
+    t = kern_ms * 1e-3
+    achieved = alg_bytes / t / 1e9
+    t_l2 = alg_bytes / (L2_PEAK_GBS * 1e9)
+    r = {"bound": "hbm", "kernel": kernel, "achieved": round(achieved, 1), "unit": "GB/s",
+         "traffic": None, "alg_bytes_per_launch": int(alg_bytes), "kernel_ms_per_launch": round(kern_ms, 4),
+         "peak_model": "alg_bytes / max(alg_bytes / 34.5 TB/s (L2), traffic / 8.6 TB/s (Infinity-Cache gather)); "
+                       "achieved = kernel-counted FT rows x (2*L1 + 4) B / kernel time"}
+    if pmc:
+        traffic = float(pmc["hbm_side_bytes_per_launch"])
+        t_ic = traffic / (IC_GATHER_GBS * 1e9)
+        peak = alg_bytes / max(t_l2, t_ic) / 1e9
+        r.update(traffic=int(traffic), traffic_source=pmc["source"], l2_hit_rate=pmc.get("l2_hit_rate"),
+                 hbm_side_GBps=round(traffic / t / 1e9, 1), hbm_frac=round(traffic / t / 1e9 / HBM_PEAK_GBS, 4))
+    else:
+        peak = L2_PEAK_GBS
+    r["peak"] = round(peak, 1)
+    r["frac"] = round(achieved / peak, 4)
+    return r
 
 
 class Ctx:
@@ -89,7 +161,7 @@ class Ctx:
         # nets: rank 0 reads, RCCL broadcast over xGMI, every rank loads from memory
         big_p, small_p, label = synthnet.net_paths() if self.rank == 0 else (None, None, None)
         blobs = [self.comm.broadcast_bytes(open(p, "rb").read() if self.rank == 0 else b"") for p in (big_p, small_p)]
-        self.big_p, self.small_p = big_p, small_p
+        self.blobs = blobs
         self.net_label = self.comm.broadcast_obj(label)
         self.nn = G.GpuNnue(big_bytes=blobs[0], small_bytes=blobs[1], devices=[self.local])
         if args.swizzle >= 0:
@@ -103,39 +175,37 @@ class Ctx:
         self.options = {"xcd_swizzle": self.nn.get_option(G.OPT_XCD_SWIZZLE),
                         "king_sort": self.nn.get_option(G.OPT_KING_SORT),
                         "incremental_children": self.nn.get_option(G.OPT_INCREMENTAL_CHILDREN),
-                        "chain": self._opt(G.OPT_CHAIN), "king_cache": self._opt(G.OPT_KING_CACHE)}
+                        "chain": self.nn.get_option(G.OPT_CHAIN), "king_cache": self.nn.get_option(G.OPT_KING_CACHE)}
+        self._onets = None
 
-    def _opt(self, option):
-        try:
-            return self.nn.get_option(option)
-        except self.G.GnError:  # an older library (A/B runs through GPU_NNUE_LIB)
-            return None
+    def oracle_nets(self):
+        """(oracle module, big net, small net) from the broadcast images (rank-local CPU)."""
+        if self._onets is None:
+            from oracle import oracle as O
+            O.build()
+            self._onets = (O, O.Net(data=self.blobs[0]), O.Net(data=self.blobs[1]))
+        return self._onets
+
+    def shard(self, items_per_rank):
+        """(first, count) of this rank's items by the library's partitioner (equal weights)."""
+        b = self.G.partition(items_per_rank * self.world, self.world)
+        return b[self.rank], b[self.rank + 1] - b[self.rank]
 
     def barrier_sync(self):
         self.comm.barrier()
         self.torch.cuda.synchronize()
-
-    def max_over_ranks(self, x: float) -> float:
-        return self.comm.max(x)
-
-    def gather_checksums(self, c: int):
-        return self.comm.gather_i64(c)
 
     def close(self):
         self.comm.close()
         self.nn.close()
 
 
-def checksum(arr: np.ndarray) -> int:
-    return int(np.bitwise_xor.reduce(arr.view(np.uint32).astype(np.uint64) * np.uint64(2654435761)))
-
-
-def run_eval(c: Ctx, wl: dict, n: int, steps: int, warmup: int, max_plies: int):
+def run_eval(c: Ctx, wl: dict, n: int, steps: int, warmup: int, max_plies: int, check: int):
     """Full-refresh batch evaluation of n device-resident positions per GPU."""
     G, nn, mode = c.G, c.nn, wl["mode"]
     d_b, d_o = nn.alloc(n * 32), nn.alloc(n * 16)
     t = time.perf_counter()
-    first, _ = c.comm.shard(n)
+    first, _ = c.shard(n)
     nn.random_positions_device(SEED, first, n, max_plies, d_b)
     nn.synchronize()
     gen_s = time.perf_counter() - t
@@ -144,91 +214,165 @@ def run_eval(c: Ctx, wl: dict, n: int, steps: int, warmup: int, max_plies: int):
     nn.synchronize()
     c.barrier_sync()
     t0 = time.perf_counter()
-    _, stage = nn.time_evaluate_device(d_b, n, mode, d_o, steps, per_kernel=True)
+    _, stage, rows = nn.time_evaluate_device(d_b, n, mode, d_o, steps, per_kernel=True, rows=True)
     c.barrier_sync()
-    wall = c.max_over_ranks(time.perf_counter() - t0)
+    wall = c.comm.max(time.perf_counter() - t0)
     out, boards = d_o.download(G.EVAL_DTYPE, n), d_b.download(G.BOARD_DTYPE, n)
+    checksum = nn.checksum_device(d_o, n * 16)
     d_b.free(), d_o.free()
     pieces = popcounts(boards["occ"])
-    row = 2 * wl["l1"] + 4  # one feature: L1 int16 weights + the bucket's int32 PSQT weight
-    if mode == 0:
-        big = (out["flags"] & G.FLAG_SMALLNET) == 0
-        alg = 2 * int(pieces[big].sum()) * row + int(big.sum()) * 40
-    else:
-        alg = 2 * int(pieces.sum()) * row + n * 40
+    alg = rows * (2 * wl["l1"] + 4) + n * 40
     k = 1 if mode == 2 else 2
-    return dict(value=c.world * n * steps / wall, wall=wall, stage=stage, kern_ms=stage[k], alg=alg, out=out,
-                boards=boards, pieces=pieces, gen_s=gen_s,
-                kernel=f"eval_net<{wl['l1']}> ({EVAL_STAGES[k]})")
+    r = dict(value=c.world * n * steps / wall, wall=wall, stage=stage, kern_ms=stage[k], alg=alg, rows=rows, out=out,
+             boards=boards, pieces=pieces, gen_s=gen_s, checksum=checksum,
+             kernel=f"eval_net<{wl['l1']}> ({EVAL_STAGES[k]})")
+    if check:  # the timed launch's own outputs, first `check` positions, against the oracle
+        O, big, small = c.oracle_nets()
+        k = min(check, n)
+        fens = [G.board_to_fen(b) for b in boards[:k]]
+        exp = O.eval_fens(big if mode != 2 else None, small if mode != 1 else None, fens, mode,
+                          threads=host_threads())
+        r["oracle_check"] = {"positions": k, "mismatches": int(np.count_nonzero(exp != out[:k])),
+                             "of": "the timed launch's outputs"}
+    return r
 
 
-def run_expand(c: Ctx, wl: dict, games: int, steps: int, warmup: int):
-    """Games x 81 parents, every legal child, incremental evaluation."""
+def run_expand(c: Ctx, wl: dict, games: int, steps: int, warmup: int, check: int):
+    """Games x 81 parents, every legal child, incremental evaluation; verifies the timed outputs."""
     G, nn, mode = c.G, c.nn, wl["mode"]
     n = games * (PLIES + 1)
     d_p = nn.alloc(n * 32)
     t = time.perf_counter()
-    first, _ = c.comm.shard(games)
+    first, _ = c.shard(games)
     nn.random_games_device(SEED, first, games, PLIES, d_p)
     nn.synchronize()
     gen_s = time.perf_counter() - t
+    # one untimed expansion sizes the output buffers (and warms up); then W warmup steps
+    _, total, _, _ = nn.time_expand_device(d_p, n, mode, 1)
+    out = {"po": nn.alloc(n * 16), "off": nn.alloc((n + 1) * 4), "mv": nn.alloc(max(total, 1) * 2),
+           "co": nn.alloc(max(total, 1) * 16), "cap": total}
     if warmup:
-        nn.time_expand_device(d_p, n, mode, warmup)
+        nn.time_expand_device(d_p, n, mode, warmup, outputs=out)
     c.barrier_sync()
     t0 = time.perf_counter()
-    _, children, stage, rows = nn.time_expand_device(d_p, n, mode, steps)
+    _, children, stage, rows = nn.time_expand_device(d_p, n, mode, steps, outputs=out)
     c.barrier_sync()
-    wall = c.max_over_ranks(time.perf_counter() - t0)
+    wall = c.comm.max(time.perf_counter() - t0)
+    fallbacks = nn.get_option(G.STAT_CHAIN_FALLBACKS)
     parents = d_p.download(G.BOARD_DTYPE, n)
+    sums = (nn.checksum_device(out["po"], n * 16), nn.checksum_device(out["co"], children * 16),
+            nn.checksum_device(out["mv"], children * 2), nn.checksum_device(out["off"], (n + 1) * 4))
+    r = dict(value=c.world * (n + children) * steps / wall, wall=wall, stage=stage, kern_ms=stage[5 if mode != 2 else 4],
+             alg=rows * (2 * wl["l1"] + 4) + n * 32 + children * (24 + 8), rows=rows, parents=parents, n=n,
+             children=children, gen_s=gen_s, checksum=sums[0] ^ sums[1], chain_fallbacks=fallbacks,
+             kernel=f"expand_stream<{wl['l1']}>" if wl["l1"] != 128 else f"expand_eval<{wl['l1']}>")
+    if check:
+        ver = {}
+        # (1) sampled parents of the timed outputs, with all their children, against the oracle
+        O, big, small = c.oracle_nets()
+        rng = np.random.default_rng(1234 + c.rank)
+        idx = np.unique(np.concatenate([rng.choice(n, size=min(check, n), replace=False),
+                                        np.arange(min(81, n))]))  # + one whole game (its chain and king cache)
+        offs = out["off"].download(np.uint32, n + 1)
+        fens = [G.board_to_fen(parents[i]) for i in idx]
+        pev = out["po"].download(G.EVAL_DTYPE, n)
+
+        def one(j):
+            i = int(idx[j])
+            lo, hi = int(offs[i]), int(offs[i + 1])
+            mv = out["mv"].download(np.uint16, hi - lo, offset=lo)
+            ev = out["co"].download(G.EVAL_DTYPE, hi - lo, offset=lo)
+            p_exp, m_exp, k_exp = O.expand_eval(big if mode != 2 else None, small if mode != 1 else None, fens[j],
+                                                mode, incremental=True)
+            got = dict(zip(mv.tolist(), map(tuple, ev.tolist())))
+            return int(got != dict(zip(m_exp, map(tuple, k_exp.tolist()))) or tuple(pev[i]) != p_exp), hi - lo
+
+        with cf.ThreadPoolExecutor(host_threads()) as ex:
+            res = list(ex.map(one, range(len(idx))))
+        ver["oracle"] = {"parents": len(idx), "children": sum(x[1] for x in res),
+                         "mismatching_parents": sum(x[0] for x in res),
+                         "of": "the timed expansion's outputs (random parents + the first whole game)"}
+        # (2) every output of the timed step against the plain path: one workgroup per parent,
+        # every parent refreshed, no king cache (GN_OPT_CHAIN 1, GN_OPT_KING_CACHE 0)
+        opts = (nn.get_option(G.OPT_CHAIN), nn.get_option(G.OPT_KING_CACHE))
+        try:
+            nn.set_option(G.OPT_CHAIN, 1)
+            nn.set_option(G.OPT_KING_CACHE, 0)
+            _, t2, _, _ = nn.time_expand_device(d_p, n, mode, 1, outputs=out)
+        finally:
+            nn.set_option(G.OPT_CHAIN, opts[0])
+            nn.set_option(G.OPT_KING_CACHE, opts[1])
+        ref = (nn.checksum_device(out["po"], n * 16), nn.checksum_device(out["co"], t2 * 16),
+               nn.checksum_device(out["mv"], t2 * 2), nn.checksum_device(out["off"], (n + 1) * 4))
+        ver["vs_plain_path"] = {"equal": bool(ref == sums and t2 == children), "parents": n, "children": children,
+                                "checksum_timed": f"{sums[0] ^ sums[1]:016x}",
+                                "checksum_plain": f"{ref[0] ^ ref[1]:016x}",
+                                "plain_path": "GN_OPT_CHAIN=1, GN_OPT_KING_CACHE=0 (refresh-started parents)"}
+        r["oracle_check"] = ver
+    for b in ("po", "off", "mv", "co"):
+        out[b].free()
     d_p.free()
-    l1 = wl["l1"]
-    alg = rows * (2 * l1 + 4) + n * 32 + children * (24 + 8)
-    k = 5 if mode != 2 else 4
-    return dict(value=c.world * (n + children) * steps / wall, wall=wall, stage=stage, kern_ms=stage[k], alg=alg,
-                rows=rows, parents=parents, n=n, children=children, gen_s=gen_s, kernel=f"expand_stream<{l1}>" if l1 != 128 else f"expand_eval<{l1}>")
-
-
-def oracle_threads():
-    return max(1, min(16, os.cpu_count() or 1))
+    return r
 
 
 def cpu_baseline_eval(c: Ctx, boards, mode, budget_s):
-    """Oracle (CPU restatement, scalar C -O3 -march=x86-64-v3) on a bounded sample."""
-    from oracle import oracle as O
-    big = O.Net(c.big_p) if mode != 2 else None
-    small = O.Net(c.small_p) if mode != 1 else None
-    th = oracle_threads()
-    fens = [c.G.board_to_fen(b) for b in boards]
-    done, reps, t = 0, 0, time.perf_counter()
-    while True:
-        O.eval_fens(big, small, fens, mode, threads=th)
-        done, reps = done + len(fens), reps + 1
-        dt = time.perf_counter() - t
-        if dt >= budget_s or reps >= 200:
-            break
+    """The oracle built -O3 -march=native on this GPU's share of host cores, full refresh per
+    position (a batch of unrelated FENs has no parent to update from)."""
+    O, big, small = c.oracle_nets()
+    O.build(native=True)
+    O.use_library(O.NATIVE_LIB_PATH)
+    try:
+        th, info = host_threads(), cpuinfo()
+        fens = [c.G.board_to_fen(b) for b in boards]
+        done, reps, t = 0, 0, time.perf_counter()
+        while True:
+            O.eval_fens(big if mode != 2 else None, small if mode != 1 else None, fens, mode, threads=th)
+            done, reps = done + len(fens), reps + 1
+            dt = time.perf_counter() - t
+            if dt >= budget_s or reps >= 200:
+                break
+    finally:
+        O.use_library(os.path.join(O.HERE, "_build", "liboracle.so"))
     return {"value": round(done / dt, 1), "unit": "evals/s", "cores": th, "kind": "port",
             "sample": f"{len(fens)} positions of rank 0's batch x {reps} passes = {done} evals in {dt:.1f} s; "
-                      f"oracle/oracle.c scalar C -O3 -march=x86-64-v3 (AVX2 build class), {th} threads, {cpu_model()}"}
+                      f"oracle/oracle.c -O3 -march=native (fishnet's Cpu::detect class on this host: "
+                      f"{fishnet_cpu_class(info)}), full refresh per position, {th} threads = this GPU's share "
+                      f"of the host ({os.cpu_count()} logical CPUs), {info['model']}"}
 
 
 def cpu_baseline_expand(c: Ctx, parents, mode, budget_s):
-    """Oracle: every parent + every legal child (make-move + full refresh) on a bounded sample."""
-    from oracle import oracle as O
-    big = O.Net(c.big_p) if mode != 2 else None
-    small = O.Net(c.small_p) if mode != 1 else None
-    th = oracle_threads()
-    done, t = 0, time.perf_counter()
-    with cf.ThreadPoolExecutor(th) as ex:  # ctypes releases the GIL inside the C call
-        for k in range(0, len(parents), th * 8):  # FEN text per chunk (the oracle's input), timed with it
-            fens = [c.G.board_to_fen(b) for b in parents[k:k + th * 8]]
-            done += sum(1 + len(r[1]) for r in ex.map(lambda f: O.expand_eval(big, small, f, mode), fens))
+    """The oracle built -O3 -march=native on this GPU's share of host cores: every parent + all
+    its legal children, children updated incrementally from the parent's accumulators."""
+    O, big, small = c.oracle_nets()
+    O.build(native=True)
+    O.use_library(O.NATIVE_LIB_PATH)
+    try:
+        th, info = host_threads(), cpuinfo()
+        fens = [c.G.board_to_fen(b) for b in parents]  # the oracle's input form, prepared untimed
+        done, k, chunk, t = 0, 0, max(64, 16 * th), time.perf_counter()
+        while k < len(fens):
+            _, counts, _ = O.expand_eval_batch(big if mode != 2 else None, small if mode != 1 else None,
+                                               fens[k:k + chunk], mode, incremental=True, threads=th)
+            done += len(counts) + int(counts[counts > 0].sum())
+            k += chunk
             if time.perf_counter() - t >= budget_s:
                 break
-    dt = time.perf_counter() - t
+        dt = time.perf_counter() - t
+    finally:
+        O.use_library(os.path.join(O.HERE, "_build", "liboracle.so"))
     return {"value": round(done / dt, 1), "unit": "evals/s", "cores": th, "kind": "port",
-            "sample": f"{done} evals (parents of rank 0's games + all their legal children) in {dt:.1f} s; "
-                      f"oracle/oracle.c (mailbox movegen, full-refresh NNUE) scalar C -O3 -march=x86-64-v3, "
-                      f"{th} threads, {cpu_model()}"}
+            "sample": f"{done} evals ({k} parents of rank 0's games + all their legal children) in {dt:.1f} s; "
+                      f"oracle/oracle.c -O3 -march=native (fishnet's Cpu::detect class on this host: "
+                      f"{fishnet_cpu_class(info)}), children incremental from the parent accumulators, "
+                      f"{th} threads = this GPU's share of the host ({os.cpu_count()} logical CPUs), {info['model']}"}
+
+
+def load_pmc(workload, n):
+    p = os.path.join(ROOT, "profiles", "latest_pmc.json")
+    if not os.path.exists(p):
+        return None
+    e = json.load(open(p)).get(workload)
+    return e if e and e.get("positions") == n and e.get("abi", 1) >= 2 else None
 
 
 def main():
@@ -242,7 +386,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true")
-    ap.add_argument("--check", type=int, default=1024, help="positions / parents re-checked against the oracle")
+    ap.add_argument("--check", type=int, default=256,
+                    help="expand: parents (with children) of the timed outputs re-checked against the oracle, plus "
+                         "the plain-path checksum; eval: positions (x16, >= 4096)")
     ap.add_argument("--swizzle", type=int, default=-1, help="GN_OPT_XCD_SWIZZLE mask (-1: library default)")
     ap.add_argument("--king-sort", type=int, default=-1, help="GN_OPT_KING_SORT (-1: library default)")
     ap.add_argument("--chain", type=int, default=None, help="GN_OPT_CHAIN (None: library default; -k: exactly k)")
@@ -254,65 +400,44 @@ def main():
     wl = WORKLOADS[args.workload]
     mode = wl["mode"]
     n = args.positions or wl["n"]
+    eval_check = max(4096, 16 * args.check) if args.check else 0
     if args.workload == "expand":
-        r = run_expand(c, wl, n, args.steps, args.warmup)
+        r = run_expand(c, wl, n, args.steps, args.warmup, args.check)
         cfg = {"workload": wl["config"], "games_per_gpu": n, "parents_per_gpu": r["n"],
                "children_per_gpu": r["children"], "evals_per_step_per_gpu": r["n"] + r["children"],
                "evals_per_step_all_gpus": c.world * (r["n"] + r["children"]), "plies": PLIES,
-               "ft_rows_per_step_per_gpu": r["rows"]}
+               "ft_rows_per_step_per_gpu": r["rows"], "chain_fallbacks": r["chain_fallbacks"]}
         stage_names = G.EXPAND_STAGES
         data = f"synthetic: seeded random 80-ply games generated on the GPU; nets {c.net_label}"
     else:
-        r = run_eval(c, wl, n, args.steps, args.warmup, args.max_plies)
+        r = run_eval(c, wl, n, args.steps, args.warmup, args.max_plies, eval_check)
         cfg = {"workload": wl["config"], "positions_per_gpu": n, "global_batch": n * c.world,
-               "mean_pieces": round(float(r["pieces"].mean()), 3), "max_plies": args.max_plies}
+               "mean_pieces": round(float(r["pieces"].mean()), 3), "max_plies": args.max_plies,
+               "ft_rows_per_step_per_gpu": r["rows"]}
         stage_names = EVAL_STAGES
         data = f"synthetic: seeded random-playout positions generated on the GPU; nets {c.net_label}"
     cfg.update({"mode": ["full", "big", "small"][mode], "parallelism": f"dp{c.world} (sharded, no collective)",
                 "options": c.options})
-    achieved = r["alg"] / (r["kern_ms"] * 1e-3) / 1e9
+    roof = roofline(r["alg"], r["kern_ms"], r["kernel"], load_pmc(args.workload, n))
+    roof["stage_ms"] = {k: round(v, 4) for k, v in zip(stage_names, r["stage"])}
     line = {
         "metric": METRIC, "value": round(r["value"], 1), "unit": "evals/s", "n_gpus": c.world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(r["wall"] * 1e3 / args.steps, 3),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int16/int8",
-        "data": data, "config": cfg,
-        "roofline": {"bound": "hbm", "kernel": r["kernel"], "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                     "alg_bytes_per_launch": r["alg"], "kernel_ms_per_launch": round(r["kern_ms"], 4),
-                     "stage_ms": {k: round(v, 4) for k, v in zip(stage_names, r["stage"])}},
+        "data": data, "config": cfg, "roofline": roof,
     }
-    pmc = os.path.join(ROOT, "profiles", "latest_pmc.json")
-    if os.path.exists(pmc):
-        p = json.load(open(pmc)).get(args.workload)
-        if p and p.get("positions") == n:
-            line["roofline"]["traffic"] = p["hbm_side_bytes_per_launch"]
-            line["roofline"]["traffic_source"] = p["source"]
-
-    if c.rank == 0 and args.check:
-        from oracle import oracle as O
-        big = O.Net(c.big_p) if mode != 2 else None
-        small = O.Net(c.small_p) if mode != 1 else None
-        if args.workload == "expand":
-            idx = np.linspace(0, r["n"] - 1, min(args.check, 64)).astype(int)
-            fens = [G.board_to_fen(r["parents"][i]) for i in idx]
-            _, offs, moves, kids = c.nn.expand_and_evaluate(fens, mode)
-            bad = 0
-            for i, fen in enumerate(fens):
-                _, m_exp, k_exp = O.expand_eval(big, small, fen, mode)
-                got = dict(zip(moves[offs[i]:offs[i + 1]].tolist(), map(tuple, kids[offs[i]:offs[i + 1]].tolist())))
-                bad += got != dict(zip(m_exp, map(tuple, k_exp.tolist())))
-            line["oracle_check"] = {"parents": len(fens), "children": int(offs[-1]), "mismatching_parents": bad}
-        else:
-            k = min(args.check, n)
-            fens = [G.board_to_fen(b) for b in r["boards"][:k]]
-            exp = O.eval_fens(big, small, fens, mode, threads=oracle_threads())
-            line["oracle_check"] = {"positions": k, "mismatches": int(np.count_nonzero(exp != r["out"][:k]))}
-    if "out" in r:
-        line["rank_checksums"] = c.gather_checksums(checksum(r["out"]))
+    # per-rank verification results and checksums (all ranks check their own timed outputs)
+    chk = r.get("oracle_check")
+    if chk is not None:
+        bad = (chk["oracle"]["mismatching_parents"] + (0 if chk["vs_plain_path"]["equal"] else 1)
+               if args.workload == "expand" else chk["mismatches"])
+        line["oracle_check"] = chk
+        line["rank_check_failures"] = c.comm.gather_i64(int(bad))
+    line["rank_checksums"] = [f"{x:016x}" for x in c.comm.gather_i64(int(r["checksum"]) & 0x7FFFFFFFFFFFFFFF)]
 
     if c.rank == 0 and not args.no_cpu_baseline:
         if args.workload == "expand":
-            line["cpu_baseline"] = cpu_baseline_expand(c, r["parents"][:400_000], mode, args.cpu_seconds)
+            line["cpu_baseline"] = cpu_baseline_expand(c, r["parents"][:200_000], mode, args.cpu_seconds)
         else:
             line["cpu_baseline"] = cpu_baseline_eval(c, r["boards"][:200_000], mode, args.cpu_seconds)
 
@@ -320,12 +445,15 @@ def main():
         sec = {}
         for name in ("big16m", "small1m"):
             w = WORKLOADS[name]
-            s = run_eval(c, w, w["n"], 3, 1, args.max_plies)
-            a = s["alg"] / (s["kern_ms"] * 1e-3) / 1e9
+            s = run_eval(c, w, w["n"], 3, 1, args.max_plies, 4096 if args.check else 0)
+            rf = roofline(s["alg"], s["kern_ms"], s["kernel"], load_pmc(name, w["n"]))
             sec[name] = {"workload": w["config"], "value": round(s["value"], 1), "unit": "evals/s",
-                         "kernel": s["kernel"], "kernel_ms": round(s["kern_ms"], 4), "achieved_GBps": round(a, 1),
-                         "frac_of_hbm_peak": round(a / HBM_PEAK_GBS, 4),
-                         "mean_pieces": round(float(s["pieces"].mean()), 3)}
+                         "kernel": s["kernel"], "kernel_ms": round(s["kern_ms"], 4), "ft_rows": s["rows"],
+                         "achieved_GBps": rf["achieved"], "peak_GBps": rf["peak"], "frac": rf["frac"],
+                         "traffic": rf["traffic"], "mean_pieces": round(float(s["pieces"].mean()), 3)}
+            if "oracle_check" in s:
+                sec[name]["oracle_check"] = s["oracle_check"]
+                sec[name]["rank_check_failures"] = c.comm.gather_i64(s["oracle_check"]["mismatches"])
         line["secondary"] = sec
 
     if c.rank == 0:

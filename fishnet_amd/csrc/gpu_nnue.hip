@@ -208,7 +208,30 @@ struct Dev {
   int chain_k = 1;          // block length of the current expansion (1: no chaining)
   void *scan_tmp = nullptr;
   size_t scan_bytes = 0;
+  // Cross-stream ordering of the library-owned scratch above: every launch sequence
+  // waits for the previous one when it runs on another stream (gn_*_device take a
+  // caller stream and return while their kernels are still queued).
+  hipEvent_t done = nullptr;
+  hipStream_t done_on = nullptr;
   std::mutex mu;
+};
+
+// Called under d.mu before a launch sequence on stream s / after it.
+static hipError_t seq_begin(Dev &d, hipStream_t s) {
+  if (d.done_on && d.done_on != s) return hipStreamWaitEvent(s, d.done, 0);
+  return hipSuccess;
+}
+static hipError_t seq_end(Dev &d, hipStream_t s) {
+  hipError_t e = hipEventRecord(d.done, s);
+  if (e == hipSuccess) d.done_on = s;
+  return e;
+}
+struct SeqGuard { // seq_begin now, seq_end when the scope ends (d.mu held throughout)
+  Dev &d;
+  hipStream_t s;
+  hipError_t e;
+  SeqGuard(Dev &d_, hipStream_t s_) : d(d_), s(s_) { e = seq_begin(d, s); }
+  ~SeqGuard() { (void)seq_end(d, s); }
 };
 
 struct gn_ctx {
@@ -240,6 +263,13 @@ static gn_eval_params default_params() {
   P.value_clamp = 31506;
   const int32_t pv[5] = {208, 781, 825, 1276, 2538};
   memcpy(P.piece_value, pv, sizeof(pv));
+  const double wa[4] = {-37.45051876, 121.19101539, -132.78783573, 420.70576692};
+  memcpy(P.wdl_a, wa, sizeof(wa));
+  P.wdl_material_min = 17;
+  P.wdl_material_max = 78;
+  P.wdl_material_anchor = 58;
+  const int32_t ww[5] = {1, 3, 3, 5, 9};
+  memcpy(P.wdl_piece_weight, ww, sizeof(ww));
   return P;
 }
 
@@ -294,6 +324,8 @@ static void destroy(gn_ctx *ctx) {
     if (d.scan_tmp) (void)hipFree(d.scan_tmp);
     if (d.sort_tmp) (void)hipFree(d.sort_tmp);
     d.kkeys.release(), d.kkeys2.release(), d.kidx.release(), d.kperm.release();
+    d.nslot.release(), d.tickets.release(), d.ksnap.release();
+    if (d.done) (void)hipEventDestroy(d.done);
     if (d.stream) (void)hipStreamDestroy(d.stream);
   }
   delete ctx;
@@ -332,6 +364,7 @@ static int create(const uint8_t *big, size_t big_len, const uint8_t *small, size
     d.id = id;
     HIP_TRY(hipSetDevice(id));
     HIP_TRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreateWithFlags(&d.done, hipEventDisableTiming));
     HIP_TRY(hipMalloc(&d.tables, sizeof(Tables)));
     HIP_TRY(hipMemcpy(d.tables, &host_tables(), sizeof(Tables), hipMemcpyHostToDevice));
     for (int w = 0; w < 2; ++w)
@@ -365,7 +398,7 @@ struct KernelTimes {
 // Launch sequence of one evaluation.  ev (optional) = 5 events recorded between
 // the stages [classify(+)] [small net (+reeval)] [big net] [finalize].
 static int evaluate_on(gn_ctx *ctx, Dev &d, const gn_board *b, size_t n, int mode, gn_eval *out, hipStream_t s,
-                       hipEvent_t *ev) {
+                       hipEvent_t *ev, unsigned long long *rows_out = nullptr) {
   if (mode < GN_MODE_FULL || mode > GN_MODE_SMALL) return fail(GN_E_INVALID, "bad mode %d", mode);
   if ((mode != GN_MODE_SMALL && !d.has[BIG]) || (mode != GN_MODE_BIG && !d.has[SMALL]))
     return fail(GN_E_NONET, "mode %d needs a network that is not loaded", mode);
@@ -394,11 +427,13 @@ static int evaluate_on(gn_ctx *ctx, Dev &d, const gn_board *b, size_t n, int mod
   const int swz = (ctx->swizzle >> 1) & 1;
   HIP_TRY(mark(1));
   if (mode != GN_MODE_BIG)
-    HIP_TRY(launch_eval_net(d.net[SMALL], b, mode == GN_MODE_FULL ? d.nsm.p : nullptr, n, d.osm.p, perm, swz, s));
+    HIP_TRY(launch_eval_net(d.net[SMALL], b, mode == GN_MODE_FULL ? d.nsm.p : nullptr, n, d.osm.p, perm, swz, s,
+                            mode == GN_MODE_SMALL ? rows_out : nullptr));
   if (mode == GN_MODE_FULL) HIP_TRY(launch_reeval(d.osm.p, d.nsm.p, n, P, d.nbg.p, s));
   HIP_TRY(mark(2));
   if (mode != GN_MODE_SMALL)
-    HIP_TRY(launch_eval_net(d.net[BIG], b, mode == GN_MODE_FULL ? d.nbg.p : nullptr, n, d.obg.p, perm, swz, s));
+    HIP_TRY(launch_eval_net(d.net[BIG], b, mode == GN_MODE_FULL ? d.nbg.p : nullptr, n, d.obg.p, perm, swz, s,
+                            rows_out));
   HIP_TRY(mark(3));
   HIP_TRY(launch_finalize(b, n, mode, d.osm.p, d.obg.p, d.nsm.p, d.nbg.p, P, d.tables, out, s));
   HIP_TRY(mark(4));
@@ -449,7 +484,7 @@ static int generate_children(Dev &d, const gn_board *parents, size_t n, gn_board
   d.chain_k = want_deltas ? chain_k : 1;
   if (d.chain_k > 1) {
     HIP_TRY(d.nslot.ensure(n));
-    HIP_TRY(d.tickets.ensure(CARRY_SLOTS));
+    HIP_TRY(d.tickets.ensure(CARRY_SLOTS + 1));
     HIP_TRY(d.ksnap.ensure((size_t)CARRY_SLOTS * 128 * 8));
   }
   HIP_TRY(d.counts.ensure(n + 1));
@@ -463,12 +498,12 @@ static int generate_children(Dev &d, const gn_board *parents, size_t n, gn_board
   HIP_TRY(hipStreamSynchronize(s));
   *total = (size_t)t;
   if (ev) HIP_TRY(hipEventRecord(ev[1], s));
+  if ((children_or_null || moves) && t > cap) // caller-owned child buffers hold cap entries
+    return fail(GN_E_CAPACITY, "%zu children exceed capacity %zu", (size_t)t, cap);
   gn_board *children = children_or_null;
   if (!children) {
     HIP_TRY(d.frontier[1].ensure(std::max<size_t>(t, 1)));
     children = d.frontier[1].p;
-  } else if (t > cap) {
-    return fail(GN_E_CAPACITY, "%zu children exceed capacity %zu", (size_t)t, cap);
   }
   if (want_deltas) HIP_TRY(d.deltas.ensure(std::max<size_t>(t, 1)));
   if (t) HIP_TRY(launch_write_children(parents, n, d.tables, d.offsets.p, children, moves,
@@ -546,45 +581,77 @@ static int expand_evaluate(gn_ctx *ctx, Dev &d, const gn_board *parents, size_t 
   return GN_OK;
 }
 
+// ---------------------------------------------------------- sharding -----
+// The one partitioner of the library and of bench.py / fishnet_amd/dist.py (through
+// gn_partition): contiguous item ranges, cut so that shard k starts at the first item
+// whose weight prefix reaches k/n_shards of the total (weights NULL: all 1, i.e. equal
+// ranges).  Items are games (weight = positions) or parents (weight 1), so a game is
+// never split and each device keeps a game's consecutive parents for the chained walk
+// ("contiguous ranges of parents, game-aligned, per GPU"; the
+// reference's analog is the worker fan-out, /root/reference/src/main.rs:151-161).
+static void partition(const uint32_t *weights, size_t n, int ns, size_t *bounds) {
+  uint64_t total = 0;
+  for (size_t i = 0; i < n; ++i) total += weights ? weights[i] : 1u;
+  bounds[0] = 0;
+  size_t i = 0;
+  uint64_t acc = 0;
+  for (int k = 1; k < ns; ++k) {
+    const uint64_t target = (total * (uint64_t)k + (uint64_t)ns - 1) / (uint64_t)ns; // ceil(k * total / ns)
+    while (i < n && acc < target) acc += weights ? weights[i++] : (++i, 1u);
+    bounds[k] = i;
+  }
+  bounds[ns] = n;
+}
+
+// Runs f(k) for every device k on its own host thread (one device: inline) with that
+// device's lock held; returns the first failing code with its message.
+template <class F>
+static int for_each_device(gn_ctx *ctx, F &&f) {
+  const size_t nd = ctx->devs.size();
+  std::vector<int> rcs(nd, GN_OK);
+  std::vector<std::string> errs(nd);
+  auto work = [&](size_t k) {
+    Dev &d = *ctx->devs[k];
+    std::lock_guard<std::mutex> lk(d.mu);
+    rcs[k] = f(k, d);
+    if (rcs[k]) errs[k] = g_err;
+  };
+  if (nd == 1) work(0);
+  else {
+    std::vector<std::thread> th;
+    for (size_t k = 0; k < nd; ++k) th.emplace_back(work, k);
+    for (auto &t : th) t.join();
+  }
+  for (size_t k = 0; k < nd; ++k)
+    if (rcs[k]) {
+      g_err = errs[k];
+      return rcs[k];
+    }
+  return GN_OK;
+}
+
 // Host boards -> device(s) -> gn_eval: contiguous shards, one host thread per device.
 static int evaluate_boards_host(gn_ctx *ctx, const gn_board *boards, size_t n, int mode, gn_eval *out) {
   if (!n) return GN_OK;
   try {
-    const size_t nd = ctx->devs.size(), per = (n + nd - 1) / nd;
-    std::vector<int> rcs(nd, GN_OK);
-    std::vector<std::string> errs(nd);
-    auto work = [&](size_t k) {
-      const size_t lo = k * per, hi = std::min(n, lo + per);
-      if (lo >= hi) return;
-      Dev &d = *ctx->devs[k];
-      std::lock_guard<std::mutex> lk(d.mu);
-      auto run = [&]() -> int {
-        HIP_TRY(hipSetDevice(d.id));
-        HIP_TRY(d.io_boards.ensure(hi - lo));
-        HIP_TRY(d.io_out.ensure(hi - lo));
-        HIP_TRY(hipMemcpyAsync(d.io_boards.p, boards + lo, (hi - lo) * sizeof(gn_board), hipMemcpyHostToDevice,
-                               d.stream));
-        int r = evaluate_on(ctx, d, d.io_boards.p, hi - lo, mode, d.io_out.p, d.stream, nullptr);
-        if (r) return r;
-        HIP_TRY(hipMemcpyAsync(out + lo, d.io_out.p, (hi - lo) * sizeof(gn_eval), hipMemcpyDeviceToHost, d.stream));
-        HIP_TRY(hipStreamSynchronize(d.stream));
-        return GN_OK;
-      };
-      rcs[k] = run();
-      if (rcs[k]) errs[k] = g_err;
-    };
-    if (nd == 1) work(0);
-    else {
-      std::vector<std::thread> th;
-      for (size_t k = 0; k < nd; ++k) th.emplace_back(work, k);
-      for (auto &t : th) t.join();
-    }
-    for (size_t k = 0; k < nd; ++k)
-      if (rcs[k]) {
-        g_err = errs[k];
-        return rcs[k];
-      }
-    return GN_OK;
+    std::vector<size_t> b(ctx->devs.size() + 1);
+    partition(nullptr, n, (int)ctx->devs.size(), b.data());
+    return for_each_device(ctx, [&](size_t k, Dev &d) -> int {
+      const size_t lo = b[k], hi = b[k + 1];
+      if (lo >= hi) return GN_OK;
+      HIP_TRY(hipSetDevice(d.id));
+      SeqGuard sg(d, d.stream);
+      HIP_TRY(sg.e);
+      HIP_TRY(d.io_boards.ensure(hi - lo));
+      HIP_TRY(d.io_out.ensure(hi - lo));
+      HIP_TRY(hipMemcpyAsync(d.io_boards.p, boards + lo, (hi - lo) * sizeof(gn_board), hipMemcpyHostToDevice,
+                             d.stream));
+      int r = evaluate_on(ctx, d, d.io_boards.p, hi - lo, mode, d.io_out.p, d.stream, nullptr);
+      if (r) return r;
+      HIP_TRY(hipMemcpyAsync(out + lo, d.io_out.p, (hi - lo) * sizeof(gn_eval), hipMemcpyDeviceToHost, d.stream));
+      HIP_TRY(hipStreamSynchronize(d.stream));
+      return GN_OK;
+    });
   } catch (const std::bad_alloc &) {
     return fail(GN_E_NOMEM, "host allocation failed");
   } catch (...) {
@@ -592,52 +659,103 @@ static int evaluate_boards_host(gn_ctx *ctx, const gn_board *boards, size_t n, i
   }
 }
 
-// Host parent boards -> every legal child (device 0) -> parent/child gn_eval.
+// Host parent boards -> every legal child -> parent/child gn_eval, sharded over every
+// device of the context: parents [bounds[k], bounds[k + 1]) on device k (bounds from
+// partition(); NULL = equal ranges).  Two passes with all device locks held: child
+// counts per shard (so every shard knows where its children go in the caller's
+// arrays), then generation + evaluation + download into those places.
 static int expand_boards_host(gn_ctx *ctx, const gn_board *boards, size_t n, int mode, gn_eval *parent_out,
-                              uint32_t *child_offsets, uint16_t *child_moves, gn_eval *child_out, size_t cap) {
-  Dev *d = slot(ctx, 0);
-  if (!d) return fail(GN_E_INVALID, "bad context");
+                              uint32_t *child_offsets, uint16_t *child_moves, gn_eval *child_out, size_t cap,
+                              const size_t *bounds_in = nullptr) {
+  if (!slot(ctx, 0)) return fail(GN_E_INVALID, "bad context");
   if (!n) {
     child_offsets[0] = 0;
     return GN_OK;
   }
   try {
-    int rc = GN_OK;
-    std::lock_guard<std::mutex> lk(d->mu);
-    HIP_TRY(hipSetDevice(d->id));
-    hipStream_t s = d->stream;
-    HIP_TRY(d->io_boards.ensure(n));
-    HIP_TRY(hipMemcpyAsync(d->io_boards.p, boards, n * sizeof(gn_board), hipMemcpyHostToDevice, s));
-    // size the move buffer from the counts first (generate_children syncs for the total)
-    HIP_TRY(d->counts.ensure(n + 1));
-    HIP_TRY(d->offsets.ensure(n + 1));
-    HIP_TRY(hipMemsetAsync(d->counts.p + n, 0, sizeof(uint64_t), s));
-    HIP_TRY(launch_count_children(d->io_boards.p, n, d->tables, d->counts.p, s));
-    HIP_TRY(exclusive_scan_u64(d->counts.p, d->offsets.p, n + 1, d->scan_tmp, d->scan_bytes, s));
-    std::vector<uint64_t> off(n + 1);
-    HIP_TRY(hipMemcpyAsync(off.data(), d->offsets.p, (n + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
-    const size_t total = (size_t)off[n];
+    const size_t nd = ctx->devs.size();
+    std::vector<size_t> b(nd + 1);
+    if (bounds_in) std::copy(bounds_in, bounds_in + nd + 1, b.begin());
+    else partition(nullptr, n, (int)nd, b.data());
+    // every device lock for the whole call (in device order), so the two passes see the
+    // same device state
+    std::vector<std::unique_lock<std::mutex>> locks;
+    for (auto &dp : ctx->devs) locks.emplace_back(dp->mu);
+    std::vector<std::vector<uint64_t>> off(nd);
+    std::vector<int> rcs(nd, GN_OK);
+    std::vector<std::string> errs(nd);
+    auto parallel = [&](auto &&f) {
+      auto work = [&](size_t k) {
+        rcs[k] = b[k] < b[k + 1] ? f(k, *ctx->devs[k], b[k], b[k + 1] - b[k]) : GN_OK;
+        if (rcs[k]) errs[k] = g_err;
+      };
+      if (nd == 1) work(0);
+      else {
+        std::vector<std::thread> th;
+        for (size_t k = 0; k < nd; ++k) th.emplace_back(work, k);
+        for (auto &t : th) t.join();
+      }
+      for (size_t k = 0; k < nd; ++k)
+        if (rcs[k]) {
+          g_err = errs[k];
+          return rcs[k];
+        }
+      return (int)GN_OK;
+    };
+    // pass 1: upload + child counts + scan + offsets to the host
+    int rc = parallel([&](size_t k, Dev &d, size_t lo, size_t m) -> int {
+      HIP_TRY(hipSetDevice(d.id));
+      SeqGuard sg(d, d.stream);
+      HIP_TRY(sg.e);
+      hipStream_t s = d.stream;
+      HIP_TRY(d.io_boards.ensure(m));
+      HIP_TRY(hipMemcpyAsync(d.io_boards.p, boards + lo, m * sizeof(gn_board), hipMemcpyHostToDevice, s));
+      HIP_TRY(d.counts.ensure(m + 1));
+      HIP_TRY(d.offsets.ensure(m + 1));
+      HIP_TRY(hipMemsetAsync(d.counts.p + m, 0, sizeof(uint64_t), s));
+      HIP_TRY(launch_count_children(d.io_boards.p, m, d.tables, d.counts.p, s));
+      HIP_TRY(exclusive_scan_u64(d.counts.p, d.offsets.p, m + 1, d.scan_tmp, d.scan_bytes, s));
+      off[k].resize(m + 1);
+      HIP_TRY(hipMemcpyAsync(off[k].data(), d.offsets.p, (m + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+      HIP_TRY(hipStreamSynchronize(s));
+      return GN_OK;
+    });
+    if (rc) return rc;
+    std::vector<uint64_t> base(nd + 1, 0);
+    for (size_t k = 0; k < nd; ++k) base[k + 1] = base[k] + (b[k] < b[k + 1] ? off[k].back() : 0);
+    const uint64_t total = base[nd];
     if (total > 0xFFFFFFFFull) return fail(GN_E_CAPACITY, "children exceed 32-bit offsets");
-    for (size_t i = 0; i <= n; ++i) child_offsets[i] = (uint32_t)off[i];
-    if (total > cap) return fail(GN_E_CAPACITY, "%zu children exceed capacity %zu", total, cap);
+    for (size_t k = 0; k < nd; ++k)
+      for (size_t i = b[k]; i < b[k + 1]; ++i) child_offsets[i] = (uint32_t)(base[k] + off[k][i - b[k]]);
+    child_offsets[n] = (uint32_t)total;
+    if (total > cap) return fail(GN_E_CAPACITY, "%zu children exceed capacity %zu", (size_t)total, cap);
     if (total && (!child_moves || !child_out)) return fail(GN_E_INVALID, "NULL child buffer");
-    HIP_TRY(d->moves.ensure(std::max<size_t>(total, 1)));
-    size_t t = 0;
-    rc = generate_children(*d, d->io_boards.p, n, nullptr, 0, d->moves.p, ctx->incremental, &t, s, nullptr, nullptr,
-                           chain_len(ctx, *d, n));
-    if (rc) return rc;
-    HIP_TRY(d->io_out.ensure(n));
-    HIP_TRY(d->io_out2.ensure(std::max<size_t>(t, 1)));
-    rc = expand_evaluate(ctx, *d, d->io_boards.p, n, d->frontier[1].p, t, mode, d->io_out.p, d->io_out2.p, s, nullptr);
-    if (rc) return rc;
-    if (t) {
-      HIP_TRY(hipMemcpyAsync(child_out, d->io_out2.p, t * sizeof(gn_eval), hipMemcpyDeviceToHost, s));
-      HIP_TRY(hipMemcpyAsync(child_moves, d->moves.p, t * sizeof(uint16_t), hipMemcpyDeviceToHost, s));
-    }
-    if (parent_out) HIP_TRY(hipMemcpyAsync(parent_out, d->io_out.p, n * sizeof(gn_eval), hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
-    return GN_OK;
+    // pass 2: children + deltas, incremental evaluation, results into the caller's arrays
+    return parallel([&](size_t k, Dev &d, size_t lo, size_t m) -> int {
+      HIP_TRY(hipSetDevice(d.id));
+      SeqGuard sg(d, d.stream);
+      HIP_TRY(sg.e);
+      hipStream_t s = d.stream;
+      const size_t tk = (size_t)off[k].back();
+      HIP_TRY(d.moves.ensure(std::max<size_t>(tk, 1)));
+      size_t t = 0;
+      int r = generate_children(d, d.io_boards.p, m, nullptr, d.moves.cap, d.moves.p, ctx->incremental, &t, s, nullptr,
+                                nullptr, chain_len(ctx, d, m));
+      if (r) return r;
+      if (t != tk) return fail(GN_E_HIP, "child count changed between passes (%zu != %zu)", t, tk);
+      HIP_TRY(d.io_out.ensure(m));
+      HIP_TRY(d.io_out2.ensure(std::max<size_t>(t, 1)));
+      r = expand_evaluate(ctx, d, d.io_boards.p, m, d.frontier[1].p, t, mode, d.io_out.p, d.io_out2.p, s, nullptr);
+      if (r) return r;
+      if (t) {
+        HIP_TRY(hipMemcpyAsync(child_out + base[k], d.io_out2.p, t * sizeof(gn_eval), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(child_moves + base[k], d.moves.p, t * sizeof(uint16_t), hipMemcpyDeviceToHost, s));
+      }
+      if (parent_out)
+        HIP_TRY(hipMemcpyAsync(parent_out + lo, d.io_out.p, m * sizeof(gn_eval), hipMemcpyDeviceToHost, s));
+      HIP_TRY(hipStreamSynchronize(s));
+      return GN_OK;
+    });
   } catch (const std::bad_alloc &) {
     return fail(GN_E_NOMEM, "host allocation failed");
   } catch (...) {
@@ -796,15 +914,16 @@ int gn_evaluate_games(gn_ctx *ctx, const gn_game *games, size_t n_games, int mod
     if (total && !position_out) return fail(GN_E_INVALID, "position_out is NULL");
     // positions to evaluate: every non-skipped position of every replayed game
     std::vector<gn_board> ev;
-    std::vector<uint32_t> where;
+    std::vector<uint32_t> where, per_game(n_games, 0);
     for (size_t i = 0; i < n_games; ++i)
       for (size_t k = 0; k < rep[i].boards.size(); ++k) {
         const size_t at = position_offsets[i] + k;
         if (rep[i].skip[k]) {
-          position_out[at] = gn_eval{0, 0, 0, GN_FLAG_SKIPPED};
+          position_out[at] = gn_eval{0, 0, 0, 0, (uint16_t)GN_FLAG_SKIPPED};
         } else {
           ev.push_back(rep[i].boards[k]);
           where.push_back((uint32_t)at);
+          ++per_game[i];
         }
       }
     std::vector<gn_eval> res(ev.size());
@@ -814,8 +933,17 @@ int gn_evaluate_games(gn_ctx *ctx, const gn_game *games, size_t n_games, int mod
       rc = evaluate_boards_host(ctx, ev.data(), ev.size(), mode, res.data());
     } else {
       coff.assign(ev.size() + 1, 0);
+      // game-aligned device shards, weighted by evaluated positions
+      const size_t nd = ctx->devs.size();
+      std::vector<size_t> gb(nd + 1), eb(nd + 1);
+      partition(per_game.data(), n_games, (int)nd, gb.data());
+      size_t acc = 0, g = 0;
+      for (size_t k = 0; k <= nd; ++k) {
+        for (; g < gb[k]; ++g) acc += per_game[g];
+        eb[k] = acc;
+      }
       rc = expand_boards_host(ctx, ev.data(), ev.size(), mode, res.data(), coff.data(), child_moves, child_out,
-                              child_cap);
+                              child_cap, eb.data());
       if (rc == GN_OK || rc == GN_E_CAPACITY) { // child offsets over all positions (skipped: no children)
         size_t e = 0;
         for (size_t at = 0; at < total; ++at) {
@@ -834,6 +962,16 @@ int gn_evaluate_games(gn_ctx *ctx, const gn_game *games, size_t n_games, int mod
   } catch (...) {
     return fail(GN_E_INVALID, "unexpected exception");
   }
+}
+
+int gn_partition(const uint32_t *weights, size_t n_items, int n_shards, size_t *bounds) {
+  if (n_shards <= 0 || !bounds) return fail(GN_E_INVALID, "bad shard count / NULL bounds");
+  try {
+    partition(weights, n_items, n_shards, bounds);
+  } catch (...) {
+    return fail(GN_E_INVALID, "unexpected exception");
+  }
+  return GN_OK;
 }
 
 int gn_abi_version(void) { return GN_ABI_VERSION; }
@@ -904,8 +1042,10 @@ int gn_get_eval_params(const gn_ctx *ctx, gn_eval_params *out) {
 
 int gn_set_eval_params(gn_ctx *ctx, const gn_eval_params *p) {
   if (!ctx || !p) return fail(GN_E_INVALID, "NULL argument");
-  if (p->material_base == 0 || p->rule50_div == 0 || p->complexity_div_small == 0 || p->complexity_div_big == 0)
+  if (p->material_base == 0 || p->rule50_div == 0 || p->complexity_div_small == 0 || p->complexity_div_big == 0 ||
+      p->wdl_material_anchor == 0)
     return fail(GN_E_INVALID, "zero divisor in eval params");
+  if (p->wdl_material_min > p->wdl_material_max) return fail(GN_E_INVALID, "wdl material range is empty");
   ctx->P = *p;
   return GN_OK;
 }
@@ -945,6 +1085,23 @@ int gn_board_to_fen(const gn_board *board, char *buf, size_t buflen) {
   return GN_OK;
 }
 
+int gn_boards_to_fens(const gn_board *boards, size_t n, char *buf, size_t stride) {
+  if (n && (!boards || !buf)) return fail(GN_E_INVALID, "NULL argument");
+  if (stride < 100) return fail(GN_E_INVALID, "stride < 100");
+  try {
+    parallel_for(n, 4096, [&](size_t lo, size_t hi) {
+      for (size_t i = lo; i < hi; ++i) {
+        Board B;
+        char *o = buf + i * stride;
+        if (!unpack(boards[i], B) || board_to_fen(B, o, stride) < 0) o[0] = '\0';
+      }
+    });
+  } catch (...) {
+    return fail(GN_E_NOMEM, "thread start failed");
+  }
+  return GN_OK;
+}
+
 int gn_random_positions(uint64_t seed, size_t first_index, size_t n, int max_plies, gn_board *out) {
   if (n && !out) return fail(GN_E_INVALID, "NULL argument");
   if (max_plies < 0) return fail(GN_E_INVALID, "max_plies < 0");
@@ -965,16 +1122,21 @@ int gn_evaluate_device(gn_ctx *ctx, int device_slot, const gn_board *d_boards, s
   if (n && (!d_boards || !d_out)) return fail(GN_E_INVALID, "NULL buffer");
   std::lock_guard<std::mutex> lk(d->mu);
   HIP_TRY(hipSetDevice(d->id));
-  return evaluate_on(ctx, *d, d_boards, n, mode, d_out, stream ? (hipStream_t)stream : d->stream, nullptr);
+  hipStream_t s = stream ? (hipStream_t)stream : d->stream;
+  SeqGuard sg(*d, s);
+  HIP_TRY(sg.e);
+  return evaluate_on(ctx, *d, d_boards, n, mode, d_out, s, nullptr);
 }
 
 int gn_time_evaluate_device(gn_ctx *ctx, int device_slot, const gn_board *d_boards, size_t n, int mode,
-                            gn_eval *d_out, int iters, float *ms_total, float *per_kernel_ms) {
+                            gn_eval *d_out, int iters, float *ms_total, float *per_kernel_ms, uint64_t *ft_rows) {
   Dev *d = slot(ctx, device_slot);
   if (!d) return fail(GN_E_INVALID, "bad context or device slot");
   if (iters <= 0 || !ms_total) return fail(GN_E_INVALID, "bad iters / ms_total");
   std::lock_guard<std::mutex> lk(d->mu);
   HIP_TRY(hipSetDevice(d->id));
+  SeqGuard sg(*d, d->stream);
+  HIP_TRY(sg.e);
   std::vector<hipEvent_t> ev((size_t)iters * 5 + 2, nullptr);
   auto cleanup = [&] {
     for (auto &e : ev)
@@ -986,9 +1148,14 @@ int gn_time_evaluate_device(gn_ctx *ctx, int device_slot, const gn_board *d_boar
       return fail(GN_E_HIP, "hipEventCreate failed");
     }
   int rc = GN_OK;
+  if (ft_rows) {
+    HIP_TRY(d->sum.ensure(2));
+    HIP_TRY(hipMemsetAsync(d->sum.p, 0, sizeof(unsigned long long), d->stream));
+  }
   hipError_t he = hipEventRecord(ev[0], d->stream);
   for (int it = 0; it < iters && rc == GN_OK && he == hipSuccess; ++it)
-    rc = evaluate_on(ctx, *d, d_boards, n, mode, d_out, d->stream, per_kernel_ms ? &ev[2 + 5 * it] : nullptr);
+    rc = evaluate_on(ctx, *d, d_boards, n, mode, d_out, d->stream, per_kernel_ms ? &ev[2 + 5 * it] : nullptr,
+                     ft_rows && it == 0 ? d->sum.p : nullptr);
   if (rc == GN_OK && he == hipSuccess) he = hipEventRecord(ev[1], d->stream);
   if (rc == GN_OK && he == hipSuccess) he = hipEventSynchronize(ev[1]);
   if (rc == GN_OK && he == hipSuccess) he = hipEventElapsedTime(ms_total, ev[0], ev[1]);
@@ -1004,6 +1171,11 @@ int gn_time_evaluate_device(gn_ctx *ctx, int device_slot, const gn_board *d_boar
   }
   cleanup();
   if (rc) return rc;
+  if (ft_rows && he == hipSuccess) {
+    unsigned long long r = 0;
+    he = hipMemcpy(&r, d->sum.p, sizeof(r), hipMemcpyDeviceToHost);
+    *ft_rows = r;
+  }
   if (he != hipSuccess) return fail(GN_E_HIP, "timing failed: %s", hipGetErrorString(he));
   return GN_OK;
 }
@@ -1016,8 +1188,9 @@ int gn_random_positions_device(gn_ctx *ctx, int device_slot, uint64_t seed, size
   if (max_plies < 0) return fail(GN_E_INVALID, "max_plies < 0");
   std::lock_guard<std::mutex> lk(d->mu);
   HIP_TRY(hipSetDevice(d->id));
-  HIP_TRY(launch_random_positions(seed, first_index, n, max_plies, d->tables, d_out,
-                                  stream ? (hipStream_t)stream : d->stream));
+  SeqGuard sg(*d, stream ? (hipStream_t)stream : d->stream);
+  HIP_TRY(sg.e);
+  HIP_TRY(launch_random_positions(seed, first_index, n, max_plies, d->tables, d_out, sg.s));
   return GN_OK;
 }
 
@@ -1040,7 +1213,10 @@ int gn_device_free(gn_ctx *ctx, int device_slot, void *ptr) {
 int gn_memcpy_h2d(gn_ctx *ctx, int device_slot, void *dst, const void *src, size_t bytes) {
   Dev *d = slot(ctx, device_slot);
   if (!d) return fail(GN_E_INVALID, "bad argument");
+  std::lock_guard<std::mutex> lk(d->mu);
   HIP_TRY(hipSetDevice(d->id));
+  SeqGuard sg(*d, d->stream);
+  HIP_TRY(sg.e);
   HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, d->stream));
   HIP_TRY(hipStreamSynchronize(d->stream));
   return GN_OK;
@@ -1049,7 +1225,10 @@ int gn_memcpy_h2d(gn_ctx *ctx, int device_slot, void *dst, const void *src, size
 int gn_memcpy_d2h(gn_ctx *ctx, int device_slot, void *dst, const void *src, size_t bytes) {
   Dev *d = slot(ctx, device_slot);
   if (!d) return fail(GN_E_INVALID, "bad argument");
+  std::lock_guard<std::mutex> lk(d->mu);
   HIP_TRY(hipSetDevice(d->id));
+  SeqGuard sg(*d, d->stream);
+  HIP_TRY(sg.e);
   HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, d->stream));
   HIP_TRY(hipStreamSynchronize(d->stream));
   return GN_OK;
@@ -1058,7 +1237,9 @@ int gn_memcpy_d2h(gn_ctx *ctx, int device_slot, void *dst, const void *src, size
 int gn_synchronize(gn_ctx *ctx, int device_slot) {
   Dev *d = slot(ctx, device_slot);
   if (!d) return fail(GN_E_INVALID, "bad argument");
+  std::lock_guard<std::mutex> lk(d->mu);
   HIP_TRY(hipSetDevice(d->id));
+  if (d->done_on) HIP_TRY(hipEventSynchronize(d->done)); // the last launch sequence, on whatever stream
   HIP_TRY(hipStreamSynchronize(d->stream));
   return GN_OK;
 }
@@ -1092,6 +1273,8 @@ int gn_expand_device(gn_ctx *ctx, int device_slot, const gn_board *d_parents, si
   std::lock_guard<std::mutex> lk(d->mu);
   HIP_TRY(hipSetDevice(d->id));
   hipStream_t s = stream ? (hipStream_t)stream : d->stream;
+  SeqGuard sg(*d, s);
+  HIP_TRY(sg.e);
   *total = 0;
   if (!n) return GN_OK;
   if (!d_children || !d_moves || !d_child_out) return fail(GN_E_INVALID, "NULL child buffer");
@@ -1112,12 +1295,15 @@ int gn_expand_device(gn_ctx *ctx, int device_slot, const gn_board *d_parents, si
 }
 
 int gn_time_expand_device(gn_ctx *ctx, int device_slot, const gn_board *d_parents, size_t n, int mode, int iters,
-                          float *ms_total, size_t *total, float *stage_ms, uint64_t *ft_rows) {
+                          float *ms_total, size_t *total, float *stage_ms, uint64_t *ft_rows, gn_eval *d_parent_out,
+                          uint32_t *d_offsets, uint16_t *d_moves, gn_eval *d_child_out, size_t cap) {
   Dev *d = slot(ctx, device_slot);
   if (!d || !ms_total || !total || iters <= 0) return fail(GN_E_INVALID, "bad argument");
   std::lock_guard<std::mutex> lk(d->mu);
   HIP_TRY(hipSetDevice(d->id));
   hipStream_t s = d->stream;
+  SeqGuard sg(*d, s);
+  HIP_TRY(sg.e);
   const int NE = 8; // start, [count+scan], [total read], [write], [classify], [small], [big], [finalize]
   std::vector<hipEvent_t> ev((size_t)iters * NE + 2, nullptr);
   auto cleanup = [&] {
@@ -1138,14 +1324,19 @@ int gn_time_expand_device(gn_ctx *ctx, int device_slot, const gn_board *d_parent
     hipEvent_t *e = &ev[2 + (size_t)NE * it];
     he = hipEventRecord(e[0], s);
     if (he != hipSuccess) break;
-    rc = generate_children(*d, d_parents, n, nullptr, 0, nullptr, ctx->incremental, &t, s, e + 1,
+    rc = generate_children(*d, d_parents, n, nullptr, cap, d_moves, ctx->incremental, &t, s, e + 1,
                            it == 0 ? d->sum.p : nullptr, chain_len(ctx, *d, n));
     if (rc) break;
+    if (d_child_out && t > cap) {
+      rc = fail(GN_E_CAPACITY, "%zu children exceed capacity %zu", t, cap);
+      break;
+    }
     HIP_TRY(d->io_out.ensure(n));
     HIP_TRY(d->io_out2.ensure(std::max<size_t>(t, 1)));
-    rc = expand_evaluate(ctx, *d, d_parents, n, d->frontier[1].p, t, mode, d->io_out.p, d->io_out2.p, s, e + 4,
-                         it == 0 ? d->sum.p + 1 : nullptr);
+    rc = expand_evaluate(ctx, *d, d_parents, n, d->frontier[1].p, t, mode, d_parent_out ? d_parent_out : d->io_out.p,
+                         d_child_out ? d_child_out : d->io_out2.p, s, e + 4, it == 0 ? d->sum.p + 1 : nullptr);
   }
+  if (rc == GN_OK && he == hipSuccess && d_offsets) he = launch_offsets_u32(d->offsets.p, n + 1, d_offsets, s);
   if (rc == GN_OK && he == hipSuccess) he = hipEventRecord(ev[1], s);
   if (rc == GN_OK && he == hipSuccess) he = hipEventSynchronize(ev[1]);
   if (rc == GN_OK && he == hipSuccess) he = hipEventElapsedTime(ms_total, ev[0], ev[1]);
@@ -1171,6 +1362,23 @@ int gn_time_expand_device(gn_ctx *ctx, int device_slot, const gn_board *d_parent
   return GN_OK;
 }
 
+int gn_checksum_device(gn_ctx *ctx, int device_slot, const void *d_ptr, size_t bytes, uint64_t *sum) {
+  Dev *d = slot(ctx, device_slot);
+  if (!d || !sum || (bytes && !d_ptr)) return fail(GN_E_INVALID, "bad argument");
+  std::lock_guard<std::mutex> lk(d->mu);
+  HIP_TRY(hipSetDevice(d->id));
+  SeqGuard sg(*d, d->stream);
+  HIP_TRY(sg.e);
+  HIP_TRY(d->sum.ensure(2));
+  HIP_TRY(hipMemsetAsync(d->sum.p, 0, sizeof(unsigned long long), d->stream));
+  HIP_TRY(launch_checksum(d_ptr, bytes, d->sum.p, d->stream));
+  unsigned long long r = 0;
+  HIP_TRY(hipMemcpyAsync(&r, d->sum.p, sizeof(r), hipMemcpyDeviceToHost, d->stream));
+  HIP_TRY(hipStreamSynchronize(d->stream));
+  *sum = r;
+  return GN_OK;
+}
+
 int gn_random_games_device(gn_ctx *ctx, int device_slot, uint64_t seed, size_t first_game, size_t n_games, int plies,
                            gn_board *d_out, void *stream) {
   Dev *d = slot(ctx, device_slot);
@@ -1179,8 +1387,9 @@ int gn_random_games_device(gn_ctx *ctx, int device_slot, uint64_t seed, size_t f
   if (plies < 0 || plies > 1000) return fail(GN_E_INVALID, "plies out of range");
   std::lock_guard<std::mutex> lk(d->mu);
   HIP_TRY(hipSetDevice(d->id));
-  HIP_TRY(launch_random_games(seed, first_game, n_games, plies, d->tables, d_out,
-                              stream ? (hipStream_t)stream : d->stream));
+  SeqGuard sg(*d, stream ? (hipStream_t)stream : d->stream);
+  HIP_TRY(sg.e);
+  HIP_TRY(launch_random_games(seed, first_game, n_games, plies, d->tables, d_out, sg.s));
   return GN_OK;
 }
 
@@ -1226,6 +1435,21 @@ int gn_get_option(const gn_ctx *ctx, int option, int64_t *value) {
   case GN_OPT_CHAIN:
     *value = ctx->chain;
     return GN_OK;
+  case GN_STAT_CHAIN_FALLBACKS: { // read-only: blocks of the last chained expansion per device, summed
+    int64_t sum = 0;
+    for (auto &dp : ctx->devs) {
+      Dev &d = *dp;
+      std::lock_guard<std::mutex> lk(d.mu);
+      if (!d.tickets.p) continue;
+      HIP_TRY(hipSetDevice(d.id));
+      if (d.done_on) HIP_TRY(hipEventSynchronize(d.done));
+      uint32_t f = 0;
+      HIP_TRY(hipMemcpy(&f, d.tickets.p + CARRY_SLOTS, sizeof(f), hipMemcpyDeviceToHost));
+      sum += f;
+    }
+    *value = sum;
+    return GN_OK;
+  }
   default:
     return fail(GN_E_INVALID, "unknown option %d", option);
   }
@@ -1263,6 +1487,8 @@ int gn_perft(gn_ctx *ctx, const char *fen, int depth, uint64_t *nodes) {
   std::lock_guard<std::mutex> lk(d->mu);
   HIP_TRY(hipSetDevice(d->id));
   hipStream_t s = d->stream;
+  SeqGuard sg(*d, s);
+  HIP_TRY(sg.e);
   gn_board root;
   pack(B, root);
   HIP_TRY(d->frontier[0].ensure(1));

@@ -12,11 +12,17 @@ namespace gn {
 // need[i] != 0 (need == nullptr: all); other entries of out are untouched.
 // perm (optional): slot q evaluates boards[perm[q]] and writes out[perm[q]].
 // swz: XCD-aware tile order (each XCD gets a contiguous range of tiles).
+// rows_out (optional): += FT rows the gather reads (common-row base counted once per tile).
 hipError_t launch_eval_net(const NetDevice &net, const gn_board *boards, const uint8_t *need, size_t n,
-                           int2 *out, const uint32_t *perm, int swz, hipStream_t s);
+                           int2 *out, const uint32_t *perm, int swz, hipStream_t s,
+                           unsigned long long *rows_out = nullptr);
+// *out += position-sensitive checksum of bytes at p (caller zeroes *out)
+hipError_t launch_checksum(const void *p, size_t bytes, unsigned long long *out, hipStream_t s);
 // permutation of [0, n) ordering positions by (white king, black king) square, then
-// (placement) by the pieces of the first two ranks (king_keys_kernel), which serve
-// the big net's common-row base; kings only (16-bit keys) otherwise
+// (placement) by 30 home-square bits, one per square of ranks 1, 2, 7, 8 without
+// e1 / e8, set when the start position's piece still stands there
+// (king_keys_kernel), which serve the big net's common-row base; kings only
+// (16-bit keys) otherwise
 hipError_t king_sort(const gn_board *boards, size_t n, uint64_t *keys, uint32_t *idx, uint64_t *keys_out,
                      uint32_t *perm, bool placement, void *&temp, size_t &temp_bytes, hipStream_t s);
 // Incremental evaluation of parents + all their children (children of parent

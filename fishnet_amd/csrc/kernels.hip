@@ -384,7 +384,8 @@ __device__ __forceinline__ void layer_stack_wave(const NetDevice &net, const uin
 template <int L1, int PAR>
 __global__ void __launch_bounds__(2 * (L1 / 16) * PAR) __attribute__((amdgpu_waves_per_eu(PAR == 1 ? 1 : 6)))
     eval_net_kernel(NetDevice net, const gn_board *__restrict__ boards, const uint8_t *__restrict__ need,
-                    size_t n, int2 *__restrict__ out, const uint32_t *__restrict__ perm, unsigned tiles, int swz) {
+                    size_t n, int2 *__restrict__ out, const uint32_t *__restrict__ perm, unsigned tiles, int swz,
+                    unsigned long long *__restrict__ rows_out) {
   constexpr int G = L1 / 16;
   constexpr int NT = 2 * G * PAR;
   constexpr int NW = NT / 64;
@@ -502,6 +503,13 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR) __attribute__((amdgpu_wav
     }
   }
   __syncthreads();
+  if (rows_out && tid == 0) { // FT rows this tile gathers: common rows once, then each position's own
+    unsigned long long r = 0;
+    int any = 0;
+    for (int sl = 0; sl < TILE; ++sl)
+      if (nfeat[sl]) r += (unsigned long long)(nfeat[sl] - ccnt), any = 1;
+    if (any) atomicAdd(rows_out, 2ull * (r + (unsigned long long)ccnt));
+  }
 
   // ---- phase 1: gather-accumulate + transform into the LDS tile (h: absolute perspective
   // for the big net, relative for the small net)
@@ -1123,19 +1131,33 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
    }
    const uint32_t pend = blk * K + K < np ? blk * K + K : np;
    const uint32_t cslot = v % CARRY_SLOTS;
+   // Slot ownership: tickets[cslot] counts the workgroups w = cslot (mod CARRY_SLOTS) that
+   // are done with the slot (used it or not); this one may use it once all v / CARRY_SLOTS
+   // earlier ones are.  The wait is bounded: on timeout the block runs without carry rows
+   // and king cache (identical results, more rows), still counts itself done at the end,
+   // and adds 1 to tickets[CARRY_SLOTS] (the fallback count).
+   bool own = false;
    if (K > 1) {
-     if (tid == 0)
-       while (__hip_atomic_load(tickets + cslot, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != v / CARRY_SLOTS)
+     __shared__ int sown;
+     if (tid == 0) {
+       int it = 0;
+       while (__hip_atomic_load(tickets + cslot, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < v / CARRY_SLOTS &&
+              ++it < 20000)
          __builtin_amdgcn_s_sleep(8);
+       sown = it < 20000;
+       if (!sown) atomicAdd(tickets + CARRY_SLOTS, 1u);
+     }
      __syncthreads();
+     own = sown;
      // King cache (per block: written and read by this workgroup only): one accumulator
      // row + one placement snapshot per (perspective, king square); empty at block start.
-     if (kc) {
+     if (kc && own) {
        for (int i = tid; i < 256; i += NT)
          *reinterpret_cast<uint4 *>(ksnap + (size_t)cslot * 1024 + 4 * i) = make_uint4(0, 0, 0, 0);
        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
      }
    }
+   const bool kcb = kc && own; // this block's king cache
    int carry_ok = 0; // the previous parent stored its next-parent accumulators
    for (uint32_t p = blk * K; p < pend; ++p) {
     GN_STAMP_INIT();
@@ -1167,7 +1189,7 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
     GN_STAMP(0);
     // slot of the child that is the next parent (-1: none)
     int nxq = -1;
-    if (K > 1 && p + 1 < pend) {
+    if (own && p + 1 < pend) {
       const int ns = next_slot[p];
       if (ns != 255 && ns < total - 1 && (!need_child || need_child[off + ns])) nxq = ns + 1;
     }
@@ -1236,7 +1258,7 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
         // no accumulator, so it goes to whichever list is shorter and the two wave
         // groups finish the stream together.
         const bool ref0 = (kinds & 3) == 2, ref1 = (kinds >> 2) == 2;
-        const int nr = (ref0 ? n0 : ref1 ? n1 : 0) + (kc && (ref0 || ref1) ? 1 : 0); // + a king-cache store entry
+        const int nr = (ref0 ? n0 : ref1 ? n1 : 0) + (kcb && (ref0 || ref1) ? 1 : 0); // + a king-cache store entry
         const int d0 = ref0 ? 0 : n0 - (hit0 ? 1 : 0), d1 = ref1 ? 0 : n1 - (hit1 ? 1 : 0);
         const uint32_t c = (uint32_t)d0 | (uint32_t)d1 << 10 | (uint32_t)nr << 20;
         uint32_t inc = c;
@@ -1326,7 +1348,7 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
               king_move_row(pbd, hh, sq01 & 0xFFFF, kt, sq23 & 0xFFFF, sq23 >> 16, lane, pos, &cpc);
           // King cache (not for castling): start from the accumulator this block last
           // stored for (hh, kt) and apply the placement difference, when that is shorter.
-          const bool kuse = kc && (sq23 & 0xFFFF) == 64;
+          const bool kuse = kcb && (sq23 & 0xFFFF) == 64;
           const uint32_t kcr = (uint32_t)KC_ROW0 + 128 * cslot + 64 * hh + kt;
           int ne = cn + 1 + (kuse ? 1 : 0), spc = 0;
           bool kh = false;
@@ -1583,24 +1605,28 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
     }
     GN_STAMP_FLUSH();
    }
-   if (K > 1) { // release the carry slot to the workgroup CARRY_SLOTS dispatches later
+   if (K > 1) { // done with the slot (every wave's stores completed before the barrier)
+     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
      __syncthreads();
-     if (tid == 0) __hip_atomic_store(tickets + cslot, v / CARRY_SLOTS + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+     if (tid == 0) __hip_atomic_fetch_add(tickets + cslot, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
    }
   }
 }
 
 hipError_t launch_eval_net(const NetDevice &net, const gn_board *boards, const uint8_t *need, size_t n, int2 *out,
-                           const uint32_t *perm, int swz, hipStream_t s) {
+                           const uint32_t *perm, int swz, hipStream_t s, unsigned long long *rows_out) {
   if (!n) return hipSuccess;
   const unsigned tiles = (unsigned)((n + 15) / 16);
   const unsigned grid = swz ? 8 * ((tiles + 7) / 8) : tiles;
   if (net.L1 == 3072) {
-    hipLaunchKernelGGL((eval_net_kernel<3072, 1>), dim3(grid), dim3(384), 0, s, net, boards, need, n, out, perm, tiles, swz);
+    hipLaunchKernelGGL((eval_net_kernel<3072, 1>), dim3(grid), dim3(384), 0, s, net, boards, need, n, out, perm, tiles, swz,
+                       rows_out);
   } else if (net.L1 == 128) {
-    hipLaunchKernelGGL((eval_net_kernel<128, 16>), dim3(grid), dim3(256), 0, s, net, boards, need, n, out, perm, tiles, swz);
+    hipLaunchKernelGGL((eval_net_kernel<128, 16>), dim3(grid), dim3(256), 0, s, net, boards, need, n, out, perm, tiles, swz,
+                       rows_out);
   } else if (net.L1 == 1024) {
-    hipLaunchKernelGGL((eval_net_kernel<1024, 1>), dim3(grid), dim3(128), 0, s, net, boards, need, n, out, perm, tiles, swz);
+    hipLaunchKernelGGL((eval_net_kernel<1024, 1>), dim3(grid), dim3(128), 0, s, net, boards, need, n, out, perm, tiles, swz,
+                       rows_out);
   } else {
     return hipErrorInvalidValue;
   }
@@ -1689,7 +1715,8 @@ __global__ void finalize_kernel(const gn_board *__restrict__ boards, size_t n, i
   v = clampi(v, -P.value_clamp, P.value_clamp);
   if (small) flags |= GN_FLAG_SMALLNET;
   if (in_check(B, T)) flags |= GN_FLAG_IN_CHECK;
-  e.psqt = o.x, e.positional = o.y, e.final_v = v, e.flags = flags;
+  e.psqt = o.x, e.positional = o.y, e.final_v = v, e.flags = (uint16_t)flags;
+  e.final_cp = wdl_to_cp(v, wdl_material(B, P), P);
   out[i] = e;
 }
 
@@ -1879,6 +1906,31 @@ __global__ void king_keys_kernel(const gn_board *__restrict__ boards, size_t n, 
   idx[i] = (uint32_t)i;
 }
 
+// Position-sensitive 64-bit checksum of a device buffer: sum over 8-byte words w_i of
+// splitmix64(w_i ^ (i * golden)) (wrapping), so equal buffers give equal sums and a
+// moved or changed word changes it.  Tail bytes are zero-padded into a last word.
+__global__ void checksum_kernel(const uint8_t *__restrict__ p, size_t bytes, unsigned long long *__restrict__ out) {
+  const size_t nw = (bytes + 7) / 8;
+  unsigned long long acc = 0;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < nw; i += (size_t)gridDim.x * blockDim.x) {
+    uint64_t w = 0;
+    if (8 * i + 8 <= bytes) w = *reinterpret_cast<const uint64_t *>(p + 8 * i);
+    else
+      for (size_t k = 8 * i; k < bytes; ++k) w |= (uint64_t)p[k] << (8 * (k - 8 * i));
+    acc += Xoshiro::mix(w ^ (i * 0x9E3779B97F4A7C15ull));
+  }
+  for (int off = 32; off; off >>= 1) acc += __shfl_down(acc, off, 64);
+  if ((threadIdx.x & 63) == 0 && acc) atomicAdd(out, acc);
+}
+
+hipError_t launch_checksum(const void *p, size_t bytes, unsigned long long *out, hipStream_t s) {
+  if (!bytes) return hipSuccess;
+  const size_t nw = (bytes + 7) / 8;
+  const unsigned g = (unsigned)std::min<size_t>(8192, (nw + 255) / 256);
+  hipLaunchKernelGGL(checksum_kernel, dim3(g), dim3(256), 0, s, (const uint8_t *)p, bytes, out);
+  return hipGetLastError();
+}
+
 __global__ void offsets_u32_kernel(const uint64_t *__restrict__ in, size_t n, uint32_t *__restrict__ out) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) out[i] = (uint32_t)in[i];
@@ -1988,7 +2040,7 @@ hipError_t launch_expand_net(const NetDevice &net, const gn_board *parents, size
   if (chained) { // one workgroup per block (never persistent: the slot tickets assume dispatch order)
     const size_t nblk = (n + chain_k - 1) / chain_k;
     g = (unsigned)(swz ? 8 * ((nblk + 7) / 8) : nblk);
-    hipError_t e = hipMemsetAsync(tickets, 0, CARRY_SLOTS * sizeof(uint32_t), s);
+    hipError_t e = hipMemsetAsync(tickets, 0, (CARRY_SLOTS + 1) * sizeof(uint32_t), s); // + the fallback count
     if (e != hipSuccess) return e;
   }
   static const int ablate = getenv("GN_ABLATE") ? atoi(getenv("GN_ABLATE")) : 0; // timing diagnostics only

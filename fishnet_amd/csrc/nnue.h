@@ -137,6 +137,27 @@ GN_HD int packed_features(const gn_board &p, uint16_t *rows_white, uint16_t *row
   return c;
 }
 
+// UCIEngine::to_cp (Stockfish 17-era uci.cpp, SURVEY.md §8a row a18, recalled):
+// a = p_a(m) of the win-rate model, m = clamp(material, lo, hi) / anchor, and
+// cp = round(100 * v / a).  Evaluated in double in Stockfish's operation order
+// with contraction off (Stockfish's gcc -std=c++17 build does not fuse), rounded
+// half away from zero as std::round; saturated to int16 (see gn_eval).
+GN_HD int wdl_material(const Board &B, const gn_eval_params &P) {
+  int m = 0;
+#pragma unroll
+  for (int pt = PAWN; pt <= QUEEN; ++pt) m += P.wdl_piece_weight[pt - 1] * popcnt(B.byType[pt]);
+  return m;
+}
+GN_HD int16_t wdl_to_cp(int32_t v, int material, const gn_eval_params &P) {
+#pragma clang fp contract(off)
+  const int lo = P.wdl_material_min, hi = P.wdl_material_max;
+  const int mc = material < lo ? lo : material > hi ? hi : material;
+  const double m = (double)mc / (double)P.wdl_material_anchor;
+  const double a = ((P.wdl_a[0] * m + P.wdl_a[1]) * m + P.wdl_a[2]) * m + P.wdl_a[3];
+  const double cp = round((double)(100 * (int64_t)v) / a);
+  return (int16_t)(cp > 32767.0 ? 32767 : cp < -32767.0 ? -32767 : (int)cp);
+}
+
 // 32-bit hashes stored in .nnue files
 inline uint32_t affine_hash(uint32_t prev, uint32_t outs) {
   uint32_t h = 0xCC03DAE4u + outs;

@@ -23,10 +23,20 @@ class ShardComm:
             kw = {"device_id": self.device} if self.backend == "nccl" else {}
             dist.init_process_group(self.backend, **kw)
 
-    # ---- sharding: contiguous, game-aligned ranges (weak scaling) ----------
+    # ---- sharding: the library's partitioner (gn_partition), game-aligned ----
     def shard(self, per_rank: int) -> tuple[int, int]:
-        """[first, first + per_rank) of the global index space owned by this rank."""
-        return self.rank * per_rank, per_rank
+        """[first, first + per_rank) of the global index space owned by this rank (weak
+        scaling: equal weights, so every rank gets per_rank items)."""
+        first, last = self.shard_weighted([1] * 0, per_rank * self.world)
+        return first, last - first
+
+    def shard_weighted(self, weights, n_items=None) -> tuple[int, int]:
+        """[first, last) items of this rank: contiguous ranges cut at item boundaries
+        (games), balanced by weight (positions per game); weights empty: equal weights."""
+        from fishnet_amd import gpu_nnue
+        n = len(weights) if n_items is None else n_items
+        b = gpu_nnue.partition(n, self.world, weights if len(weights) else None)
+        return b[self.rank], b[self.rank + 1]
 
     # ---- collectives ---------------------------------------------------------
     def broadcast_bytes(self, data: bytes, src: int = 0) -> bytes:
@@ -69,22 +79,29 @@ class ShardComm:
         return [int(v.item()) for v in lst]
 
     def gather_array(self, arr, dst: int = 0):
-        """Gathers equally sized numpy arrays (e.g. gn_eval records) to dst."""
+        """Gathers numpy arrays of one dtype (e.g. gn_eval records; lengths may differ per
+        rank) to dst: the list of every rank's array on dst, None elsewhere."""
         import numpy as np
         if self.world == 1:
             return [arr]
         torch, dist = self.torch, self.dist
-        raw = torch.frombuffer(bytearray(np.ascontiguousarray(arr).tobytes()), dtype=torch.uint8).to(self.device)
-        outs = [torch.empty_like(raw) for _ in range(self.world)] if self.rank == dst else None
+        data = np.ascontiguousarray(arr).tobytes()
+        sizes = self.gather_i64(len(data))
+        pad = max(sizes)
+        raw = torch.zeros(max(pad, 1), dtype=torch.uint8)
+        if data:
+            raw[:len(data)] = torch.frombuffer(bytearray(data), dtype=torch.uint8)
+        raw = raw.to(self.device)
         if self.backend == "nccl":
             lst = [torch.empty_like(raw) for _ in range(self.world)]
             dist.all_gather(lst, raw)
             outs = lst if self.rank == dst else None
         else:
+            outs = [torch.empty_like(raw) for _ in range(self.world)] if self.rank == dst else None
             dist.gather(raw, outs, dst=dst)
         if self.rank != dst:
             return None
-        return [np.frombuffer(o.cpu().numpy().tobytes(), dtype=arr.dtype) for o in outs]
+        return [np.frombuffer(o.cpu().numpy().tobytes()[:sz], dtype=arr.dtype) for o, sz in zip(outs, sizes)]
 
     def close(self):
         if self.world > 1 and self.dist.is_initialized():

@@ -24,7 +24,8 @@ ERRORS = {-1: "INVALID", -2: "IO", -3: "FORMAT", -4: "HIP", -5: "NOMEM", -6: "CA
           -7: "NODEVICE", -8: "NONET", -9: "ILLEGAL_MOVE"}
 E_INVALID, E_CAPACITY, E_ILLEGAL_MOVE = -1, -6, -9
 
-EVAL_DTYPE = np.dtype([("psqt", "<i4"), ("positional", "<i4"), ("final_v", "<i4"), ("flags", "<u4")])
+EVAL_DTYPE = np.dtype([("psqt", "<i4"), ("positional", "<i4"), ("final_v", "<i4"), ("final_cp", "<i2"),
+                       ("flags", "<u2")])
 BOARD_DTYPE = np.dtype([("occ", "<u8"), ("pc", "u1", (16,)), ("stm_ep", "u1"), ("reserved", "u1"),
                         ("castle", "<u2"), ("rule50", "<u2"), ("fullmove", "<u2")])
 assert EVAL_DTYPE.itemsize == 16 and BOARD_DTYPE.itemsize == 32
@@ -36,8 +37,10 @@ EXPORTS = ["gn_load_net", "gn_load_net_memory", "gn_free", "gn_last_error", "gn_
            "gn_device_alloc", "gn_device_free", "gn_memcpy_h2d", "gn_memcpy_d2h", "gn_synchronize",
            "gn_time_evaluate_device", "gn_random_positions_device", "gn_set_option", "gn_get_option",
            "gn_time_expand_device", "gn_random_games_device", "gn_replay_game", "gn_evaluate_games",
-           "gn_net_sha256"]
+           "gn_net_sha256", "gn_partition", "gn_checksum_device",
+           "gn_boards_to_fens"]
 OPT_INCREMENTAL_CHILDREN, OPT_XCD_SWIZZLE, OPT_KING_SORT, OPT_CHAIN, OPT_KING_CACHE = 1, 2, 3, 4, 5
+STAT_CHAIN_FALLBACKS = 100
 EXPAND_STAGES = ["count_scan", "total_readback", "write_children", "classify", "small_net", "big_net", "finalize"]
 
 
@@ -51,7 +54,9 @@ class EvalParams(C.Structure):
     _fields_ = [(n, C.c_int32) for n in (
         "small_net_threshold", "psqt_weight", "positional_weight", "reeval_threshold",
         "complexity_div_small", "complexity_div_big", "material_pawn_small", "material_pawn_big",
-        "material_base", "rule50_div", "value_clamp")] + [("piece_value", C.c_int32 * 5)]
+        "material_base", "rule50_div", "value_clamp")] + [
+        ("piece_value", C.c_int32 * 5), ("wdl_a", C.c_double * 4), ("wdl_material_min", C.c_int32),
+        ("wdl_material_max", C.c_int32), ("wdl_material_anchor", C.c_int32), ("wdl_piece_weight", C.c_int32 * 5)]
 
 
 class GnGame(C.Structure):
@@ -109,15 +114,18 @@ def lib():
         "gn_memcpy_h2d": [vp, i32, vp, vp, sz],
         "gn_memcpy_d2h": [vp, i32, vp, vp, sz],
         "gn_synchronize": [vp, i32],
-        "gn_time_evaluate_device": [vp, i32, vp, sz, i32, vp, i32, C.POINTER(C.c_float), vp],
+        "gn_time_evaluate_device": [vp, i32, vp, sz, i32, vp, i32, C.POINTER(C.c_float), vp, C.POINTER(C.c_uint64)],
+        "gn_checksum_device": [vp, i32, vp, sz, C.POINTER(C.c_uint64)],
         "gn_random_positions_device": [vp, i32, C.c_uint64, sz, sz, i32, vp, vp],
         "gn_set_option": [vp, i32, C.c_int64],
         "gn_get_option": [vp, i32, C.POINTER(C.c_int64)],
         "gn_time_expand_device": [vp, i32, vp, sz, i32, i32, C.POINTER(C.c_float), C.POINTER(sz), vp,
-                                  C.POINTER(C.c_uint64)],
+                                  C.POINTER(C.c_uint64), vp, vp, vp, vp, sz],
         "gn_random_games_device": [vp, i32, C.c_uint64, sz, sz, i32, vp, vp],
         "gn_replay_game": [C.POINTER(GnGame), vp, vp, vp, sz, C.POINTER(sz)],
         "gn_net_sha256": [vp, sz, C.c_char_p],
+        "gn_partition": [vp, sz, i32, vp],
+        "gn_boards_to_fens": [vp, sz, vp, sz],
         "gn_evaluate_games": [vp, vp, sz, i32, i32, vp, vp, vp, sz, vp, vp, vp, sz],
     }
     for name, args in sig.items():
@@ -158,6 +166,14 @@ def board_to_fen(board) -> str:
     return buf.value.decode()
 
 
+def boards_to_fens(boards) -> list:
+    """FENs of many boards at once (gn_boards_to_fens, multithreaded C)."""
+    b = np.ascontiguousarray(np.asarray(boards, dtype=BOARD_DTYPE).reshape(-1))
+    buf = np.zeros((len(b), 100), dtype=np.uint8)
+    _check(lib().gn_boards_to_fens(b.ctypes.data, len(b), buf.ctypes.data, 100))
+    return [bytes(r[:np.argmin(r)]).decode() for r in buf] if len(b) else []
+
+
 def random_positions(seed: int, first: int, n: int, max_plies: int = 160):
     boards = np.zeros(n, dtype=BOARD_DTYPE)
     _check(lib().gn_random_positions(seed, first, n, max_plies, boards.ctypes.data))
@@ -187,6 +203,14 @@ def net_sha256(data: bytes) -> str:
     return out.value.decode()
 
 
+def partition(n_items: int, n_shards: int, weights=None):
+    """gn_partition: bounds[n_shards + 1] of contiguous shards (the library's and bench's one partitioner)."""
+    b = np.zeros(n_shards + 1, dtype=np.uint64)
+    w = None if weights is None else np.ascontiguousarray(weights, dtype=np.uint32)
+    _check(lib().gn_partition(None if w is None else w.ctypes.data, n_items, n_shards, b.ctypes.data))
+    return [int(x) for x in b]
+
+
 def default_eval_params() -> EvalParams:
     p = EvalParams()
     _check(lib().gn_get_eval_params(None, C.byref(p)))
@@ -208,9 +232,13 @@ class DeviceBuffer:
         assert a.nbytes <= self.nbytes
         _check(lib().gn_memcpy_h2d(self.ctx.h, self.slot, self.ptr, a.ctypes.data, a.nbytes))
 
-    def download(self, dtype, count):
+    def download(self, dtype, count, offset=0):
+        """count elements of dtype starting at element `offset`."""
         out = np.empty(count, dtype=dtype)
-        _check(lib().gn_memcpy_d2h(self.ctx.h, self.slot, out.ctypes.data, self.ptr, out.nbytes))
+        if count:
+            src = C.c_void_p(self.addr + offset * np.dtype(dtype).itemsize)
+            assert (offset + count) * np.dtype(dtype).itemsize <= self.nbytes
+            _check(lib().gn_memcpy_d2h(self.ctx.h, self.slot, out.ctypes.data, src, out.nbytes))
         return out
 
     def free(self):
@@ -352,22 +380,35 @@ class GpuNnue:
     def random_games_device(self, seed, first_game, n_games, plies, d_out: DeviceBuffer, stream=None, slot=0):
         _check(lib().gn_random_games_device(self.h, slot, seed, first_game, n_games, plies, d_out.ptr, stream))
 
-    def time_expand_device(self, d_parents: DeviceBuffer, n, mode, iters, slot=0):
+    def time_expand_device(self, d_parents: DeviceBuffer, n, mode, iters, slot=0, outputs=None):
+        """outputs: optional dict of DeviceBuffers po (parents), off (u32 offsets), mv (moves), co (children)
+        plus cap; they receive the timed expansion's results."""
         ms, total, rows = C.c_float(), C.c_size_t(), C.c_uint64()
         st = (C.c_float * 7)()
+        o = outputs or {}
+        ptr = lambda k: o[k].ptr if k in o else None
         _check(lib().gn_time_expand_device(self.h, slot, d_parents.ptr, n, mode, iters, C.byref(ms),
-                                           C.byref(total), st, C.byref(rows)))
+                                           C.byref(total), st, C.byref(rows), ptr("po"), ptr("off"), ptr("mv"),
+                                           ptr("co"), o.get("cap", 0)))
         return ms.value, total.value, list(st), rows.value
+
+    def checksum_device(self, d_buf: DeviceBuffer, nbytes=None, offset=0, slot=0):
+        """gn_checksum_device over nbytes of d_buf starting at byte offset."""
+        v = C.c_uint64()
+        _check(lib().gn_checksum_device(self.h, slot, C.c_void_p(d_buf.addr + offset),
+                                        d_buf.nbytes - offset if nbytes is None else nbytes, C.byref(v)))
+        return v.value
 
     def synchronize(self, slot=0):
         _check(lib().gn_synchronize(self.h, slot))
 
-    def time_evaluate_device(self, d_boards, n, mode, d_out, iters, per_kernel=True, slot=0):
-        ms = C.c_float()
+    def time_evaluate_device(self, d_boards, n, mode, d_out, iters, per_kernel=True, slot=0, rows=False):
+        ms, r = C.c_float(), C.c_uint64()
         pk = (C.c_float * 4)() if per_kernel else None
         _check(lib().gn_time_evaluate_device(self.h, slot, d_boards.ptr, n, mode, d_out.ptr, iters,
-                                             C.byref(ms), pk))
-        return ms.value, (list(pk) if per_kernel else None)
+                                             C.byref(ms), pk, C.byref(r) if rows else None))
+        out = (ms.value, (list(pk) if per_kernel else None))
+        return out + (r.value,) if rows else out
 
     def expand_device(self, d_parents, n, mode, d_parent_out, d_offsets, d_children, d_moves, d_child_out,
                       cap, stream=None, slot=0):

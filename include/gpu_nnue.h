@@ -29,7 +29,9 @@
 extern "C" {
 #endif
 
-#define GN_ABI_VERSION 1
+/* v2: gn_eval carries final_cp (UCIEngine::to_cp) and 16-bit flags; gn_eval_params
+ * carries the win-rate model; expansion shards over every device of the context. */
+#define GN_ABI_VERSION 2
 
 #if defined(__GNUC__)
 #define GN_API __attribute__((visibility("default")))
@@ -63,10 +65,11 @@ extern "C" {
                                          tiles (bit 1, batch evaluation); 0: dispatch order */
 #define GN_OPT_KING_SORT 3            /* 1 (default): evaluate a batch in (white king, black
                                          king) square order for L2 / Infinity-Cache
-                                         locality, then (big net) by the pieces of the
-                                         first two ranks so that 16-position tiles share
-                                         rows gathered once per tile; results in input
-                                         order; 0: input order                            */
+                                         locality, then (big net) by 30 home-square bits
+                                         (ranks 1, 2, 7, 8 without e1/e8: the start
+                                         position's piece still stands there) so that
+                                         16-position tiles share rows gathered once per
+                                         tile; results in input order; 0: input order     */
 #define GN_OPT_KING_CACHE 5           /* 1 (default): with the chained walk, a king-move
                                          child's refresh starts from the accumulator the
                                          workgroup last computed for that (perspective,
@@ -83,6 +86,12 @@ extern "C" {
                                          -k: exactly k.  0, 1 or -1: every parent
                                          refreshes.  Results are identical either way.    */
 
+/* read-only statistics (gn_get_option) */
+#define GN_STAT_CHAIN_FALLBACKS 100   /* blocks of the last chained expansion (per device,
+                                         summed) that found their carry / king-cache slot
+                                         still in use after a bounded wait and ran
+                                         without it (results identical, more rows)       */
+
 /* per-position flags */
 #define GN_FLAG_IN_CHECK 1u /* side to move in check: Stockfish has no static eval
                                (Eval::evaluate asserts !checkers); values are still
@@ -94,12 +103,18 @@ extern "C" {
 
 /* One result.  psqt/positional are Network::evaluate's NetworkOutput (already
  * divided by OutputScale = 16) of the net that produced final_v; final_v is
- * Eval::evaluate(pos, optimism = 0) in internal Value units; all side-to-move POV. */
+ * Eval::evaluate(pos, optimism = 0) in internal Value units; final_cp is
+ * final_v in centipawns as Stockfish prints it (UCIEngine::to_cp: the win-rate
+ * model's a(material), round(100 * v / a)), i.e. the `score cp` fishnet parses
+ * (/root/reference/src/stockfish.rs:419-427) and posts; all side-to-move POV.
+ * |final_cp| <= 100 * value_clamp / min a < 2^15 for the default parameters;
+ * it saturates at +-32767 for parameters that would exceed it. */
 typedef struct gn_eval {
   int32_t psqt;
   int32_t positional;
   int32_t final_v;
-  uint32_t flags;
+  int16_t final_cp;
+  uint16_t flags;
 } gn_eval;
 
 /* Packed position, 32 bytes, the device input format.
@@ -136,6 +151,17 @@ typedef struct gn_eval_params {
   int32_t rule50_div;          /* 212   v -= v * rule50 / div                        */
   int32_t value_clamp;         /* 31506 |v| <= VALUE_TB_WIN_IN_MAX_PLY - 1           */
   int32_t piece_value[5];      /* 208 781 825 1276 2538 (P N B R Q)                  */
+  /* UCIEngine::to_cp / win_rate_params (Stockfish 17-era uci.cpp; recalled, parity
+   * unpinned like the constants above):
+   *   material = sum wdl_piece_weight[pt] * count(pt) over both colours (P N B R Q)
+   *   m = clamp(material, wdl_material_min, wdl_material_max) / (double)wdl_material_anchor
+   *   a = ((wdl_a[0] * m + wdl_a[1]) * m + wdl_a[2]) * m + wdl_a[3]   (no FMA contraction)
+   *   final_cp = round(100 * final_v / a)                             (half away from zero) */
+  double wdl_a[4];             /* -37.45051876 121.19101539 -132.78783573 420.70576692 */
+  int32_t wdl_material_min;    /* 17 */
+  int32_t wdl_material_max;    /* 78 */
+  int32_t wdl_material_anchor; /* 58 */
+  int32_t wdl_piece_weight[5]; /* 1 3 3 5 9 */
 } gn_eval_params;
 
 typedef struct gn_ctx gn_ctx;
@@ -172,7 +198,8 @@ GN_API int gn_net_info(const gn_ctx *ctx, int *big_l1, uint32_t *big_hash, int *
 GN_API int gn_evaluate_batch(gn_ctx *ctx, const char *const *fens, size_t n, gn_eval *out);
 GN_API int gn_evaluate_batch_mode(gn_ctx *ctx, const char *const *fens, size_t n, int mode, gn_eval *out);
 
-/* Every parent plus every legal child of it.  child_offsets[n+1] receives the
+/* Every parent plus every legal child of it, sharded over every device of the
+ * context (gn_partition, one host thread per device).  child_offsets[n+1] receives the
  * prefix sums (children of parent i are [child_offsets[i], child_offsets[i+1])),
  * child_moves / child_out receive one entry per child in the order the device
  * generator emits them (moves in Stockfish 16-bit encoding; castling = king
@@ -210,7 +237,9 @@ GN_API int gn_replay_game(const gn_game *game, gn_board *positions, uint8_t *ski
 /* Replay + evaluate n_games batches at once.  position_offsets[n_games + 1]:
  * positions of game g are [position_offsets[g], position_offsets[g + 1]);
  * game_status[g] = GN_OK or that game's GN_E_* (a failed game has no positions;
- * the other games are still evaluated and the call returns GN_OK).  Skipped
+ * the other games are still evaluated and the call returns GN_OK).  Games are
+ * sharded over the devices of the context, never split (gn_partition weighted by
+ * evaluated positions), so a game's consecutive positions share a device.  Skipped
  * positions get GN_FLAG_SKIPPED and no children.  with_children != 0: also every
  * legal child of every evaluated position, child_offsets[total positions + 1]
  * indexed by position (as gn_expand_and_evaluate).  GN_E_CAPACITY when the
@@ -221,6 +250,15 @@ GN_API int gn_evaluate_games(gn_ctx *ctx, const gn_game *games, size_t n_games, 
                              size_t position_cap, uint32_t *child_offsets, uint16_t *child_moves,
                              gn_eval *child_out, size_t child_cap);
 
+/* The partitioner the library uses to shard work over the devices of a context and
+ * that multi-process callers use to shard over ranks: contiguous ranges of n_items
+ * items, bounds[k] = first item of shard k, bounds[n_shards] = n_items; shard k
+ * starts at the first item whose weight prefix reaches ceil(k * total / n_shards)
+ * (weights NULL: every item weighs 1).  gn_evaluate_games shards games weighted
+ * by evaluated positions; gn_expand_and_evaluate / gn_evaluate_batch shard parents /
+ * positions equally.  Host only. */
+GN_API int gn_partition(const uint32_t *weights, size_t n_items, int n_shards, size_t *bounds);
+
 /* Legal-move-tree node count from fen to depth (GPU movegen, breadth-first). */
 GN_API int gn_perft(gn_ctx *ctx, const char *fen, int depth, uint64_t *nodes);
 
@@ -230,6 +268,9 @@ GN_API int gn_perft(gn_ctx *ctx, const char *fen, int depth, uint64_t *nodes);
 GN_API int gn_pack_fens(const char *const *fens, size_t n, gn_board *out, uint8_t *ok);
 /* Packed board -> FEN text (Chess960-aware X-FEN castling); buf >= 100 bytes. */
 GN_API int gn_board_to_fen(const gn_board *board, char *buf, size_t buflen);
+/* n boards -> n NUL-terminated FENs at buf + i * stride (stride >= 100); an invalid
+ * board gives "".  Host only, multithreaded. */
+GN_API int gn_boards_to_fens(const gn_board *boards, size_t n, char *buf, size_t stride);
 /* Deterministic random-playout positions (xoshiro256**, seed + index): plays
  * k ~ U{0..max_plies} uniformly random legal plies from the start position
  * (stopping at mate/stalemate), resampling positions in check. Host only. */
@@ -254,7 +295,11 @@ GN_API int gn_expand_device(gn_ctx *ctx, int device_slot, const gn_board *d_pare
                      uint16_t *d_moves, gn_eval *d_child_out, size_t cap, size_t *total, void *stream);
 /* Time `iters` complete expansions of device-resident parents (child count +
  * scan + child generation with deltas + evaluation of parents and children in
- * `mode`), library-owned output buffers.  *total = children per expansion;
+ * `mode`).  Outputs go to the caller's device buffers when given (d_parent_out[n],
+ * d_offsets[n + 1], d_moves[cap], d_child_out[cap]; GN_E_CAPACITY when the
+ * children exceed cap), else to library-owned buffers; every iteration writes the
+ * same values, so after the call they hold the timed expansion's results.
+ * *total = children per expansion;
  * stage_ms (optional, length 7) = average ms of [count+scan, total read-back,
  * write children, classify, small net, big net, finalize]; ft_rows (optional)
  * = feature-transformer rows one incremental expansion gathers: for the big
@@ -262,7 +307,13 @@ GN_API int gn_expand_device(gn_ctx *ctx, int device_slot, const gn_board *d_pare
  * GN_OPT_CHAIN, GN_OPT_KING_CACHE), else parent refreshes + child deltas /
  * king-move refreshes; 0 when not incremental. */
 GN_API int gn_time_expand_device(gn_ctx *ctx, int device_slot, const gn_board *d_parents, size_t n, int mode,
-                                 int iters, float *ms_total, size_t *total, float *stage_ms, uint64_t *ft_rows);
+                                 int iters, float *ms_total, size_t *total, float *stage_ms, uint64_t *ft_rows,
+                                 gn_eval *d_parent_out, uint32_t *d_offsets, uint16_t *d_moves,
+                                 gn_eval *d_child_out, size_t cap);
+/* *sum = position-sensitive 64-bit checksum of `bytes` bytes at device pointer d_ptr
+ * (sum over 8-byte words w_i of splitmix64(w_i ^ i * 0x9E3779B97F4A7C15), wrapping):
+ * compares large device-resident results without a download. */
+GN_API int gn_checksum_device(gn_ctx *ctx, int device_slot, const void *d_ptr, size_t bytes, uint64_t *sum);
 /* n_games random games of `plies` plies (xoshiro256**, seed + game index) on
  * the GPU: d_out[g * (plies + 1) + k] = position after k plies of game g (a
  * game that ends early repeats its final position).  Asynchronous. */
@@ -278,9 +329,11 @@ GN_API int gn_synchronize(gn_ctx *ctx, int device_slot);
  * on the launch stream; *ms_total = elapsed time.  per_kernel_ms (optional,
  * length 4) receives the average per-call time of the [classify(+reeval),
  * small net, big net, finalize] stages, from events recorded between the
- * launches of that same timed pass (one host sync at the end). */
+ * launches of that same timed pass (one host sync at the end).  ft_rows
+ * (optional) = feature-transformer rows one call's gather reads (the big net's,
+ * or the small net's in GN_MODE_SMALL), counted by the kernel. */
 GN_API int gn_time_evaluate_device(gn_ctx *ctx, int device_slot, const gn_board *d_boards, size_t n, int mode,
-                            gn_eval *d_out, int iters, float *ms_total, float *per_kernel_ms);
+                            gn_eval *d_out, int iters, float *ms_total, float *per_kernel_ms, uint64_t *ft_rows);
 
 #ifdef __cplusplus
 }

@@ -20,12 +20,16 @@
  *   - layer stack propagate (SqrClippedReLU, ClippedReLU, skip)    [SURVEY a16]
  *   - Network::evaluate bucket + OutputScale                       [SURVEY a17]
  *   - Eval::evaluate epilogue, Stockfish 17.1 constants            [SURVEY a18]
+ *   - UCIEngine::to_cp: win_rate_params' a(material) polynomial,
+ *     round(100 * v / a) in double, no FMA contraction (the Makefile
+ *     builds with -ffp-contract=off)                               [SURVEY a18]
  * Integer overflow follows two's complement wrapping, which is what the
  * reference's compiled x86 code does for these expressions.
  */
 #include "oracle.h"
 
 #include <ctype.h>
+#include <math.h>
 #include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -626,14 +630,57 @@ static int clampi(int v, int lo, int hi) { return v < lo ? lo : v > hi ? hi : v;
 static int32_t wmul(int32_t a, int32_t b) { return (int32_t)((uint32_t)a * (uint32_t)b); }
 static int32_t wadd(int32_t a, int32_t b) { return (int32_t)((uint32_t)a + (uint32_t)b); }
 
-/* Network::evaluate: returns {psqt / 16, positional / 16} (side-to-move POV) */
-static void net_output(const or_net *net, const pos_t *p, int32_t *psqt_out, int32_t *pos_out) {
-  int L1 = net->L1, H = L1 / 2;
+/* both perspectives' accumulators of one position */
+typedef struct {
   int16_t acc[2][4096];
   int32_t ps[2][8];
+} accs_t;
+
+static void refresh(const or_net *net, const pos_t *p, accs_t *a) {
+  accumulate(net, p, WHITE, a->acc[WHITE], a->ps[WHITE]);
+  accumulate(net, p, BLACK, a->acc[BLACK], a->ps[BLACK]);
+}
+
+/* Incremental update parent -> child (what Stockfish's update_accumulator does with
+ * DirtyPiece, restated on the mailbox): a perspective whose king square changed is
+ * refreshed; otherwise every square whose piece differs subtracts the parent piece's
+ * row and adds the child piece's row.  Wrapping int16 adds, so it equals a refresh. */
+static void update(const or_net *net, const pos_t *p, const accs_t *pa, const pos_t *q, accs_t *qa) {
+  const int L1 = net->L1;
+  for (int h = 0; h < 2; ++h) {
+    const int kq = king_sq(q, h);
+    if (kq != king_sq(p, h)) {
+      accumulate(net, q, h, qa->acc[h], qa->ps[h]);
+      continue;
+    }
+    int16_t *acc = qa->acc[h];
+    int32_t *ps = qa->ps[h];
+    memcpy(acc, pa->acc[h], sizeof(int16_t) * (size_t)L1);
+    memcpy(ps, pa->ps[h], sizeof(int32_t) * 8);
+    for (int sq = 0; sq < 64; ++sq) {
+      if (p->b[sq] == q->b[sq]) continue;
+      if (p->b[sq]) {
+        const size_t idx = (size_t)make_index(h, sq, p->b[sq], kq);
+        const int16_t *w = net->ft_w + idx * (size_t)L1;
+        for (int i = 0; i < L1; ++i) acc[i] = (int16_t)(uint16_t)((uint16_t)acc[i] - (uint16_t)w[i]);
+        for (int b = 0; b < 8; ++b) ps[b] = (int32_t)((uint32_t)ps[b] - (uint32_t)net->psqt_w[idx * 8 + b]);
+      }
+      if (q->b[sq]) {
+        const size_t idx = (size_t)make_index(h, sq, q->b[sq], kq);
+        const int16_t *w = net->ft_w + idx * (size_t)L1;
+        for (int i = 0; i < L1; ++i) acc[i] = (int16_t)(uint16_t)((uint16_t)acc[i] + (uint16_t)w[i]);
+        for (int b = 0; b < 8; ++b) ps[b] = (int32_t)((uint32_t)ps[b] + (uint32_t)net->psqt_w[idx * 8 + b]);
+      }
+    }
+  }
+}
+
+/* Network::evaluate from accumulators: {psqt / 16, positional / 16} (side-to-move POV) */
+static void net_output_acc(const or_net *net, const pos_t *p, const accs_t *a, int32_t *psqt_out, int32_t *pos_out) {
+  int L1 = net->L1, H = L1 / 2;
   uint8_t x[4096];
-  accumulate(net, p, WHITE, acc[WHITE], ps[WHITE]);
-  accumulate(net, p, BLACK, acc[BLACK], ps[BLACK]);
+  const int16_t(*acc)[4096] = a->acc;
+  const int32_t(*ps)[8] = a->ps;
   int persp[2] = {p->stm, !p->stm};
   for (int k = 0; k < 2; ++k)
     for (int j = 0; j < H; ++j) {
@@ -670,6 +717,13 @@ static void net_output(const or_net *net, const pos_t *p, int32_t *psqt_out, int
   *pos_out = positional / 16;
 }
 
+/* Network::evaluate: returns {psqt / 16, positional / 16} (side-to-move POV) */
+static void net_output(const or_net *net, const pos_t *p, int32_t *psqt_out, int32_t *pos_out) {
+  static __thread accs_t a;
+  refresh(net, p, &a);
+  net_output_acc(net, p, &a, psqt_out, pos_out);
+}
+
 /* ------------------------------------------------------------ evaluate -- */
 static const int PIECE_VALUE[7] = {0, 208, 781, 825, 1276, 2538, 0};
 
@@ -685,18 +739,58 @@ static void material(const pos_t *p, int *pawns, int npm[2]) {
   pawns[0] = np[0], pawns[1] = np[1];
 }
 
-static void evaluate(const or_net *big, const or_net *small, const pos_t *p, int mode, or_eval *out) {
+/* UCIEngine::to_cp (uci.cpp, Stockfish 17 era; recalled, parity unpinned):
+ *   material = P + 3N + 3B + 5R + 9Q over both colours,
+ *   m = clamp(material, 17, 78) / 58.0,
+ *   a = ((as[0] m + as[1]) m + as[2]) m + as[3],
+ *   cp = round(100 * v / a). */
+static int16_t to_cp(const pos_t *p, int32_t v) {
+  static const int W[7] = {0, 1, 3, 3, 5, 9, 0};
+  static const double as[4] = {-37.45051876, 121.19101539, -132.78783573, 420.70576692};
+  int material = 0;
+  for (int sq = 0; sq < 64; ++sq)
+    if (p->b[sq]) material += W[TYPE_OF(p->b[sq])];
+  double m = (double)(material < 17 ? 17 : material > 78 ? 78 : material) / 58.0;
+  double a = (((as[0] * m + as[1]) * m + as[2]) * m) + as[3];
+  double cp = round((double)(100 * (long long)v) / a);
+  if (cp > 32767.0) cp = 32767.0;
+  if (cp < -32767.0) cp = -32767.0;
+  return (int16_t)cp;
+}
+
+/* Where a position's accumulators come from: a full refresh (src == NULL), or an
+ * incremental update from its parent's (src->parent with src->pacc[net], computed on
+ * first use; net 0 = big, 1 = small). */
+typedef struct {
+  const pos_t *parent;
+  accs_t *pacc[2];
+  int have[2];
+  accs_t *child; /* scratch for the child's accumulators */
+} acc_src_t;
+
+static void output_of(const or_net *net, int which, const pos_t *p, acc_src_t *src, int32_t *psqt, int32_t *pos) {
+  if (!src) {
+    net_output(net, p, psqt, pos);
+    return;
+  }
+  if (!src->have[which]) refresh(net, src->parent, src->pacc[which]), src->have[which] = 1;
+  update(net, src->parent, src->pacc[which], p, src->child);
+  net_output_acc(net, p, src->child, psqt, pos);
+}
+
+static void evaluate_src(const or_net *big, const or_net *small, const pos_t *p, int mode, or_eval *out,
+                         acc_src_t *src) {
   int pawns[2], npm[2], us = p->stm;
   material(p, pawns, npm);
   int simple = 208 * (pawns[us] - pawns[!us]) + (npm[us] - npm[!us]);
   int small_net = mode == OR_MODE_SMALL ? 1 : mode == OR_MODE_BIG ? 0 : (abs(simple) > 962);
   uint32_t flags = 0;
   int32_t psqt, positional, nnue;
-  if (small_net) net_output(small, p, &psqt, &positional);
-  else net_output(big, p, &psqt, &positional);
+  if (small_net) output_of(small, 1, p, src, &psqt, &positional);
+  else output_of(big, 0, p, src, &psqt, &positional);
   nnue = wadd(wmul(125, psqt), wmul(131, positional)) / 128;
   if (mode == OR_MODE_FULL && small_net && abs(nnue) < 236) {
-    net_output(big, p, &psqt, &positional);
+    output_of(big, 0, p, src, &psqt, &positional);
     nnue = wadd(wmul(125, psqt), wmul(131, positional)) / 128;
     small_net = 0;
     flags |= OR_FLAG_REEVAL;
@@ -709,7 +803,12 @@ static void evaluate(const or_net *big, const or_net *small, const pos_t *p, int
   v = clampi(v, -31506, 31506);
   if (small_net) flags |= OR_FLAG_SMALLNET;
   if (in_check(p)) flags |= OR_FLAG_IN_CHECK;
-  out->psqt = psqt, out->positional = positional, out->final_v = v, out->flags = flags;
+  out->psqt = psqt, out->positional = positional, out->final_v = v, out->flags = (uint16_t)flags;
+  out->final_cp = to_cp(p, v);
+}
+
+static void evaluate(const or_net *big, const or_net *small, const pos_t *p, int mode, or_eval *out) {
+  evaluate_src(big, small, p, mode, out, NULL);
 }
 
 int or_eval_fen(const or_net *big, const or_net *small, const char *fen, int mode, or_eval *out) {
@@ -807,4 +906,77 @@ int or_expand_eval(const or_net *big, const or_net *small, const char *fen, int 
     evaluate(big, small, &q, mode, &children[i]);
   }
   return n;
+}
+
+/* Parent + every legal child with the children's accumulators updated incrementally
+ * from the parent's (update() above) instead of refreshed: Stockfish's own CPU
+ * strategy.  Same results as or_expand_eval. */
+int or_expand_eval_inc(const or_net *big, const or_net *small, const char *fen, int mode, or_eval *parent,
+                       uint16_t *moves, or_eval *children, int cap) {
+  static __thread accs_t pa[2], ca;
+  pos_t p;
+  uint16_t mv[256];
+  if (parse_fen(fen, &p)) {
+    memset(parent, 0, sizeof(*parent));
+    parent->flags = OR_FLAG_BAD_FEN;
+    return -1;
+  }
+  acc_src_t src = {&p, {&pa[0], &pa[1]}, {0, 0}, &ca};
+  evaluate(big, small, &p, mode, parent);
+  int n = gen_legal(&p, mv);
+  if (n > cap) return -2;
+  for (int i = 0; i < n; ++i) {
+    pos_t q;
+    do_move(&p, mv[i], &q);
+    moves[i] = mv[i];
+    evaluate_src(big, small, &q, mode, &children[i], &src);
+  }
+  return n;
+}
+
+typedef struct {
+  const or_net *big, *small;
+  const char *const *fens;
+  int mode, incremental;
+  or_eval *parents, *children; /* children: 256 per parent (optional) */
+  int32_t *counts;
+  size_t next, n;
+  pthread_mutex_t mu;
+} bjob_t;
+
+static void *expand_worker(void *arg) {
+  bjob_t *j = (bjob_t *)arg;
+  uint16_t mv[256];
+  or_eval kids[256];
+  for (;;) {
+    pthread_mutex_lock(&j->mu);
+    size_t lo = j->next, hi = lo + 16 < j->n ? lo + 16 : j->n;
+    j->next = hi;
+    pthread_mutex_unlock(&j->mu);
+    if (lo >= hi) break;
+    for (size_t i = lo; i < hi; ++i) {
+      or_eval *ko = j->children ? j->children + 256 * i : kids;
+      int c = j->incremental ? or_expand_eval_inc(j->big, j->small, j->fens[i], j->mode, &j->parents[i], mv, ko, 256)
+                             : or_expand_eval(j->big, j->small, j->fens[i], j->mode, &j->parents[i], mv, ko, 256);
+      j->counts[i] = c;
+    }
+  }
+  return NULL;
+}
+
+int or_expand_eval_batch(const or_net *big, const or_net *small, const char *const *fens, size_t n, int mode,
+                         int incremental, int threads, or_eval *parents, int32_t *child_counts, or_eval *children) {
+  bjob_t j = {big, small, fens, mode, incremental, parents, children, child_counts, 0, n, PTHREAD_MUTEX_INITIALIZER};
+  if (threads > 1024) threads = 1024;
+  if (threads <= 1) {
+    expand_worker(&j);
+    return 0;
+  }
+  pthread_t th[1024];
+  int created[1024] = {0};
+  for (int t = 0; t < threads; ++t) created[t] = pthread_create(&th[t], NULL, expand_worker, &j) == 0;
+  expand_worker(&j);
+  for (int t = 0; t < threads; ++t)
+    if (created[t]) pthread_join(th[t], NULL);
+  return 0;
 }

@@ -43,7 +43,8 @@ typedef struct {
   int32_t psqt;       /* NetworkOutput.psqt of the net that produced final  */
   int32_t positional; /* NetworkOutput.positional of that net               */
   int32_t final_v;    /* Eval::evaluate(optimism = 0), side-to-move POV     */
-  uint32_t flags;
+  int16_t final_cp;   /* UCIEngine::to_cp(final_v): the printed centipawns  */
+  uint16_t flags;
 } or_eval;
 
 typedef struct or_net or_net;
@@ -82,6 +83,16 @@ uint64_t or_perft(const char *fen, int depth); /* UINT64_MAX on a bad FEN */
  * negative on error / cap overflow. */
 int or_expand_eval(const or_net *big, const or_net *small, const char *fen, int mode,
                    or_eval *parent, uint16_t *moves, or_eval *children, int cap);
+
+/* or_expand_eval with the children's accumulators updated incrementally from the
+ * parent's (a king move refreshes that perspective), as Stockfish does on the CPU. */
+int or_expand_eval_inc(const or_net *big, const or_net *small, const char *fen, int mode,
+                       or_eval *parent, uint16_t *moves, or_eval *children, int cap);
+/* n parents expanded by `threads` POSIX threads (work-stealing in chunks of 16):
+ * parents[i], child_counts[i] (negative: bad FEN), children[256 * i + k] when
+ * children is not NULL.  incremental selects or_expand_eval_inc / or_expand_eval. */
+int or_expand_eval_batch(const or_net *big, const or_net *small, const char *const *fens, size_t n, int mode,
+                         int incremental, int threads, or_eval *parents, int32_t *child_counts, or_eval *children);
 
 #ifdef __cplusplus
 }

@@ -15,6 +15,8 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "_build", "liboracle.so")
+# the same source built -O3 -march=native (bench.py's cpu_baseline; integer-identical results)
+NATIVE_LIB_PATH = os.path.join(HERE, "_build", "liboracle_native.so")
 
 MODE_FULL, MODE_BIG, MODE_SMALL = 0, 1, 2
 FLAG_IN_CHECK, FLAG_SMALLNET, FLAG_BAD_FEN, FLAG_REEVAL = 1, 2, 4, 8
@@ -22,24 +24,32 @@ FLAG_IN_CHECK, FLAG_SMALLNET, FLAG_BAD_FEN, FLAG_REEVAL = 1, 2, 4, 8
 
 class OrEval(C.Structure):
     _fields_ = [("psqt", C.c_int32), ("positional", C.c_int32),
-                ("final_v", C.c_int32), ("flags", C.c_uint32)]
+                ("final_v", C.c_int32), ("final_cp", C.c_int16), ("flags", C.c_uint16)]
 
 
 EVAL_DTYPE = np.dtype([("psqt", "<i4"), ("positional", "<i4"),
-                       ("final_v", "<i4"), ("flags", "<u4")])
+                       ("final_v", "<i4"), ("final_cp", "<i2"), ("flags", "<u2")])
 
 _lib = None
 
 
-def build():
-    subprocess.run(["make", "-s", "-C", HERE], check=True)
+def build(native=False):
+    subprocess.run(["make", "-s", "-C", HERE] + (["native"] if native else []), check=True)
+
+
+def use_library(path):
+    """Switch the oracle to another build of the same source (Net objects made before stay
+    valid: same struct layout, same libc allocator)."""
+    global _lib, LIB_PATH
+    LIB_PATH, _lib = path, None
+    return lib()
 
 
 def lib():
     global _lib
     if _lib is None:
         if not os.path.exists(LIB_PATH):
-            build()
+            build(native=LIB_PATH == NATIVE_LIB_PATH)
         L = C.CDLL(LIB_PATH)
         L.or_net_load.argtypes = [C.c_char_p, C.POINTER(C.c_void_p), C.c_char_p, C.c_int]
         L.or_net_load_mem.argtypes = [C.c_void_p, C.c_size_t, C.POINTER(C.c_void_p), C.c_char_p, C.c_int]
@@ -62,6 +72,9 @@ def lib():
         L.or_perft.restype = C.c_uint64
         L.or_expand_eval.argtypes = [C.c_void_p, C.c_void_p, C.c_char_p, C.c_int, C.POINTER(OrEval),
                                      C.POINTER(C.c_uint16), C.c_void_p, C.c_int]
+        L.or_expand_eval_inc.argtypes = L.or_expand_eval.argtypes
+        L.or_expand_eval_batch.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(C.c_char_p), C.c_size_t, C.c_int,
+                                           C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
         _lib = L
     return _lib
 
@@ -108,7 +121,7 @@ def _h(net):
 def eval_fen(big, small, fen, mode=MODE_FULL):
     out = OrEval()
     lib().or_eval_fen(_h(big), _h(small), fen.encode(), mode, C.byref(out))
-    return (out.psqt, out.positional, out.final_v, out.flags)
+    return (out.psqt, out.positional, out.final_v, out.final_cp, out.flags)
 
 
 def eval_fens(big, small, fens, mode=MODE_FULL, threads=1):
@@ -171,16 +184,28 @@ def perft(fen, depth):
     return v
 
 
-def expand_eval(big, small, fen, mode=MODE_FULL):
+def expand_eval(big, small, fen, mode=MODE_FULL, incremental=False):
     parent = OrEval()
     moves = (C.c_uint16 * 256)()
     kids = np.zeros(256, dtype=EVAL_DTYPE)
-    n = lib().or_expand_eval(_h(big), _h(small), fen.encode(), mode, C.byref(parent), moves,
-                             kids.ctypes.data, 256)
+    f = lib().or_expand_eval_inc if incremental else lib().or_expand_eval
+    n = f(_h(big), _h(small), fen.encode(), mode, C.byref(parent), moves, kids.ctypes.data, 256)
     if n < 0:
         raise ValueError("bad fen")
-    return ((parent.psqt, parent.positional, parent.final_v, parent.flags),
+    return ((parent.psqt, parent.positional, parent.final_v, parent.final_cp, parent.flags),
             list(moves[:n]), kids[:n].copy())
+
+
+def expand_eval_batch(big, small, fens, mode=MODE_FULL, incremental=True, threads=1, keep_children=False):
+    """n parents + all children on `threads` C threads: (parents[n], child_counts[n], children[n, 256] or None)."""
+    n = len(fens)
+    arr = (C.c_char_p * n)(*[f.encode() for f in fens])
+    parents = np.zeros(n, dtype=EVAL_DTYPE)
+    counts = np.zeros(n, dtype=np.int32)
+    kids = np.zeros((n, 256), dtype=EVAL_DTYPE) if keep_children else None
+    lib().or_expand_eval_batch(_h(big), _h(small), arr, n, mode, int(incremental), threads, parents.ctypes.data,
+                               counts.ctypes.data, None if kids is None else kids.ctypes.data)
+    return parents, counts, kids
 
 
 def move_to_uci(m):

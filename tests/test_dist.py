@@ -1,4 +1,7 @@
-"""The N>1 plumbing (fishnet_amd/dist.py) with world_size 2 on CPU ("gloo")."""
+"""The N>1 path (fishnet_amd/dist.py) with world_size 2 on CPU ("gloo"): the net
+broadcast, the library's partitioner (gn_partition) cutting game-aligned shards,
+every rank evaluating its own shard (the CPU oracle stands in for the rank's GPU),
+and rank 0 checking the gathered results against a single-process evaluation."""
 import hashlib
 import os
 import socket
@@ -9,11 +12,23 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
+# three short lichess-shaped batches (root FEN + UCI moves) of different lengths
+GAMES = [
+    ("rnbqkbnr/pppppppp/8/8/8/8/PPPPPPPP/RNBQKBNR w KQkq - 0 1", "e2e4 c7c5 g1f3 d7d6 d2d4 c5d4 f3d4 g8f6 b1c3 a7a6"),
+    ("rnbqkbnr/pppppppp/8/8/8/8/PPPPPPPP/RNBQKBNR w KQkq - 0 1", "d2d4 d7d5 c2c4 e7e6"),
+    ("r3k2r/p1ppqpb1/bn2pnp1/3PN3/1p2P3/2N2Q1p/PPPBBPPP/R3K2R w KQkq - 0 1", "e1g1 e8c8 a2a3 b4c3 d2c3"),
+    ("4k3/8/8/8/8/8/4P3/4K3 w - - 0 1", "e2e4 e8d7 e4e5 d7e6 e1e2"),
+]
+
 
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         return s.getsockname()[1]
+
+
+def _game_fens(O):
+    return [O.replay_game(root, moves)[0] for root, moves in GAMES]
 
 
 def _worker(rank, world, port, q):
@@ -23,26 +38,33 @@ def _worker(rank, world, port, q):
     try:
         from fishnet_amd import synthnet
         from fishnet_amd.dist import ShardComm
+        from oracle import oracle as O
         comm = ShardComm("gloo")
-        blob = synthnet.synth_net_bytes(32, 5) if rank == 0 else b""
+        blob = open(synthnet.cached_synth_net(128, 2), "rb").read() if rank == 0 else b""
         got = comm.broadcast_bytes(blob)
         label = comm.broadcast_obj("synthetic" if rank == 0 else None)
         first, count = comm.shard(1000)
         mx = comm.max(float(rank + 1))
         sums = comm.gather_i64(1000 + rank)
-        evals = np.zeros(4, dtype=[("psqt", "<i4"), ("positional", "<i4"), ("final_v", "<i4"), ("flags", "<u4")])
-        evals["psqt"] = rank
+        # this rank's games (weights = positions per game), evaluated with the net it received
+        games = _game_fens(O)
+        g0, g1 = comm.shard_weighted([len(g) for g in games])
+        net = O.Net(data=got)
+        mine = [f for g in games[g0:g1] for f in g]
+        evals = O.eval_fens(None, net, mine, O.MODE_SMALL) if mine else np.zeros(0, dtype=O.EVAL_DTYPE)
         gathered = comm.gather_array(evals)
         comm.close()
-        q.put((rank, len(got), hashlib.sha256(got).hexdigest(), label, first, count, mx, sums,
-               None if gathered is None else [int(g["psqt"][0]) for g in gathered]))
+        q.put((rank, len(got), hashlib.sha256(got).hexdigest(), label, first, count, mx, sums, (g0, g1),
+               None if gathered is None else np.concatenate(gathered).tobytes()))
     except Exception as e:  # surface the failure to the parent
         q.put((rank, "error", repr(e)))
 
 
-def test_two_rank_gloo_plumbing():
+def test_two_rank_gloo_shards_evaluate():
     import multiprocessing as mp
     from fishnet_amd import synthnet
+    from oracle import oracle as O
+    O.build()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -51,15 +73,31 @@ def test_two_rank_gloo_plumbing():
         p.start()
     res = {}
     for _ in range(2):
-        item = q.get(timeout=120)
+        item = q.get(timeout=180)
         res[item[0]] = item
     for p in ps:
         p.join(timeout=60)
     assert all(r[1] != "error" for r in res.values()), res
-    blob = synthnet.synth_net_bytes(32, 5)
+    blob = open(synthnet.cached_synth_net(128, 2), "rb").read()
     for r in (0, 1):
-        _, ln, hsh, label, first, count, mx, sums, gathered = res[r]
+        _, ln, hsh, label, first, count, mx, sums, _, _ = res[r]
         assert ln == len(blob) and hsh == hashlib.sha256(blob).hexdigest() and label == "synthetic"
         assert (first, count) == (1000 * r, 1000)
         assert mx == 2.0 and sums == [1000, 1001]
-    assert res[0][8] == [0, 1] and res[1][8] is None
+    # game-aligned shards covering every game once, balanced by positions (11+5 | 6+6)
+    assert res[0][8] == (0, 2) and res[1][8] == (2, 4)
+    games = _game_fens(O)
+    exp = O.eval_fens(None, O.Net(data=blob), [f for g in games for f in g], O.MODE_SMALL)
+    assert res[0][9] == exp.tobytes() and res[1][9] is None
+
+
+def test_partition_is_game_aligned_and_balanced():
+    from fishnet_amd import gpu_nnue as G
+    assert G.partition(10, 3) == [0, 4, 7, 10]
+    assert G.partition(8, 8) == list(range(9)) and G.partition(0, 4) == [0, 0, 0, 0, 0]
+    w = [81] * 5 + [3] * 50 + [200]
+    b = G.partition(len(w), 4, w)
+    assert b[0] == 0 and b[-1] == len(w) and all(x <= y for x, y in zip(b, b[1:]))
+    tot = sum(w)
+    for k in range(1, 4):  # shard k starts at the first game whose prefix reaches k/4 of the positions
+        assert sum(w[:b[k]]) >= -(-tot * k // 4) and (b[k] == 0 or sum(w[:b[k] - 1]) < -(-tot * k // 4))

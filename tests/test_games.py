@@ -148,7 +148,7 @@ def test_evaluate_games_vs_oracle(gpu_ctx, oracle_nets, oracle_lib, mode):
         got = o["evals"]
         for i in range(len(fens)):
             if i in skip:
-                assert tuple(got[i]) == (0, 0, 0, G.FLAG_SKIPPED)
+                assert tuple(got[i]) == (0, 0, 0, 0, G.FLAG_SKIPPED)
             else:
                 assert tuple(got[i]) == tuple(exp[i]), (fens[i], got[i], exp[i])
 

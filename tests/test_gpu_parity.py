@@ -354,3 +354,169 @@ def test_common_row_base_tiles(gpu_ctx, oracle_nets, oracle_lib, ksort):
             assert got[32]["flags"] & G.FLAG_BAD_FEN and got[100]["flags"] & G.FLAG_BAD_FEN
     finally:
         gpu_ctx.set_option(G.OPT_KING_SORT, 1)
+
+
+def test_chained_walk_at_bench_scale(gpu_ctx, oracle_nets, oracle_lib):
+    """The chained walk + king cache at more than 2 x CARRY_SLOTS (2,048) blocks, so carry and
+    king-cache slots are handed between workgroups and reused: 4,200 whole 80-ply games
+    (340,200 parents, ~10 M children) against the plain path (one workgroup per parent,
+    every parent refreshed, no king cache) by device checksums of every output, and 240
+    sampled parents with all their children against the oracle."""
+    from fishnet_amd import gpu_nnue as G
+    games, plies = 4200, 80
+    n = games * (plies + 1)
+    d_b = gpu_ctx.alloc(n * 32)
+    gpu_ctx.random_games_device(0x5EED0000 + 4200, 0, games, plies, d_b)
+    gpu_ctx.synchronize()
+    _, total, _, _ = gpu_ctx.time_expand_device(d_b, n, 1, 1)
+    out = {"po": gpu_ctx.alloc(n * 16), "off": gpu_ctx.alloc((n + 1) * 4), "mv": gpu_ctx.alloc(total * 2),
+           "co": gpu_ctx.alloc(total * 16), "cap": total}
+
+    def run(k, kc):
+        gpu_ctx.set_option(G.OPT_CHAIN, k)
+        gpu_ctx.set_option(G.OPT_KING_CACHE, kc)
+        _, t, _, rows = gpu_ctx.time_expand_device(d_b, n, 1, 1, outputs=out)
+        assert t == total
+        return tuple(gpu_ctx.checksum_device(out[b], nb) for b, nb in
+                     (("po", n * 16), ("off", (n + 1) * 4), ("mv", t * 2), ("co", t * 16))), rows
+
+    try:
+        plain, rows_plain = run(1, 0)
+        for k, kc in ((-81, 1), (81, 1), (-27, 1), (-81, 0)):
+            got, rows = run(k, kc)
+            assert got == plain, (k, kc)
+            assert rows < rows_plain, (k, kc, rows, rows_plain)  # the chain / cache really engaged
+        got, _ = run(81, 1)  # leave the default configuration's outputs in the buffers
+    finally:
+        gpu_ctx.set_option(G.OPT_CHAIN, 81)
+        gpu_ctx.set_option(G.OPT_KING_CACHE, 1)
+    big, small = oracle_nets
+    boards = d_b.download(G.BOARD_DTYPE, n)
+    offs = out["off"].download(np.uint32, n + 1)
+    pev = out["po"].download(G.EVAL_DTYPE, n)
+    rng = np.random.default_rng(7)
+    idx = np.concatenate([rng.choice(n, 200, replace=False), np.arange(n - 40, n)])  # + the end of the last game
+    for i in idx:
+        fen = G.board_to_fen(boards[i])
+        lo, hi = int(offs[i]), int(offs[i + 1])
+        mv = out["mv"].download(np.uint16, hi - lo, offset=lo)
+        ev = out["co"].download(G.EVAL_DTYPE, hi - lo, offset=lo)
+        p_exp, m_exp, k_exp = oracle_lib.expand_eval(big, small, fen, 1, incremental=True)
+        assert tuple(pev[i]) == p_exp, fen
+        assert dict(zip(mv.tolist(), map(tuple, ev.tolist()))) == dict(zip(m_exp, map(tuple, k_exp.tolist()))), fen
+
+
+def test_small_net_one_million_vs_oracle(gpu_ctx, oracle_nets, oracle_lib):
+    """configs[1] at its full size: 1,048,576 random-playout positions, small net, bit-exact
+    against the multithreaded oracle."""
+    from fishnet_amd import gpu_nnue as G
+    n = 1 << 20
+    d_b, d_o = gpu_ctx.alloc(n * 32), gpu_ctx.alloc(n * 16)
+    gpu_ctx.random_positions_device(0x5EED0000, 0, n, 160, d_b)
+    gpu_ctx.evaluate_device(d_b, n, G.MODE_SMALL, d_o)
+    gpu_ctx.synchronize()
+    got = d_o.download(G.EVAL_DTYPE, n)
+    fens = G.boards_to_fens(d_b.download(G.BOARD_DTYPE, n))
+    _, small = oracle_nets
+    exp = oracle_lib.eval_fens(None, small, fens, 2, threads=16)
+    _cmp(got, exp, fens)
+
+
+def test_two_device_slots_shard_expansion_and_games(synth_big_path, synth_small_path, oracle_nets, oracle_lib):
+    """A context over two device slots (both on GPU 0 here) shards gn_expand_and_evaluate by
+    parents and gn_evaluate_games(with_children) by whole games (gn_partition) and returns
+    exactly the single-device results."""
+    from fishnet_amd import gpu_nnue as G
+    one = G.GpuNnue(synth_big_path, synth_small_path, devices=[0])
+    two = G.GpuNnue(synth_big_path, synth_small_path, devices=[0, 0])
+    try:
+        fens = special_fens() + random_fens(301, 31337)
+        for mode in (0, 1):
+            a, b = one.expand_and_evaluate(fens, mode), two.expand_and_evaluate(fens, mode)
+            assert all(np.array_equal(x, y) for x, y in zip(a, b)), mode
+        games = [("rnbqkbnr/pppppppp/8/8/8/8/PPPPPPPP/RNBQKBNR w KQkq - 0 1",
+                  "e2e4 e7e5 g1f3 b8c6 f1b5 a7a6 b5a4 g8f6 e1g1 f8e7 f1e1 b7b5 a4b3 d7d6", (0, 3)),
+                 ("r3k2r/p1ppqpb1/bn2pnp1/3PN3/1p2P3/2N2Q1p/PPPBBPPP/R3K2R w KQkq - 0 1", "e1g1 e8c8", ()),
+                 ("4k3/8/8/8/8/8/4P3/4K3 w - - 0 1", "e2e4 e8d7 e4e5", (1,))] * 5
+        ra, rb = one.evaluate_games(games, 0, children=True), two.evaluate_games(games, 0, children=True)
+        for x, y in zip(ra, rb):
+            assert x["status"] == y["status"] and np.array_equal(x["evals"], y["evals"])
+            assert all(np.array_equal(c1[0], c2[0]) and np.array_equal(c1[1], c2[1])
+                       for c1, c2 in zip(x["children"], y["children"]))
+        big, small = oracle_nets
+        fens0 = oracle_lib.replay_game(games[0][0], games[0][1])[0]
+        for i, fen in enumerate(fens0):
+            if i in (0, 3):
+                continue
+            p_exp, m_exp, k_exp = oracle_lib.expand_eval(big, small, fen, 0)
+            assert tuple(rb[0]["evals"][i]) == p_exp
+            mv, ev = rb[0]["children"][i]
+            assert dict(zip(mv.tolist(), map(tuple, ev.tolist()))) == dict(zip(m_exp, map(tuple, k_exp.tolist())))
+    finally:
+        one.close()
+        two.close()
+
+
+def test_caller_stream_and_context_stream_do_not_race(gpu_ctx):
+    """gn_evaluate_device on a caller stream returns while its kernels are queued; a call on
+    the context stream right after must not overwrite the first call's library scratch
+    (king-sort permutation, net outputs): each result equals its own synchronous run."""
+    import torch
+    from fishnet_amd import gpu_nnue as G
+    n = 1 << 18
+    bufs = [(gpu_ctx.alloc(n * 32), gpu_ctx.alloc(n * 16)) for _ in range(2)]
+    for k, (d_b, _) in enumerate(bufs):
+        gpu_ctx.random_positions_device(100 + k, 0, n, 160, d_b)
+    exp = []
+    for d_b, d_o in bufs:
+        gpu_ctx.evaluate_device(d_b, n, 0, d_o)
+        gpu_ctx.synchronize()
+        exp.append(d_o.download(G.EVAL_DTYPE, n))
+    s = torch.cuda.Stream()
+    for rep in range(3):
+        for _, d_o in bufs:
+            d_o.upload(np.zeros(n, dtype=G.EVAL_DTYPE))
+        gpu_ctx.evaluate_device(bufs[0][0], n, 0, bufs[0][1], stream=s.cuda_stream)
+        gpu_ctx.evaluate_device(bufs[1][0], n, 0, bufs[1][1])
+        gpu_ctx.synchronize()
+        s.synchronize()
+        for (_, d_o), e in zip(bufs, exp):
+            assert np.array_equal(d_o.download(G.EVAL_DTYPE, n), e), rep
+
+
+def test_common_row_base_under_int16_wrap_and_shared_kings(oracle_lib):
+    """the common-row base with the int16-wrapping stress net, and tiles whose
+    positions share their kings (and so the common rows) but differ in the side to move and
+    the PSQT bucket: the per-position PSQT of the common rows at each position's own bucket."""
+    from fishnet_amd import gpu_nnue as G, synthnet
+    p = synthnet.cached_synth_net(3072, 11, stress=True)
+    ctx = G.GpuNnue(p, None)
+    on = oracle_lib.Net(p)
+    base = "r3k2r/pppq1ppp/2np1n2/2b1p3/2B1P3/2NP1N2/PPPQ1PPP/R3K2R {} KQkq - 0 1"
+    fens = []
+    # 16 positions: same kings and most pieces, stm alternating, pawns removed to change buckets
+    pawns = ["a2", "b2", "c2", "f2", "g2", "h2", "a7", "b7"]
+    for k in range(16):
+        f = base.format("wb"[k & 1])
+        board = oracle_lib._placement(f)
+        for sq in pawns[:k // 2]:
+            board.pop((int(sq[1]) - 1) * 8 + ord(sq[0]) - 97, None)
+        rows = []
+        for r in range(7, -1, -1):
+            row, e = "", 0
+            for fl in range(8):
+                pc = board.get(r * 8 + fl)
+                if pc is None:
+                    e += 1
+                else:
+                    row += (str(e) if e else "") + pc
+                    e = 0
+            rows.append(row + (str(e) if e else ""))
+        fens.append("/".join(rows) + " " + f.split(" ", 1)[1])
+    fens = fens * 3 + special_fens() + random_fens(300, 4711)
+    try:
+        for ks in (1, 0):
+            ctx.set_option(G.OPT_KING_SORT, ks)
+            _cmp(ctx.evaluate_batch(fens, 1), oracle_lib.eval_fens(on, None, fens, 1, threads=8), fens)
+    finally:
+        ctx.close()

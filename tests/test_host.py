@@ -28,7 +28,7 @@ def test_library_exports_every_header_symbol(G):
     for s in syms:
         assert hasattr(lib, s), s
     assert sorted(G.EXPORTS) == syms
-    assert lib.gn_abi_version() == 1
+    assert lib.gn_abi_version() == 2
 
 
 def test_structs_match_header(G):
@@ -37,6 +37,11 @@ def test_structs_match_header(G):
     assert (p.small_net_threshold, p.psqt_weight, p.positional_weight, p.reeval_threshold) == (962, 125, 131, 236)
     assert (p.complexity_div_big, p.material_pawn_big, p.material_base, p.rule50_div) == (18000, 535, 77777, 212)
     assert list(p.piece_value) == [208, 781, 825, 1276, 2538] and p.value_clamp == 31506
+    assert list(p.wdl_a) == [-37.45051876, 121.19101539, -132.78783573, 420.70576692]
+    assert (p.wdl_material_min, p.wdl_material_max, p.wdl_material_anchor) == (17, 78, 58)
+    assert list(p.wdl_piece_weight) == [1, 3, 3, 5, 9]
+    import ctypes
+    assert ctypes.sizeof(p) == 128
 
 
 def _fens():
@@ -60,7 +65,7 @@ def test_random_positions_deterministic_and_legal(G, oracle_lib):
     for brd in a:
         fen = G.board_to_fen(brd)
         assert oracle_lib.normalize_fen(fen) == fen
-        assert oracle_lib.eval_fen(None, None, fen, 3)[3] & oracle_lib.FLAG_BAD_FEN == 0
+        assert oracle_lib.eval_fen(None, None, fen, 3)[-1] & oracle_lib.FLAG_BAD_FEN == 0
         assert len(oracle_lib.legal_moves(fen)) > 0 or True
 
 

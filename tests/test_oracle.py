@@ -8,6 +8,7 @@
 """
 import hashlib
 import json
+import math
 import os
 
 import numpy as np
@@ -76,9 +77,40 @@ def test_goldens_regenerate_identically(oracle_lib, oracle_nets, synth_big_path,
 
 def test_goldens_cover_every_branch():
     g = json.load(open(os.path.join(HERE, "golden", "eval_goldens.json")))
-    flags = [r[4] for r in g["results"]["full"]]
+    assert g["columns"][-1] == "flags"
+    flags = [r[-1] for r in g["results"]["full"]]
     assert any(f & 1 for f in flags) and any(f & 2 for f in flags) and any(f & 8 for f in flags)
     assert any(f & 10 == 0 for f in flags)
+
+
+def py_to_cp(v, fen):
+    """Third restatement of UCIEngine::to_cp (win_rate_params' a(material)), Python floats
+    (IEEE double, no contraction) with std::round's half-away-from-zero."""
+    w = {"p": 1, "n": 3, "b": 3, "r": 5, "q": 9}
+    material = sum(w.get(ch.lower(), 0) for ch in fen.split()[0] if ch.isalpha())
+    m = min(max(material, 17), 78) / 58.0
+    a = (((-37.45051876 * m + 121.19101539) * m + -132.78783573) * m) + 420.70576692
+    x = 100 * v / a
+    return int(math.floor(x + 0.5)) if x >= 0 else -int(math.floor(-x + 0.5))
+
+
+def test_final_cp_restated_three_ways(oracle_lib, oracle_nets):
+    """final_cp of every golden row = to_cp(final_v) by an independent Python restatement, and
+    hand-computed anchors: a(58 material) = sum of the coefficients = 371.1484..."""
+    g = json.load(open(os.path.join(HERE, "golden", "eval_goldens.json")))
+    ci, vi = g["columns"].index("final_cp"), g["columns"].index("final_v")
+    n = 0
+    for rows in g["results"].values():
+        for r in rows:
+            assert r[ci] == py_to_cp(r[vi], r[0]), r
+            n += 1
+    assert n > 200
+    start = "rnbqkbnr/pppppppp/8/8/8/8/PPPPPPPP/RNBQKBNR w KQkq - 0 1"  # material 78 (clamped at 78)
+    assert py_to_cp(372, "4k3/8/8/8/8/8/8/4K3 w - - 0 1") == round(37200 / (((-37.45051876 * (17 / 58) + 121.19101539)
+                                                                            * (17 / 58) - 132.78783573) * (17 / 58) + 420.70576692))
+    m = 78 / 58.0
+    a78 = ((-37.45051876 * m + 121.19101539) * m - 132.78783573) * m + 420.70576692
+    assert py_to_cp(-1000, start) == -round(100000 / a78)
 
 
 # ---------------------------------------------------------------- numpy ----
@@ -155,3 +187,24 @@ def test_net_parser_rejects_corruption(oracle_lib, synth_small_path):
         with pytest.raises(ValueError):
             oracle_lib.Net(data=bad)
     assert oracle_lib.Net(data=data).l1 == 128
+
+
+@pytest.mark.parametrize("stress", [False, True])
+def test_incremental_oracle_equals_refresh(oracle_lib, stress):
+    """or_expand_eval_inc (children updated from the parent's accumulators, the CPU
+    baseline's mode) gives exactly or_expand_eval's full refreshes, also when the int16
+    accumulators wrap."""
+    from fishnet_amd import synthnet
+    small = oracle_lib.Net(synthnet.cached_synth_net(128, 7 if stress else 2, stress))
+    big = oracle_lib.Net(synthnet.cached_synth_net(3072, 11 if stress else 1, stress))
+    fens = [l.strip() for l in open(os.path.join(HERE, "golden", "special_fens.txt"))
+            if l.strip() and not l.startswith("#")]
+    for mode in (0, 1, 2):
+        for fen in fens:
+            a = oracle_lib.expand_eval(big, small, fen, mode)
+            b = oracle_lib.expand_eval(big, small, fen, mode, incremental=True)
+            assert a[0] == b[0] and a[1] == b[1] and np.array_equal(a[2], b[2]), (mode, fen)
+        par, cnt, kids = oracle_lib.expand_eval_batch(big, small, fens, mode, True, threads=4, keep_children=True)
+        for i, fen in enumerate(fens):
+            p_exp, m_exp, k_exp = oracle_lib.expand_eval(big, small, fen, mode)
+            assert tuple(par[i]) == p_exp and cnt[i] == len(m_exp) and np.array_equal(kids[i, :cnt[i]], k_exp)

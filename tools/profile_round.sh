@@ -12,7 +12,7 @@ cat $OUT/bench.json
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- \
     python bench.py --no-cpu-baseline --check 0 > $OUT/trace.log 2>&1 || { tail -20 $OUT/trace.log; exit 1; }
 echo "trace done"
-for wl in expand big16m; do
+for wl in ${WLS:-expand big16m small1m}; do
   ARGS="--workload $wl --steps 1 --warmup 0 --no-cpu-baseline --no-secondary --check 0"
   timeout -k 10 200 python bench.py $ARGS > $OUT/bench_$wl.json 2> $OUT/bench_$wl.err || exit 1
   timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch_$wl -o run --output-format csv -- python bench.py $ARGS > $OUT/pmc_fetch_$wl.log 2>&1 || exit 1
