@@ -323,7 +323,7 @@ def cpu_baseline_eval(c: Ctx, boards, mode, budget_s):
     O.use_library(O.NATIVE_LIB_PATH)
     try:
         th, info = host_threads(), cpuinfo()
-        fens = [c.G.board_to_fen(b) for b in boards]
+        fens = c.G.boards_to_fens(boards)
         done, reps, t = 0, 0, time.perf_counter()
         while True:
             O.eval_fens(big if mode != 2 else None, small if mode != 1 else None, fens, mode, threads=th)
@@ -348,20 +348,22 @@ def cpu_baseline_expand(c: Ctx, parents, mode, budget_s):
     O.use_library(O.NATIVE_LIB_PATH)
     try:
         th, info = host_threads(), cpuinfo()
-        fens = [c.G.board_to_fen(b) for b in parents]  # the oracle's input form, prepared untimed
+        fens = c.G.boards_to_fens(parents)  # the oracle's input form, prepared untimed
         done, k, chunk, t = 0, 0, max(64, 16 * th), time.perf_counter()
-        while k < len(fens):
+        while True:  # passes over the sample until the budget is spent
             _, counts, _ = O.expand_eval_batch(big if mode != 2 else None, small if mode != 1 else None,
-                                               fens[k:k + chunk], mode, incremental=True, threads=th)
+                                               fens[k % len(fens):k % len(fens) + chunk], mode, incremental=True,
+                                               threads=th)
             done += len(counts) + int(counts[counts > 0].sum())
-            k += chunk
+            k += len(counts)
             if time.perf_counter() - t >= budget_s:
                 break
         dt = time.perf_counter() - t
     finally:
         O.use_library(os.path.join(O.HERE, "_build", "liboracle.so"))
     return {"value": round(done / dt, 1), "unit": "evals/s", "cores": th, "kind": "port",
-            "sample": f"{done} evals ({k} parents of rank 0's games + all their legal children) in {dt:.1f} s; "
+            "sample": f"{done} evals ({k} parents of rank 0's games, {len(fens)} distinct, + all their legal children) "
+                      f"in {dt:.1f} s; "
                       f"oracle/oracle.c -O3 -march=native (fishnet's Cpu::detect class on this host: "
                       f"{fishnet_cpu_class(info)}), children incremental from the parent accumulators, "
                       f"{th} threads = this GPU's share of the host ({os.cpu_count()} logical CPUs), {info['model']}"}
@@ -437,7 +439,7 @@ def main():
 
     if c.rank == 0 and not args.no_cpu_baseline:
         if args.workload == "expand":
-            line["cpu_baseline"] = cpu_baseline_expand(c, r["parents"][:200_000], mode, args.cpu_seconds)
+            line["cpu_baseline"] = cpu_baseline_expand(c, r["parents"][:1_000_000], mode, args.cpu_seconds)
         else:
             line["cpu_baseline"] = cpu_baseline_eval(c, r["boards"][:200_000], mode, args.cpu_seconds)
 

@@ -461,7 +461,7 @@ def test_caller_stream_and_context_stream_do_not_race(gpu_ctx):
     """gn_evaluate_device on a caller stream returns while its kernels are queued; a call on
     the context stream right after must not overwrite the first call's library scratch
     (king-sort permutation, net outputs): each result equals its own synchronous run."""
-    import torch
+    import ctypes
     from fishnet_amd import gpu_nnue as G
     n = 1 << 18
     bufs = [(gpu_ctx.alloc(n * 32), gpu_ctx.alloc(n * 16)) for _ in range(2)]
@@ -472,16 +472,21 @@ def test_caller_stream_and_context_stream_do_not_race(gpu_ctx):
         gpu_ctx.evaluate_device(d_b, n, 0, d_o)
         gpu_ctx.synchronize()
         exp.append(d_o.download(G.EVAL_DTYPE, n))
-    s = torch.cuda.Stream()
-    for rep in range(3):
-        for _, d_o in bufs:
-            d_o.upload(np.zeros(n, dtype=G.EVAL_DTYPE))
-        gpu_ctx.evaluate_device(bufs[0][0], n, 0, bufs[0][1], stream=s.cuda_stream)
-        gpu_ctx.evaluate_device(bufs[1][0], n, 0, bufs[1][1])
-        gpu_ctx.synchronize()
-        s.synchronize()
-        for (_, d_o), e in zip(bufs, exp):
-            assert np.array_equal(d_o.download(G.EVAL_DTYPE, n), e), rep
+    hip = ctypes.CDLL("libamdhip64.so")  # the runtime libgpu_nnue is linked against
+    s = ctypes.c_void_p()
+    assert hip.hipStreamCreate(ctypes.byref(s)) == 0
+    try:
+        for rep in range(3):
+            for _, d_o in bufs:
+                d_o.upload(np.zeros(n, dtype=G.EVAL_DTYPE))
+            gpu_ctx.evaluate_device(bufs[0][0], n, 0, bufs[0][1], stream=s)
+            gpu_ctx.evaluate_device(bufs[1][0], n, 0, bufs[1][1])
+            gpu_ctx.synchronize()
+            assert hip.hipStreamSynchronize(s) == 0
+            for (_, d_o), e in zip(bufs, exp):
+                assert np.array_equal(d_o.download(G.EVAL_DTYPE, n), e), rep
+    finally:
+        hip.hipStreamDestroy(s)
 
 
 def test_common_row_base_under_int16_wrap_and_shared_kings(oracle_lib):
