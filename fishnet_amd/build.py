@@ -14,8 +14,8 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIBDIR = os.path.join(HERE, "lib")
 LIB = os.path.join(LIBDIR, "libgpu_nnue.so")
-SOURCES = ["gpu_nnue.hip", "kernels.hip"]
-HEADERS = ["chess.h", "host_board.h", "nnue.h", "kernels.h", "sha256.h"]
+SOURCES = ["gpu_nnue.hip", "kernels.hip", "stream.hip"]
+HEADERS = ["chess.h", "host_board.h", "nnue.h", "kernels.h", "sha256.h", "device_util.h"]
 ARCH = "gfx950"
 
 

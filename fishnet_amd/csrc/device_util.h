@@ -1,0 +1,255 @@
+// device_util.h — device helpers shared by the kernels of libgpu_nnue (kernels.hip,
+// stream.hip): wrapping integer ops, FT row loads, wave-parallel feature extraction
+// (lane = square), the transform, and the one-wave layer stack.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "nnue.h"
+
+namespace gn {
+
+typedef unsigned short ushort8 __attribute__((ext_vector_type(8)));
+typedef int int4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ int32_t wmul(int32_t a, int32_t b) { return (int32_t)((uint32_t)a * (uint32_t)b); }
+__device__ __forceinline__ int32_t wadd(int32_t a, int32_t b) { return (int32_t)((uint32_t)a + (uint32_t)b); }
+__device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : v > hi ? hi : v; }
+// feature row index as gathered: clamped into the table so that no stale or
+// corrupt index can ever address outside the weights (indices built by this
+// library are always < FT_INPUTS; the clamp is a single v_min per row)
+__device__ __forceinline__ uint32_t ft_row(uint32_t idx) { return idx < FT_INPUTS ? idx : FT_INPUTS - 1; }
+
+__device__ __forceinline__ void load_tables(Tables &dst, const Tables *src) {
+  const uint4 *s = reinterpret_cast<const uint4 *>(src);
+  uint4 *d = reinterpret_cast<uint4 *>(&dst);
+  for (int i = threadIdx.x; i < (int)(sizeof(Tables) / 16); i += blockDim.x) d[i] = s[i];
+  __syncthreads();
+}
+
+// Wave-uniform value as an SGPR (readfirstlane) when U: descriptors and row
+// indices of a slot perspective are the same for every lane of a wave whenever a
+// perspective group is a whole number of waves (PAR == 1, L1 / 16 % 64 == 0), so
+// control flow on them is scalar and the row offsets fold into the load's SGPR base.
+template <bool U>
+__device__ __forceinline__ int uni(int x) {
+  if constexpr (U) return __builtin_amdgcn_readfirstlane(x);
+  else return x;
+}
+
+// FT row loads as SGPR base + 32-bit VGPR offset (the table is < 4 GiB): one VGPR
+// per address instead of a 64-bit pointer, and the +L1 half folds into the
+// instruction's immediate offset
+__device__ __forceinline__ ushort8 ldft(const uint8_t *__restrict__ ft, uint32_t off) {
+  return *reinterpret_cast<const ushort8 *>(ft + off);
+}
+__device__ __forceinline__ uint32_t ldpd(const uint8_t *__restrict__ ft, uint32_t off) {
+  return *reinterpret_cast<const uint32_t *>(ft + off);
+}
+__device__ __forceinline__ int4v ldps(const uint8_t *__restrict__ ft, uint32_t off) {
+  return *reinterpret_cast<const int4v *>(ft + off);
+}
+
+// --------------------------------------------------- feature extraction --
+// One wave turns a packed board into its HalfKAv2_hm rows, lane = square:
+// the lane's rank among occupied squares is a popcount, king squares and
+// validity come from ballots.  Writes rows_w[k] / rows_b[k] (k = square
+// order) for the non-null outputs; returns the piece count, or 0 (nothing
+// written) for an invalid board.  Must be called by all 64 lanes of a wave.
+__device__ __forceinline__ int wave_features(const gn_board &p, uint16_t *rows_w, uint16_t *rows_b, int lane) {
+  const uint64_t occ = p.occ;
+  const int c = popcnt(occ);
+  const bool has = (occ >> lane) & 1;
+  const int k = popcnt(occ & ((1ull << lane) - 1));
+  uint64_t wlo, whi;
+  piece_words(p, wlo, whi);
+  const int pc = has && k < 32 ? piece_nibble(wlo, whi, k) : 0;
+  const int pt = pc & 7;
+  const uint64_t bad = __ballot(has && (pt < PAWN || pt > KING));
+  const uint64_t wkb = __ballot(has && pc == make_piece(WHITE, KING));
+  const uint64_t bkb = __ballot(has && pc == make_piece(BLACK, KING));
+  if (c < 2 || c > 32 || bad || popcnt(wkb) != 1 || popcnt(bkb) != 1) return 0;
+  if (has) {
+    if (rows_w) rows_w[k] = (uint16_t)feature_index(WHITE, lane, pc, __builtin_ctzll(wkb));
+    if (rows_b) rows_b[k] = (uint16_t)feature_index(BLACK, lane, pc, __builtin_ctzll(bkb));
+  }
+  return c;
+}
+
+// piece nibble on this lane's square (0: empty); lane = square.
+__device__ __forceinline__ int lane_piece(const gn_board &p, int lane) {
+  const uint64_t occ = p.occ;
+  const bool has = (occ >> lane) & 1;
+  const int k = popcnt(occ & ((1ull << lane) - 1));
+  uint64_t wlo, whi;
+  piece_words(p, wlo, whi);
+  return has && k < 32 ? piece_nibble(wlo, whi, k) : 0;
+}
+
+// wave_features without the squares of excl (the tile's common rows, eval_net):
+// rows in square order among occ & ~excl; returns the full piece count (bucket) or 0.
+__device__ __forceinline__ int wave_features_excl(const gn_board &p, uint16_t *rows_w, uint16_t *rows_b, int lane,
+                                                  uint64_t excl) {
+  const uint64_t occ = p.occ;
+  const int c = popcnt(occ);
+  const bool has = (occ >> lane) & 1;
+  const int pc = lane_piece(p, lane);
+  const int pt = pc & 7;
+  const uint64_t bad = __ballot(has && (pt < PAWN || pt > KING));
+  const uint64_t wkb = __ballot(has && pc == make_piece(WHITE, KING));
+  const uint64_t bkb = __ballot(has && pc == make_piece(BLACK, KING));
+  if (c < 2 || c > 32 || bad || popcnt(wkb) != 1 || popcnt(bkb) != 1) return 0;
+  if (has && !((excl >> lane) & 1)) {
+    const int k = popcnt(occ & ~excl & ((1ull << lane) - 1));
+    rows_w[k] = (uint16_t)feature_index(WHITE, lane, pc, __builtin_ctzll(wkb));
+    rows_b[k] = (uint16_t)feature_index(BLACK, lane, pc, __builtin_ctzll(bkb));
+  }
+  return c;
+}
+
+// Rows of perspective h of a child in which h's own king moved, straight from
+// the parent board (lane = square): the king goes kfrom -> kto (capturing
+// whatever stood there) and, for castling, the rook rfrom -> rto (64 = none).
+// The parent must be valid (its rows were extracted).  All 64 lanes.
+__device__ __forceinline__ void wave_features_king_move(const gn_board &p, int h, int kfrom, int kto, int rfrom,
+                                                        int rto, uint16_t *rows, int lane) {
+  const uint64_t occ = p.occ;
+  const bool has = (occ >> lane) & 1;
+  const int k = popcnt(occ & ((1ull << lane) - 1));
+  uint64_t wlo, whi;
+  piece_words(p, wlo, whi);
+  int pc = has && k < 32 ? piece_nibble(wlo, whi, k) : 0;
+  if (lane == kfrom || lane == rfrom) pc = 0;
+  if (lane == rto) pc = make_piece(h, ROOK);
+  if (lane == kto) pc = make_piece(h, KING);
+  const uint64_t cocc = __ballot(pc != 0);
+  if (pc) rows[popcnt(cocc & ((1ull << lane) - 1))] = (uint16_t)feature_index(h, lane, pc, kto);
+}
+
+// FeatureTransformer::transform for 8 columns pairs of one perspective, packed
+// 16-bit math: clamp both halves to [0, 254] (the doubled domain), multiply
+// (<= 64516, fits u16), >> 9, then v_perm the low bytes into 8 u8 outputs.
+typedef short short2v __attribute__((ext_vector_type(2)));
+typedef unsigned short ushort2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint2 transform8(ushort8 lo, ushort8 hi) {
+  uint32_t o[4];
+  const short2v z = {0, 0}, m = {254, 254};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    short2v a = {(short)lo[2 * i], (short)lo[2 * i + 1]}, b = {(short)hi[2 * i], (short)hi[2 * i + 1]};
+    a = __builtin_elementwise_min(__builtin_elementwise_max(a, z), m);
+    b = __builtin_elementwise_min(__builtin_elementwise_max(b, z), m);
+    ushort2v pr = __builtin_bit_cast(ushort2v, a) * __builtin_bit_cast(ushort2v, b);
+    pr = pr >> (ushort2v){9, 9};
+    o[i] = __builtin_bit_cast(uint32_t, pr);
+  }
+  return make_uint2(__builtin_amdgcn_perm(o[1], o[0], 0x06040200u), __builtin_amdgcn_perm(o[3], o[2], 0x06040200u));
+}
+
+// Layer stack of one bucket by ONE wave (expand_stream): fc_0 accumulates all L1/64
+// k-steps in registers (no partial sums through LDS, no workgroup barrier), so the
+// wave can run it while the rest of the workgroup builds the next tile.  The fc_0
+// result is in the lane layout of the MFMA accumulator, which is exactly what the
+// epilogue of layer_stack_tile reads back from LDS, so the math below is the same.
+// in1: this wave's 16 x 32 B, fwd: its 16 ints (LDS, private to the wave).
+template <int L1, class Valid, class Emit>
+__device__ __forceinline__ void layer_stack_wave(const NetDevice &net, const uint8_t *xt, uint8_t (*in1)[32],
+                                                 int32_t *fwd, const int32_t (*psq)[2], int b, int lane,
+                                                 Valid &&valid, Emit &&emit) {
+  constexpr int XS = L1 + 16, KS = L1 / 64, BATCH = KS % 6 == 0 ? 6 : 4;
+  static_assert(KS % BATCH == 0, "k-steps per batch");
+  const int row = lane & 15, kg = lane >> 4;
+  // fc_1 / fc_2 parameters first: their latency hides behind fc_0
+  const int4v zero = {0, 0, 0, 0};
+  int4v wl = zero, wh = zero;
+  if (kg < 2) {
+    wl = *reinterpret_cast<const int4v *>(net.w1 + ((size_t)b * 32 + row) * 32 + kg * 16);
+    wh = *reinterpret_cast<const int4v *>(net.w1 + ((size_t)b * 32 + 16 + row) * 32 + kg * 16);
+  }
+  const int32_t bias0 = net.b0[b * 16 + row];
+  const int32_t b1l = net.b1[b * 32 + row], b1h = net.b1[b * 32 + 16 + row];
+  const int32_t w2l = net.w2[b * 32 + row], w2h = net.w2[b * 32 + 16 + row];
+  const int32_t b2v = net.b2[b];
+  const int8_t *wb = net.w0 + ((size_t)b * 16 + row) * L1 + kg * 16;
+  const uint8_t *xa = xt + row * XS + kg * 16;
+  int4v acc = zero;
+#pragma unroll 1
+  for (int k0 = 0; k0 < KS; k0 += BATCH) {
+    int4v w[BATCH], a[BATCH];
+#pragma unroll
+    for (int j = 0; j < BATCH; ++j) w[j] = *reinterpret_cast<const int4v *>(wb + 64 * (k0 + j));
+#pragma unroll
+    for (int j = 0; j < BATCH; ++j) a[j] = *reinterpret_cast<const int4v *>(xa + 64 * (k0 + j));
+#pragma unroll
+    for (int j = 0; j < BATCH; ++j) acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[j], w[j], acc, 0, 0, 0);
+  }
+  // SqrClippedReLU / ClippedReLU of fc_0 outputs 0..14, skip term from output 15
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int pos = 4 * kg + i;
+    const int32_t v = wadd(acc[i], bias0);
+    if (row < 15) {
+      const long long s2 = ((long long)v * v) >> 19;
+      in1[pos][row] = (uint8_t)(s2 < 127 ? s2 : 127);
+      in1[pos][15 + row] = (uint8_t)clampi(v >> 6, 0, 127);
+    } else {
+      fwd[pos] = wmul(v, 600 * 16) / (127 * 64);
+      in1[pos][30] = 0;
+      in1[pos][31] = 0;
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const int4v a1 = kg < 2 ? *reinterpret_cast<const int4v *>(&in1[row][kg * 16]) : zero;
+  const int4v cl = __builtin_amdgcn_mfma_i32_16x16x64_i8(a1, wl, zero, 0, 0, 0);
+  const int4v ch = __builtin_amdgcn_mfma_i32_16x16x64_i8(a1, wh, zero, 0, 0, 0);
+  int32_t part[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int32_t l = clampi(wadd(cl[i], b1l) >> 6, 0, 127), hh = clampi(wadd(ch[i], b1h) >> 6, 0, 127);
+    part[i] = w2l * l + w2h * hh;
+  }
+#pragma unroll
+  for (int off = 8; off; off >>= 1)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) part[i] = wadd(part[i], __shfl_xor(part[i], off, 16));
+  if (row == 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int pos = 4 * kg + i;
+      if (valid(pos, b)) {
+        const int32_t positional = wadd(wadd(b2v, part[i]), fwd[pos]);
+        const int32_t psqt = (int32_t)((uint32_t)psq[pos][0] - (uint32_t)psq[pos][1]) / 2;
+        emit(pos, make_int2(psqt / 16, positional / 16));
+      }
+    }
+  }
+}
+
+// rows of perspective h of a child whose h-king moved kf -> kt (castling: rook rf -> rt,
+// 64 = none), from the parent board, lane = square: the row of this lane's piece in
+// the child (or -1) and its rank among the child's pieces.  All 64 lanes.
+__device__ __forceinline__ int king_move_row(const gn_board &pb, int h, int kf, int kt, int rf, int rt, int lane,
+                                             int &pos, int *piece = nullptr) {
+  const uint64_t occ = pb.occ;
+  const bool has = (occ >> lane) & 1;
+  const int k = popcnt(occ & ((1ull << lane) - 1));
+  uint64_t wlo, whi;
+  piece_words(pb, wlo, whi);
+  int pc = has && k < 32 ? piece_nibble(wlo, whi, k) : 0;
+  if (lane == kf || lane == rf) pc = 0;
+  if (lane == rt) pc = make_piece(h, ROOK);
+  if (lane == kt) pc = make_piece(h, KING);
+  const uint64_t cocc = __ballot(pc != 0);
+  pos = popcnt(cocc & ((1ull << lane) - 1));
+  if (piece) *piece = pc;
+  return pc ? feature_index(h, lane, pc, kt) : -1;
+}
+
+__device__ __forceinline__ int32_t wave_sum(int32_t v) {
+#pragma unroll
+  for (int off = 32; off; off >>= 1) v = wadd(v, __shfl_xor(v, off));
+  return v;
+}
+
+} // namespace gn

@@ -206,6 +206,13 @@ struct Dev {
   DevBuf<uint32_t> tickets; // chained walk: per carry slot, how many workgroups are done with it
   DevBuf<uint32_t> ksnap;   // king cache: per slot x (perspective, king square) a 32-B placement snapshot
   int chain_k = 1;          // block length of the current expansion (1: no chaining)
+  // planned expansion (stream.hip): per-parent entry bounds and their scan, the entry
+  // lists, tile descriptors, the scratch-slot pool and the error word
+  DevBuf<uint64_t> ebound, eoff;
+  DevBuf<uint32_t> ent, pool, perr;
+  DevBuf<TileDesc> tiles;
+  uint64_t etot = 0;        // eoff[n] of the current expansion
+  bool planned = false;     // the last expansion ran the planned kernels (perr is meaningful)
   void *scan_tmp = nullptr;
   size_t scan_bytes = 0;
   // Cross-stream ordering of the library-owned scratch above: every launch sequence
@@ -226,6 +233,17 @@ static hipError_t seq_end(Dev &d, hipStream_t s) {
   if (e == hipSuccess) d.done_on = s;
   return e;
 }
+// After a synchronised planned expansion: its device error word (entry overflow or no
+// scratch slot; neither can happen by construction, but a wrong result must not pass).
+static int check_plan(Dev &d, hipStream_t s) {
+  if (!d.planned || !d.perr.p) return GN_OK;
+  uint32_t e = 0;
+  HIP_TRY(hipMemcpyAsync(&e, d.perr.p, sizeof(e), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  if (e) return fail(GN_E_HIP, "planned expansion failed on the device (error bits 0x%x)", e);
+  return GN_OK;
+}
+
 struct SeqGuard { // seq_begin now, seq_end when the scope ends (d.mu held throughout)
   Dev &d;
   hipStream_t s;
@@ -325,6 +343,7 @@ static void destroy(gn_ctx *ctx) {
     if (d.sort_tmp) (void)hipFree(d.sort_tmp);
     d.kkeys.release(), d.kkeys2.release(), d.kidx.release(), d.kperm.release();
     d.nslot.release(), d.tickets.release(), d.ksnap.release();
+    d.ebound.release(), d.eoff.release(), d.ent.release(), d.pool.release(), d.perr.release(), d.tiles.release();
     if (d.done) (void)hipEventDestroy(d.done);
     if (d.stream) (void)hipStreamDestroy(d.stream);
   }
@@ -478,10 +497,19 @@ static int chain_len(const gn_ctx *ctx, Dev &d, size_t n) {
   return (int)k;
 }
 
+// The big net's expansion runs planned (stream.hip) unless GN_STREAM=old selects the
+// round-1 single-kernel expand_stream (A/B timing); both give identical results.
+static bool plan_path(const gn_ctx *ctx, const Dev &d) {
+  static const bool old = getenv("GN_STREAM") && !strcmp(getenv("GN_STREAM"), "old");
+  static const bool legacy = getenv("GN_EXPAND_LEGACY") && atoi(getenv("GN_EXPAND_LEGACY"));
+  return !old && !legacy && ctx->incremental && d.has[BIG] && (d.net[BIG].L1 == 3072 || d.net[BIG].L1 == 1024);
+}
+
 static int generate_children(Dev &d, const gn_board *parents, size_t n, gn_board *children_or_null, size_t cap,
                              uint16_t *moves, bool want_deltas, size_t *total, hipStream_t s, hipEvent_t *ev,
-                             unsigned long long *rows = nullptr, int chain_k = 1) {
+                             unsigned long long *rows = nullptr, int chain_k = 1, bool plan = false) {
   d.chain_k = want_deltas ? chain_k : 1;
+  d.planned = want_deltas && plan;
   if (d.chain_k > 1) {
     HIP_TRY(d.nslot.ensure(n));
     HIP_TRY(d.tickets.ensure(CARRY_SLOTS + 1));
@@ -490,11 +518,18 @@ static int generate_children(Dev &d, const gn_board *parents, size_t n, gn_board
   HIP_TRY(d.counts.ensure(n + 1));
   HIP_TRY(d.offsets.ensure(n + 1));
   HIP_TRY(hipMemsetAsync(d.counts.p + n, 0, sizeof(uint64_t), s));
-  HIP_TRY(launch_count_children(parents, n, d.tables, d.counts.p, s));
+  if (d.planned) {
+    HIP_TRY(d.ebound.ensure(n + 1));
+    HIP_TRY(d.eoff.ensure(n + 1));
+    HIP_TRY(hipMemsetAsync(d.ebound.p + n, 0, sizeof(uint64_t), s));
+  }
+  HIP_TRY(launch_count_children(parents, n, d.tables, d.counts.p, s, d.planned ? d.ebound.p : nullptr));
   HIP_TRY(exclusive_scan_u64(d.counts.p, d.offsets.p, n + 1, d.scan_tmp, d.scan_bytes, s));
+  if (d.planned) HIP_TRY(exclusive_scan_u64(d.ebound.p, d.eoff.p, n + 1, d.scan_tmp, d.scan_bytes, s));
   if (ev) HIP_TRY(hipEventRecord(ev[0], s));
   uint64_t t = 0;
   HIP_TRY(hipMemcpyAsync(&t, d.offsets.p + n, sizeof(t), hipMemcpyDeviceToHost, s));
+  if (d.planned) HIP_TRY(hipMemcpyAsync(&d.etot, d.eoff.p + n, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
   *total = (size_t)t;
   if (ev) HIP_TRY(hipEventRecord(ev[1], s));
@@ -568,10 +603,23 @@ static int expand_evaluate(gn_ctx *ctx, Dev &d, const gn_board *parents, size_t 
   HIP_TRY(mark(1));
   if (mode != GN_MODE_SMALL) {
     const bool f = mode == GN_MODE_FULL;
-    HIP_TRY(launch_expand_net(d.net[BIG], parents, n, off, children, dl, f ? d.p_nbg.p : nullptr,
-                              f ? d.nbg.p : nullptr, d.p_obg.p, d.obg.p, ctx->swizzle & 1,
-                              d.chain_k > 1 ? d.nslot.p : nullptr, d.tickets.p, d.chain_k,
-                              ctx->king_cache ? d.ksnap.p : nullptr, rows_out, s));
+    if (d.planned) {
+      const size_t K = (size_t)std::max(1, d.chain_k), nblk = (n + K - 1) / K;
+      HIP_TRY(d.ent.ensure(d.etot + 16 * (nblk + 1)));
+      HIP_TRY(d.tiles.ensure((n + total) / 16 + nblk + 2));
+      HIP_TRY(d.pool.ensure(64));
+      HIP_TRY(d.perr.ensure(1));
+      HIP_TRY(hipMemsetAsync(d.perr.p, 0, sizeof(uint32_t), s));
+      HIP_TRY(launch_plan_stream(d.net[BIG], parents, n, off, dl, f ? d.p_nbg.p : nullptr, f ? d.nbg.p : nullptr,
+                                 d.p_obg.p, d.obg.p, ctx->swizzle & 1, d.chain_k > 1 ? d.nslot.p : nullptr,
+                                 d.chain_k, ctx->king_cache ? 1 : 0, d.eoff.p, d.ent.p, d.tiles.p, d.pool.p,
+                                 d.perr.p, rows_out, s));
+    } else {
+      HIP_TRY(launch_expand_net(d.net[BIG], parents, n, off, children, dl, f ? d.p_nbg.p : nullptr,
+                                f ? d.nbg.p : nullptr, d.p_obg.p, d.obg.p, ctx->swizzle & 1,
+                                d.chain_k > 1 ? d.nslot.p : nullptr, d.tickets.p, d.chain_k,
+                                ctx->king_cache ? d.ksnap.p : nullptr, rows_out, s));
+    }
   }
   HIP_TRY(mark(2));
   HIP_TRY(launch_finalize(children, total, mode, d.osm.p, d.obg.p, d.nsm.p, d.nbg.p, P, d.tables, child_out, s));
@@ -740,7 +788,7 @@ static int expand_boards_host(gn_ctx *ctx, const gn_board *boards, size_t n, int
       HIP_TRY(d.moves.ensure(std::max<size_t>(tk, 1)));
       size_t t = 0;
       int r = generate_children(d, d.io_boards.p, m, nullptr, d.moves.cap, d.moves.p, ctx->incremental, &t, s, nullptr,
-                                nullptr, chain_len(ctx, d, m));
+                                nullptr, chain_len(ctx, d, m), plan_path(ctx, d));
       if (r) return r;
       if (t != tk) return fail(GN_E_HIP, "child count changed between passes (%zu != %zu)", t, tk);
       HIP_TRY(d.io_out.ensure(m));
@@ -754,7 +802,7 @@ static int expand_boards_host(gn_ctx *ctx, const gn_board *boards, size_t n, int
       if (parent_out)
         HIP_TRY(hipMemcpyAsync(parent_out + lo, d.io_out.p, m * sizeof(gn_eval), hipMemcpyDeviceToHost, s));
       HIP_TRY(hipStreamSynchronize(s));
-      return GN_OK;
+      return check_plan(d, s);
     });
   } catch (const std::bad_alloc &) {
     return fail(GN_E_NOMEM, "host allocation failed");
@@ -1280,7 +1328,7 @@ int gn_expand_device(gn_ctx *ctx, int device_slot, const gn_board *d_parents, si
   if (!d_children || !d_moves || !d_child_out) return fail(GN_E_INVALID, "NULL child buffer");
   size_t t = 0;
   int rc = generate_children(*d, d_parents, n, d_children, cap, d_moves, ctx->incremental, &t, s, nullptr, nullptr,
-                             chain_len(ctx, *d, n));
+                             chain_len(ctx, *d, n), plan_path(ctx, *d));
   *total = t;
   if (t > 0xFFFFFFFFull) return fail(GN_E_CAPACITY, "%zu children exceed 32-bit offsets", t);
   HIP_TRY(launch_offsets_u32(d->offsets.p, n + 1, d_offsets, s));
@@ -1291,7 +1339,7 @@ int gn_expand_device(gn_ctx *ctx, int device_slot, const gn_board *d_parents, si
   rc = expand_evaluate(ctx, *d, d_parents, n, d_children, t, mode, d_parent_out, d_child_out, s, nullptr);
   if (rc) return rc;
   HIP_TRY(hipStreamSynchronize(s));
-  return GN_OK;
+  return check_plan(*d, s);
 }
 
 int gn_time_expand_device(gn_ctx *ctx, int device_slot, const gn_board *d_parents, size_t n, int mode, int iters,
@@ -1325,7 +1373,7 @@ int gn_time_expand_device(gn_ctx *ctx, int device_slot, const gn_board *d_parent
     he = hipEventRecord(e[0], s);
     if (he != hipSuccess) break;
     rc = generate_children(*d, d_parents, n, nullptr, cap, d_moves, ctx->incremental, &t, s, e + 1,
-                           it == 0 ? d->sum.p : nullptr, chain_len(ctx, *d, n));
+                           it == 0 ? d->sum.p : nullptr, chain_len(ctx, *d, n), plan_path(ctx, *d));
     if (rc) break;
     if (d_child_out && t > cap) {
       rc = fail(GN_E_CAPACITY, "%zu children exceed capacity %zu", t, cap);
@@ -1353,6 +1401,7 @@ int gn_time_expand_device(gn_ctx *ctx, int device_slot, const gn_board *d_parent
   cleanup();
   *total = t;
   if (rc) return rc;
+  if (he == hipSuccess && (rc = check_plan(*d, s)) != GN_OK) return rc;
   if (ft_rows && he == hipSuccess) {
     unsigned long long r[2] = {0, 0};
     he = hipMemcpy(r, d->sum.p, sizeof(r), hipMemcpyDeviceToHost);

@@ -1,0 +1,645 @@
+// stream.hip — the planned expansion of the big nets (default for L1 = 3072 / 1024).
+//
+// The incremental evaluation of every parent and every legal child (SURVEY.md §8a
+// rows a13-a17, "children are derived from the parent accumulator by incremental
+// add/sub deltas") in two kernels:
+//
+//   plan_kernel         one wave per block of consecutive parents (a game): turns the
+//                       block's slots [parent, its children, next parent, ...] into
+//                       two lists of row entries (one per absolute perspective) and a
+//                       descriptor per 16-slot tile, in HBM.  Every decision that is
+//                       sequential inside a block is made here: the sibling cache, the
+//                       chain carry (parent p + 1 starts from parent p's child that is
+//                       its position), the king cache (Stockfish's AccumulatorCaches
+//                       analog: a king-move refresh starts from the accumulator the
+//                       block last computed for that perspective and king square, plus
+//                       the placement difference), the list balance, and every PSQT
+//                       sum (PSQT never enters the row stream).
+//   stream_eval_kernel  one workgroup per block: each perspective group of waves walks
+//                       its list with a 4-deep register ring of row loads, transforms at
+//                       each slot's last entry into the LDS tile, and after each tile
+//                       all waves run fc_0 as int8 MFMAs; one wave per bucket finishes
+//                       fc_1 / fc_2 and writes the outputs while the others stream on.
+//
+// Entry (u32), shared by the two kernels:
+//   [18:0] row: an FT row, or (SCR) a row of the workgroup's scratch slot: 0 / 1 the
+//          carry row of perspective 0 / 1, 2 + 64 h + ksq the king-cache row of (h, ksq)
+//   [19] SUB   [21:20] init before this entry: 0 none, 1 ZERO (lo = row; with SUB: keep,
+//          a store-only entry), 2 PACC (lo = parent - row, saved as the sibling base),
+//          3 BASE (lo = base +- row)   [22] LAST entry of its slot   [26:23] slot in tile
+//   [27] side (0: the perspective to move)   [28] PAR_E (the parent slot: its accumulator
+//   becomes pacc)   [29] NXT (store the slot's accumulator to this list's carry row)
+//   [30] SCR   [31] KST (store the slot's accumulator to the row of this entry)
+// Lists are padded per tile to a multiple of 4 with no-op entries (ZERO | SUB) so every
+// ring step issues the same loads.
+#include "device_util.h"
+#include "kernels.h"
+
+#ifndef GN_EXPAND_WPE
+#define GN_EXPAND_WPE 5
+#endif
+
+namespace gn {
+namespace ps {
+constexpr uint32_t ROW = (1u << 19) - 1, SUB = 1u << 19, I_ZERO = 1u << 20, I_PACC = 2u << 20, I_BASE = 3u << 20,
+                   INIT = 3u << 20, LAST = 1u << 22, SLOT_SH = 23, SIDE_SH = 27, PAR_E = 1u << 28, NXT = 1u << 29,
+                   SCR = 1u << 30, KST = 1u << 31;
+constexpr uint32_t PAD = (uint32_t)FT_BIAS_ROW | I_ZERO | SUB;
+__device__ __forceinline__ uint32_t tmpl(int slot, int side) {
+  return (uint32_t)slot << SLOT_SH | (uint32_t)side << SIDE_SH;
+}
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+} // namespace ps
+
+// ------------------------------------------------------------------- plan --
+template <int L1>
+__global__ void __launch_bounds__(256)
+    plan_kernel(NetDevice net, const gn_board *__restrict__ parents, const uint64_t *__restrict__ offsets,
+                const ChildDelta *__restrict__ deltas, const uint8_t *__restrict__ need_parent,
+                const uint8_t *__restrict__ need_child, const uint8_t *__restrict__ next_slot, uint32_t np, uint32_t K,
+                int kc, const uint64_t *__restrict__ eoff, uint32_t *__restrict__ ent, TileDesc *__restrict__ tiles,
+                unsigned long long *__restrict__ rows_out, uint32_t *__restrict__ err) {
+  using namespace ps;
+  constexpr uint32_t RS = 2 * L1 + 32;
+  __shared__ uint32_t ksnap[4][128][8]; // per wave: placement (64 nibbles) of each king-cache row
+  __shared__ uint8_t kstate[4][128];    // bit 0: row holds an accumulator, bit 1: the list that stored it
+  __shared__ uint16_t prow_s[4][2][32];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint32_t blk = blockIdx.x * 4 + (uint32_t)w;
+  const uint32_t nblk = (np + K - 1) / K;
+  if (blk >= nblk) return; // the whole wave (no workgroup barriers in this kernel)
+  const __amdgpu_buffer_rsrc_t ftr =
+      __builtin_amdgcn_make_buffer_rsrc((void *)net.ft, 0, (int)((size_t)FT_ROWS * RS), 0x00020000);
+  auto psqt = [&](uint32_t row, int bucket) -> int32_t {
+    return (int32_t)__builtin_amdgcn_raw_buffer_load_b32(ftr, row * RS + 2 * L1 + 4 * bucket, 0, 0);
+  };
+  const uint32_t pbeg = blk * K, pend = pbeg + K < np ? pbeg + K : np;
+  const uint64_t us_b = pbeg + offsets[pbeg];
+  const uint64_t rbeg = eoff[pbeg] + 16ull * blk, rend = eoff[pend] + 16ull * (blk + 1);
+  uint32_t *E0 = ent + rbeg, *E1 = ent + rend - 1;
+  TileDesc *T = tiles + us_b / 16 + blk;
+  auto put = [&](int g, uint32_t i, uint32_t v) {
+    if (g) E1[-(int64_t)i] = v;
+    else E0[i] = v;
+  };
+  for (int i = lane; i < 128; i += 64) kstate[w][i] = 0;
+  uint16_t(*prow)[32] = prow_s[w];
+  uint32_t len0 = 0, len1 = 0, tile_k = 0, p_first = pbeg;
+  int t_fill = 0, carried = 0;
+  unsigned long long rows = 0;
+
+  auto flush = [&]() {
+    // pad both lists of the tile to a multiple of 4 with no-op entries
+    if (lane < 3) {
+      if (len0 + lane < ((len0 + 3) & ~3u)) put(0, len0 + lane, PAD);
+      if (len1 + lane < ((len1 + 3) & ~3u)) put(1, len1 + lane, PAD);
+    }
+    len0 = (len0 + 3) & ~3u, len1 = (len1 + 3) & ~3u;
+    TileDesc *d = T + tile_k;
+    if (lane >= t_fill && lane < 16) d->meta[lane] = 0;
+    if (lane == 0) d->e_end[0] = len0, d->e_end[1] = len1, d->p_first = p_first, d->nslots = (uint32_t)t_fill;
+    ++tile_k, t_fill = 0;
+  };
+
+  for (uint32_t p = pbeg; p < pend; ++p) {
+    const uint64_t off = offsets[p];
+    const int nch = (int)(offsets[p + 1] - off), total = 1 + nch;
+    const gn_board pb = parents[p];
+    const int P = wave_features(pb, prow[0], prow[1], lane);
+    ps::wave_sync();
+    int want = 0;
+    for (int q = lane; q < total; q += 64)
+      want |= q == 0 ? (need_parent ? need_parent[p] : 1) : (need_child ? need_child[off + q - 1] : 1);
+    const bool live = __ballot(want) != 0 && P != 0;
+    const int have = live ? carried : 0;
+    carried = 0;
+    const int stm = pb.stm_ep >> 7;
+    const int bp = P ? (P - 1) / 4 : 0, b2 = P >= 2 ? (P - 2) / 4 : bp;
+    // parent PSQT per perspective at the two buckets its children can have (lane = (h, row))
+    int32_t pp[2][2] = {{0, 0}, {0, 0}};
+    int nxq = -1; // slot (1 + child index) of the child that is the next parent
+    if (live) {
+      const int hh = lane >> 5, k = lane & 31;
+      int32_t a = 0, b = 0;
+      if (k < P) a = psqt(prow[hh][k], bp), b = psqt(prow[hh][k], b2);
+#pragma unroll
+      for (int o = 16; o; o >>= 1) a = wadd(a, __shfl_xor(a, o)), b = wadd(b, __shfl_xor(b, o));
+      pp[0][0] = __builtin_amdgcn_readlane(a, 0), pp[0][1] = __builtin_amdgcn_readlane(b, 0);
+      pp[1][0] = __builtin_amdgcn_readlane(a, 32), pp[1][1] = __builtin_amdgcn_readlane(b, 32);
+      if (K > 1 && p + 1 < pend) {
+        const int ns = next_slot[p];
+        if (ns != 255 && ns < nch && (!need_child || need_child[off + ns])) nxq = ns + 1;
+      }
+      carried = nxq > 0;
+    }
+    int ckey0 = -1, ckey1 = -1; // sibling keys carried across this parent's segments
+
+    for (int q0 = 0; q0 < total;) {
+      if (t_fill == 0) p_first = p;
+      const int seg = 16 - t_fill < total - q0 ? 16 - t_fill : total - q0;
+      const int q = q0 + lane, t = t_fill + lane;
+      const bool in = lane < seg;
+      // ---- descriptor of this lane's slot
+      int vld = 0, cst = 0, cnt = 1, kinds = 0, n0 = 0, n1 = 0, s0 = 0, s1 = 0;
+      uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
+      if (in && live) {
+        if (q == 0) {
+          vld = need_parent ? need_parent[p] : 1;
+          cst = stm, cnt = P, kinds = 3 | 3 << 2;
+        } else if ((vld = need_child ? need_child[off + q - 1] : 1)) {
+          const uint32_t *src = reinterpret_cast<const uint32_t *>(deltas + off + q - 1);
+          w0 = src[0], w1 = src[1], w2 = src[2], w3 = src[3];
+          const uint32_t meta = src[4];
+          cst = (meta >> 10) & 1;
+          cnt = (meta >> 14) & 63;
+          if (meta & (1u << 8)) kinds |= 2, n0 = cnt + 1;
+          else kinds |= 1, s0 = meta & 3, n0 = s0 + ((meta >> 2) & 3);
+          if (meta & (1u << 9)) kinds |= 2 << 2, n1 = cnt + 1;
+          else kinds |= 1 << 2, s1 = (meta >> 4) & 3, n1 = s1 + ((meta >> 6) & 3);
+        }
+      }
+      const int bk = (cnt - 1) / 4;
+      // ---- sibling cache: a delta child whose from-row equals the previous delta child's (in
+      // the same list) starts from the cached (parent - from-row) and drops that entry
+      const int key0 = (kinds & 3) == 1 ? (int)(w0 & 0xFFFF) : -1;
+      const int key1 = (kinds >> 2) == 1 ? (int)(w2 & 0xFFFF) : -1;
+      const uint64_t km0 = __ballot(key0 >= 0), km1 = __ballot(key1 >= 0), lt = (1ull << lane) - 1;
+      const int pk0 = __shfl(key0, (km0 & lt) ? 63 - __builtin_clzll(km0 & lt) : 0);
+      const int pk1 = __shfl(key1, (km1 & lt) ? 63 - __builtin_clzll(km1 & lt) : 0);
+      const bool hit0 = key0 >= 0 && key0 == ((km0 & lt) ? pk0 : ckey0);
+      const bool hit1 = key1 >= 0 && key1 == ((km1 & lt) ? pk1 : ckey1);
+      if (km0) ckey0 = __builtin_amdgcn_readlane(key0, 63 - __builtin_clzll(km0));
+      if (km1) ckey1 = __builtin_amdgcn_readlane(key1, 63 - __builtin_clzll(km1));
+      // ---- entries of the parent and of delta perspectives (prefix sums over the lanes)
+      const bool ref0 = (kinds & 3) == 2, ref1 = (kinds >> 2) == 2;
+      int d0 = 0, d1 = 0;
+      if (kinds == 15) d0 = d1 = have ? 1 : P + 1;
+      else {
+        if ((kinds & 3) == 1) d0 = n0 - (hit0 ? 1 : 0);
+        if ((kinds >> 2) == 1) d1 = n1 - (hit1 ? 1 : 0);
+      }
+      const uint32_t c = (uint32_t)d0 | (uint32_t)d1 << 16;
+      uint32_t inc = c;
+#pragma unroll
+      for (int dd = 1; dd < 64; dd <<= 1) {
+        const uint32_t o = __shfl_up(inc, dd);
+        if (lane >= dd) inc += o;
+      }
+      const uint32_t exc = inc - c, tot = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+      const uint32_t t0w = tmpl(t, cst != 0), t1w = tmpl(t, cst != 1);
+      const bool nx = q == nxq;
+      if (in && live) {
+        auto delta = [&](int g, uint32_t at, uint32_t lo2, uint32_t hi2, int s, int n, bool hit, uint32_t tw,
+                         uint32_t L) {
+          const uint32_t i0 = lo2 & 0xFFFF, i1 = lo2 >> 16, i2 = hi2 & 0xFFFF, i3 = hi2 >> 16;
+          auto cl = [](uint32_t r) { return r < (uint32_t)FT_INPUTS ? r : (uint32_t)FT_BIAS_ROW; };
+          const uint32_t r1 = cl(s >= 2 ? i1 : i2), r2 = cl(s >= 2 ? i2 : i3), r3 = cl(i3);
+          const uint32_t f1 = s >= 2 ? SUB : 0u;
+          if (!hit) {
+            put(g, at, cl(i0) | tw | SUB | I_PACC | (n == 1 ? L : 0u));
+            if (n > 1) put(g, at + 1, r1 | tw | f1 | (n == 2 ? L : 0u));
+            if (n > 2) put(g, at + 2, r2 | tw | (n == 3 ? L : 0u));
+            if (n > 3) put(g, at + 3, r3 | tw | L);
+          } else { // the from-row is in the cached base
+            put(g, at, r1 | tw | f1 | I_BASE | (n == 2 ? L : 0u));
+            if (n > 2) put(g, at + 1, r2 | tw | (n == 3 ? L : 0u));
+            if (n > 3) put(g, at + 2, r3 | tw | L);
+          }
+        };
+        if ((kinds & 3) == 1) delta(0, len0 + (exc & 0xFFFF), w0, w1, s0, n0, hit0, t0w, LAST | (nx ? NXT : 0u));
+        if ((kinds >> 2) == 1) delta(1, len1 + (exc >> 16), w2, w3, s1, n1, hit1, t1w, LAST | (nx ? NXT : 0u));
+        if (kinds == 15) {
+          if (have) { // the parent from the carry rows: one entry per list
+            put(0, len0 + (exc & 0xFFFF), SCR | 0u | t0w | I_ZERO | PAR_E | LAST);
+            put(1, len1 + (exc >> 16), SCR | 1u | t1w | I_ZERO | PAR_E | LAST);
+          } else { // bias entry; the parent's rows follow (below, lane = row)
+            put(0, len0 + (exc & 0xFFFF), (uint32_t)FT_BIAS_ROW | t0w | I_ZERO | PAR_E);
+            put(1, len1 + (exc >> 16), (uint32_t)FT_BIAS_ROW | t1w | I_ZERO | PAR_E);
+          }
+        }
+        // PSQT of the slot by side (a king-move perspective is written by its job below)
+        int32_t v[2] = {0, 0};
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+          const int kd = hh ? kinds >> 2 : kinds & 3;
+          if (kd == 3) v[hh] = pp[hh][0];
+          if (kd == 1) {
+            const uint32_t lo2 = hh ? w2 : w0, hi2 = hh ? w3 : w1;
+            const int s = hh ? s1 : s0, n = hh ? n1 : n0;
+            const uint32_t i0 = lo2 & 0xFFFF, i1 = lo2 >> 16, i2 = hi2 & 0xFFFF, i3 = hi2 >> 16;
+            const uint32_t r1 = s >= 2 ? i1 : i2, r2 = s >= 2 ? i2 : i3;
+            const int32_t a0 = psqt(ft_row(i0), bk), a1 = psqt(ft_row(r1), bk);
+            const int32_t a2 = n > 2 ? psqt(ft_row(r2), bk) : 0, a3 = n > 3 ? psqt(ft_row(i3), bk) : 0;
+            v[hh] = wadd(pp[hh][bk == bp ? 0 : 1], wadd(wadd(-a0, s >= 2 ? -a1 : a1), wadd(a2, a3)));
+          }
+          if (kd != 2) T[tile_k].psq[t][hh != cst] = v[hh];
+        }
+      }
+      if (in) T[tile_k].meta[t] = (uint8_t)((in && live && vld ? 1 : 0) | bk << 1 | (q == 0 ? 16 : 0));
+      // the parent's rows (lane = row) after its bias entry (the parent is lane 0 of its segment)
+      if (live && q0 == 0 && !have) {
+        const uint32_t tp0 = tmpl(t_fill, stm != 0), tp1 = tmpl(t_fill, stm != 1);
+        if (lane < P) {
+          put(0, len0 + 1 + lane, ft_row(prow[0][lane]) | tp0 | PAR_E | (lane == P - 1 ? LAST : 0u));
+          put(1, len1 + 1 + lane, ft_row(prow[1][lane]) | tp1 | PAR_E | (lane == P - 1 ? LAST : 0u));
+        }
+      }
+      len0 += tot & 0xFFFF, len1 += tot >> 16;
+      rows += (tot & 0xFFFF) + (tot >> 16);
+      // ---- king-move refreshes, one job per slot in slot order, lane = square
+      uint64_t jm = __ballot(in && live && vld && (ref0 || ref1));
+      while (jm) {
+        const int l = __builtin_ctzll(jm);
+        jm &= jm - 1;
+        const int hh = __builtin_amdgcn_readlane((int)ref1, l), st = __builtin_amdgcn_readlane(cst, l);
+        const int cn = __builtin_amdgcn_readlane(cnt, l), tl = t_fill + l;
+        const bool nxl = q0 + l == nxq;
+        const uint32_t sq01 = (uint32_t)__builtin_amdgcn_readlane((int)(hh ? w2 : w0), l),
+                       sq23 = (uint32_t)__builtin_amdgcn_readlane((int)(hh ? w3 : w1), l);
+        const int kt = (int)(sq01 >> 16);
+        int pos, cpc;
+        const int row = king_move_row(pb, hh, sq01 & 0xFFFF, kt, sq23 & 0xFFFF, sq23 >> 16, lane, pos, &cpc);
+        const int cb = (cn - 1) / 4;
+        const int32_t ps_sum = wave_sum(row >= 0 ? psqt((uint32_t)row, cb) : 0);
+        if (lane == 0) T[tile_k].psq[tl][hh != st] = ps_sum;
+        const uint32_t tw = tmpl(tl, hh != st);
+        const bool kuse = kc && (sq23 & 0xFFFF) == 64; // not castling
+        const int kci = 64 * hh + kt;
+        const int kst = kuse ? kstate[w][kci] : 0;
+        bool hit = false;
+        uint64_t bs = 0, ba = 0;
+        int spc = 0;
+        if (kst & 1) {
+          const uint32_t wv = lane < 8 ? ksnap[w][kci][lane] : 0u;
+          spc = (int)((__shfl(wv, lane >> 3) >> (4 * (lane & 7))) & 15);
+          bs = __ballot(spc != cpc && spc != 0);
+          ba = __ballot(spc != cpc && cpc != 0);
+          const int nd = popcnt(bs) + popcnt(ba);
+          hit = nd < cn && (!nxl || ((kst >> 1) & 1) == hh);
+        }
+        const int g = hit ? (kst >> 1) & 1 : nxl ? hh : (len0 <= len1 ? 0 : 1);
+        const uint32_t base = g ? len1 : len0;
+        const uint32_t L = LAST | (nxl ? NXT : 0u);
+        const uint32_t krow = SCR | (uint32_t)(2 + kci);
+        int ne;
+        if (hit) {
+          const int nd = popcnt(bs) + popcnt(ba);
+          ne = nd + 2;
+          const int ps = 1 + popcnt(bs & lt), pa = 1 + popcnt(bs) + popcnt(ba & lt);
+          if (lane == 0) put(g, base, krow | tw | I_ZERO);
+          if ((bs >> lane) & 1) put(g, base + ps, (uint32_t)feature_index(hh, lane, spc, kt) | tw | SUB);
+          if ((ba >> lane) & 1) put(g, base + pa, (uint32_t)row | tw);
+          if (lane == 0) put(g, base + ne - 1, krow | tw | I_ZERO | SUB | KST | L);
+          rows += (unsigned long long)(nd + 1);
+        } else {
+          ne = cn + 1 + (kuse ? 1 : 0);
+          if (lane == 0) put(g, base, (uint32_t)FT_BIAS_ROW | tw | I_ZERO);
+          if (row >= 0 && pos < cn) put(g, base + 1 + pos, (uint32_t)row | tw | (!kuse && pos == cn - 1 ? L : 0u));
+          if (kuse && lane == 0) put(g, base + ne - 1, krow | tw | I_ZERO | SUB | KST | L);
+          rows += (unsigned long long)(cn + 1);
+        }
+        if (kuse) { // the cache row now holds this child's accumulator, stored by list g
+          uint32_t x = (uint32_t)cpc << (4 * (lane & 7));
+          x |= __shfl_xor(x, 1);
+          x |= __shfl_xor(x, 2);
+          x |= __shfl_xor(x, 4);
+          if ((lane & 7) == 0) ksnap[w][kci][lane >> 3] = x;
+          if (lane == 0) kstate[w][kci] = (uint8_t)(1 | g << 1);
+          ps::wave_sync();
+        }
+        if (g) len1 += (uint32_t)ne;
+        else len0 += (uint32_t)ne;
+      }
+      t_fill += seg, q0 += seg;
+      if (t_fill == 16) flush();
+    }
+  }
+  if (t_fill) flush();
+  if (lane == 0) {
+    if ((uint64_t)len0 + len1 > rend - rbeg) atomicOr(err, 1u); // cannot happen: eoff bounds the entries
+    if (rows_out) atomicAdd(rows_out, rows);
+  }
+}
+
+// ----------------------------------------------------------------- stream --
+template <int L1>
+__global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_EXPAND_WPE)))
+    stream_eval_kernel(NetDevice net, const uint64_t *__restrict__ offsets, uint32_t np, uint32_t K, int swz,
+                       const uint64_t *__restrict__ eoff, const uint32_t *__restrict__ ent,
+                       const TileDesc *__restrict__ tiles, int2 *__restrict__ out_parent, int2 *__restrict__ out_child,
+                       uint32_t *__restrict__ pool, int use_scr, uint32_t *__restrict__ err) {
+  using namespace ps;
+  constexpr int G = L1 / 16; // threads per perspective group (whole waves)
+  constexpr int NT = 2 * G, NW = NT / 64, TILE = 16, XS = L1 + 16, KS = L1 / 64, KPW = KS / NW;
+  constexpr uint32_t RS = 2 * L1 + 32;
+  static_assert(G % 64 == 0 && KS % NW == 0 && KPW % 2 == 0, "geometry");
+  __shared__ __attribute__((aligned(16))) uint8_t xt[TILE * XS];
+  __shared__ int32_t acc0[2][256];
+  __shared__ __attribute__((aligned(16))) uint8_t in1[2][TILE][32];
+  __shared__ int32_t fwd[2][TILE];
+  __shared__ uint32_t sslot;
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hu = __builtin_amdgcn_readfirstlane((tid / G) & 1);
+  const __amdgpu_buffer_rsrc_t ftr = __builtin_amdgcn_make_buffer_rsrc(
+      (void *)net.ft, 0, (int)(((size_t)FT_ROWS + (size_t)SCR_ROWS * SCR_SLOTS) * RS), 0x00020000);
+  for (int i = tid; i < 512; i += NT) (&acc0[0][0])[i] = 0;
+  const uint32_t nblk = (np + K - 1) / K;
+  const uint32_t vgrid = swz ? 8 * ((nblk + 7) / 8) : nblk;
+  uint32_t v = blockIdx.x;
+  if (v >= vgrid) return;
+  uint32_t blk = v;
+  if (swz) {
+    const uint32_t b8 = (nblk + 7) / 8;
+    blk = (v & 7) * b8 + (v >> 3);
+    if (blk >= nblk) return;
+  }
+  const uint32_t pbeg = blk * K, pend = pbeg + K < np ? pbeg + K : np;
+  const uint64_t us_b = pbeg + offsets[pbeg], us_e = pend + offsets[pend];
+  const uint32_t ntiles = (uint32_t)((us_e - us_b + 15) / 16);
+  const TileDesc *T = tiles + us_b / 16 + blk;
+  const uint64_t rbeg = eoff[pbeg] + 16ull * blk, rend = eoff[pend] + 16ull * (blk + 1);
+  const __amdgpu_buffer_rsrc_t er_ = __builtin_amdgcn_make_buffer_rsrc((void *)(ent + rbeg), 0,
+                                                                       (int)((rend - rbeg) * 4), 0x00020000);
+  const uint32_t rsz = (uint32_t)(rend - rbeg);
+  // ---- scratch slot (carry + king-cache rows) from this XCD's pool: never waits on another
+  // workgroup; the pool (POOL_PER_XCD slots) outnumbers the workgroups an XCD holds
+  uint32_t scr = 0, my_slot = 0;
+  if (use_scr) {
+    if (tid == 0) {
+      uint32_t x;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+      x &= 7;
+      uint32_t *wd = pool + 8 * x;
+      int got = -1;
+      for (int it = 0; it < 4096 && got < 0; ++it) {
+        const int wi = (int)((it + (v >> 3)) & 7);
+        uint32_t cur = __hip_atomic_load(wd + wi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        while (cur != 0xFFFFFFFFu) {
+          const int bit = __builtin_ctz(~cur);
+          const uint32_t old = __hip_atomic_fetch_or(wd + wi, 1u << bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (!(old & (1u << bit))) {
+            got = (int)(x * POOL_PER_XCD + 32 * wi + bit);
+            break;
+          }
+          cur = old | (1u << bit);
+        }
+        if (got < 0 && wi == 7) __builtin_amdgcn_s_sleep(4);
+      }
+      if (got < 0) atomicOr(err, 2u), got = 0; // cannot happen (pool > resident workgroups); reported
+      sslot = (uint32_t)got;
+    }
+    __syncthreads();
+    my_slot = sslot;
+    scr = (uint32_t)FT_ROWS + (uint32_t)SCR_ROWS * my_slot;
+  }
+
+  // ---- per-thread stream state across the block's tiles
+  ushort8 pacc_lo = {}, pacc_hi = {}, base_lo = {}, base_hi = {};
+  uint32_t es = 0;              // this group's position in its list
+  uint32_t cur_c = 0xFFFFFFFFu; // entry chunk (64 entries) held in ev, the next one in evn
+  uint32_t ev = 0, evn = 0;
+  uint32_t bq = 0; // buckets done (acc0 / in1 / fwd buffer parity)
+  auto chunk = [&](uint32_t c) -> uint32_t {
+    int tl = tid;
+    asm volatile("" : "+v"(tl));
+    const uint32_t i = c * 64 + (uint32_t)(tl & 63);
+    return __builtin_amdgcn_raw_buffer_load_b32(er_, 4 * (hu ? rsz - 1 - i : i), 0, 0);
+  };
+
+#pragma unroll 1
+  for (uint32_t k = 0; k < ntiles; ++k) {
+    const TileDesc *D = T + k;
+    const uint32_t e_end = __builtin_amdgcn_readfirstlane(D->e_end[hu]);
+    const uint32_t p_first = __builtin_amdgcn_readfirstlane(D->p_first);
+    uint32_t mw[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      mw[i] = (uint32_t)__builtin_amdgcn_readfirstlane((int)reinterpret_cast<const uint32_t *>(D->meta)[i]);
+    // ---- the row stream of this group's list segment
+    {
+      int tl = tid;
+      asm volatile("" : "+v"(tl));
+      const int jt = tl % G;
+      const uint32_t j16 = 16 * jt;
+      const uint32_t n = e_end - es;
+      ushort8 rlo[4], rhi[4];
+      uint32_t er[4];
+      ushort8 lo = {}, hi = {};
+      auto issue = [&](int r, uint32_t i) {
+        const uint32_t c = i >> 6;
+        if (c != cur_c) { // scalar branch: next chunk (prefetched) and the one after
+          if (c == cur_c + 1) ev = evn;
+          else ev = chunk(c);
+          evn = chunk(c + 1);
+          cur_c = c;
+        }
+        const uint32_t e = er[r] = (uint32_t)__builtin_amdgcn_readlane((int)ev, (int)(i & 63));
+        const uint32_t row = (e & SCR) ? scr + (e & ROW) : (e & ROW);
+        rlo[r] = __builtin_bit_cast(ushort8, __builtin_amdgcn_raw_buffer_load_b128(ftr, j16, row * RS, 0));
+        rhi[r] = __builtin_bit_cast(ushort8, __builtin_amdgcn_raw_buffer_load_b128(ftr, j16 + L1, row * RS, 0));
+      };
+      auto consume = [&](int r) {
+        const uint32_t e = er[r];
+        const uint32_t init = e & INIT;
+        // scalar branches; the empty asm keeps the compiler from if-converting them into
+        // selects over every alternative
+        if (init == I_ZERO) {
+          asm volatile("");
+          if (!(e & SUB)) lo = rlo[r], hi = rhi[r];
+        } else if (init == I_PACC) {
+          asm volatile("");
+          lo = pacc_lo - rlo[r], hi = pacc_hi - rhi[r];
+          base_lo = lo, base_hi = hi;
+        } else if (init == I_BASE) {
+          if (e & SUB) {
+            asm volatile("");
+            lo = base_lo - rlo[r], hi = base_hi - rhi[r];
+          } else {
+            asm volatile("");
+            lo = base_lo + rlo[r], hi = base_hi + rhi[r];
+          }
+        } else if (e & SUB) {
+          asm volatile("");
+          lo -= rlo[r], hi -= rhi[r];
+        } else {
+          asm volatile("");
+          lo += rlo[r], hi += rhi[r];
+        }
+        if (e & LAST) {
+          const int sl = (e >> SLOT_SH) & 15, side = (e >> SIDE_SH) & 1;
+          *reinterpret_cast<uint2 *>(xt + sl * XS + side * (L1 / 2) + 8 * jt) = transform8(lo, hi);
+          if (e & PAR_E) {
+            asm volatile("");
+            pacc_lo = lo, pacc_hi = hi;
+          }
+          if (e & (KST | NXT)) { // accumulator stores: king-cache row and / or this list's carry row
+            asm volatile("");
+            uint32_t so = (scr + (uint32_t)hu) * RS;
+            if (e & KST) so = (scr + (e & ROW)) * RS;
+            for (int rep = (e & KST) && (e & NXT) ? 2 : 1; rep; --rep) {
+              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(int4v, lo), ftr, j16, so, 0);
+              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(int4v, hi), ftr, j16 + L1, so, 0);
+              so = (scr + (uint32_t)hu) * RS;
+            }
+          }
+        }
+      };
+      if (n) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) issue(r, es + (uint32_t)r);
+#pragma unroll 1
+        for (uint32_t i = 0; i + 4 < n; i += 4) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            consume(r);
+            issue(r, es + i + 4 + (uint32_t)r);
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) consume(r);
+      }
+      es = e_end;
+    }
+    __syncthreads();
+    // ---- layer stack: per bucket of the tile, fc_0 by all waves (int8 MFMA over this wave's
+    // k-steps, partial sums by LDS integer atomics, exact), then one wave finishes it
+    uint32_t bm = 0, pm = 0;
+#pragma unroll
+    for (int sl = 0; sl < TILE; ++sl) {
+      const uint32_t m = (mw[sl >> 2] >> (8 * (sl & 3))) & 0xFF;
+      if (m & 1) bm |= 1u << ((m >> 1) & 7);
+      if (m & 16) pm |= 1u << sl;
+    }
+    const uint64_t u0 = us_b + 16ull * k;
+#pragma unroll 1
+    for (uint32_t mm = bm; mm; mm &= mm - 1) {
+      const int b = __builtin_ctz(mm);
+      const int buf = (int)(bq & 1);
+      int tl = tid;
+      asm volatile("" : "+v"(tl));
+      const int ln = tl & 63, row = ln & 15, kg = ln >> 4;
+      {
+        const uint8_t *xa = xt + row * XS + kg * 16 + 64 * KPW * wave;
+        const int8_t *wb = net.w0 + ((size_t)b * 16 + row) * L1 + kg * 16 + 64 * KPW * wave;
+        int4v acc = {0, 0, 0, 0};
+#pragma unroll
+        for (int k0 = 0; k0 < KPW; k0 += 4) {
+          int4v wv[4], av[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) wv[j] = k0 + j < KPW ? *reinterpret_cast<const int4v *>(wb + 64 * (k0 + j)) : int4v{};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) av[j] = k0 + j < KPW ? *reinterpret_cast<const int4v *>(xa + 64 * (k0 + j)) : int4v{};
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (k0 + j < KPW) acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(av[j], wv[j], acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) atomicAdd(&acc0[buf][(4 * kg + i) * 16 + row], acc[i]);
+      }
+      __syncthreads();
+      if (wave == (int)(bq % NW)) { // fc_0 activations, fc_1, fc_2, outputs of bucket b
+        const int32_t bias0 = net.b0[b * 16 + row];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int pos = 4 * kg + i;
+          const int32_t vv = wadd(acc0[buf][pos * 16 + row], bias0);
+          if (row < 15) {
+            const long long s2 = ((long long)vv * vv) >> 19;
+            in1[buf][pos][row] = (uint8_t)(s2 < 127 ? s2 : 127);
+            in1[buf][pos][15 + row] = (uint8_t)clampi(vv >> 6, 0, 127);
+          } else {
+            fwd[buf][pos] = wmul(vv, 600 * 16) / (127 * 64);
+            in1[buf][pos][30] = 0;
+            in1[buf][pos][31] = 0;
+          }
+        }
+        ps::wave_sync();
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc0[buf][(4 * kg + i) * 16 + row] = 0; // free for bucket bq + 2
+        const int4v zero = {0, 0, 0, 0};
+        int4v wl = zero, wh = zero, a1 = zero;
+        if (kg < 2) {
+          wl = *reinterpret_cast<const int4v *>(net.w1 + ((size_t)b * 32 + row) * 32 + kg * 16);
+          wh = *reinterpret_cast<const int4v *>(net.w1 + ((size_t)b * 32 + 16 + row) * 32 + kg * 16);
+          a1 = *reinterpret_cast<const int4v *>(&in1[buf][row][kg * 16]);
+        }
+        const int4v cl = __builtin_amdgcn_mfma_i32_16x16x64_i8(a1, wl, zero, 0, 0, 0);
+        const int4v ch = __builtin_amdgcn_mfma_i32_16x16x64_i8(a1, wh, zero, 0, 0, 0);
+        const int32_t b1l = net.b1[b * 32 + row], b1h = net.b1[b * 32 + 16 + row];
+        const int32_t w2l = net.w2[b * 32 + row], w2h = net.w2[b * 32 + 16 + row];
+        int32_t part[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int32_t l = clampi(wadd(cl[i], b1l) >> 6, 0, 127), hh = clampi(wadd(ch[i], b1h) >> 6, 0, 127);
+          part[i] = w2l * l + w2h * hh;
+        }
+#pragma unroll
+        for (int off = 8; off; off >>= 1)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) part[i] = wadd(part[i], __shfl_xor(part[i], off, 16));
+        if (row == 0) {
+          const int32_t b2v = net.b2[b];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int pos = 4 * kg + i;
+            const uint32_t m = (mw[pos >> 2] >> (8 * (pos & 3))) & 0xFF;
+            if ((m & 1) && (int)((m >> 1) & 7) == b) {
+              const int32_t positional = wadd(wadd(b2v, part[i]), fwd[buf][pos]);
+              const int32_t psqt = (int32_t)((uint32_t)D->psq[pos][0] - (uint32_t)D->psq[pos][1]) / 2;
+              const int2 val = make_int2(psqt / 16, positional / 16);
+              const uint32_t P = p_first + (uint32_t)__builtin_popcount(pm & ((2u << pos) - 1)) - (pm & 1);
+              if ((pm >> pos) & 1) out_parent[P] = val;
+              else out_child[u0 + pos - P - 1] = val;
+            }
+          }
+        }
+      }
+      ++bq;
+    }
+  }
+  if (use_scr) { // every wave's stores are complete before the slot goes back to the pool
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0)
+      __hip_atomic_fetch_and(pool + 8 * (my_slot / POOL_PER_XCD) + (my_slot % POOL_PER_XCD) / 32,
+                             ~(1u << (my_slot % 32)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+hipError_t launch_plan_stream(const NetDevice &net, const gn_board *parents, size_t n, const uint64_t *offsets,
+                              const ChildDelta *deltas, const uint8_t *need_parent, const uint8_t *need_child,
+                              int2 *out_parent, int2 *out_child, int swz, const uint8_t *next_slot, int chain_k,
+                              int kc, const uint64_t *eoff, uint32_t *ent, TileDesc *tiles, uint32_t *pool,
+                              uint32_t *err, unsigned long long *rows_out, hipStream_t s) {
+  if (!n) return hipSuccess;
+  if (n >= 0x80000000ull) return hipErrorInvalidValue; // 32-bit parent indices in the kernels
+  const uint32_t K = chain_k > 1 && next_slot ? (uint32_t)chain_k : 1u;
+  const int scr = K > 1 || kc; // carry rows or king cache in use
+  const uint32_t nblk = (uint32_t)((n + K - 1) / K);
+  hipError_t e = hipMemsetAsync(pool, 0, 64 * sizeof(uint32_t), s);
+  if (e != hipSuccess) return e;
+  const unsigned pg = (nblk + 3) / 4, g = swz ? 8 * ((nblk + 7) / 8) : nblk;
+  if (net.L1 == 3072) {
+    hipLaunchKernelGGL((plan_kernel<3072>), dim3(pg), dim3(256), 0, s, net, parents, offsets, deltas, need_parent,
+                       need_child, K > 1 ? next_slot : nullptr, (uint32_t)n, K, K > 1 ? kc : 0, eoff, ent, tiles,
+                       rows_out, err);
+    hipLaunchKernelGGL((stream_eval_kernel<3072>), dim3(g), dim3(384), 0, s, net, offsets, (uint32_t)n, K, swz, eoff,
+                       ent, tiles, out_parent, out_child, pool, scr, err);
+  } else if (net.L1 == 1024) {
+    hipLaunchKernelGGL((plan_kernel<1024>), dim3(pg), dim3(256), 0, s, net, parents, offsets, deltas, need_parent,
+                       need_child, K > 1 ? next_slot : nullptr, (uint32_t)n, K, K > 1 ? kc : 0, eoff, ent, tiles,
+                       rows_out, err);
+    hipLaunchKernelGGL((stream_eval_kernel<1024>), dim3(g), dim3(128), 0, s, net, offsets, (uint32_t)n, K, swz, eoff,
+                       ent, tiles, out_parent, out_child, pool, scr, err);
+  } else {
+    return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+} // namespace gn
