@@ -31,7 +31,10 @@
 //   becomes pacc)   [29] NXT (store the slot's accumulator to this list's carry row)
 //   [30] SCR   [31] KST (store the slot's accumulator to the row of this entry)
 // Lists are padded per tile to a multiple of 4 with no-op entries (ZERO | SUB) so every
-// ring step issues the same loads.
+// ring step issues the same loads.  The ring issues a row load 4 entries before it
+// consumes it, so an entry that loads a scratch row sits at least 4 entries after the
+// last store to scratch in its list (no-op entries are inserted when needed): the load
+// is then issued after the store, by the same lanes.  Tiles restart the ring.
 #include "device_util.h"
 #include "kernels.h"
 
@@ -89,8 +92,16 @@ __global__ void __launch_bounds__(256)
   for (int i = lane; i < 128; i += 64) kstate[w][i] = 0;
   uint16_t(*prow)[32] = prow_s[w];
   uint32_t len0 = 0, len1 = 0, tile_k = 0, p_first = pbeg;
+  uint32_t safe0 = 0, safe1 = 0; // first index of each list at which a scratch row may be loaded
   int t_fill = 0, carried = 0;
   unsigned long long rows = 0;
+  auto pad_to = [&](int g, uint32_t target) { // no-op entries up to target (lane-parallel, < 64)
+    uint32_t &len = g ? len1 : len0;
+    if (len < target) {
+      if ((uint32_t)lane < target - len) put(g, len + lane, PAD);
+      len = target;
+    }
+  };
 
   auto flush = [&]() {
     // pad both lists of the tile to a multiple of 4 with no-op entries
@@ -99,6 +110,7 @@ __global__ void __launch_bounds__(256)
       if (len1 + lane < ((len1 + 3) & ~3u)) put(1, len1 + lane, PAD);
     }
     len0 = (len0 + 3) & ~3u, len1 = (len1 + 3) & ~3u;
+    safe0 = safe1 = 0; // the next tile restarts the ring after these stores were consumed
     TileDesc *d = T + tile_k;
     if (lane >= t_fill && lane < 16) d->meta[lane] = 0;
     if (lane == 0) d->e_end[0] = len0, d->e_end[1] = len1, d->p_first = p_first, d->nslots = (uint32_t)t_fill;
@@ -175,6 +187,10 @@ __global__ void __launch_bounds__(256)
       if (km0) ckey0 = __builtin_amdgcn_readlane(key0, 63 - __builtin_clzll(km0));
       if (km1) ckey1 = __builtin_amdgcn_readlane(key1, 63 - __builtin_clzll(km1));
       // ---- entries of the parent and of delta perspectives (prefix sums over the lanes)
+      if (live && q0 == 0 && have) { // the parent loads the carry rows: after their stores
+        pad_to(0, safe0);
+        pad_to(1, safe1);
+      }
       const bool ref0 = (kinds & 3) == 2, ref1 = (kinds >> 2) == 2;
       int d0 = 0, d1 = 0;
       if (kinds == 15) d0 = d1 = have ? 1 : P + 1;
@@ -248,6 +264,17 @@ __global__ void __launch_bounds__(256)
           put(1, len1 + 1 + lane, ft_row(prow[1][lane]) | tp1 | PAR_E | (lane == P - 1 ? LAST : 0u));
         }
       }
+      { // a delta child that is the next parent stores its carry rows at its last entry
+        const uint64_t nxm = __ballot(in && live && nx);
+        if (nxm) {
+          const int l = __builtin_ctzll(nxm);
+          const uint32_t e0 = (uint32_t)__builtin_amdgcn_readlane((int)(inc & 0xFFFF), l);
+          const uint32_t e1 = (uint32_t)__builtin_amdgcn_readlane((int)(inc >> 16), l);
+          const int kd = __builtin_amdgcn_readlane(kinds, l);
+          if ((kd & 3) == 1) safe0 = len0 + e0 - 1 + 4; // inclusive prefix: last entry at inc - 1
+          if ((kd >> 2) == 1) safe1 = len1 + e1 - 1 + 4;
+        }
+      }
       len0 += tot & 0xFFFF, len1 += tot >> 16;
       rows += (tot & 0xFFFF) + (tot >> 16);
       // ---- king-move refreshes, one job per slot in slot order, lane = square
@@ -282,6 +309,7 @@ __global__ void __launch_bounds__(256)
           hit = nd < cn && (!nxl || ((kst >> 1) & 1) == hh);
         }
         const int g = hit ? (kst >> 1) & 1 : nxl ? hh : (len0 <= len1 ? 0 : 1);
+        if (hit) pad_to(g, g ? safe1 : safe0); // the cache row load after the list's last scratch store
         const uint32_t base = g ? len1 : len0;
         const uint32_t L = LAST | (nxl ? NXT : 0u);
         const uint32_t krow = SCR | (uint32_t)(2 + kci);
@@ -310,6 +338,10 @@ __global__ void __launch_bounds__(256)
           if ((lane & 7) == 0) ksnap[w][kci][lane >> 3] = x;
           if (lane == 0) kstate[w][kci] = (uint8_t)(1 | g << 1);
           ps::wave_sync();
+        }
+        if (kuse || nxl) { // this slot's last entry stores to scratch
+          uint32_t &sf = g ? safe1 : safe0;
+          sf = base + (uint32_t)ne - 1 + 4;
         }
         if (g) len1 += (uint32_t)ne;
         else len0 += (uint32_t)ne;
@@ -401,7 +433,8 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
   // ---- per-thread stream state across the block's tiles
   ushort8 pacc_lo = {}, pacc_hi = {}, base_lo = {}, base_hi = {};
   uint32_t es = 0;              // this group's position in its list
-  uint32_t cur_c = 0xFFFFFFFFu; // entry chunk (64 entries) held in ev, the next one in evn
+  uint32_t cur_c = 0xFFFFFFF0u; // entry chunk (64 entries) held in ev, the next one in evn (none yet:
+                                // cur_c + 1 must not wrap to chunk 0)
   uint32_t ev = 0, evn = 0;
   uint32_t bq = 0; // buckets done (acc0 / in1 / fwd buffer parity)
   auto chunk = [&](uint32_t c) -> uint32_t {
