@@ -34,7 +34,9 @@
 // ring step issues the same loads.  The ring issues a row load 4 entries before it
 // consumes it, so an entry that loads a scratch row sits at least 4 entries after the
 // last store to scratch in its list (no-op entries are inserted when needed): the load
-// is then issued after the store, by the same lanes.  Tiles restart the ring.
+// is then issued after the store, by the same lanes.  The ring runs across tiles.
+#include <stdlib.h>
+
 #include "device_util.h"
 #include "kernels.h"
 
@@ -110,7 +112,6 @@ __global__ void __launch_bounds__(256)
       if (len1 + lane < ((len1 + 3) & ~3u)) put(1, len1 + lane, PAD);
     }
     len0 = (len0 + 3) & ~3u, len1 = (len1 + 3) & ~3u;
-    safe0 = safe1 = 0; // the next tile restarts the ring after these stores were consumed
     TileDesc *d = T + tile_k;
     if (lane >= t_fill && lane < 16) d->meta[lane] = 0;
     if (lane == 0) d->e_end[0] = len0, d->e_end[1] = len1, d->p_first = p_first, d->nslots = (uint32_t)t_fill;
@@ -363,7 +364,7 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
     stream_eval_kernel(NetDevice net, const uint64_t *__restrict__ offsets, uint32_t np, uint32_t K, int swz,
                        const uint64_t *__restrict__ eoff, const uint32_t *__restrict__ ent,
                        const TileDesc *__restrict__ tiles, int2 *__restrict__ out_parent, int2 *__restrict__ out_child,
-                       uint32_t *__restrict__ pool, int use_scr, uint32_t *__restrict__ err) {
+                       uint32_t *__restrict__ pool, int use_scr, uint32_t *__restrict__ err, int ablate) {
   using namespace ps;
   constexpr int G = L1 / 16; // threads per perspective group (whole waves)
   constexpr int NT = 2 * G, NW = NT / 64, TILE = 16, XS = L1 + 16, KS = L1 / 64, KPW = KS / NW;
@@ -430,19 +431,90 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
     scr = (uint32_t)FT_ROWS + (uint32_t)SCR_ROWS * my_slot;
   }
 
-  // ---- per-thread stream state across the block's tiles
+  // ---- per-thread stream state: ONE continuous pipeline per group over the block's list.
+  // Entries arrive through scalar loads (their own counter, lgkmcnt), 4 at a time and two
+  // groups of 4 ahead, so waiting for an entry never waits for the row loads in flight;
+  // rows are loaded one group of 4 ahead of consumption, also across tile boundaries
+  // (the next tile's first rows are in flight during this tile's layer stack).
   ushort8 pacc_lo = {}, pacc_hi = {}, base_lo = {}, base_hi = {};
-  uint32_t es = 0;              // this group's position in its list
-  uint32_t cur_c = 0xFFFFFFF0u; // entry chunk (64 entries) held in ev, the next one in evn (none yet:
-                                // cur_c + 1 must not wrap to chunk 0)
-  uint32_t ev = 0, evn = 0;
+  ushort8 rlo[4], rhi[4];
+  uint32_t er[4];
   uint32_t bq = 0; // buckets done (acc0 / in1 / fwd buffer parity)
-  auto chunk = [&](uint32_t c) -> uint32_t {
-    int tl = tid;
-    asm volatile("" : "+v"(tl));
-    const uint32_t i = c * 64 + (uint32_t)(tl & 63);
-    return __builtin_amdgcn_raw_buffer_load_b32(er_, 4 * (hu ? rsz - 1 - i : i), 0, 0);
+  typedef uint32_t u4e __attribute__((ext_vector_type(4), aligned(4)));
+  typedef const __attribute__((address_space(4))) u4e cu4e;
+  typedef const __attribute__((address_space(4))) uint32_t cu32;
+  cu32 *EL = (cu32 *)(hu ? ent + rend : ent + rbeg);
+  // entries i .. i + 3 of this group's list by one s_load_dwordx4 (list 1 is stored
+  // downward: its 4 entries arrive reversed, see ent4)
+  auto group = [&](uint32_t i) -> u4e { return *(cu4e *)(hu ? EL - 4 - i : EL + i); };
+  auto ent4 = [&](const u4e v, int r) -> uint32_t { return hu ? v[3 - r] : v[r]; };
+  int tl0 = tid;
+  asm volatile("" : "+v"(tl0));
+  const int jt = tl0 % G;
+  const uint32_t j16 = 16 * jt;
+  auto issue = [&](int r, uint32_t e) {
+    er[r] = e;
+    uint32_t row = (e & SCR) ? scr + (e & ROW) : (e & ROW);
+    if (ablate & 2) row = FT_BIAS_ROW; // timing diagnostics only: every row from L1 / L2
+    rlo[r] = __builtin_bit_cast(ushort8, __builtin_amdgcn_raw_buffer_load_b128(ftr, j16, row * RS, 0));
+    rhi[r] = __builtin_bit_cast(ushort8, __builtin_amdgcn_raw_buffer_load_b128(ftr, j16 + L1, row * RS, 0));
   };
+  ushort8 lo = {}, hi = {};
+  auto consume = [&](int r) {
+    const uint32_t e = er[r];
+    const uint32_t init = e & INIT;
+    // scalar branches; the empty asm keeps the compiler from if-converting them into
+    // selects over every alternative
+    if (init == I_ZERO) {
+      asm volatile("");
+      if (!(e & SUB)) lo = rlo[r], hi = rhi[r];
+    } else if (init == I_PACC) {
+      asm volatile("");
+      lo = pacc_lo - rlo[r], hi = pacc_hi - rhi[r];
+      base_lo = lo, base_hi = hi;
+    } else if (init == I_BASE) {
+      if (e & SUB) {
+        asm volatile("");
+        lo = base_lo - rlo[r], hi = base_hi - rhi[r];
+      } else {
+        asm volatile("");
+        lo = base_lo + rlo[r], hi = base_hi + rhi[r];
+      }
+    } else if (e & SUB) {
+      asm volatile("");
+      lo -= rlo[r], hi -= rhi[r];
+    } else {
+      asm volatile("");
+      lo += rlo[r], hi += rhi[r];
+    }
+    if (e & LAST) {
+      const int sl = (e >> SLOT_SH) & 15, side = (e >> SIDE_SH) & 1;
+      *reinterpret_cast<uint2 *>(xt + sl * XS + side * (L1 / 2) + 8 * jt) = transform8(lo, hi);
+      if (e & PAR_E) {
+        asm volatile("");
+        pacc_lo = lo, pacc_hi = hi;
+      }
+      if (e & (KST | NXT)) { // accumulator stores: king-cache row and / or this list's carry row
+        asm volatile("");
+        uint32_t so = (scr + (uint32_t)hu) * RS;
+        if (e & KST) so = (scr + (e & ROW)) * RS;
+        for (int rep = (e & KST) && (e & NXT) ? 2 : 1; rep; --rep) {
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(int4v, lo), ftr, j16, so, 0);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(int4v, hi), ftr, j16 + L1, so, 0);
+          so = (scr + (uint32_t)hu) * RS;
+        }
+        // drain here (vmcnt(0)): with a store pending, loads and stores would be counted out of
+        // order and every later wait of the ring would become vmcnt(0); stores are rare
+        __builtin_amdgcn_s_waitcnt(0x0F70);
+      }
+    }
+  };
+  uint32_t pos = 0; // the group of 4 entries whose rows are in flight starts here
+  u4e gp = group(4); // the entries whose rows the next revolution issues (prefetched)
+  {
+    const u4e g0 = group(0);
+    issue(0, ent4(g0, 0)), issue(1, ent4(g0, 1)), issue(2, ent4(g0, 2)), issue(3, ent4(g0, 3));
+  }
 
 #pragma unroll 1
   for (uint32_t k = 0; k < ntiles; ++k) {
@@ -453,92 +525,27 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
 #pragma unroll
     for (int i = 0; i < 4; ++i)
       mw[i] = (uint32_t)__builtin_amdgcn_readfirstlane((int)reinterpret_cast<const uint32_t *>(D->meta)[i]);
-    // ---- the row stream of this group's list segment
-    {
-      int tl = tid;
-      asm volatile("" : "+v"(tl));
-      const int jt = tl % G;
-      const uint32_t j16 = 16 * jt;
-      const uint32_t n = e_end - es;
-      ushort8 rlo[4], rhi[4];
-      uint32_t er[4];
-      ushort8 lo = {}, hi = {};
-      auto issue = [&](int r, uint32_t i) {
-        const uint32_t c = i >> 6;
-        if (c != cur_c) { // scalar branch: next chunk (prefetched) and the one after
-          if (c == cur_c + 1) ev = evn;
-          else ev = chunk(c);
-          evn = chunk(c + 1);
-          cur_c = c;
-        }
-        const uint32_t e = er[r] = (uint32_t)__builtin_amdgcn_readlane((int)ev, (int)(i & 63));
-        const uint32_t row = (e & SCR) ? scr + (e & ROW) : (e & ROW);
-        rlo[r] = __builtin_bit_cast(ushort8, __builtin_amdgcn_raw_buffer_load_b128(ftr, j16, row * RS, 0));
-        rhi[r] = __builtin_bit_cast(ushort8, __builtin_amdgcn_raw_buffer_load_b128(ftr, j16 + L1, row * RS, 0));
-      };
-      auto consume = [&](int r) {
-        const uint32_t e = er[r];
-        const uint32_t init = e & INIT;
-        // scalar branches; the empty asm keeps the compiler from if-converting them into
-        // selects over every alternative
-        if (init == I_ZERO) {
-          asm volatile("");
-          if (!(e & SUB)) lo = rlo[r], hi = rhi[r];
-        } else if (init == I_PACC) {
-          asm volatile("");
-          lo = pacc_lo - rlo[r], hi = pacc_hi - rhi[r];
-          base_lo = lo, base_hi = hi;
-        } else if (init == I_BASE) {
-          if (e & SUB) {
-            asm volatile("");
-            lo = base_lo - rlo[r], hi = base_hi - rhi[r];
-          } else {
-            asm volatile("");
-            lo = base_lo + rlo[r], hi = base_hi + rhi[r];
-          }
-        } else if (e & SUB) {
-          asm volatile("");
-          lo -= rlo[r], hi -= rhi[r];
-        } else {
-          asm volatile("");
-          lo += rlo[r], hi += rhi[r];
-        }
-        if (e & LAST) {
-          const int sl = (e >> SLOT_SH) & 15, side = (e >> SIDE_SH) & 1;
-          *reinterpret_cast<uint2 *>(xt + sl * XS + side * (L1 / 2) + 8 * jt) = transform8(lo, hi);
-          if (e & PAR_E) {
-            asm volatile("");
-            pacc_lo = lo, pacc_hi = hi;
-          }
-          if (e & (KST | NXT)) { // accumulator stores: king-cache row and / or this list's carry row
-            asm volatile("");
-            uint32_t so = (scr + (uint32_t)hu) * RS;
-            if (e & KST) so = (scr + (e & ROW)) * RS;
-            for (int rep = (e & KST) && (e & NXT) ? 2 : 1; rep; --rep) {
-              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(int4v, lo), ftr, j16, so, 0);
-              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(int4v, hi), ftr, j16 + L1, so, 0);
-              so = (scr + (uint32_t)hu) * RS;
-            }
-          }
-        }
-      };
-      if (n) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) issue(r, es + (uint32_t)r);
+    // ---- the row stream of this group's list segment [pos, e_end) (a multiple of 4): a
+    // counted loop of its own (the empty asm keeps it from being fused with the tile loop,
+    // which would merge its wait counts with the layer stack's)
+    const uint32_t nrev = (e_end - pos) >> 2;
 #pragma unroll 1
-        for (uint32_t i = 0; i + 4 < n; i += 4) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            consume(r);
-            issue(r, es + i + 4 + (uint32_t)r);
-          }
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) consume(r);
-      }
-      es = e_end;
+    for (uint32_t t = 0; t < nrev; ++t) {
+      // scalar loads complete out of order, so any use waits for all of them: wait once here
+      // (lgkmcnt(0): the prefetch of the previous revolution), take this revolution's entries,
+      // and only then prefetch the next group, which nothing uses before the next revolution
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      const u4e gw = gp;
+      gp = group(pos + 8);
+      consume(0), issue(0, ent4(gw, 0));
+      consume(1), issue(1, ent4(gw, 1));
+      consume(2), issue(2, ent4(gw, 2));
+      consume(3), issue(3, ent4(gw, 3));
+      pos += 4;
     }
+    asm volatile("" ::: "memory");
     __syncthreads();
+    if (ablate & 4) continue; // timing diagnostics only: no layer stack
     // ---- layer stack: per bucket of the tile, fc_0 by all waves (int8 MFMA over this wave's
     // k-steps, partial sums by LDS integer atomics, exact), then one wave finishes it
     uint32_t bm = 0, pm = 0;
@@ -560,16 +567,17 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
         const uint8_t *xa = xt + row * XS + kg * 16 + 64 * KPW * wave;
         const int8_t *wb = net.w0 + ((size_t)b * 16 + row) * L1 + kg * 16 + 64 * KPW * wave;
         int4v acc = {0, 0, 0, 0};
+        // (batches of FB k-steps: the next tile's rows stay in flight in registers meanwhile)
+        constexpr int FB = 2;
 #pragma unroll
-        for (int k0 = 0; k0 < KPW; k0 += 4) {
-          int4v wv[4], av[4];
+        for (int k0 = 0; k0 < KPW; k0 += FB) {
+          int4v wv[FB], av[FB];
 #pragma unroll
-          for (int j = 0; j < 4; ++j) wv[j] = k0 + j < KPW ? *reinterpret_cast<const int4v *>(wb + 64 * (k0 + j)) : int4v{};
+          for (int j = 0; j < FB; ++j) wv[j] = *reinterpret_cast<const int4v *>(wb + 64 * (k0 + j));
 #pragma unroll
-          for (int j = 0; j < 4; ++j) av[j] = k0 + j < KPW ? *reinterpret_cast<const int4v *>(xa + 64 * (k0 + j)) : int4v{};
+          for (int j = 0; j < FB; ++j) av[j] = *reinterpret_cast<const int4v *>(xa + 64 * (k0 + j));
 #pragma unroll
-          for (int j = 0; j < 4; ++j)
-            if (k0 + j < KPW) acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(av[j], wv[j], acc, 0, 0, 0);
+          for (int j = 0; j < FB; ++j) acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(av[j], wv[j], acc, 0, 0, 0);
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i) atomicAdd(&acc0[buf][(4 * kg + i) * 16 + row], acc[i]);
@@ -631,6 +639,7 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
             }
           }
         }
+        __builtin_amdgcn_s_waitcnt(0x0F70); // no store pending into the stream (see consume)
       }
       ++bq;
     }
@@ -657,18 +666,19 @@ hipError_t launch_plan_stream(const NetDevice &net, const gn_board *parents, siz
   hipError_t e = hipMemsetAsync(pool, 0, 64 * sizeof(uint32_t), s);
   if (e != hipSuccess) return e;
   const unsigned pg = (nblk + 3) / 4, g = swz ? 8 * ((nblk + 7) / 8) : nblk;
+  static const int ablate = getenv("GN_ABLATE") ? atoi(getenv("GN_ABLATE")) : 0; // timing diagnostics only
   if (net.L1 == 3072) {
     hipLaunchKernelGGL((plan_kernel<3072>), dim3(pg), dim3(256), 0, s, net, parents, offsets, deltas, need_parent,
                        need_child, K > 1 ? next_slot : nullptr, (uint32_t)n, K, K > 1 ? kc : 0, eoff, ent, tiles,
                        rows_out, err);
     hipLaunchKernelGGL((stream_eval_kernel<3072>), dim3(g), dim3(384), 0, s, net, offsets, (uint32_t)n, K, swz, eoff,
-                       ent, tiles, out_parent, out_child, pool, scr, err);
+                       ent, tiles, out_parent, out_child, pool, scr, err, ablate);
   } else if (net.L1 == 1024) {
     hipLaunchKernelGGL((plan_kernel<1024>), dim3(pg), dim3(256), 0, s, net, parents, offsets, deltas, need_parent,
                        need_child, K > 1 ? next_slot : nullptr, (uint32_t)n, K, K > 1 ? kc : 0, eoff, ent, tiles,
                        rows_out, err);
     hipLaunchKernelGGL((stream_eval_kernel<1024>), dim3(g), dim3(128), 0, s, net, offsets, (uint32_t)n, K, swz, eoff,
-                       ent, tiles, out_parent, out_child, pool, scr, err);
+                       ent, tiles, out_parent, out_child, pool, scr, err, ablate);
   } else {
     return hipErrorInvalidValue;
   }
