@@ -211,6 +211,7 @@ struct Dev {
   DevBuf<uint64_t> ebound, eoff;
   DevBuf<uint32_t> ent, pool, perr;
   DevBuf<TileDesc> tiles;
+  DevBuf<uint32_t> btiles; // tiles per block of the planned expansion
   uint64_t etot = 0;        // eoff[n] of the current expansion
   bool planned = false;     // the last expansion ran the planned kernels (perr is meaningful)
   void *scan_tmp = nullptr;
@@ -343,7 +344,7 @@ static void destroy(gn_ctx *ctx) {
     if (d.sort_tmp) (void)hipFree(d.sort_tmp);
     d.kkeys.release(), d.kkeys2.release(), d.kidx.release(), d.kperm.release();
     d.nslot.release(), d.tickets.release(), d.ksnap.release();
-    d.ebound.release(), d.eoff.release(), d.ent.release(), d.pool.release(), d.perr.release(), d.tiles.release();
+    d.ebound.release(), d.eoff.release(), d.ent.release(), d.pool.release(), d.perr.release(), d.tiles.release(), d.btiles.release();
     if (d.done) (void)hipEventDestroy(d.done);
     if (d.stream) (void)hipStreamDestroy(d.stream);
   }
@@ -606,13 +607,14 @@ static int expand_evaluate(gn_ctx *ctx, Dev &d, const gn_board *parents, size_t 
     if (d.planned) {
       const size_t K = (size_t)std::max(1, d.chain_k), nblk = (n + K - 1) / K;
       HIP_TRY(d.ent.ensure(d.etot + 16 * (nblk + 1)));
-      HIP_TRY(d.tiles.ensure((n + total) / 16 + nblk + 2));
+      HIP_TRY(d.tiles.ensure((n + total) / 16 + (K + 2) * nblk + 2));
+      HIP_TRY(d.btiles.ensure(nblk + 1));
       HIP_TRY(d.pool.ensure(64));
       HIP_TRY(d.perr.ensure(1));
       HIP_TRY(hipMemsetAsync(d.perr.p, 0, sizeof(uint32_t), s));
       HIP_TRY(launch_plan_stream(d.net[BIG], parents, n, off, dl, f ? d.p_nbg.p : nullptr, f ? d.nbg.p : nullptr,
                                  d.p_obg.p, d.obg.p, ctx->swizzle & 1, d.chain_k > 1 ? d.nslot.p : nullptr,
-                                 d.chain_k, ctx->king_cache ? 1 : 0, d.eoff.p, d.ent.p, d.tiles.p, d.pool.p,
+                                 d.chain_k, ctx->king_cache ? 1 : 0, d.eoff.p, d.ent.p, d.tiles.p, d.btiles.p, d.pool.p,
                                  d.perr.p, rows_out, s));
     } else {
       HIP_TRY(launch_expand_net(d.net[BIG], parents, n, off, children, dl, f ? d.p_nbg.p : nullptr,

@@ -41,21 +41,23 @@ hipError_t launch_expand_net(const NetDevice &net, const gn_board *parents, size
 // accumulator for (perspective, king square) when the placement difference is shorter.
 // rows_out (optional, big-net row stream only): += FT rows gathered (bias, carry and
 // king-cache rows included).
-// Planned expansion (stream.hip): one descriptor per 16-slot tile of a block (slots =
-// [parent, its children, next parent, ...] of the block's consecutive parents).
-// e_end: list 0 / list 1 entries of the block up to the end of this tile (padded to a
-// multiple of 4); p_first: the parent owning slot 0; meta[t]: bit 0 evaluated, bits 1-3
-// bucket, bit 4 a parent slot; psq[t][side]: the slot's PSQT accumulators at its bucket
-// (side 0: the perspective to move).
+// Planned expansion (stream.hip): one descriptor per tile of <= 16 consecutive slots of a
+// block (slots = [parent, its children, next parent, ...] of the block's consecutive
+// parents) with <= 2 buckets among its evaluated slots.  e_end: list 0 / list 1 entries
+// of the block up to the end of this tile (padded to a multiple of 4); p_first: the
+// parent owning slot 0; first: the block-relative index of slot 0; meta[t]: bit 0
+// evaluated, bits 1-3 bucket, bit 4 a parent slot, bit 5 the slot's side to move;
+// psq[t][side]: the slot's PSQT accumulators at its bucket (side 0: the perspective to move).
 struct TileDesc {
   uint32_t e_end[2];
   uint32_t p_first;
-  uint32_t nslots;
+  uint32_t first;
   uint8_t meta[16];
   int32_t psq[16][2];
 };
 static_assert(sizeof(TileDesc) == 160, "TileDesc is 160 bytes");
-// Tiles of a block start at tiles + (pbeg + offsets[pbeg]) / 16 + block, entries at
+// Tiles of a block start at tiles + (pbeg + offsets[pbeg]) / 16 + 17 * block (btiles[block]
+// of them), entries at
 // ent + eoff[pbeg] + 16 * block (list 0 upward, list 1 downward from the region's end,
 // eoff = exclusive scan of write_children's per-parent entry bounds).  pool: 64 words
 // (zeroed here), err: bit 0 entry overflow, bit 1 no scratch slot.  rows_out: += FT rows
@@ -63,8 +65,8 @@ static_assert(sizeof(TileDesc) == 160, "TileDesc is 160 bytes");
 hipError_t launch_plan_stream(const NetDevice &net, const gn_board *parents, size_t n, const uint64_t *offsets,
                               const ChildDelta *deltas, const uint8_t *need_parent, const uint8_t *need_child,
                               int2 *out_parent, int2 *out_child, int swz, const uint8_t *next_slot, int chain_k,
-                              int kc, const uint64_t *eoff, uint32_t *ent, TileDesc *tiles, uint32_t *pool,
-                              uint32_t *err, unsigned long long *rows_out, hipStream_t s);
+                              int kc, const uint64_t *eoff, uint32_t *ent, TileDesc *tiles, uint32_t *btiles,
+                              uint32_t *pool, uint32_t *err, unsigned long long *rows_out, hipStream_t s);
 // GN_MODE_FULL preparation: need_small = valid && |simple_eval| > threshold,
 // need_big = valid && !need_small.
 hipError_t launch_classify(const gn_board *boards, size_t n, const gn_eval_params &P, uint8_t *need_small,

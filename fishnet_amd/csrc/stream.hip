@@ -35,13 +35,29 @@
 // consumes it, so an entry that loads a scratch row sits at least 4 entries after the
 // last store to scratch in its list (no-op entries are inserted when needed): the load
 // is then issued after the store, by the same lanes.  The ring runs across tiles.
+#include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include "device_util.h"
 #include "kernels.h"
 
+#ifndef GN_ASM_RING
+#define GN_ASM_RING 0 // measured: 307 ms with, 259 ms without (the compiler's own waits are the faster ring)
+#endif
 #ifndef GN_EXPAND_WPE
 #define GN_EXPAND_WPE 5
+#endif
+
+#ifdef GN_STREAM_PROF
+// diagnostics build only: per-phase s_memtime cycles summed over waves, and list balance
+__device__ unsigned long long gn_sp[8]; // [0] stream [1] barrier wait [2] layer stack [3] tiles
+                                       // [4] sum max(n0, n1) [5] sum n0 + n1
+#define SP_T() __builtin_amdgcn_s_memtime()
+#define SP_ADD(k, v) atomicAdd(&gn_sp[k], (unsigned long long)(v))
+#else
+#define SP_T() 0ull
+#define SP_ADD(k, v) (void)0
 #endif
 
 namespace gn {
@@ -67,7 +83,7 @@ __global__ void __launch_bounds__(256)
                 const ChildDelta *__restrict__ deltas, const uint8_t *__restrict__ need_parent,
                 const uint8_t *__restrict__ need_child, const uint8_t *__restrict__ next_slot, uint32_t np, uint32_t K,
                 int kc, const uint64_t *__restrict__ eoff, uint32_t *__restrict__ ent, TileDesc *__restrict__ tiles,
-                unsigned long long *__restrict__ rows_out, uint32_t *__restrict__ err) {
+                uint32_t *__restrict__ btiles, unsigned long long *__restrict__ rows_out, uint32_t *__restrict__ err) {
   using namespace ps;
   constexpr uint32_t RS = 2 * L1 + 32;
   __shared__ uint32_t ksnap[4][128][8]; // per wave: placement (64 nibbles) of each king-cache row
@@ -86,14 +102,16 @@ __global__ void __launch_bounds__(256)
   const uint64_t us_b = pbeg + offsets[pbeg];
   const uint64_t rbeg = eoff[pbeg] + 16ull * blk, rend = eoff[pend] + 16ull * (blk + 1);
   uint32_t *E0 = ent + rbeg, *E1 = ent + rend - 1;
-  TileDesc *T = tiles + us_b / 16 + blk;
+  // a block's tiles: <= ceil(slots / 16) + one bucket cut per parent (a parent's own slots hold
+  // <= 2 buckets, so a tile is cut at most once per parent), hence this base
+  TileDesc *T = tiles + us_b / 16 + (uint64_t)(K + 2) * blk;
   auto put = [&](int g, uint32_t i, uint32_t v) {
     if (g) E1[-(int64_t)i] = v;
     else E0[i] = v;
   };
   for (int i = lane; i < 128; i += 64) kstate[w][i] = 0;
   uint16_t(*prow)[32] = prow_s[w];
-  uint32_t len0 = 0, len1 = 0, tile_k = 0, p_first = pbeg;
+  uint32_t len0 = 0, len1 = 0, tile_k = 0, p_first = pbeg, u_fill = 0, t_first = 0, tile_bm = 0;
   uint32_t safe0 = 0, safe1 = 0; // first index of each list at which a scratch row may be loaded
   int t_fill = 0, carried = 0;
   unsigned long long rows = 0;
@@ -114,8 +132,8 @@ __global__ void __launch_bounds__(256)
     len0 = (len0 + 3) & ~3u, len1 = (len1 + 3) & ~3u;
     TileDesc *d = T + tile_k;
     if (lane >= t_fill && lane < 16) d->meta[lane] = 0;
-    if (lane == 0) d->e_end[0] = len0, d->e_end[1] = len1, d->p_first = p_first, d->nslots = (uint32_t)t_fill;
-    ++tile_k, t_fill = 0;
+    if (lane == 0) d->e_end[0] = len0, d->e_end[1] = len1, d->p_first = p_first, d->first = t_first;
+    ++tile_k, t_fill = 0, tile_bm = 0;
   };
 
   for (uint32_t p = pbeg; p < pend; ++p) {
@@ -152,14 +170,13 @@ __global__ void __launch_bounds__(256)
     int ckey0 = -1, ckey1 = -1; // sibling keys carried across this parent's segments
 
     for (int q0 = 0; q0 < total;) {
-      if (t_fill == 0) p_first = p;
-      const int seg = 16 - t_fill < total - q0 ? 16 - t_fill : total - q0;
+      if (t_fill == 0) p_first = p, t_first = u_fill;
+      const int cand = 16 - t_fill < total - q0 ? 16 - t_fill : total - q0;
       const int q = q0 + lane, t = t_fill + lane;
-      const bool in = lane < seg;
       // ---- descriptor of this lane's slot
       int vld = 0, cst = 0, cnt = 1, kinds = 0, n0 = 0, n1 = 0, s0 = 0, s1 = 0;
       uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
-      if (in && live) {
+      if (lane < cand && live) {
         if (q == 0) {
           vld = need_parent ? need_parent[p] : 1;
           cst = stm, cnt = P, kinds = 3 | 3 << 2;
@@ -176,6 +193,27 @@ __global__ void __launch_bounds__(256)
         }
       }
       const int bk = (cnt - 1) / 4;
+      // ---- the segment: the slots that keep the tile at <= 2 buckets among evaluated slots
+      int seg = cand;
+      {
+        uint32_t bits = lane < cand && live && vld ? 1u << bk : 0u;
+#pragma unroll
+        for (int dd = 1; dd < 64; dd <<= 1) {
+          const uint32_t o = __shfl_up(bits, dd);
+          if (lane >= dd) bits |= o;
+        }
+        const uint64_t ok = __ballot(lane >= cand || __builtin_popcount(tile_bm | bits) <= 2);
+        const int lead = ok == ~0ull ? 64 : __builtin_ctzll(~ok);
+        if (lead < cand) seg = lead; // tiles cut early keep <= 2 buckets (the stream's fc_0 buffers)
+        if (seg == 0) { // the tile is full of other buckets: close it and take the slots again
+          flush();
+          continue;
+        }
+        const uint32_t segbits = (uint32_t)__builtin_amdgcn_readlane((int)bits, seg - 1);
+        tile_bm |= segbits;
+      }
+      const bool in = lane < seg;
+      if (!in) vld = 0, kinds = 0, n0 = n1 = s0 = s1 = 0, w0 = w1 = w2 = w3 = 0;
       // ---- sibling cache: a delta child whose from-row equals the previous delta child's (in
       // the same list) starts from the cached (parent - from-row) and drops that entry
       const int key0 = (kinds & 3) == 1 ? (int)(w0 & 0xFFFF) : -1;
@@ -256,7 +294,7 @@ __global__ void __launch_bounds__(256)
           if (kd != 2) T[tile_k].psq[t][hh != cst] = v[hh];
         }
       }
-      if (in) T[tile_k].meta[t] = (uint8_t)((in && live && vld ? 1 : 0) | bk << 1 | (q == 0 ? 16 : 0));
+      if (in) T[tile_k].meta[t] = (uint8_t)((live && vld ? 1 : 0) | bk << 1 | (q == 0 ? 16 : 0) | cst << 5);
       // the parent's rows (lane = row) after its bias entry (the parent is lane 0 of its segment)
       if (live && q0 == 0 && !have) {
         const uint32_t tp0 = tmpl(t_fill, stm != 0), tp1 = tmpl(t_fill, stm != 1);
@@ -347,11 +385,12 @@ __global__ void __launch_bounds__(256)
         if (g) len1 += (uint32_t)ne;
         else len0 += (uint32_t)ne;
       }
-      t_fill += seg, q0 += seg;
+      t_fill += seg, q0 += seg, u_fill += (uint32_t)seg;
       if (t_fill == 16) flush();
     }
   }
   if (t_fill) flush();
+  if (lane == 0) btiles[blk] = tile_k;
   if (lane == 0) {
     if ((uint64_t)len0 + len1 > rend - rbeg) atomicOr(err, 1u); // cannot happen: eoff bounds the entries
     if (rows_out) atomicAdd(rows_out, rows);
@@ -363,7 +402,8 @@ template <int L1>
 __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_EXPAND_WPE)))
     stream_eval_kernel(NetDevice net, const uint64_t *__restrict__ offsets, uint32_t np, uint32_t K, int swz,
                        const uint64_t *__restrict__ eoff, const uint32_t *__restrict__ ent,
-                       const TileDesc *__restrict__ tiles, int2 *__restrict__ out_parent, int2 *__restrict__ out_child,
+                       const TileDesc *__restrict__ tiles, const uint32_t *__restrict__ btiles,
+                       int2 *__restrict__ out_parent, int2 *__restrict__ out_child,
                        uint32_t *__restrict__ pool, int use_scr, uint32_t *__restrict__ err, int ablate) {
   using namespace ps;
   constexpr int G = L1 / 16; // threads per perspective group (whole waves)
@@ -392,13 +432,10 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
     if (blk >= nblk) return;
   }
   const uint32_t pbeg = blk * K, pend = pbeg + K < np ? pbeg + K : np;
-  const uint64_t us_b = pbeg + offsets[pbeg], us_e = pend + offsets[pend];
-  const uint32_t ntiles = (uint32_t)((us_e - us_b + 15) / 16);
-  const TileDesc *T = tiles + us_b / 16 + blk;
+  const uint64_t us_b = pbeg + offsets[pbeg];
+  const uint32_t ntiles = btiles[blk];
+  const TileDesc *T = tiles + us_b / 16 + (uint64_t)(K + 2) * blk; // as plan_kernel
   const uint64_t rbeg = eoff[pbeg] + 16ull * blk, rend = eoff[pend] + 16ull * (blk + 1);
-  const __amdgpu_buffer_rsrc_t er_ = __builtin_amdgcn_make_buffer_rsrc((void *)(ent + rbeg), 0,
-                                                                       (int)((rend - rbeg) * 4), 0x00020000);
-  const uint32_t rsz = (uint32_t)(rend - rbeg);
   // ---- scratch slot (carry + king-cache rows) from this XCD's pool: never waits on another
   // workgroup; the pool (POOL_PER_XCD slots) outnumbers the workgroups an XCD holds
   uint32_t scr = 0, my_slot = 0;
@@ -452,15 +489,45 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
   asm volatile("" : "+v"(tl0));
   const int jt = tl0 % G;
   const uint32_t j16 = 16 * jt;
+#if GN_ASM_RING
+  typedef int sq4 __attribute__((ext_vector_type(4)));
+  const uint64_t ftp = (uint64_t)(uintptr_t)net.ft;
+  const sq4 rsq = {__builtin_amdgcn_readfirstlane((int)(uint32_t)ftp),
+                   __builtin_amdgcn_readfirstlane((int)(uint32_t)(ftp >> 32) & 0xFFFF),
+                   (int)(((size_t)FT_ROWS + (size_t)SCR_ROWS * SCR_SLOTS) * RS), 0x00020000};
+#endif
   auto issue = [&](int r, uint32_t e) {
     er[r] = e;
     uint32_t row = (e & SCR) ? scr + (e & ROW) : (e & ROW);
+    if (e & KST) row = FT_BIAS_ROW; // a store-only entry: load the (L1-resident) bias row
     if (ablate & 2) row = FT_BIAS_ROW; // timing diagnostics only: every row from L1 / L2
+#if GN_ASM_RING
+    // the ring's loads are invisible to the compiler's wait insertion (which, merging the
+    // paths of the entry kinds at the loop head, waits for far more of the ring than an entry
+    // needs); consume() waits for exactly its own row: see ring_wait
+    asm volatile("buffer_load_dwordx4 %0, %2, %3, %4 offen\n\t"
+                 "buffer_load_dwordx4 %1, %2, %3, %4 offen offset:%5"
+                 : "=&v"(rlo[r]), "=&v"(rhi[r])
+                 : "v"(j16), "s"(rsq), "s"(row * RS), "n"(L1));
+#else
     rlo[r] = __builtin_bit_cast(ushort8, __builtin_amdgcn_raw_buffer_load_b128(ftr, j16, row * RS, 0));
     rhi[r] = __builtin_bit_cast(ushort8, __builtin_amdgcn_raw_buffer_load_b128(ftr, j16 + L1, row * RS, 0));
+#endif
+  };
+  // before entry r is consumed: its two loads are the oldest of the 8 in flight (the 3 later
+  // entries of the last revolution and the earlier ones of this one were issued since); any
+  // other memory operation in between (a drained store, the layer stack's loads) only makes
+  // vmcnt(6) wait for more.  The "+v" ties the row registers to the wait: no use before it.
+  auto ring_wait = [&](int r) {
+#if GN_ASM_RING
+    asm volatile("s_waitcnt vmcnt(6)" : "+v"(rlo[r]), "+v"(rhi[r]));
+#else
+    (void)r;
+#endif
   };
   ushort8 lo = {}, hi = {};
   auto consume = [&](int r) {
+    ring_wait(r);
     const uint32_t e = er[r];
     const uint32_t init = e & INIT;
     // scalar branches; the empty asm keeps the compiler from if-converting them into
@@ -516,11 +583,22 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
     issue(0, ent4(g0, 0)), issue(1, ent4(g0, 1)), issue(2, ent4(g0, 2)), issue(3, ent4(g0, 3));
   }
 
+  unsigned long long sp_s = 0, sp_w = 0, sp_l = 0, sp_m = 0, sp_n = 0;
+  uint32_t sp_e0 = 0, sp_e1 = 0;
 #pragma unroll 1
   for (uint32_t k = 0; k < ntiles; ++k) {
     const TileDesc *D = T + k;
+    const unsigned long long t0 = SP_T();
+#ifdef GN_STREAM_PROF
+    if (wave == 0) {
+      const uint32_t a0 = D->e_end[0], a1 = D->e_end[1];
+      sp_m += (a0 - sp_e0) > (a1 - sp_e1) ? (a0 - sp_e0) : (a1 - sp_e1), sp_n += a0 - sp_e0 + a1 - sp_e1;
+      sp_e0 = a0, sp_e1 = a1;
+    }
+#endif
     const uint32_t e_end = __builtin_amdgcn_readfirstlane(D->e_end[hu]);
     const uint32_t p_first = __builtin_amdgcn_readfirstlane(D->p_first);
+    const uint32_t first = __builtin_amdgcn_readfirstlane(D->first);
     uint32_t mw[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -544,7 +622,10 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
       pos += 4;
     }
     asm volatile("" ::: "memory");
+    const unsigned long long t1 = SP_T();
     __syncthreads();
+    const unsigned long long t2 = SP_T();
+    sp_s += t1 - t0, sp_w += t2 - t1;
     if (ablate & 4) continue; // timing diagnostics only: no layer stack
     // ---- layer stack: per bucket of the tile, fc_0 by all waves (int8 MFMA over this wave's
     // k-steps, partial sums by LDS integer atomics, exact), then one wave finishes it
@@ -555,7 +636,7 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
       if (m & 1) bm |= 1u << ((m >> 1) & 7);
       if (m & 16) pm |= 1u << sl;
     }
-    const uint64_t u0 = us_b + 16ull * k;
+    const uint64_t u0 = us_b + first;
 #pragma unroll 1
     for (uint32_t mm = bm; mm; mm &= mm - 1) {
       const int b = __builtin_ctz(mm);
@@ -639,11 +720,22 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
             }
           }
         }
-        __builtin_amdgcn_s_waitcnt(0x0F70); // no store pending into the stream (see consume)
+#if !GN_ASM_RING
+        __builtin_amdgcn_s_waitcnt(0x0F70); // no store pending into the compiler-tracked ring
+#endif
       }
       ++bq;
     }
+    sp_l += SP_T() - t2;
   }
+#ifdef GN_STREAM_PROF
+  if ((tid & 63) == 0) {
+    SP_ADD(0, sp_s), SP_ADD(1, sp_w), SP_ADD(2, sp_l);
+    if (wave == 0) SP_ADD(3, ntiles), SP_ADD(4, sp_m), SP_ADD(5, sp_n);
+  }
+#else
+  (void)sp_s, (void)sp_w, (void)sp_l, (void)sp_m, (void)sp_n, (void)sp_e0, (void)sp_e1;
+#endif
   if (use_scr) { // every wave's stores are complete before the slot goes back to the pool
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -656,8 +748,8 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
 hipError_t launch_plan_stream(const NetDevice &net, const gn_board *parents, size_t n, const uint64_t *offsets,
                               const ChildDelta *deltas, const uint8_t *need_parent, const uint8_t *need_child,
                               int2 *out_parent, int2 *out_child, int swz, const uint8_t *next_slot, int chain_k,
-                              int kc, const uint64_t *eoff, uint32_t *ent, TileDesc *tiles, uint32_t *pool,
-                              uint32_t *err, unsigned long long *rows_out, hipStream_t s) {
+                              int kc, const uint64_t *eoff, uint32_t *ent, TileDesc *tiles, uint32_t *btiles,
+                              uint32_t *pool, uint32_t *err, unsigned long long *rows_out, hipStream_t s) {
   if (!n) return hipSuccess;
   if (n >= 0x80000000ull) return hipErrorInvalidValue; // 32-bit parent indices in the kernels
   const uint32_t K = chain_k > 1 && next_slot ? (uint32_t)chain_k : 1u;
@@ -670,18 +762,30 @@ hipError_t launch_plan_stream(const NetDevice &net, const gn_board *parents, siz
   if (net.L1 == 3072) {
     hipLaunchKernelGGL((plan_kernel<3072>), dim3(pg), dim3(256), 0, s, net, parents, offsets, deltas, need_parent,
                        need_child, K > 1 ? next_slot : nullptr, (uint32_t)n, K, K > 1 ? kc : 0, eoff, ent, tiles,
-                       rows_out, err);
+                       btiles, rows_out, err);
     hipLaunchKernelGGL((stream_eval_kernel<3072>), dim3(g), dim3(384), 0, s, net, offsets, (uint32_t)n, K, swz, eoff,
-                       ent, tiles, out_parent, out_child, pool, scr, err, ablate);
+                       ent, tiles, btiles, out_parent, out_child, pool, scr, err, ablate);
   } else if (net.L1 == 1024) {
     hipLaunchKernelGGL((plan_kernel<1024>), dim3(pg), dim3(256), 0, s, net, parents, offsets, deltas, need_parent,
                        need_child, K > 1 ? next_slot : nullptr, (uint32_t)n, K, K > 1 ? kc : 0, eoff, ent, tiles,
-                       rows_out, err);
+                       btiles, rows_out, err);
     hipLaunchKernelGGL((stream_eval_kernel<1024>), dim3(g), dim3(128), 0, s, net, offsets, (uint32_t)n, K, swz, eoff,
-                       ent, tiles, out_parent, out_child, pool, scr, err, ablate);
+                       ent, tiles, btiles, out_parent, out_child, pool, scr, err, ablate);
   } else {
     return hipErrorInvalidValue;
   }
+#ifdef GN_STREAM_PROF
+  {
+    unsigned long long c[8];
+    (void)hipStreamSynchronize(s);
+    (void)hipMemcpyFromSymbol(c, HIP_SYMBOL(gn_sp), sizeof(c));
+    fprintf(stderr, "stream prof: wave-cycles stream %llu barrier %llu ls %llu; tiles %llu; "
+                    "entries max-list %llu sum %llu (balance %.3f)\n",
+            c[0], c[1], c[2], c[3], c[4], c[5], c[5] ? 2.0 * c[4] / c[5] : 0.0);
+    memset(c, 0, sizeof(c));
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(gn_sp), c, sizeof(c));
+  }
+#endif
   return hipGetLastError();
 }
 

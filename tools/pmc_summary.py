@@ -26,8 +26,8 @@ import sys
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-DOMINANT = {"expand": "expand_stream_kernel<3072", "big16m": "eval_net_kernel<3072", "small1m": "eval_net_kernel<128"}
-# (the round-2 planned stream kernel is named stream_eval_kernel; pass --kernel expand=... to override)
+DOMINANT = {"expand": "stream_eval_kernel<3072", "big16m": "eval_net_kernel<3072", "small1m": "eval_net_kernel<128"}
+# (round 1: expand_stream_kernel; pass --kernel expand=... to override)
 N_SIMD = 256 * 4  # CUs x SIMDs
 
 
