@@ -128,22 +128,32 @@ struct Board {
 
 // Runtime-selected bitboards through unrolled constant indices only: keeps a
 // Board in VGPRs on the device (no scratch) and can never index out of range.
+// Each select mask is opaque to the optimiser, which would otherwise fold the
+// constant-index updates back into one update at a runtime index and so move the
+// whole Board to scratch memory (measured: 96 B/lane in the child kernel).
+GN_HD Bitboard sel_mask(int t, int sel, Bitboard b) {
+  Bitboard m = (t == sel) ? b : 0;
+#ifdef __HIP_DEVICE_COMPILE__
+  asm("" : "+v"(m));
+#endif
+  return m;
+}
 GN_HD Bitboard color_bb(const Board &B, int c) { return c ? B.byColor[1] : B.byColor[0]; }
 GN_HD void xor_color(Board &B, int c, Bitboard b) {
-  if (c) B.byColor[1] ^= b;
-  else B.byColor[0] ^= b;
+  B.byColor[0] ^= sel_mask(0, c, b);
+  B.byColor[1] ^= sel_mask(1, c, b);
 }
 GN_HD void or_color(Board &B, int c, Bitboard b) {
-  if (c) B.byColor[1] |= b;
-  else B.byColor[0] |= b;
+  B.byColor[0] |= sel_mask(0, c, b);
+  B.byColor[1] |= sel_mask(1, c, b);
 }
 GN_HD void xor_type(Board &B, int pt, Bitboard b) {
 #pragma unroll
-  for (int t = PAWN; t <= KING; ++t) B.byType[t] ^= (t == pt) ? b : 0;
+  for (int t = PAWN; t <= KING; ++t) B.byType[t] ^= sel_mask(t, pt, b);
 }
 GN_HD void or_type(Board &B, int pt, Bitboard b) {
 #pragma unroll
-  for (int t = PAWN; t <= KING; ++t) B.byType[t] |= (t == pt) ? b : 0;
+  for (int t = PAWN; t <= KING; ++t) B.byType[t] |= sel_mask(t, pt, b);
 }
 
 GN_HD int piece_on(const Board &B, int s) {

@@ -193,7 +193,8 @@ struct Dev {
   DevBuf<gn_eval> io_out, io_out2;
   DevBuf<uint64_t> counts, offsets;
   DevBuf<uint32_t> off32;
-  DevBuf<uint16_t> moves;
+  DevBuf<uint16_t> moves, moves_tmp; // moves_tmp: when the caller keeps no moves
+  DevBuf<uint32_t> owner;             // parent of each child (write_children scratch)
   DevBuf<ChildDelta> deltas;
   DevBuf<uint64_t> kkeys, kkeys2; // king-sort keys
   DevBuf<uint32_t> kidx, kperm;   // king-sort permutation
@@ -212,6 +213,8 @@ struct Dev {
   DevBuf<uint32_t> ent, pool, perr;
   DevBuf<TileDesc> tiles;
   DevBuf<uint32_t> btiles; // tiles per block of the planned expansion
+  DevBuf<uint16_t> bkeys, bkeys2; // block_order scratch
+  DevBuf<uint32_t> bidx, border;  // block_order: identity, then the order
   uint64_t etot = 0;        // eoff[n] of the current expansion
   bool planned = false;     // the last expansion ran the planned kernels (perr is meaningful)
   void *scan_tmp = nullptr;
@@ -221,6 +224,18 @@ struct Dev {
   // caller stream and return while their kernels are still queued).
   hipEvent_t done = nullptr;
   hipStream_t done_on = nullptr;
+  // The planned expansion runs as a pipeline of block ranges on two library streams
+  // (range c + 1's child generation and plan overlap range c's row stream); the caller's
+  // stream forks to them at go and joins them at join[].
+  hipStream_t aux[2] = {nullptr, nullptr};
+  hipEvent_t go = nullptr, join[2] = {nullptr, nullptr};
+  // generate_children(defer = true): write_children is left to the pipeline
+  bool defer_write = false;
+  gn_board *dw_children = nullptr;
+  uint16_t *dw_moves = nullptr;
+  unsigned long long *dw_rows = nullptr;
+  static constexpr size_t MAX_CHUNKS = 4;
+  uint64_t cbound[MAX_CHUNKS + 1] = {}; // children offsets at the range boundaries
   std::mutex mu;
 };
 
@@ -296,17 +311,23 @@ static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 static int upload_net(Dev &d, int which, const HostNet &h) {
   const size_t RS = 2 * (size_t)h.L1 + 32;
-  size_t off[8], o = 0;
+  size_t off[9], o = 0;
   const int carry = h.L1 == 128 ? 0 : CARRY_SLOTS; // the chained walk's scratch rows
-  const size_t sz[8] = {((size_t)FT_ROWS + 4 * (size_t)carry + 128 * (size_t)carry) * RS, h.bias.size() * 2, h.w0.size(), h.b0.size() * 4,
-                        h.w1.size(), h.b1.size() * 4, h.w2.size(), h.b2.size() * 4};
-  const void *src[8] = {h.ft.data(), h.bias.data(), h.w0.data(), h.b0.data(),
-                        h.w1.data(), h.b1.data(), h.w2.data(), h.b2.data()};
-  for (int i = 0; i < 8; ++i) off[i] = o, o += align256(sz[i]);
+  // the PSQT weights once more as [bucket][row] (721 KB: L2-resident for the plan kernel's
+  // scattered 4-byte reads, which would otherwise each touch a 6 KB FT row)
+  std::vector<int32_t> psqt((size_t)PSQT_BUCKETS * FT_ROWS);
+  for (size_t r = 0; r < (size_t)FT_ROWS; ++r)
+    for (int b = 0; b < PSQT_BUCKETS; ++b)
+      memcpy(&psqt[(size_t)b * FT_ROWS + r], h.ft.data() + r * RS + 2 * (size_t)h.L1 + 4 * b, 4);
+  const size_t sz[9] = {((size_t)FT_ROWS + 4 * (size_t)carry + 128 * (size_t)carry) * RS, h.bias.size() * 2, h.w0.size(), h.b0.size() * 4,
+                        h.w1.size(), h.b1.size() * 4, h.w2.size(), h.b2.size() * 4, psqt.size() * 4};
+  const void *src[9] = {h.ft.data(), h.bias.data(), h.w0.data(), h.b0.data(),
+                        h.w1.data(), h.b1.data(), h.w2.data(), h.b2.data(), psqt.data()};
+  for (int i = 0; i < 9; ++i) off[i] = o, o += align256(sz[i]);
   uint8_t *m = nullptr;
   if (hipMalloc(&m, o) != hipSuccess) return fail(GN_E_NOMEM, "device allocation of %zu bytes failed", o);
   d.net_mem[which] = m;
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < 9; ++i)
     HIP_TRY(hipMemcpy(m + off[i], src[i], i == 0 ? (size_t)FT_ROWS * RS : sz[i], hipMemcpyHostToDevice));
   if (carry) HIP_TRY(hipMemset(m + off[0] + (size_t)FT_ROWS * RS, 0, 4 * (size_t)carry * RS));
   NetDevice &n = d.net[which];
@@ -322,6 +343,7 @@ static int upload_net(Dev &d, int which, const HostNet &h) {
   n.b1 = reinterpret_cast<const int32_t *>(m + off[5]);
   n.w2 = reinterpret_cast<const int8_t *>(m + off[6]);
   n.b2 = reinterpret_cast<const int32_t *>(m + off[7]);
+  n.psqt = reinterpret_cast<const int32_t *>(m + off[8]);
   d.has[which] = true;
   return GN_OK;
 }
@@ -339,12 +361,19 @@ static void destroy(gn_ctx *ctx) {
     d.io_boards.release(), d.frontier[0].release(), d.frontier[1].release();
     d.io_out.release(), d.io_out2.release(), d.counts.release(), d.offsets.release();
     d.off32.release(), d.moves.release(), d.sum.release(), d.deltas.release();
+    d.moves_tmp.release(), d.owner.release();
     d.p_osm.release(), d.p_obg.release(), d.p_nsm.release(), d.p_nbg.release();
     if (d.scan_tmp) (void)hipFree(d.scan_tmp);
     if (d.sort_tmp) (void)hipFree(d.sort_tmp);
     d.kkeys.release(), d.kkeys2.release(), d.kidx.release(), d.kperm.release();
     d.nslot.release(), d.tickets.release(), d.ksnap.release();
     d.ebound.release(), d.eoff.release(), d.ent.release(), d.pool.release(), d.perr.release(), d.tiles.release(), d.btiles.release();
+    d.bkeys.release(), d.bkeys2.release(), d.bidx.release(), d.border.release();
+    for (int i = 0; i < 2; ++i) {
+      if (d.aux[i]) (void)hipStreamSynchronize(d.aux[i]), (void)hipStreamDestroy(d.aux[i]);
+      if (d.join[i]) (void)hipEventDestroy(d.join[i]);
+    }
+    if (d.go) (void)hipEventDestroy(d.go);
     if (d.done) (void)hipEventDestroy(d.done);
     if (d.stream) (void)hipStreamDestroy(d.stream);
   }
@@ -385,6 +414,11 @@ static int create(const uint8_t *big, size_t big_len, const uint8_t *small, size
     HIP_TRY(hipSetDevice(id));
     HIP_TRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
     HIP_TRY(hipEventCreateWithFlags(&d.done, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&d.go, hipEventDisableTiming));
+    for (int i = 0; i < 2; ++i) {
+      HIP_TRY(hipStreamCreateWithFlags(&d.aux[i], hipStreamNonBlocking));
+      HIP_TRY(hipEventCreateWithFlags(&d.join[i], hipEventDisableTiming));
+    }
     HIP_TRY(hipMalloc(&d.tables, sizeof(Tables)));
     HIP_TRY(hipMemcpy(d.tables, &host_tables(), sizeof(Tables), hipMemcpyHostToDevice));
     for (int w = 0; w < 2; ++w)
@@ -506,11 +540,38 @@ static bool plan_path(const gn_ctx *ctx, const Dev &d) {
   return !old && !legacy && ctx->incremental && d.has[BIG] && (d.net[BIG].L1 == 3072 || d.net[BIG].L1 == 1024);
 }
 
+// Block ranges of the planned expansion's pipeline (expand_evaluate), GN_EXPAND_CHUNKS
+// (<= 4; default 1).  Measured on the 49,152-game line: 4 ranges on two streams take the
+// same 296 ms as the serial 259 ms stream + 19 ms plan + 15.5 ms children + 5 ms finalize,
+// the overlapped kernels slowing the row stream by what they add (they share its CUs and
+// its L2), so the serial order is the default; the pipeline stays for A/B runs.
+static size_t expand_chunks(size_t nblk) {
+  static const int env = getenv("GN_EXPAND_CHUNKS") ? atoi(getenv("GN_EXPAND_CHUNKS")) : 1;
+  const size_t c = env > 0 ? (size_t)env : 1;
+  return std::max<size_t>(1, std::min<size_t>(std::min<size_t>(c, Dev::MAX_CHUNKS), std::max<size_t>(nblk, 1)));
+}
+
+// finalize of parents [pa, pb) and children [ca, cb) (their net outputs in the Dev buffers)
+static int finalize_range(gn_ctx *ctx, Dev &d, const gn_board *parents, const gn_board *children, int mode,
+                          gn_eval *parent_out, gn_eval *child_out, size_t pa, size_t pb, size_t ca, size_t cb,
+                          hipStream_t s) {
+  auto o = [](auto *p, size_t k) { return p ? p + k : p; };
+  const gn_eval_params &P = ctx->P;
+  HIP_TRY(launch_finalize(children + ca, cb - ca, mode, o(d.osm.p, ca), o(d.obg.p, ca), o(d.nsm.p, ca), o(d.nbg.p, ca),
+                          P, d.tables, child_out + ca, s));
+  if (parent_out)
+    HIP_TRY(launch_finalize(parents + pa, pb - pa, mode, o(d.p_osm.p, pa), o(d.p_obg.p, pa), o(d.p_nsm.p, pa),
+                            o(d.p_nbg.p, pa), P, d.tables, parent_out + pa, s));
+  return GN_OK;
+}
+
 static int generate_children(Dev &d, const gn_board *parents, size_t n, gn_board *children_or_null, size_t cap,
                              uint16_t *moves, bool want_deltas, size_t *total, hipStream_t s, hipEvent_t *ev,
-                             unsigned long long *rows = nullptr, int chain_k = 1, bool plan = false) {
+                             unsigned long long *rows = nullptr, int chain_k = 1, bool plan = false,
+                             bool defer = false) {
   d.chain_k = want_deltas ? chain_k : 1;
   d.planned = want_deltas && plan;
+  d.defer_write = false;
   if (d.chain_k > 1) {
     HIP_TRY(d.nslot.ensure(n));
     HIP_TRY(d.tickets.ensure(CARRY_SLOTS + 1));
@@ -531,8 +592,19 @@ static int generate_children(Dev &d, const gn_board *parents, size_t n, gn_board
   uint64_t t = 0;
   HIP_TRY(hipMemcpyAsync(&t, d.offsets.p + n, sizeof(t), hipMemcpyDeviceToHost, s));
   if (d.planned) HIP_TRY(hipMemcpyAsync(&d.etot, d.eoff.p + n, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+  if (d.planned) { // children offsets at the pipeline's range boundaries (expand_evaluate)
+    const size_t K = (size_t)std::max(1, d.chain_k), nblk = (n + K - 1) / K, C = expand_chunks(nblk);
+    d.cbound[0] = 0;
+    for (size_t c = 1; c < C; ++c)
+      HIP_TRY(hipMemcpyAsync(&d.cbound[c], d.offsets.p + std::min(nblk * c / C * K, n), sizeof(uint64_t),
+                             hipMemcpyDeviceToHost, s));
+  }
   HIP_TRY(hipStreamSynchronize(s));
   *total = (size_t)t;
+  if (d.planned) {
+    const size_t K = (size_t)std::max(1, d.chain_k), nblk = (n + K - 1) / K;
+    d.cbound[expand_chunks(nblk)] = t;
+  }
   if (ev) HIP_TRY(hipEventRecord(ev[1], s));
   if ((children_or_null || moves) && t > cap) // caller-owned child buffers hold cap entries
     return fail(GN_E_CAPACITY, "%zu children exceed capacity %zu", (size_t)t, cap);
@@ -542,9 +614,19 @@ static int generate_children(Dev &d, const gn_board *parents, size_t n, gn_board
     children = d.frontier[1].p;
   }
   if (want_deltas) HIP_TRY(d.deltas.ensure(std::max<size_t>(t, 1)));
-  if (t) HIP_TRY(launch_write_children(parents, n, d.tables, d.offsets.p, children, moves,
-                                        want_deltas ? d.deltas.p : nullptr, d.chain_k > 1 ? d.nslot.p : nullptr,
-                                        d.chain_k, rows, s));
+  HIP_TRY(d.owner.ensure(std::max<size_t>(t, 1)));
+  if (!moves) {
+    HIP_TRY(d.moves_tmp.ensure(std::max<size_t>(t, 1)));
+    moves = d.moves_tmp.p;
+  }
+  if (d.planned && defer && t && expand_chunks((n + d.chain_k - 1) / std::max(1, d.chain_k)) > 1) {
+    // expand_evaluate writes the children range by range, in its pipeline
+    d.defer_write = true, d.dw_children = children, d.dw_moves = moves, d.dw_rows = rows;
+  } else if (t) {
+    HIP_TRY(launch_write_children(parents, n, d.tables, d.offsets.p, 0, t, children, moves, d.owner.p,
+                                  want_deltas ? d.deltas.p : nullptr, d.chain_k > 1 ? d.nslot.p : nullptr, d.chain_k,
+                                  rows, s));
+  }
   if (ev) HIP_TRY(hipEventRecord(ev[2], s));
   return GN_OK;
 }
@@ -584,6 +666,7 @@ static int expand_evaluate(gn_ctx *ctx, Dev &d, const gn_board *parents, size_t 
   }
   auto mark = [&](int k) -> hipError_t { return ev ? hipEventRecord(ev[k], s) : hipSuccess; };
   const gn_eval_params &P = ctx->P;
+  bool piped = false; // finalize ran inside the big net's pipeline
   const uint64_t *off = d.offsets.p;
   const ChildDelta *dl = d.deltas.p;
   if (mode == GN_MODE_FULL) {
@@ -612,10 +695,58 @@ static int expand_evaluate(gn_ctx *ctx, Dev &d, const gn_board *parents, size_t 
       HIP_TRY(d.pool.ensure(64));
       HIP_TRY(d.perr.ensure(1));
       HIP_TRY(hipMemsetAsync(d.perr.p, 0, sizeof(uint32_t), s));
-      HIP_TRY(launch_plan_stream(d.net[BIG], parents, n, off, dl, f ? d.p_nbg.p : nullptr, f ? d.nbg.p : nullptr,
-                                 d.p_obg.p, d.obg.p, ctx->swizzle & 1, d.chain_k > 1 ? d.nslot.p : nullptr,
-                                 d.chain_k, ctx->king_cache ? 1 : 0, d.eoff.p, d.ent.p, d.tiles.p, d.btiles.p, d.pool.p,
-                                 d.perr.p, rows_out, s));
+      HIP_TRY(hipMemsetAsync(d.pool.p, 0, 64 * sizeof(uint32_t), s));
+      // block ranges as a pipeline: range c's row stream (memory-bound, the whole GPU)
+      // overlaps range c + 1's child generation and plan (latency-bound) and range c - 1's
+      // finalize; results do not depend on the split (every index is absolute)
+      const size_t C = expand_chunks(nblk);
+      // XCD-local block order (one range only: a range's order must stay inside it)
+      static const bool bsort = !getenv("GN_BLOCK_SORT") || atoi(getenv("GN_BLOCK_SORT"));
+      const uint32_t *order = nullptr;
+      if (bsort && C == 1 && ctx->king_sort && nblk > 1) {
+        HIP_TRY(d.bkeys.ensure(nblk));
+        HIP_TRY(d.bkeys2.ensure(nblk));
+        HIP_TRY(d.bidx.ensure(nblk));
+        HIP_TRY(d.border.ensure(nblk));
+        HIP_TRY(block_order(parents, n, (uint32_t)K, (uint32_t)nblk, d.bkeys.p, d.bidx.p, d.bkeys2.p, d.border.p,
+                            d.sort_tmp, d.sort_bytes, s));
+        order = d.border.p;
+      }
+      auto run = [&](size_t c, hipStream_t sc) -> int {
+        const size_t b0 = nblk * c / C, b1 = nblk * (c + 1) / C, pa = b0 * K, pb = std::min(b1 * K, n);
+        if (d.defer_write)
+          HIP_TRY(launch_write_children(parents + pa, pb - pa, d.tables, off + pa, d.cbound[c],
+                                        d.cbound[c + 1] - d.cbound[c], d.dw_children, d.dw_moves, d.owner.p,
+                                        d.deltas.p, d.chain_k > 1 ? d.nslot.p + pa : nullptr, d.chain_k, d.dw_rows,
+                                        sc));
+        HIP_TRY(launch_plan_stream(d.net[BIG], parents, n, off, dl, f ? d.p_nbg.p : nullptr, f ? d.nbg.p : nullptr,
+                                   d.p_obg.p, d.obg.p, ctx->swizzle & 1, d.chain_k > 1 ? d.nslot.p : nullptr,
+                                   d.chain_k, ctx->king_cache ? 1 : 0, d.eoff.p, d.ent.p, d.tiles.p, d.btiles.p,
+                                   d.pool.p, d.perr.p, rows_out, b0, b1, order, sc));
+        if (C > 1) { // this range's finalize (after the join when not pipelined)
+          int rc = finalize_range(ctx, d, parents, children, mode, parent_out, child_out, pa, pb, d.cbound[c],
+                                  d.cbound[c + 1], sc);
+          if (rc) return rc;
+        }
+        return GN_OK;
+      };
+      if (C == 1 && !d.defer_write) {
+        int rc = run(0, s);
+        if (rc) return rc;
+      } else {
+        HIP_TRY(hipEventRecord(d.go, s));
+        for (int i = 0; i < 2; ++i) HIP_TRY(hipStreamWaitEvent(d.aux[i], d.go, 0));
+        for (size_t c = 0; c < C; ++c) {
+          int rc = run(c, d.aux[c & 1]);
+          if (rc) return rc;
+        }
+        for (int i = 0; i < 2; ++i) {
+          HIP_TRY(hipEventRecord(d.join[i], d.aux[i]));
+          HIP_TRY(hipStreamWaitEvent(s, d.join[i], 0));
+        }
+        d.defer_write = false;
+        if (C > 1) piped = true;
+      }
     } else {
       HIP_TRY(launch_expand_net(d.net[BIG], parents, n, off, children, dl, f ? d.p_nbg.p : nullptr,
                                 f ? d.nbg.p : nullptr, d.p_obg.p, d.obg.p, ctx->swizzle & 1,
@@ -624,9 +755,10 @@ static int expand_evaluate(gn_ctx *ctx, Dev &d, const gn_board *parents, size_t 
     }
   }
   HIP_TRY(mark(2));
-  HIP_TRY(launch_finalize(children, total, mode, d.osm.p, d.obg.p, d.nsm.p, d.nbg.p, P, d.tables, child_out, s));
-  if (parent_out)
-    HIP_TRY(launch_finalize(parents, n, mode, d.p_osm.p, d.p_obg.p, d.p_nsm.p, d.p_nbg.p, P, d.tables, parent_out, s));
+  if (!piped) {
+    int rc = finalize_range(ctx, d, parents, children, mode, parent_out, child_out, 0, n, 0, total, s);
+    if (rc) return rc;
+  }
   HIP_TRY(mark(3));
   return GN_OK;
 }
@@ -790,7 +922,7 @@ static int expand_boards_host(gn_ctx *ctx, const gn_board *boards, size_t n, int
       HIP_TRY(d.moves.ensure(std::max<size_t>(tk, 1)));
       size_t t = 0;
       int r = generate_children(d, d.io_boards.p, m, nullptr, d.moves.cap, d.moves.p, ctx->incremental, &t, s, nullptr,
-                                nullptr, chain_len(ctx, d, m), plan_path(ctx, d));
+                                nullptr, chain_len(ctx, d, m), plan_path(ctx, d), mode == GN_MODE_BIG);
       if (r) return r;
       if (t != tk) return fail(GN_E_HIP, "child count changed between passes (%zu != %zu)", t, tk);
       HIP_TRY(d.io_out.ensure(m));
@@ -1330,7 +1462,7 @@ int gn_expand_device(gn_ctx *ctx, int device_slot, const gn_board *d_parents, si
   if (!d_children || !d_moves || !d_child_out) return fail(GN_E_INVALID, "NULL child buffer");
   size_t t = 0;
   int rc = generate_children(*d, d_parents, n, d_children, cap, d_moves, ctx->incremental, &t, s, nullptr, nullptr,
-                             chain_len(ctx, *d, n), plan_path(ctx, *d));
+                             chain_len(ctx, *d, n), plan_path(ctx, *d), mode == GN_MODE_BIG);
   *total = t;
   if (t > 0xFFFFFFFFull) return fail(GN_E_CAPACITY, "%zu children exceed 32-bit offsets", t);
   HIP_TRY(launch_offsets_u32(d->offsets.p, n + 1, d_offsets, s));
@@ -1374,8 +1506,12 @@ int gn_time_expand_device(gn_ctx *ctx, int device_slot, const gn_board *d_parent
     hipEvent_t *e = &ev[2 + (size_t)NE * it];
     he = hipEventRecord(e[0], s);
     if (he != hipSuccess) break;
+    // rows by write_children's formula only when no planned row stream counts them (a
+    // per-wave atomic over every child would sit in the timed region)
+    const bool planned = plan_path(ctx, *d);
     rc = generate_children(*d, d_parents, n, nullptr, cap, d_moves, ctx->incremental, &t, s, e + 1,
-                           it == 0 ? d->sum.p : nullptr, chain_len(ctx, *d, n), plan_path(ctx, *d));
+                           it == 0 && !planned ? d->sum.p : nullptr, chain_len(ctx, *d, n), planned,
+                           mode == GN_MODE_BIG);
     if (rc) break;
     if (d_child_out && t > cap) {
       rc = fail(GN_E_CAPACITY, "%zu children exceed capacity %zu", t, cap);

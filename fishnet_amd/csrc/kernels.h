@@ -23,6 +23,10 @@ hipError_t launch_checksum(const void *p, size_t bytes, unsigned long long *out,
 // e1 / e8, set when the start position's piece still stands there
 // (king_keys_kernel), which serve the big net's common-row base; kings only
 // (16-bit keys) otherwise
+// order[]: the nblk blocks (K consecutive parents each) sorted by their middle parent's
+// king squares (stream_eval_kernel's XCD-local order); keys / idx / keys_out: nblk scratch.
+hipError_t block_order(const gn_board *parents, size_t n, uint32_t K, uint32_t nblk, uint16_t *keys, uint32_t *idx,
+                       uint16_t *keys_out, uint32_t *order, void *&temp, size_t &temp_bytes, hipStream_t s);
 hipError_t king_sort(const gn_board *boards, size_t n, uint64_t *keys, uint32_t *idx, uint64_t *keys_out,
                      uint32_t *perm, bool placement, void *&temp, size_t &temp_bytes, hipStream_t s);
 // Incremental evaluation of parents + all their children (children of parent
@@ -56,17 +60,19 @@ struct TileDesc {
   int32_t psq[16][2];
 };
 static_assert(sizeof(TileDesc) == 160, "TileDesc is 160 bytes");
-// Tiles of a block start at tiles + (pbeg + offsets[pbeg]) / 16 + 17 * block (btiles[block]
-// of them), entries at
-// ent + eoff[pbeg] + 16 * block (list 0 upward, list 1 downward from the region's end,
-// eoff = exclusive scan of write_children's per-parent entry bounds).  pool: 64 words
-// (zeroed here), err: bit 0 entry overflow, bit 1 no scratch slot.  rows_out: += FT rows
-// the stream gathers (bias, carry and king-cache rows included).
+// Tiles of a block start at tiles + (pbeg + offsets[pbeg]) / 16 + (K + 2) * block (btiles[block]
+// of them), entries at ent + eoff[pbeg] + 16 * block (list 0 upward, list 1 downward from
+// the region's end, eoff = exclusive scan of write_children's per-parent entry bounds).
+// One call plans and evaluates blocks [b0, b1) of the n parents (every index absolute, so
+// block ranges can run as a pipeline on different streams).  pool: 64 words, zeroed by the
+// caller before the first range; err: bit 0 entry overflow, bit 1 no scratch slot.
+// rows_out: += FT rows the stream gathers (bias, carry and king-cache rows included).
 hipError_t launch_plan_stream(const NetDevice &net, const gn_board *parents, size_t n, const uint64_t *offsets,
                               const ChildDelta *deltas, const uint8_t *need_parent, const uint8_t *need_child,
                               int2 *out_parent, int2 *out_child, int swz, const uint8_t *next_slot, int chain_k,
                               int kc, const uint64_t *eoff, uint32_t *ent, TileDesc *tiles, uint32_t *btiles,
-                              uint32_t *pool, uint32_t *err, unsigned long long *rows_out, hipStream_t s);
+                              uint32_t *pool, uint32_t *err, unsigned long long *rows_out, size_t b0, size_t b1,
+                              const uint32_t *order, hipStream_t s);
 // GN_MODE_FULL preparation: need_small = valid && |simple_eval| > threshold,
 // need_big = valid && !need_small.
 hipError_t launch_classify(const gn_board *boards, size_t n, const gn_eval_params &P, uint8_t *need_small,
@@ -82,10 +88,13 @@ hipError_t launch_finalize(const gn_board *boards, size_t n, int mode, const int
 // upper bound of the planned expansion's list entries (stream.hip)
 hipError_t launch_count_children(const gn_board *boards, size_t n, const Tables *tables, uint64_t *counts,
                                  hipStream_t s, uint64_t *ebound = nullptr);
-// children of every board at offsets[i] (exclusive prefix sums of counts)
-hipError_t launch_write_children(const gn_board *boards, size_t n, const Tables *tables,
-                                 const uint64_t *offsets, gn_board *children, uint16_t *moves, ChildDelta *deltas,
-                                 uint8_t *next_slot, int chain_k, unsigned long long *rows, hipStream_t s);
+// children of every board at offsets[i] (exclusive prefix sums of counts): their moves,
+// owning board (owner, scratch) and, for children [c0, c0 + nc) (all children of these
+// boards), the child boards, deltas and chained-walk links.  moves / owner: required.
+hipError_t launch_write_children(const gn_board *boards, size_t n, const Tables *tables, const uint64_t *offsets,
+                                 size_t c0, size_t nc, gn_board *children, uint16_t *moves, uint32_t *owner,
+                                 ChildDelta *deltas, uint8_t *next_slot, int chain_k, unsigned long long *rows,
+                                 hipStream_t s);
 // sum of legal-move counts over all boards into *total (added; caller zeroes)
 hipError_t launch_count_sum(const gn_board *boards, size_t n, const Tables *tables,
                             unsigned long long *total, hipStream_t s);

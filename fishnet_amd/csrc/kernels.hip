@@ -1539,48 +1539,72 @@ __device__ __forceinline__ bool same_placement(const gn_board &a, const gn_board
   return a.occ == b.occ && x[0] == y[0] && x[1] == y[1];
 }
 
-__global__ void write_children_kernel(const gn_board *__restrict__ boards, size_t n, const Tables *__restrict__ tables,
-                                      const uint64_t *__restrict__ offsets, gn_board *__restrict__ children,
-                                      uint16_t *__restrict__ moves, ChildDelta *__restrict__ deltas,
-                                      uint8_t *__restrict__ next_slot, int chain_k,
-                                      unsigned long long *__restrict__ rows) {
+// Children in two passes: child_moves_kernel (a thread per parent) lists the legal moves
+// and the owning parent of every child; child_boards_kernel (a thread per child) makes the
+// child, its feature-transformer delta and the chained-walk link.  A thread per parent
+// writing ~31 children of 58 B each left partial L2 lines to be written back (4.5x the
+// bytes); a thread per child writes every array coalesced.
+__global__ void child_moves_kernel(const gn_board *__restrict__ boards, size_t n, const Tables *__restrict__ tables,
+                                   const uint64_t *__restrict__ offsets, uint16_t *__restrict__ moves,
+                                   uint32_t *__restrict__ owner, uint8_t *__restrict__ next_slot,
+                                   unsigned long long *__restrict__ rows) {
   __shared__ Tables T;
   load_tables(T, tables);
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
+  if (next_slot) next_slot[i] = 255; // child_boards_kernel overwrites it on a match
   Board B;
-  if (!unpack(boards[i], B)) {
-    if (next_slot) next_slot[i] = 255;
-    return;
-  }
+  if (!unpack(boards[i], B)) return;
   uint64_t k = offsets[i];
-  // feature-transformer rows the incremental evaluation will gather: the
-  // parent's refresh (both perspectives) + per child either the delta rows or
-  // a refresh of the perspective whose king moved
-  unsigned long long nrows = 2ull * popcnt(B.byType[0]);
-  // next_slot[i]: the child whose placement is boards[i + 1]'s (a game's next position),
-  // 255 if none; the chained walk then starts parent i + 1 from that child's accumulators
-  gn_board nb = {};
-  const bool look = next_slot && i + 1 < n;
-  if (look) nb = boards[i + 1];
-  const uint64_t k0 = k;
-  uint32_t ns = 255;
   gen_legal(B, T, [&](uint16_t m) {
-    gn_board pb;
-    Dirty d;
-    const Board C = do_move(B, m, &d);
-    pack(C, pb);
-    if (look && ns == 255 && same_placement(pb, nb)) ns = (uint32_t)(k - k0);
-    children[k] = pb;
-    if (moves) moves[k] = m;
-    if (deltas) deltas[k] = make_child_delta(B, C, d);
-    nrows += d.king_moved ? popcnt(C.byType[0]) + d.n_rem + d.n_add : 2 * (d.n_rem + d.n_add);
+    moves[k] = m;
+    owner[k] = (uint32_t)i;
     ++k;
   });
-  if (next_slot) next_slot[i] = (uint8_t)ns;
-  // a chained next parent gathers one carry row per perspective instead of its refresh
-  if (ns != 255 && chain_k > 1 && (i + 1) % (size_t)chain_k != 0) nrows -= 2ull * popcnt(nb.occ) - 2;
-  if (rows) atomicAdd(rows, nrows);
+  // feature-transformer rows the incremental evaluation will gather: the parent's
+  // refresh (both perspectives) here, each child's in child_boards_kernel
+  if (rows) atomicAdd(rows, 2ull * popcnt(B.byType[0]));
+}
+
+__global__ void child_boards_kernel(const gn_board *__restrict__ boards, size_t n,
+                                    const uint64_t *__restrict__ offsets, size_t c0, size_t nc,
+                                    const uint16_t *__restrict__ moves, const uint32_t *__restrict__ owner,
+                                    gn_board *__restrict__ children, ChildDelta *__restrict__ deltas,
+                                    uint8_t *__restrict__ next_slot, int chain_k, unsigned long long *__restrict__ rows) {
+  const size_t c = c0 + (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  unsigned long long nr = 0;
+  if (c < c0 + nc) {
+    const uint32_t i = owner[c];
+    Board B;
+    unpack(boards[i], B); // valid: an invalid parent has no children
+    Dirty d;
+    const Board C = do_move(B, moves[c], &d);
+    gn_board pb;
+    pack(C, pb);
+    children[c] = pb;
+    if (deltas) deltas[c] = make_child_delta(B, C, d);
+    // per child either the delta rows or a refresh of the perspective whose king moved
+    nr = d.king_moved ? popcnt(C.byType[0]) + d.n_rem + d.n_add : 2 * (d.n_rem + d.n_add);
+    // next_slot[i]: the child whose placement is boards[i + 1]'s (a game's next position;
+    // no two legal moves give one placement); the chained walk then starts parent i + 1
+    // from that child's accumulators, gathering one carry row per perspective instead of
+    // its refresh
+    if (next_slot && (size_t)i + 1 < n) {
+      const gn_board nb = boards[i + 1];
+      if (same_placement(pb, nb)) {
+        next_slot[i] = (uint8_t)(c - offsets[i]);
+        if (chain_k > 1 && ((size_t)i + 1) % (size_t)chain_k != 0) nr -= 2ull * popcnt(nb.occ) - 2;
+      }
+    }
+  }
+  if (rows) { // one atomic per workgroup
+    __shared__ unsigned long long part[4];
+#pragma unroll
+    for (int off = 32; off; off >>= 1) nr += __shfl_down(nr, off, 64);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = nr;
+    __syncthreads();
+    if (threadIdx.x == 0) atomicAdd(rows, part[0] + part[1] + part[2] + part[3]);
+  }
 }
 
 __global__ void count_sum_kernel(const gn_board *__restrict__ boards, size_t n, const Tables *__restrict__ tables,
@@ -1722,11 +1746,16 @@ hipError_t launch_count_children(const gn_board *boards, size_t n, const Tables 
 }
 
 hipError_t launch_write_children(const gn_board *boards, size_t n, const Tables *tables, const uint64_t *offsets,
-                                 gn_board *children, uint16_t *moves, ChildDelta *deltas, uint8_t *next_slot,
-                                 int chain_k, unsigned long long *rows, hipStream_t s) {
+                                 size_t c0, size_t nc, gn_board *children, uint16_t *moves, uint32_t *owner,
+                                 ChildDelta *deltas, uint8_t *next_slot, int chain_k, unsigned long long *rows,
+                                 hipStream_t s) {
   if (!n) return hipSuccess;
-  hipLaunchKernelGGL(write_children_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, boards, n, tables, offsets,
-                     children, moves, deltas, next_slot, chain_k, rows);
+  if (!moves || !owner) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(child_moves_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, boards, n, tables, offsets, moves,
+                     owner, next_slot, rows);
+  if (nc)
+    hipLaunchKernelGGL(child_boards_kernel, dim3(blocks_for(nc, 256)), dim3(256), 0, s, boards, n, offsets, c0, nc,
+                       moves, owner, children, deltas, next_slot, chain_k, rows);
   return hipGetLastError();
 }
 
@@ -1785,6 +1814,49 @@ hipError_t king_sort(const gn_board *boards, size_t n, uint64_t *keys, uint32_t 
   if (placement) return king_sort_t(boards, n, keys, idx, keys_out, perm, temp, temp_bytes, s);
   return king_sort_t(boards, n, reinterpret_cast<uint16_t *>(keys), idx, reinterpret_cast<uint16_t *>(keys_out), perm,
                      temp, temp_bytes, s);
+}
+
+// Block order of the planned expansion (stream_eval_kernel's order[]): blocks sorted by
+// the king squares of their middle parent, so that the blocks an XCD runs together (the
+// XCD swizzle gives it a contiguous eighth of this order) gather from the same king-bucket
+// slices of the FT and share the XCD's L2.  keys: uint16 (wk << 6 | bk; 4095: invalid).
+__global__ void block_keys_kernel(const gn_board *__restrict__ parents, size_t n, uint32_t K, uint32_t nblk,
+                                  uint16_t *__restrict__ keys, uint32_t *__restrict__ idx) {
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= nblk) return;
+  const size_t pb = (size_t)b * K, pe = pb + K < n ? pb + K : n;
+  const gn_board p = parents[pb + (pe - pb) / 2];
+  uint64_t wlo, whi;
+  piece_words(p, wlo, whi);
+  uint64_t o = p.occ;
+  int wk = 63, bk = 63;
+  const int c = popcnt(o) <= 32 ? popcnt(o) : 0;
+  for (int k = 0; k < c; ++k) {
+    const int sq = pop_lsb(o), pc = piece_nibble(wlo, whi, k);
+    if (pc == make_piece(WHITE, KING)) wk = sq;
+    if (pc == make_piece(BLACK, KING)) bk = sq;
+  }
+  keys[b] = (uint16_t)(wk << 6 | bk);
+  idx[b] = b;
+}
+
+hipError_t block_order(const gn_board *parents, size_t n, uint32_t K, uint32_t nblk, uint16_t *keys, uint32_t *idx,
+                       uint16_t *keys_out, uint32_t *order, void *&temp, size_t &temp_bytes, hipStream_t s) {
+  if (!nblk) return hipSuccess;
+  hipLaunchKernelGGL(block_keys_kernel, dim3(blocks_for(nblk, 256)), dim3(256), 0, s, parents, n, K, nblk, keys, idx);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  size_t need = 0;
+  e = hipcub::DeviceRadixSort::SortPairs(nullptr, need, keys, keys_out, idx, order, (int)nblk, 0, 12, s);
+  if (e != hipSuccess) return e;
+  if (need > temp_bytes) {
+    if (temp) (void)hipFree(temp);
+    temp = nullptr;
+    temp_bytes = 0;
+    if ((e = hipMalloc(&temp, need)) != hipSuccess) return e;
+    temp_bytes = need;
+  }
+  return hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, keys, keys_out, idx, order, (int)nblk, 0, 12, s);
 }
 
 hipError_t exclusive_scan_u64(const uint64_t *counts, uint64_t *offsets, size_t n1, void *&temp, size_t &temp_bytes,

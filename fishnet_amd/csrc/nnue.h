@@ -12,6 +12,7 @@
 //   w0      [8 buckets][16][L1] int8     b0 [8][16] int32    (fc_0)
 //   w1      [8][32][32] int8             b1 [8][32] int32    (fc_1, cols 30,31 pad)
 //   w2      [8][32] int8                 b2 [8] int32        (fc_2)
+//   psqt    [8 buckets][22528 + 1] int32: the PSQT weights again, bucket-major (L2-sized)
 #pragma once
 #include <stdint.h>
 
@@ -56,6 +57,7 @@ struct NetDevice {
   const int32_t *b1;
   const int8_t *w2;
   const int32_t *b2;
+  const int32_t *psqt; // [PSQT_BUCKETS][FT_ROWS]: the rows' PSQT weights by bucket (a copy)
 };
 
 // HalfKAv2_hm feature index:

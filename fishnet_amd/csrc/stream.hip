@@ -45,6 +45,9 @@
 #ifndef GN_ASM_RING
 #define GN_ASM_RING 0 // measured: 307 ms with, 259 ms without (the compiler's own waits are the faster ring)
 #endif
+#ifndef GN_PLAN_WPE
+#define GN_PLAN_WPE 4 // 128 VGPRs, no spills: 4 latency-bound plan waves per SIMD instead of 3
+#endif
 #ifndef GN_EXPAND_WPE
 #define GN_EXPAND_WPE 5
 #endif
@@ -52,7 +55,7 @@
 #ifdef GN_STREAM_PROF
 // diagnostics build only: per-phase s_memtime cycles summed over waves, and list balance
 __device__ unsigned long long gn_sp[8]; // [0] stream [1] barrier wait [2] layer stack [3] tiles
-                                       // [4] sum max(n0, n1) [5] sum n0 + n1
+                                       // [4] sum max(n0, n1) [5] sum n0 + n1 [6] / [7] no-op entries (scratch order / tile end)
 #define SP_T() __builtin_amdgcn_s_memtime()
 #define SP_ADD(k, v) atomicAdd(&gn_sp[k], (unsigned long long)(v))
 #else
@@ -78,25 +81,23 @@ __device__ __forceinline__ void wave_sync() {
 
 // ------------------------------------------------------------------- plan --
 template <int L1>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLAN_WPE)))
     plan_kernel(NetDevice net, const gn_board *__restrict__ parents, const uint64_t *__restrict__ offsets,
                 const ChildDelta *__restrict__ deltas, const uint8_t *__restrict__ need_parent,
                 const uint8_t *__restrict__ need_child, const uint8_t *__restrict__ next_slot, uint32_t np, uint32_t K,
-                int kc, const uint64_t *__restrict__ eoff, uint32_t *__restrict__ ent, TileDesc *__restrict__ tiles,
+                uint32_t b0, uint32_t b1, int kc, const uint64_t *__restrict__ eoff, uint32_t *__restrict__ ent, TileDesc *__restrict__ tiles,
                 uint32_t *__restrict__ btiles, unsigned long long *__restrict__ rows_out, uint32_t *__restrict__ err) {
   using namespace ps;
-  constexpr uint32_t RS = 2 * L1 + 32;
   __shared__ uint32_t ksnap[4][128][8]; // per wave: placement (64 nibbles) of each king-cache row
   __shared__ uint8_t kstate[4][128];    // bit 0: row holds an accumulator, bit 1: the list that stored it
   __shared__ uint16_t prow_s[4][2][32];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const uint32_t blk = blockIdx.x * 4 + (uint32_t)w;
-  const uint32_t nblk = (np + K - 1) / K;
-  if (blk >= nblk) return; // the whole wave (no workgroup barriers in this kernel)
-  const __amdgpu_buffer_rsrc_t ftr =
-      __builtin_amdgcn_make_buffer_rsrc((void *)net.ft, 0, (int)((size_t)FT_ROWS * RS), 0x00020000);
-  auto psqt = [&](uint32_t row, int bucket) -> int32_t {
-    return (int32_t)__builtin_amdgcn_raw_buffer_load_b32(ftr, row * RS + 2 * L1 + 4 * bucket, 0, 0);
+  const uint32_t blk = b0 + blockIdx.x * 4 + (uint32_t)w; // this launch plans blocks [b0, b1)
+  if (blk >= b1) return; // the whole wave (no workgroup barriers in this kernel)
+  const __amdgpu_buffer_rsrc_t pst = __builtin_amdgcn_make_buffer_rsrc(
+      (void *)net.psqt, 0, (int)((size_t)PSQT_BUCKETS * FT_ROWS * 4), 0x00020000);
+  auto psqt = [&](uint32_t row, int bucket) -> int32_t { // bucket-major copy (L2-resident)
+    return (int32_t)__builtin_amdgcn_raw_buffer_load_b32(pst, (bucket * (uint32_t)FT_ROWS + row) * 4, 0, 0);
   };
   const uint32_t pbeg = blk * K, pend = pbeg + K < np ? pbeg + K : np;
   const uint64_t us_b = pbeg + offsets[pbeg];
@@ -114,10 +115,11 @@ __global__ void __launch_bounds__(256)
   uint32_t len0 = 0, len1 = 0, tile_k = 0, p_first = pbeg, u_fill = 0, t_first = 0, tile_bm = 0;
   uint32_t safe0 = 0, safe1 = 0; // first index of each list at which a scratch row may be loaded
   int t_fill = 0, carried = 0;
-  unsigned long long rows = 0;
+  unsigned long long rows = 0, pads = 0, fpads = 0;
   auto pad_to = [&](int g, uint32_t target) { // no-op entries up to target (lane-parallel, < 64)
     uint32_t &len = g ? len1 : len0;
     if (len < target) {
+      pads += target - len;
       if ((uint32_t)lane < target - len) put(g, len + lane, PAD);
       len = target;
     }
@@ -129,6 +131,7 @@ __global__ void __launch_bounds__(256)
       if (len0 + lane < ((len0 + 3) & ~3u)) put(0, len0 + lane, PAD);
       if (len1 + lane < ((len1 + 3) & ~3u)) put(1, len1 + lane, PAD);
     }
+    fpads += (((len0 + 3) & ~3u) - len0) + (((len1 + 3) & ~3u) - len1);
     len0 = (len0 + 3) & ~3u, len1 = (len1 + 3) & ~3u;
     TileDesc *d = T + tile_k;
     if (lane >= t_fill && lane < 16) d->meta[lane] = 0;
@@ -394,16 +397,19 @@ __global__ void __launch_bounds__(256)
   if (lane == 0) {
     if ((uint64_t)len0 + len1 > rend - rbeg) atomicOr(err, 1u); // cannot happen: eoff bounds the entries
     if (rows_out) atomicAdd(rows_out, rows);
+    SP_ADD(6, pads), SP_ADD(7, fpads);
   }
+  (void)pads, (void)fpads;
 }
 
 // ----------------------------------------------------------------- stream --
 template <int L1>
 __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_EXPAND_WPE)))
-    stream_eval_kernel(NetDevice net, const uint64_t *__restrict__ offsets, uint32_t np, uint32_t K, int swz,
+    stream_eval_kernel(NetDevice net, const uint64_t *__restrict__ offsets, uint32_t np, uint32_t K, uint32_t b0,
+                       uint32_t b1, int swz,
                        const uint64_t *__restrict__ eoff, const uint32_t *__restrict__ ent,
                        const TileDesc *__restrict__ tiles, const uint32_t *__restrict__ btiles,
-                       int2 *__restrict__ out_parent, int2 *__restrict__ out_child,
+                       const uint32_t *__restrict__ order, int2 *__restrict__ out_parent, int2 *__restrict__ out_child,
                        uint32_t *__restrict__ pool, int use_scr, uint32_t *__restrict__ err, int ablate) {
   using namespace ps;
   constexpr int G = L1 / 16; // threads per perspective group (whole waves)
@@ -421,7 +427,9 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
   const __amdgpu_buffer_rsrc_t ftr = __builtin_amdgcn_make_buffer_rsrc(
       (void *)net.ft, 0, (int)(((size_t)FT_ROWS + (size_t)SCR_ROWS * SCR_SLOTS) * RS), 0x00020000);
   for (int i = tid; i < 512; i += NT) (&acc0[0][0])[i] = 0;
-  const uint32_t nblk = (np + K - 1) / K;
+  // this launch evaluates blocks [b0, b1); with swz, XCD x (= dispatch index mod 8) takes
+  // the x-th contiguous eighth of them (a block's king-sorted neighbours share its L2)
+  const uint32_t nblk = b1 - b0;
   const uint32_t vgrid = swz ? 8 * ((nblk + 7) / 8) : nblk;
   uint32_t v = blockIdx.x;
   if (v >= vgrid) return;
@@ -431,6 +439,7 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
     blk = (v & 7) * b8 + (v >> 3);
     if (blk >= nblk) return;
   }
+  blk = order ? order[blk] : blk + b0; // order: a permutation of [b0, b1) (block_order)
   const uint32_t pbeg = blk * K, pend = pbeg + K < np ? pbeg + K : np;
   const uint64_t us_b = pbeg + offsets[pbeg];
   const uint32_t ntiles = btiles[blk];
@@ -749,28 +758,28 @@ hipError_t launch_plan_stream(const NetDevice &net, const gn_board *parents, siz
                               const ChildDelta *deltas, const uint8_t *need_parent, const uint8_t *need_child,
                               int2 *out_parent, int2 *out_child, int swz, const uint8_t *next_slot, int chain_k,
                               int kc, const uint64_t *eoff, uint32_t *ent, TileDesc *tiles, uint32_t *btiles,
-                              uint32_t *pool, uint32_t *err, unsigned long long *rows_out, hipStream_t s) {
-  if (!n) return hipSuccess;
+                              uint32_t *pool, uint32_t *err, unsigned long long *rows_out, size_t b0, size_t b1,
+                              const uint32_t *order, hipStream_t s) {
+  if (!n || b1 <= b0) return hipSuccess;
   if (n >= 0x80000000ull) return hipErrorInvalidValue; // 32-bit parent indices in the kernels
   const uint32_t K = chain_k > 1 && next_slot ? (uint32_t)chain_k : 1u;
   const int scr = K > 1 || kc; // carry rows or king cache in use
-  const uint32_t nblk = (uint32_t)((n + K - 1) / K);
-  hipError_t e = hipMemsetAsync(pool, 0, 64 * sizeof(uint32_t), s);
-  if (e != hipSuccess) return e;
-  const unsigned pg = (nblk + 3) / 4, g = swz ? 8 * ((nblk + 7) / 8) : nblk;
+  if (b1 > (n + K - 1) / K) return hipErrorInvalidValue;
+  const uint32_t nb = (uint32_t)(b1 - b0), B0 = (uint32_t)b0, B1 = (uint32_t)b1;
+  const unsigned pg = (nb + 3) / 4, g = swz ? 8 * ((nb + 7) / 8) : nb;
   static const int ablate = getenv("GN_ABLATE") ? atoi(getenv("GN_ABLATE")) : 0; // timing diagnostics only
   if (net.L1 == 3072) {
     hipLaunchKernelGGL((plan_kernel<3072>), dim3(pg), dim3(256), 0, s, net, parents, offsets, deltas, need_parent,
-                       need_child, K > 1 ? next_slot : nullptr, (uint32_t)n, K, K > 1 ? kc : 0, eoff, ent, tiles,
-                       btiles, rows_out, err);
-    hipLaunchKernelGGL((stream_eval_kernel<3072>), dim3(g), dim3(384), 0, s, net, offsets, (uint32_t)n, K, swz, eoff,
-                       ent, tiles, btiles, out_parent, out_child, pool, scr, err, ablate);
+                       need_child, K > 1 ? next_slot : nullptr, (uint32_t)n, K, B0, B1, K > 1 ? kc : 0, eoff, ent,
+                       tiles, btiles, rows_out, err);
+    hipLaunchKernelGGL((stream_eval_kernel<3072>), dim3(g), dim3(384), 0, s, net, offsets, (uint32_t)n, K, B0, B1,
+                       swz, eoff, ent, tiles, btiles, order, out_parent, out_child, pool, scr, err, ablate);
   } else if (net.L1 == 1024) {
     hipLaunchKernelGGL((plan_kernel<1024>), dim3(pg), dim3(256), 0, s, net, parents, offsets, deltas, need_parent,
-                       need_child, K > 1 ? next_slot : nullptr, (uint32_t)n, K, K > 1 ? kc : 0, eoff, ent, tiles,
-                       btiles, rows_out, err);
-    hipLaunchKernelGGL((stream_eval_kernel<1024>), dim3(g), dim3(128), 0, s, net, offsets, (uint32_t)n, K, swz, eoff,
-                       ent, tiles, btiles, out_parent, out_child, pool, scr, err, ablate);
+                       need_child, K > 1 ? next_slot : nullptr, (uint32_t)n, K, B0, B1, K > 1 ? kc : 0, eoff, ent,
+                       tiles, btiles, rows_out, err);
+    hipLaunchKernelGGL((stream_eval_kernel<1024>), dim3(g), dim3(128), 0, s, net, offsets, (uint32_t)n, K, B0, B1,
+                       swz, eoff, ent, tiles, btiles, order, out_parent, out_child, pool, scr, err, ablate);
   } else {
     return hipErrorInvalidValue;
   }
@@ -780,8 +789,8 @@ hipError_t launch_plan_stream(const NetDevice &net, const gn_board *parents, siz
     (void)hipStreamSynchronize(s);
     (void)hipMemcpyFromSymbol(c, HIP_SYMBOL(gn_sp), sizeof(c));
     fprintf(stderr, "stream prof: wave-cycles stream %llu barrier %llu ls %llu; tiles %llu; "
-                    "entries max-list %llu sum %llu (balance %.3f)\n",
-            c[0], c[1], c[2], c[3], c[4], c[5], c[5] ? 2.0 * c[4] / c[5] : 0.0);
+                    "entries max-list %llu sum %llu (balance %.3f), no-op entries %llu scratch-order + %llu tile-end\n",
+            c[0], c[1], c[2], c[3], c[4], c[5], c[5] ? 2.0 * c[4] / c[5] : 0.0, c[6], c[7]);
     memset(c, 0, sizeof(c));
     (void)hipMemcpyToSymbol(HIP_SYMBOL(gn_sp), c, sizeof(c));
   }
