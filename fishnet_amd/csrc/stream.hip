@@ -42,8 +42,11 @@
 #include "device_util.h"
 #include "kernels.h"
 
+#ifndef GN_CONSUME_MAD
+#define GN_CONSUME_MAD 1
+#endif
 #ifndef GN_ASM_RING
-#define GN_ASM_RING 0 // measured: 307 ms with, 259 ms without (the compiler's own waits are the faster ring)
+#define GN_ASM_RING 1 // with GN_CONSUME_MAD: 257 ms vs 273 ms (compiler waits: a vmcnt(0) at the first entry of each revolution)
 #endif
 #ifndef GN_PLAN_WPE
 #define GN_PLAN_WPE 4 // 128 VGPRs, no spills: 4 latency-bound plan waves per SIMD instead of 3
@@ -538,6 +541,29 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
   auto consume = [&](int r) {
     ring_wait(r);
     const uint32_t e = er[r];
+#ifdef GN_ABL_SIMPLE // timing diagnostics only (wrong results): no entry-kind branches
+    lo += rlo[r], hi += rhi[r];
+    if (e & LAST) *reinterpret_cast<uint2 *>(xt + ((e >> SLOT_SH) & 15) * XS + ((e >> SIDE_SH) & 1) * (L1 / 2) + 8 * jt) = transform8(lo, hi);
+    return;
+#endif
+#if GN_CONSUME_MAD
+    // every kind of entry is one 16-bit multiply-add per dword: acc = src + sg * row with
+    // sg = +1, -1 (SUB) or 0 (a no-op: ZERO | SUB), src = acc, or 0 / the parent / the
+    // sibling base at the entry that starts a slot (wrapping int16, as the accumulators)
+    const bool nop = (e & (INIT | SUB)) == (I_ZERO | SUB);
+    const uint32_t init = nop ? 0u : (e & INIT);
+    const unsigned short sg = nop ? (unsigned short)0 : (e & SUB) ? (unsigned short)0xFFFF : (unsigned short)1;
+    if (init) {
+      const ushort8 z = {};
+      lo = init == I_PACC ? pacc_lo : init == I_BASE ? base_lo : z;
+      hi = init == I_PACC ? pacc_hi : init == I_BASE ? base_hi : z;
+    }
+    lo = rlo[r] * sg + lo, hi = rhi[r] * sg + hi;
+    if (init == I_PACC) {
+      asm volatile("");
+      base_lo = lo, base_hi = hi;
+    }
+#else
     const uint32_t init = e & INIT;
     // scalar branches; the empty asm keeps the compiler from if-converting them into
     // selects over every alternative
@@ -563,6 +589,7 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
       asm volatile("");
       lo += rlo[r], hi += rhi[r];
     }
+#endif
     if (e & LAST) {
       const int sl = (e >> SLOT_SH) & 15, side = (e >> SIDE_SH) & 1;
       *reinterpret_cast<uint2 *>(xt + sl * XS + side * (L1 / 2) + 8 * jt) = transform8(lo, hi);
