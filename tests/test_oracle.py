@@ -208,3 +208,43 @@ def test_incremental_oracle_equals_refresh(oracle_lib, stress):
         for i, fen in enumerate(fens):
             p_exp, m_exp, k_exp = oracle_lib.expand_eval(big, small, fen, mode)
             assert tuple(par[i]) == p_exp and cnt[i] == len(m_exp) and np.array_equal(kids[i, :cnt[i]], k_exp)
+
+
+def test_oracle_under_sanitizers(oracle_lib, tmp_path):
+    """The oracle built with AddressSanitizer + UBSan (oracle/Makefile `sanitize`, a driver
+    executable) over the hand-picked edge FENs plus a bad one: no sanitizer report, refresh
+    and incremental expansion equal, and the same numbers as the regular build."""
+    import shutil
+    import subprocess
+    from fishnet_amd import synthnet
+    if not shutil.which("gcc"):
+        pytest.skip("no host compiler")
+    odir = os.path.join(HERE, "..", "oracle")
+    r = subprocess.run(["make", "-s", "-C", odir, "sanitize"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    exe = os.path.join(odir, "_build", "oracle_sanitize")
+    fens = [ln.strip() for ln in open(os.path.join(HERE, "golden", "special_fens.txt"))
+            if ln.strip() and not ln.startswith("#")][:12]
+    fens.append("8/8/8/8/8/8/8/8 w - - 0 1")  # no kings: rejected
+    fpath = tmp_path / "fens.txt"
+    fpath.write_text("\n".join(fens) + "\n")
+    big_p, small_p = synthnet.cached_synth_net(3072, 1), synthnet.cached_synth_net(128, 2)
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0:exitcode=23",
+               UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1")
+    r = subprocess.run([exe, big_p, small_p, str(fpath)], capture_output=True, text=True, env=env, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "runtime error" not in r.stderr and "AddressSanitizer" not in r.stderr, r.stderr[-3000:]
+    lines = r.stdout.split("\n")
+    big, small = oracle_lib.Net(big_p), oracle_lib.Net(small_p)
+    for fen, line in zip(fens, lines):
+        if line == "bad":
+            with pytest.raises(ValueError):
+                oracle_lib.perft(fen, 1)
+            continue
+        fv, fcp, n, s, p2 = (int(x) for x in line.split())
+        e = oracle_lib.eval_fen(big, small, fen, oracle_lib.MODE_FULL)
+        _, _, kids = oracle_lib.expand_eval(big, small, fen, oracle_lib.MODE_BIG)
+        assert (fv, fcp) == (e[2], e[3]), fen
+        assert (n, s) == (len(kids), int(kids["final_v"].astype(np.int64).sum())), fen
+        assert p2 == oracle_lib.perft(fen, 2), fen
+    assert lines[len(fens) - 1] == "bad"
