@@ -15,7 +15,7 @@ CSRC = os.path.join(HERE, "csrc")
 LIBDIR = os.path.join(HERE, "lib")
 LIB = os.path.join(LIBDIR, "libgpu_nnue.so")
 SOURCES = ["gpu_nnue.hip", "kernels.hip", "stream.hip"]
-HEADERS = ["chess.h", "host_board.h", "nnue.h", "kernels.h", "sha256.h", "device_util.h"]
+HEADERS = ["chess.h", "host_board.h", "nnue.h", "kernels.h", "sha256.h", "device_util.h", "archive.h"]
 ARCH = "gfx950"
 
 

@@ -16,6 +16,7 @@
 #include <thread>
 #include <vector>
 
+#include "archive.h"
 #include "host_board.h"
 #include "kernels.h"
 #include "sha256.h"
@@ -1196,6 +1197,88 @@ int gn_load_net(const char *big_path, const char *small_path, const int *devices
     if (small_path && (rc = check_net_name(small_path, s)) != GN_OK) return rc;
     return create(big_path ? b.data() : nullptr, b.size(), small_path ? s.data() : nullptr, s.size(), devices,
                   n_devices, out);
+  } catch (const std::bad_alloc &) {
+    return fail(GN_E_NOMEM, "host allocation failed");
+  } catch (...) {
+    return fail(GN_E_INVALID, "unexpected exception");
+  }
+}
+
+// L1 width of a .nnue image from its header hashes (0: not a supported net)
+static int net_l1(const uint8_t *d, size_t n) {
+  auto u32 = [&](size_t o) { return (uint32_t)d[o] | (uint32_t)d[o + 1] << 8 | (uint32_t)d[o + 2] << 16 | (uint32_t)d[o + 3] << 24; };
+  if (n < 12 || u32(0) != NNUE_VERSION) return 0;
+  const size_t dl = u32(8);
+  if (12 + dl + 4 > n) return 0;
+  const uint32_t hash = u32(4), fth = u32(12 + dl);
+  for (int c : {3072, 1024, 128})
+    if (ft_hash(c) == fth && (ft_hash(c) ^ arch_hash(c)) == hash) return c;
+  return 0;
+}
+
+// The members of an assets archive (zstd + ar, archive.h); GN_OK or a failure.
+static int read_archive(const char *path, std::vector<uint8_t> &img, std::vector<archive::Member> &mem) {
+  std::vector<uint8_t> file;
+  if (!path || !read_file(path, file)) return fail(GN_E_IO, "cannot read %s", path ? path : "(null)");
+  std::string err;
+  if (!archive::load_image(file, img, err) || !archive::ar_members(img.data(), img.size(), mem, err))
+    return fail(GN_E_FORMAT, "%s: %s", path, err.c_str());
+  return GN_OK;
+}
+
+int gn_archive_read(const char *path, const char *member, uint8_t *buf, size_t cap, size_t *size) {
+  try {
+    if (!member || !size) return fail(GN_E_INVALID, "bad argument");
+    std::vector<uint8_t> img;
+    std::vector<archive::Member> mem;
+    int rc = read_archive(path, img, mem);
+    if (rc) return rc;
+    for (const auto &m : mem)
+      if (m.name == member) {
+        *size = m.size;
+        if (m.size > cap || (!buf && m.size)) return fail(GN_E_CAPACITY, "%s is %zu bytes", member, m.size);
+        if (m.size) memcpy(buf, img.data() + m.off, m.size);
+        return GN_OK;
+      }
+    return fail(GN_E_IO, "%s has no member %s", path, member);
+  } catch (const std::bad_alloc &) {
+    return fail(GN_E_NOMEM, "host allocation failed");
+  } catch (...) {
+    return fail(GN_E_INVALID, "unexpected exception");
+  }
+}
+
+int gn_load_net_archive(const char *path, const char *big_member, const char *small_member, const int *devices,
+                        int n_devices, gn_ctx **out) {
+  try {
+    std::vector<uint8_t> img;
+    std::vector<archive::Member> mem;
+    int rc = read_archive(path, img, mem);
+    if (rc) return rc;
+    const archive::Member *pick[2] = {nullptr, nullptr};
+    const char *want[2] = {big_member, small_member};
+    for (int w = 0; w < 2; ++w)
+      for (const auto &m : mem) {
+        const uint8_t *d = img.data() + m.off;
+        const int l1 = net_l1(d, m.size);
+        const bool ends = m.name.size() > 5 && m.name.compare(m.name.size() - 5, 5, ".nnue") == 0;
+        // by name, or the first .nnue of the right kind (big: L1 3072 / 1024, small: 128)
+        if (want[w] ? m.name == want[w] : (ends && l1 && ((w == 0) == (l1 != 128)))) {
+          pick[w] = &m;
+          break;
+        }
+      }
+    if (!pick[0] && !pick[1]) return fail(GN_E_IO, "%s holds no usable .nnue member", path);
+    if ((big_member && !pick[0]) || (small_member && !pick[1]))
+      return fail(GN_E_IO, "%s has no member %s", path, !pick[0] && big_member ? big_member : small_member);
+    for (int w = 0; w < 2; ++w)
+      if (pick[w]) { // Stockfish's name check: nn-<first 12 hex of SHA-256>.nnue
+        std::vector<uint8_t> data(img.begin() + pick[w]->off, img.begin() + pick[w]->off + pick[w]->size);
+        if ((rc = check_net_name(pick[w]->name.c_str(), data)) != GN_OK) return rc;
+      }
+    return create(pick[0] ? img.data() + pick[0]->off : nullptr, pick[0] ? pick[0]->size : 0,
+                  pick[1] ? img.data() + pick[1]->off : nullptr, pick[1] ? pick[1]->size : 0, devices, n_devices,
+                  out);
   } catch (const std::bad_alloc &) {
     return fail(GN_E_NOMEM, "host allocation failed");
   } catch (...) {

@@ -22,7 +22,7 @@ MODE_FULL, MODE_BIG, MODE_SMALL = 0, 1, 2
 FLAG_IN_CHECK, FLAG_SMALLNET, FLAG_BAD_FEN, FLAG_REEVAL, FLAG_SKIPPED = 1, 2, 4, 8, 16
 ERRORS = {-1: "INVALID", -2: "IO", -3: "FORMAT", -4: "HIP", -5: "NOMEM", -6: "CAPACITY",
           -7: "NODEVICE", -8: "NONET", -9: "ILLEGAL_MOVE"}
-E_INVALID, E_CAPACITY, E_ILLEGAL_MOVE = -1, -6, -9
+E_INVALID, E_IO, E_FORMAT, E_CAPACITY, E_ILLEGAL_MOVE = -1, -2, -3, -6, -9
 
 EVAL_DTYPE = np.dtype([("psqt", "<i4"), ("positional", "<i4"), ("final_v", "<i4"), ("final_cp", "<i2"),
                        ("flags", "<u2")])
@@ -38,7 +38,7 @@ EXPORTS = ["gn_load_net", "gn_load_net_memory", "gn_free", "gn_last_error", "gn_
            "gn_time_evaluate_device", "gn_random_positions_device", "gn_set_option", "gn_get_option",
            "gn_time_expand_device", "gn_random_games_device", "gn_replay_game", "gn_evaluate_games",
            "gn_net_sha256", "gn_partition", "gn_checksum_device",
-           "gn_boards_to_fens"]
+           "gn_boards_to_fens", "gn_load_net_archive", "gn_archive_read"]
 OPT_INCREMENTAL_CHILDREN, OPT_XCD_SWIZZLE, OPT_KING_SORT, OPT_CHAIN, OPT_KING_CACHE = 1, 2, 3, 4, 5
 STAT_CHAIN_FALLBACKS = 100
 EXPAND_STAGES = ["count_scan", "total_readback", "write_children", "classify", "small_net", "big_net", "finalize"]
@@ -127,6 +127,8 @@ def lib():
         "gn_partition": [vp, sz, i32, vp],
         "gn_boards_to_fens": [vp, sz, vp, sz],
         "gn_evaluate_games": [vp, vp, sz, i32, i32, vp, vp, vp, sz, vp, vp, vp, sz],
+        "gn_load_net_archive": [C.c_char_p, C.c_char_p, C.c_char_p, vp, i32, C.POINTER(vp)],
+        "gn_archive_read": [C.c_char_p, C.c_char_p, vp, sz, C.POINTER(sz)],
     }
     for name, args in sig.items():
         f = getattr(L, name)
@@ -253,14 +255,30 @@ class DeviceBuffer:
             pass
 
 
+def archive_read(path, member):
+    """One member of an assets archive (zstd + ar) as bytes (gn_archive_read; CPU only)."""
+    size = C.c_size_t()
+    rc = lib().gn_archive_read(path.encode(), member.encode(), None, 0, C.byref(size))
+    if rc not in (0, E_CAPACITY):
+        _check(rc)
+    buf = (C.c_uint8 * max(size.value, 1))()
+    _check(lib().gn_archive_read(path.encode(), member.encode(), buf, size.value, C.byref(size)))
+    return bytes(buf[:size.value])
+
+
 class GpuNnue:
     """load_net + evaluate_batch (the north-star `gpu_nnue` module surface)."""
 
-    def __init__(self, big_path=None, small_path=None, devices=None, big_bytes=None, small_bytes=None):
+    def __init__(self, big_path=None, small_path=None, devices=None, big_bytes=None, small_bytes=None,
+                 archive=None, big_member=None, small_member=None):
         self.h = C.c_void_p()
         devs = (C.c_int * len(devices))(*devices) if devices else None
         nd = len(devices) if devices else 0
-        if big_bytes is not None or small_bytes is not None:
+        if archive is not None:  # fishnet's assets.ar.zst (gn_load_net_archive)
+            enc = lambda x: x.encode() if x else None
+            _check(lib().gn_load_net_archive(archive.encode(), enc(big_member), enc(small_member), devs, nd,
+                                             C.byref(self.h)))
+        elif big_bytes is not None or small_bytes is not None:
             bb = (C.c_uint8 * len(big_bytes)).from_buffer_copy(big_bytes) if big_bytes is not None else None
             sb = (C.c_uint8 * len(small_bytes)).from_buffer_copy(small_bytes) if small_bytes is not None else None
             _check(lib().gn_load_net_memory(bb, len(big_bytes or b""), sb, len(small_bytes or b""), devs, nd,

@@ -179,6 +179,16 @@ GN_API int gn_load_net(const char *big_path, const char *small_path, const int *
 /* Same from in-memory .nnue images (e.g. after an RCCL broadcast). */
 GN_API int gn_load_net_memory(const uint8_t *big, size_t big_len, const uint8_t *small, size_t small_len,
                        const int *devices, int n_devices, gn_ctx **out);
+/* Nets from fishnet's asset archive (assets.ar.zst: a zstd-compressed `ar` archive, as
+ * /root/reference/build.rs:398-420 writes it and src/assets.rs:186-226 reads it; a plain
+ * `ar` works too).  big_member / small_member: member names (e.g. "nn-1c0000000000.nnue"),
+ * or NULL for the first .nnue member of that kind (big: L1 3072 / 1024; small: 128).
+ * Members named nn-<hex>.nnue are checked against their SHA-256 prefix.  zstd is
+ * decoded by the system's libzstd.so.1, opened at run time. */
+GN_API int gn_load_net_archive(const char *archive_path, const char *big_member, const char *small_member,
+                               const int *devices, int n_devices, gn_ctx **out);
+/* One member's bytes (CPU only): GN_E_CAPACITY with *size set when cap is too small. */
+GN_API int gn_archive_read(const char *archive_path, const char *member, uint8_t *buf, size_t cap, size_t *size);
 GN_API void gn_free(gn_ctx *ctx);
 GN_API const char *gn_last_error(void); /* thread-local; valid until the next call */
 GN_API int gn_abi_version(void);

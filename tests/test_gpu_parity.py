@@ -525,3 +525,30 @@ def test_common_row_base_under_int16_wrap_and_shared_kings(oracle_lib):
             _cmp(ctx.evaluate_batch(fens, 1), oracle_lib.eval_fens(on, None, fens, 1, threads=8), fens)
     finally:
         ctx.close()
+
+
+def test_nets_from_asset_archive(gpu_ctx, synth_big_path, synth_small_path, tmp_path):
+    """gn_load_net_archive: both nets out of a zstd-compressed `ar` shaped like fishnet's
+    assets.ar.zst (engine binary first, nets named nn-<sha256 prefix>.nnue), by name and
+    by kind; results equal to the file-loaded context; a renamed (hash-mismatched)
+    member is rejected."""
+    import hashlib
+    import archive_util as A
+    from fishnet_amd import gpu_nnue as G
+    big, small = open(synth_big_path, "rb").read(), open(synth_small_path, "rb").read()
+    nb = "nn-" + hashlib.sha256(big).hexdigest()[:12] + ".nnue"
+    ns = "nn-" + hashlib.sha256(small).hexdigest()[:12] + ".nnue"
+    p = tmp_path / "assets.ar.zst"
+    p.write_bytes(A.zstd(A.ar_bytes([("stockfish-x86-64-vnni512", b"\x7fELF" * 99), (nb, big), (ns, small)])))
+    fens = special_fens() + random_fens(500, 0xA5C1)
+    want = gpu_ctx.evaluate_batch(fens, 0)
+    for kw in ({}, {"big_member": nb, "small_member": ns}):
+        ctx = G.GpuNnue(archive=str(p), **kw)
+        assert ctx.net_info() == gpu_ctx.net_info()
+        assert np.array_equal(ctx.evaluate_batch(fens, 0), want)
+        ctx.close()
+    q = tmp_path / "renamed.ar.zst"
+    q.write_bytes(A.zstd(A.ar_bytes([("nn-000000000000.nnue", big), (ns, small)])))
+    with pytest.raises(G.GnError) as e:
+        G.GpuNnue(archive=str(q), big_member="nn-000000000000.nnue")
+    assert e.value.code == G.E_FORMAT

@@ -142,3 +142,32 @@ def test_net_named_by_hash_is_checked(G, synth_small_path, tmp_path):
         G.GpuNnue(None, str(good)).close()
     except G.GnError as e2:  # no GPU in this container
         assert e2.code == -7, e2
+
+
+def test_archive_read_zstd_and_ar_variants(tmp_path):
+    """gn_archive_read over fishnet-style asset archives: zstd + BSD long names (the `ar`
+    crate's Builder, /root/reference/build.rs:398-420), GNU long names, plain `ar`; odd
+    sizes (padding), a missing member, a corrupt and a truncated archive."""
+    import archive_util as A
+    from fishnet_amd import gpu_nnue as G
+    members = [("stockfish-x86-64-avx2", b"\x7fELF" + bytes(range(251))), ("nn-1c0000000000.nnue", b"big" * 1001),
+               ("nn-37f18f62d772.nnue", b"small-net" * 7), ("odd", b"x")]
+    for gnu in (False, True):
+        for compress in (True, False):
+            img = A.ar_bytes(members, gnu=gnu)
+            p = tmp_path / f"assets_{gnu}_{compress}.ar{'.zst' if compress else ''}"
+            p.write_bytes(A.zstd(img) if compress else img)
+            for name, data in members:
+                assert G.archive_read(str(p), name) == data, (gnu, compress, name)
+            with pytest.raises(G.GnError) as e:
+                G.archive_read(str(p), "nn-000000000000.nnue")
+            assert e.value.code == G.E_IO
+    bad = tmp_path / "bad.ar.zst"
+    bad.write_bytes(A.zstd(b"!<arch>\nnot a header at all" * 3))
+    with pytest.raises(G.GnError) as e:
+        G.archive_read(str(bad), "odd")
+    assert e.value.code == G.E_FORMAT
+    trunc = tmp_path / "trunc.ar.zst"
+    trunc.write_bytes(A.zstd(A.ar_bytes(members))[:-7])
+    with pytest.raises(G.GnError):
+        G.archive_read(str(trunc), "odd")
