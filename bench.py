@@ -132,7 +132,7 @@ def roofline(alg_bytes, kern_ms, kernel, pmc):
     r = {"bound": "hbm", "kernel": kernel, "achieved": round(achieved, 1), "unit": "GB/s",
          "traffic": None, "alg_bytes_per_launch": int(alg_bytes), "kernel_ms_per_launch": round(kern_ms, 4),
          "peak_model": "alg_bytes / max(alg_bytes / 34.5 TB/s (L2), traffic / 8.6 TB/s (Infinity-Cache gather)); "
-                       "achieved = kernel-counted FT rows x (2*L1 + 4) B / kernel time"}
+                       "achieved = kernel-counted FT rows x (2*L1 + 4) B (row + its 4-B list entry) / kernel time"}
     if pmc:
         traffic = float(pmc["hbm_side_bytes_per_launch"])
         t_ic = traffic / (IC_GATHER_GBS * 1e9)
@@ -259,13 +259,19 @@ def run_expand(c: Ctx, wl: dict, games: int, steps: int, warmup: int, check: int
     c.barrier_sync()
     wall = c.comm.max(time.perf_counter() - t0)
     fallbacks = nn.get_option(G.STAT_CHAIN_FALLBACKS)
+    # the big net's two kernels timed apart (HIP events on the library's stream, inside the
+    # timed region): the roofline's dominant kernel is stream_eval_kernel alone
+    plan_ms, stream_ms = nn.get_option(G.STAT_PLAN_NS) / 1e6, nn.get_option(G.STAT_STREAM_NS) / 1e6
     parents = d_p.download(G.BOARD_DTYPE, n)
     sums = (nn.checksum_device(out["po"], n * 16), nn.checksum_device(out["co"], children * 16),
             nn.checksum_device(out["mv"], children * 2), nn.checksum_device(out["off"], (n + 1) * 4))
-    r = dict(value=c.world * (n + children) * steps / wall, wall=wall, stage=stage, kern_ms=stage[5 if mode != 2 else 4],
-             alg=rows * (2 * wl["l1"] + 4) + n * 32 + children * (24 + 8), rows=rows, parents=parents, n=n,
+    planned = stream_ms > 0
+    r = dict(value=c.world * (n + children) * steps / wall, wall=wall, stage=stage,
+             kern_ms=stream_ms if planned else stage[5 if mode != 2 else 4], plan_ms=plan_ms,
+             alg=rows * (2 * wl["l1"] + 4), rows=rows, parents=parents, n=n,
              children=children, gen_s=gen_s, checksum=sums[0] ^ sums[1], chain_fallbacks=fallbacks,
-             kernel=f"expand_stream<{wl['l1']}>" if wl["l1"] != 128 else f"expand_eval<{wl['l1']}>")
+             kernel=(f"stream_eval_kernel<{wl['l1']}>" if planned else f"expand_stream<{wl['l1']}>")
+             if wl["l1"] != 128 else f"expand_eval<{wl['l1']}>")
     if check:
         ver = {}
         # (1) sampled parents of the timed outputs, with all their children, against the oracle
@@ -311,6 +317,68 @@ def run_expand(c: Ctx, wl: dict, games: int, steps: int, warmup: int, check: int
         r["oracle_check"] = ver
     for b in ("po", "off", "mv", "co"):
         out[b].free()
+    d_p.free()
+    return r
+
+
+def run_expand2(c: Ctx, games: int, mode: int, steps: int, check: int):
+    """Depth 2 (gn_expand2_device): games x 81 parents, every legal child, and every legal
+    child of every child, each level incremental from its parent's accumulators."""
+    G, nn = c.G, c.nn
+    n = games * (PLIES + 1)
+    d_p = nn.alloc(n * 32)
+    first, _ = c.shard(games)
+    nn.random_games_device(SEED + 2, first, games, PLIES, d_p)
+    nn.synchronize()
+    out = {"po": nn.alloc(n * 16), "off": nn.alloc((n + 1) * 4), "cap": 0, "gcap": 0}
+    for _ in range(3):  # sized by the library's own capacity replies (also the warmup)
+        try:
+            t, g = nn.expand2_device(d_p, n, mode, out)
+            break
+        except G.GnError as e:
+            if e.code != G.E_CAPACITY:
+                raise
+            t, g = e.need
+            if t > out["cap"]:
+                out.update(cap=t, ch=nn.alloc(t * 32), mv=nn.alloc(t * 2), co=nn.alloc(t * 16), goff=nn.alloc((t + 1) * 4))
+            if g > out["gcap"]:
+                out.update(gcap=g, gmv=nn.alloc(max(g, 1) * 2), gco=nn.alloc(max(g, 1) * 16))
+    c.barrier_sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        t, g = nn.expand2_device(d_p, n, mode, out)
+    c.barrier_sync()
+    wall = c.comm.max(time.perf_counter() - t0)
+    r = {"workload": f"depth 2: {games} random 80-ply games per MI355X = {n} parents, their {t} legal children and "
+                     f"{g} grandchildren (gn_expand2_device, big net, every level incremental)",
+         "value": round(c.world * (n + t + g) * steps / wall, 1), "unit": "evals/s",
+         "ms_per_step": round(wall * 1e3 / steps, 3), "children": t, "grandchildren": g}
+    if check:  # the timed call's own outputs: sampled children's grandchildren vs the oracle
+        O, big, small = c.oracle_nets()
+        rng = np.random.default_rng(99 + c.rank)
+        idx = np.unique(rng.choice(t, size=min(check, t), replace=False))
+        kids = out["ch"].download(G.BOARD_DTYPE, t)
+        co = out["co"].download(G.EVAL_DTYPE, t)
+        goff = out["goff"].download(np.uint32, t + 1)
+        fens = [G.board_to_fen(kids[j]) for j in idx]
+
+        def one(k):
+            j = int(idx[k])
+            lo, hi = int(goff[j]), int(goff[j + 1])
+            mv = out["gmv"].download(np.uint16, hi - lo, offset=lo)
+            ev = out["gco"].download(G.EVAL_DTYPE, hi - lo, offset=lo)
+            p_exp, m_exp, k_exp = O.expand_eval(big, small, fens[k], mode, incremental=True)
+            return int(tuple(co[j]) != p_exp or dict(zip(mv.tolist(), map(tuple, ev.tolist()))) !=
+                       dict(zip(m_exp, map(tuple, k_exp.tolist())))), hi - lo
+
+        with cf.ThreadPoolExecutor(host_threads()) as ex:
+            res = list(ex.map(one, range(len(idx))))
+        r["oracle_check"] = {"children": len(idx), "grandchildren": sum(x[1] for x in res),
+                             "mismatching_children": sum(x[0] for x in res),
+                             "of": "the timed call's outputs (random children with all their children)"}
+    for b in out.values():
+        if hasattr(b, "free"):
+            b.free()
     d_p.free()
     return r
 
@@ -422,6 +490,8 @@ def main():
                 "options": c.options})
     roof = roofline(r["alg"], r["kern_ms"], r["kernel"], load_pmc(args.workload, n))
     roof["stage_ms"] = {k: round(v, 4) for k, v in zip(stage_names, r["stage"])}
+    if r.get("plan_ms"):
+        roof["plan_kernel_ms"] = round(r["plan_ms"], 4)
     line = {
         "metric": METRIC, "value": round(r["value"], 1), "unit": "evals/s", "n_gpus": c.world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(r["wall"] * 1e3 / args.steps, 3),
@@ -456,6 +526,10 @@ def main():
             if "oracle_check" in s:
                 sec[name]["oracle_check"] = s["oracle_check"]
                 sec[name]["rank_check_failures"] = c.comm.gather_i64(s["oracle_check"]["mismatches"])
+        g2 = run_expand2(c, 2048, 1, 2, 256 if args.check else 0)
+        if "oracle_check" in g2:
+            g2["rank_check_failures"] = c.comm.gather_i64(g2["oracle_check"]["mismatching_children"])
+        sec["grandchild"] = g2
         line["secondary"] = sec
 
     if c.rank == 0:

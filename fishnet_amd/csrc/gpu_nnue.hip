@@ -235,6 +235,7 @@ struct Dev {
   gn_board *dw_children = nullptr;
   uint16_t *dw_moves = nullptr;
   unsigned long long *dw_rows = nullptr;
+  float plan_ms = 0, stream_ms = 0; // the last timed planned expansion (GN_STAT_PLAN_NS / _STREAM_NS)
   static constexpr size_t MAX_CHUNKS = 4;
   uint64_t cbound[MAX_CHUNKS + 1] = {}; // children offsets at the range boundaries
   std::mutex mu;
@@ -566,6 +567,20 @@ static int finalize_range(gn_ctx *ctx, Dev &d, const gn_board *parents, const gn
   return GN_OK;
 }
 
+// Legal-child count of n boards (a capacity query), synchronously.
+static hipError_t count_children(Dev &d, const gn_board *parents, size_t n, hipStream_t s, size_t *total) {
+  hipError_t e;
+  if ((e = d.counts.ensure(n + 1)) != hipSuccess || (e = d.offsets.ensure(n + 1)) != hipSuccess) return e;
+  if ((e = hipMemsetAsync(d.counts.p + n, 0, sizeof(uint64_t), s)) != hipSuccess) return e;
+  if ((e = launch_count_children(parents, n, d.tables, d.counts.p, s)) != hipSuccess) return e;
+  if ((e = exclusive_scan_u64(d.counts.p, d.offsets.p, n + 1, d.scan_tmp, d.scan_bytes, s)) != hipSuccess) return e;
+  uint64_t t = 0;
+  if ((e = hipMemcpyAsync(&t, d.offsets.p + n, sizeof(t), hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+  if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+  *total = (size_t)t;
+  return hipSuccess;
+}
+
 static int generate_children(Dev &d, const gn_board *parents, size_t n, gn_board *children_or_null, size_t cap,
                              uint16_t *moves, bool want_deltas, size_t *total, hipStream_t s, hipEvent_t *ev,
                              unsigned long long *rows = nullptr, int chain_k = 1, bool plan = false,
@@ -635,8 +650,9 @@ static int generate_children(Dev &d, const gn_board *parents, size_t n, gn_board
 // Evaluate parents + children after generate_children.  Incremental: the
 // expand_eval kernels (one workgroup per parent, children from the parent
 // accumulators); otherwise every child is a full refresh (evaluate_on).
-// ev (optional) gets 4 events: after classify, after the small net (+reeval),
-// after the big net, after finalize.
+// ev (optional) gets 5 events: after classify, after the small net (+reeval),
+// after the big net, after finalize, and (planned path) between its plan and stream
+// kernels (recorded before the pipeline when it runs in several ranges).
 static int expand_evaluate(gn_ctx *ctx, Dev &d, const gn_board *parents, size_t n, const gn_board *children,
                            size_t total, int mode, gn_eval *parent_out, gn_eval *child_out, hipStream_t s,
                            hipEvent_t *ev, unsigned long long *rows_out = nullptr) {
@@ -667,7 +683,8 @@ static int expand_evaluate(gn_ctx *ctx, Dev &d, const gn_board *parents, size_t 
   }
   auto mark = [&](int k) -> hipError_t { return ev ? hipEventRecord(ev[k], s) : hipSuccess; };
   const gn_eval_params &P = ctx->P;
-  bool piped = false; // finalize ran inside the big net's pipeline
+  bool piped = false;       // finalize ran inside the big net's pipeline
+  hipEvent_t mid = nullptr; // recorded between the plan and stream kernels (timing)
   const uint64_t *off = d.offsets.p;
   const ChildDelta *dl = d.deltas.p;
   if (mode == GN_MODE_FULL) {
@@ -723,7 +740,7 @@ static int expand_evaluate(gn_ctx *ctx, Dev &d, const gn_board *parents, size_t 
         HIP_TRY(launch_plan_stream(d.net[BIG], parents, n, off, dl, f ? d.p_nbg.p : nullptr, f ? d.nbg.p : nullptr,
                                    d.p_obg.p, d.obg.p, ctx->swizzle & 1, d.chain_k > 1 ? d.nslot.p : nullptr,
                                    d.chain_k, ctx->king_cache ? 1 : 0, d.eoff.p, d.ent.p, d.tiles.p, d.btiles.p,
-                                   d.pool.p, d.perr.p, rows_out, b0, b1, order, sc));
+                                   d.pool.p, d.perr.p, rows_out, b0, b1, order, mid, sc));
         if (C > 1) { // this range's finalize (after the join when not pipelined)
           int rc = finalize_range(ctx, d, parents, children, mode, parent_out, child_out, pa, pb, d.cbound[c],
                                   d.cbound[c + 1], sc);
@@ -731,10 +748,13 @@ static int expand_evaluate(gn_ctx *ctx, Dev &d, const gn_board *parents, size_t 
         }
         return GN_OK;
       };
+      mid = ev ? ev[4] : nullptr;
       if (C == 1 && !d.defer_write) {
         int rc = run(0, s);
         if (rc) return rc;
       } else {
+        if (mid) HIP_TRY(hipEventRecord(mid, s));
+        mid = nullptr;
         HIP_TRY(hipEventRecord(d.go, s));
         for (int i = 0; i < 2; ++i) HIP_TRY(hipStreamWaitEvent(d.aux[i], d.go, 0));
         for (size_t c = 0; c < C; ++c) {
@@ -1559,6 +1579,85 @@ int gn_expand_device(gn_ctx *ctx, int device_slot, const gn_board *d_parents, si
   return check_plan(*d, s);
 }
 
+// Depth 2: the children of gn_expand_device's children.  Level 2 is
+// the same machinery with the children as parents: they arrive in sibling order, so a
+// block of consecutive siblings refreshes each from its predecessor's king-cache row
+// (plan_kernel: cache row + the placement difference, a few rows instead of ~30) and
+// every grandchild is incremental from its parent's accumulator.  The children are
+// evaluated again at level 2 (as parents); those results must equal level 1's and are
+// compared on the device (GN_E_HIP if not: an internal consistency check).
+int gn_expand2_device(gn_ctx *ctx, int device_slot, const gn_board *d_parents, size_t n, int mode,
+                      gn_eval *d_parent_out, uint32_t *d_offsets, gn_board *d_children, uint16_t *d_moves,
+                      gn_eval *d_child_out, size_t cap, uint32_t *d_goffsets, uint16_t *d_gmoves,
+                      gn_eval *d_grand_out, size_t gcap, size_t *total, size_t *gtotal, void *stream) {
+  Dev *d = slot(ctx, device_slot);
+  if (!d || !total || !gtotal) return fail(GN_E_INVALID, "bad argument");
+  if (n && (!d_parents || !d_offsets)) return fail(GN_E_INVALID, "NULL buffer");
+  std::lock_guard<std::mutex> lk(d->mu);
+  HIP_TRY(hipSetDevice(d->id));
+  hipStream_t s = stream ? (hipStream_t)stream : d->stream;
+  SeqGuard sg(*d, s);
+  HIP_TRY(sg.e);
+  *total = *gtotal = 0;
+  if (!n) return GN_OK;
+  // a size query (NULL child buffers or too small): the counts, GN_E_CAPACITY
+  size_t t = 0;
+  if (!d_children || !d_moves || !d_child_out || !cap) {
+    HIP_TRY(count_children(*d, d_parents, n, s, &t));
+    *total = t;
+    return t ? fail(GN_E_CAPACITY, "%zu children exceed capacity %zu", t, cap) : GN_OK;
+  }
+  // level 1
+  int rc = generate_children(*d, d_parents, n, d_children, cap, d_moves, ctx->incremental, &t, s, nullptr, nullptr,
+                             chain_len(ctx, *d, n), plan_path(ctx, *d), mode == GN_MODE_BIG);
+  *total = t;
+  if (t > 0xFFFFFFFFull) return fail(GN_E_CAPACITY, "%zu children exceed 32-bit offsets", t);
+  HIP_TRY(launch_offsets_u32(d->offsets.p, n + 1, d_offsets, s));
+  if (rc) {
+    HIP_TRY(hipStreamSynchronize(s));
+    return rc;
+  }
+  rc = expand_evaluate(ctx, *d, d_parents, n, d_children, t, mode, d_parent_out, d_child_out, s, nullptr);
+  if (rc) return rc;
+  HIP_TRY(hipStreamSynchronize(s));
+  if ((rc = check_plan(*d, s)) != GN_OK) return rc;
+  if (!t) {
+    HIP_TRY(hipMemsetAsync(d_goffsets, 0, sizeof(uint32_t), s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return GN_OK;
+  }
+  // level 2: the children as parents (their grandchildren boards stay library-internal)
+  size_t g = 0;
+  if (!d_goffsets || !d_gmoves || !d_grand_out || !gcap) {
+    HIP_TRY(count_children(*d, d_children, t, s, &g));
+    *gtotal = g;
+    return g ? fail(GN_E_CAPACITY, "%zu grandchildren exceed capacity %zu", g, gcap) : GN_OK;
+  }
+  rc = generate_children(*d, d_children, t, nullptr, gcap, d_gmoves, ctx->incremental, &g, s, nullptr, nullptr,
+                         chain_len(ctx, *d, t), plan_path(ctx, *d), mode == GN_MODE_BIG);
+  *gtotal = g;
+  if (g > 0xFFFFFFFFull) return fail(GN_E_CAPACITY, "%zu grandchildren exceed 32-bit offsets", g);
+  HIP_TRY(launch_offsets_u32(d->offsets.p, t + 1, d_goffsets, s));
+  if (rc) {
+    HIP_TRY(hipStreamSynchronize(s));
+    return rc;
+  }
+  HIP_TRY(d->io_out.ensure(t));
+  rc = expand_evaluate(ctx, *d, d_children, t, d->frontier[1].p, g, mode, d->io_out.p, d_grand_out, s, nullptr);
+  if (rc) return rc;
+  // the children evaluated twice (level 1 as children, level 2 as parents) must agree
+  HIP_TRY(d->sum.ensure(2));
+  HIP_TRY(hipMemsetAsync(d->sum.p, 0, 2 * sizeof(unsigned long long), s));
+  HIP_TRY(launch_checksum(d_child_out, t * sizeof(gn_eval), d->sum.p, s));
+  HIP_TRY(launch_checksum(d->io_out.p, t * sizeof(gn_eval), d->sum.p + 1, s));
+  unsigned long long cs[2] = {0, 0};
+  HIP_TRY(hipMemcpyAsync(cs, d->sum.p, sizeof(cs), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  if ((rc = check_plan(*d, s)) != GN_OK) return rc;
+  if (cs[0] != cs[1]) return fail(GN_E_HIP, "depth 2: the children's level-1 and level-2 evaluations differ");
+  return GN_OK;
+}
+
 int gn_time_expand_device(gn_ctx *ctx, int device_slot, const gn_board *d_parents, size_t n, int mode, int iters,
                           float *ms_total, size_t *total, float *stage_ms, uint64_t *ft_rows, gn_eval *d_parent_out,
                           uint32_t *d_offsets, uint16_t *d_moves, gn_eval *d_child_out, size_t cap) {
@@ -1569,7 +1668,9 @@ int gn_time_expand_device(gn_ctx *ctx, int device_slot, const gn_board *d_parent
   hipStream_t s = d->stream;
   SeqGuard sg(*d, s);
   HIP_TRY(sg.e);
-  const int NE = 8; // start, [count+scan], [total read], [write], [classify], [small], [big], [finalize]
+  // start, [count+scan], [total read], [write], [classify], [small], [big], [finalize], and
+  // the planned big net's plan -> stream boundary
+  const int NE = 9;
   std::vector<hipEvent_t> ev((size_t)iters * NE + 2, nullptr);
   auto cleanup = [&] {
     for (auto &e : ev)
@@ -1618,6 +1719,17 @@ int gn_time_expand_device(gn_ctx *ctx, int device_slot, const gn_board *d_parent
         acc[k] += ms;
       }
     for (int k = 0; k < 7; ++k) stage_ms[k] = acc[k] / (float)iters;
+  }
+  if (rc == GN_OK && he == hipSuccess && d->planned) { // the big net's two kernels apart
+    float pl = 0, st = 0;
+    for (int it = 0; it < iters && he == hipSuccess; ++it) {
+      float a = 0, b = 0;
+      const size_t o = 2 + (size_t)NE * it;
+      he = hipEventElapsedTime(&a, ev[o + 5], ev[o + 8]);
+      if (he == hipSuccess) he = hipEventElapsedTime(&b, ev[o + 8], ev[o + 6]);
+      pl += a, st += b;
+    }
+    d->plan_ms = pl / (float)iters, d->stream_ms = st / (float)iters;
   }
   cleanup();
   *total = t;
@@ -1705,6 +1817,13 @@ int gn_get_option(const gn_ctx *ctx, int option, int64_t *value) {
   case GN_OPT_CHAIN:
     *value = ctx->chain;
     return GN_OK;
+  case GN_STAT_PLAN_NS:
+  case GN_STAT_STREAM_NS: { // read-only: the last gn_time_expand_device's planned kernels (max over devices)
+    float m = 0;
+    for (auto &dp : ctx->devs) m = std::max(m, option == GN_STAT_PLAN_NS ? dp->plan_ms : dp->stream_ms);
+    *value = (int64_t)((double)m * 1e6);
+    return GN_OK;
+  }
   case GN_STAT_CHAIN_FALLBACKS: { // read-only: blocks of the last chained expansion per device, summed
     int64_t sum = 0;
     for (auto &dp : ctx->devs) {

@@ -1523,12 +1523,13 @@ __global__ void count_children_kernel(const gn_board *__restrict__ boards, size_
   }
   counts[i] = c;
   if (ebound) { // planned-expansion entries of this parent (stream.hip), bounded: its refresh
-    // (bias + P rows per list) or its carry entries after <= 4 no-ops per list; per child
+    // (bias + P rows + the cache store per list, or the cache row + <= P differences + the
+    // store) or its carry entries, after <= 4 no-ops per list; per child
     // <= 4 delta entries per list, or for a king move a refresh (bias + <= P rows + the
     // cache store, after <= 4 no-ops) + the other perspective's <= 4; per-tile padding
     // (<= 3 per list per tile the parent touches)
     const uint64_t P = popcnt(B.byType[0]);
-    ebound[i] = c || P ? 2 * (P + 1) + 8 + 8 * (c - kmoves) + (P + 10) * kmoves + 6 * ((c + 1) / 16 + 2) : 0;
+    ebound[i] = c || P ? 2 * (P + 2) + 8 + 8 * (c - kmoves) + (P + 10) * kmoves + 6 * ((c + 1) / 16 + 2) : 0;
   }
 }
 

@@ -174,6 +174,39 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
       carried = nxq > 0;
     }
     int ckey0 = -1, ckey1 = -1; // sibling keys carried across this parent's segments
+    // ---- a refreshed parent starts from the king cache when the block last computed an
+    // accumulator for this perspective and king square (Stockfish's AccumulatorCaches for
+    // a refresh): cache row + the placement differences; either way the parent's
+    // accumulator is stored back to that row (a sibling batch, as in a depth-2 expansion,
+    // then refreshes every parent from its predecessor's row).  Per perspective hh, in
+    // list hh (its entries end with PAR_E: list hh's parent register).
+    int pnd[2] = {-1, -1};        // entries between the cache row and the store (< 0: full refresh)
+    bool pst[2] = {false, false}; // the refresh is stored to the cache row
+    int pkq[2] = {0, 0};          // the perspective's king square
+    // the cached placement's piece on this lane's square and the differences to ppc
+    auto cache_diff = [&](int kci, int pc, int &spc, uint64_t &bs, uint64_t &ba) {
+      const uint32_t wv = lane < 8 ? ksnap[w][kci][lane] : 0u;
+      spc = (int)((__shfl(wv, lane >> 3) >> (4 * (lane & 7))) & 15);
+      bs = __ballot(spc != pc && spc != 0), ba = __ballot(spc != pc && pc != 0);
+    };
+    if (live && !have && kc) {
+      const int ppc = lane_piece(pb, lane);
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        const uint64_t kb = __ballot(ppc == make_piece(hh, KING));
+        const int ksq = kb ? __builtin_ctzll(kb) : 0, kci = 64 * hh + ksq;
+        pkq[hh] = ksq;
+        const int kst = kstate[w][kci];
+        pst[hh] = kb != 0 && (kst == 0 || ((kst >> 1) & 1) == hh); // the row is unused or list hh's
+        if (pst[hh] && (kst & 1)) {
+          int spc;
+          uint64_t bs, ba;
+          cache_diff(kci, ppc, spc, bs, ba);
+          const int nd = popcnt(bs) + popcnt(ba);
+          if (nd < P) pnd[hh] = nd;
+        }
+      }
+    }
 
     for (int q0 = 0; q0 < total;) {
       if (t_fill == 0) p_first = p, t_first = u_fill;
@@ -232,13 +265,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
       if (km0) ckey0 = __builtin_amdgcn_readlane(key0, 63 - __builtin_clzll(km0));
       if (km1) ckey1 = __builtin_amdgcn_readlane(key1, 63 - __builtin_clzll(km1));
       // ---- entries of the parent and of delta perspectives (prefix sums over the lanes)
-      if (live && q0 == 0 && have) { // the parent loads the carry rows: after their stores
-        pad_to(0, safe0);
-        pad_to(1, safe1);
+      if (live && q0 == 0) { // the parent loads the carry / cache rows: after their stores
+        if (have || pnd[0] >= 0) pad_to(0, safe0);
+        if (have || pnd[1] >= 0) pad_to(1, safe1);
       }
       const bool ref0 = (kinds & 3) == 2, ref1 = (kinds >> 2) == 2;
       int d0 = 0, d1 = 0;
-      if (kinds == 15) d0 = d1 = have ? 1 : P + 1;
+      if (kinds == 15) {
+        d0 = have ? 1 : pnd[0] >= 0 ? pnd[0] + 2 : P + 1 + (pst[0] ? 1 : 0);
+        d1 = have ? 1 : pnd[1] >= 0 ? pnd[1] + 2 : P + 1 + (pst[1] ? 1 : 0);
+      }
       else {
         if ((kinds & 3) == 1) d0 = n0 - (hit0 ? 1 : 0);
         if ((kinds >> 2) == 1) d1 = n1 - (hit1 ? 1 : 0);
@@ -277,9 +313,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
           if (have) { // the parent from the carry rows: one entry per list
             put(0, len0 + (exc & 0xFFFF), SCR | 0u | t0w | I_ZERO | PAR_E | LAST);
             put(1, len1 + (exc >> 16), SCR | 1u | t1w | I_ZERO | PAR_E | LAST);
-          } else { // bias entry; the parent's rows follow (below, lane = row)
-            put(0, len0 + (exc & 0xFFFF), (uint32_t)FT_BIAS_ROW | t0w | I_ZERO | PAR_E);
-            put(1, len1 + (exc >> 16), (uint32_t)FT_BIAS_ROW | t1w | I_ZERO | PAR_E);
+          } else { // bias entry or the cache row; the rest follows (below, lane = square / row)
+            put(0, len0 + (exc & 0xFFFF),
+                (pnd[0] >= 0 ? SCR | (uint32_t)(2 + pkq[0]) : (uint32_t)FT_BIAS_ROW) | t0w | I_ZERO | PAR_E);
+            put(1, len1 + (exc >> 16),
+                (pnd[1] >= 0 ? SCR | (uint32_t)(2 + 64 + pkq[1]) : (uint32_t)FT_BIAS_ROW) | t1w | I_ZERO | PAR_E);
           }
         }
         // PSQT of the slot by side (a king-move perspective is written by its job below)
@@ -303,11 +341,39 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
       if (in) T[tile_k].meta[t] = (uint8_t)((live && vld ? 1 : 0) | bk << 1 | (q == 0 ? 16 : 0) | cst << 5);
       // the parent's rows (lane = row) after its bias entry (the parent is lane 0 of its segment)
       if (live && q0 == 0 && !have) {
-        const uint32_t tp0 = tmpl(t_fill, stm != 0), tp1 = tmpl(t_fill, stm != 1);
-        if (lane < P) {
-          put(0, len0 + 1 + lane, ft_row(prow[0][lane]) | tp0 | PAR_E | (lane == P - 1 ? LAST : 0u));
-          put(1, len1 + 1 + lane, ft_row(prow[1][lane]) | tp1 | PAR_E | (lane == P - 1 ? LAST : 0u));
+        const uint64_t lt2 = (1ull << lane) - 1;
+        const int ppc = kc ? lane_piece(pb, lane) : 0;
+#pragma unroll 1
+        for (int hh = 0; hh < 2; ++hh) {
+          const uint32_t tp = tmpl(t_fill, stm != hh), b0 = (hh ? len1 : len0) + 1;
+          const uint32_t krow = SCR | (uint32_t)(2 + 64 * hh + pkq[hh]);
+          if (pnd[hh] >= 0) { // the cache row's differences: removed pieces, then added ones
+            int spc;
+            uint64_t bs, ba;
+            cache_diff(64 * hh + pkq[hh], ppc, spc, bs, ba);
+            if ((bs >> lane) & 1)
+              put(hh, b0 + popcnt(bs & lt2), (uint32_t)feature_index(hh, lane, spc, pkq[hh]) | tp | SUB | PAR_E);
+            if ((ba >> lane) & 1)
+              put(hh, b0 + popcnt(bs) + popcnt(ba & lt2), (uint32_t)feature_index(hh, lane, ppc, pkq[hh]) | tp | PAR_E);
+            if (lane == 0) put(hh, b0 + pnd[hh], krow | tp | I_ZERO | SUB | KST | LAST | PAR_E);
+          } else {
+            if (lane < P)
+              put(hh, b0 + lane, ft_row(prow[hh][lane]) | tp | PAR_E | (lane == P - 1 && !pst[hh] ? LAST : 0u));
+            if (pst[hh] && lane == 0) put(hh, b0 + P, krow | tp | I_ZERO | SUB | KST | LAST | PAR_E);
+          }
+          if (pnd[hh] >= 0 || pst[hh]) { // list hh stored the row: its snapshot and state
+            uint32_t x = (uint32_t)ppc << (4 * (lane & 7));
+            x |= __shfl_xor(x, 1);
+            x |= __shfl_xor(x, 2);
+            x |= __shfl_xor(x, 4);
+            const int kci = 64 * hh + pkq[hh];
+            if ((lane & 7) == 0) ksnap[w][kci][lane >> 3] = x;
+            if (lane == 0) kstate[w][kci] = (uint8_t)(1 | hh << 1);
+            uint32_t &sf = hh ? safe1 : safe0;
+            sf = b0 + (uint32_t)(pnd[hh] >= 0 ? pnd[hh] : P) + 4; // the store's index + 4
+          }
         }
+        ps::wave_sync();
       }
       { // a delta child that is the next parent stores its carry rows at its last entry
         const uint64_t nxm = __ballot(in && live && nx);
@@ -786,7 +852,7 @@ hipError_t launch_plan_stream(const NetDevice &net, const gn_board *parents, siz
                               int2 *out_parent, int2 *out_child, int swz, const uint8_t *next_slot, int chain_k,
                               int kc, const uint64_t *eoff, uint32_t *ent, TileDesc *tiles, uint32_t *btiles,
                               uint32_t *pool, uint32_t *err, unsigned long long *rows_out, size_t b0, size_t b1,
-                              const uint32_t *order, hipStream_t s) {
+                              const uint32_t *order, hipEvent_t mid, hipStream_t s) {
   if (!n || b1 <= b0) return hipSuccess;
   if (n >= 0x80000000ull) return hipErrorInvalidValue; // 32-bit parent indices in the kernels
   const uint32_t K = chain_k > 1 && next_slot ? (uint32_t)chain_k : 1u;
@@ -799,12 +865,14 @@ hipError_t launch_plan_stream(const NetDevice &net, const gn_board *parents, siz
     hipLaunchKernelGGL((plan_kernel<3072>), dim3(pg), dim3(256), 0, s, net, parents, offsets, deltas, need_parent,
                        need_child, K > 1 ? next_slot : nullptr, (uint32_t)n, K, B0, B1, K > 1 ? kc : 0, eoff, ent,
                        tiles, btiles, rows_out, err);
+    if (mid) (void)hipEventRecord(mid, s);
     hipLaunchKernelGGL((stream_eval_kernel<3072>), dim3(g), dim3(384), 0, s, net, offsets, (uint32_t)n, K, B0, B1,
                        swz, eoff, ent, tiles, btiles, order, out_parent, out_child, pool, scr, err, ablate);
   } else if (net.L1 == 1024) {
     hipLaunchKernelGGL((plan_kernel<1024>), dim3(pg), dim3(256), 0, s, net, parents, offsets, deltas, need_parent,
                        need_child, K > 1 ? next_slot : nullptr, (uint32_t)n, K, B0, B1, K > 1 ? kc : 0, eoff, ent,
                        tiles, btiles, rows_out, err);
+    if (mid) (void)hipEventRecord(mid, s);
     hipLaunchKernelGGL((stream_eval_kernel<1024>), dim3(g), dim3(128), 0, s, net, offsets, (uint32_t)n, K, B0, B1,
                        swz, eoff, ent, tiles, btiles, order, out_parent, out_child, pool, scr, err, ablate);
   } else {

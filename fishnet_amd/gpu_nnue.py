@@ -38,9 +38,9 @@ EXPORTS = ["gn_load_net", "gn_load_net_memory", "gn_free", "gn_last_error", "gn_
            "gn_time_evaluate_device", "gn_random_positions_device", "gn_set_option", "gn_get_option",
            "gn_time_expand_device", "gn_random_games_device", "gn_replay_game", "gn_evaluate_games",
            "gn_net_sha256", "gn_partition", "gn_checksum_device",
-           "gn_boards_to_fens", "gn_load_net_archive", "gn_archive_read"]
+           "gn_boards_to_fens", "gn_load_net_archive", "gn_archive_read", "gn_expand2_device"]
 OPT_INCREMENTAL_CHILDREN, OPT_XCD_SWIZZLE, OPT_KING_SORT, OPT_CHAIN, OPT_KING_CACHE = 1, 2, 3, 4, 5
-STAT_CHAIN_FALLBACKS = 100
+STAT_CHAIN_FALLBACKS, STAT_PLAN_NS, STAT_STREAM_NS = 100, 101, 102
 EXPAND_STAGES = ["count_scan", "total_readback", "write_children", "classify", "small_net", "big_net", "finalize"]
 
 
@@ -129,6 +129,8 @@ def lib():
         "gn_evaluate_games": [vp, vp, sz, i32, i32, vp, vp, vp, sz, vp, vp, vp, sz],
         "gn_load_net_archive": [C.c_char_p, C.c_char_p, C.c_char_p, vp, i32, C.POINTER(vp)],
         "gn_archive_read": [C.c_char_p, C.c_char_p, vp, sz, C.POINTER(sz)],
+        "gn_expand2_device": [vp, i32, vp, sz, i32, vp, vp, vp, vp, vp, sz, vp, vp, vp, sz, C.POINTER(sz),
+                              C.POINTER(sz), vp],
     }
     for name, args in sig.items():
         f = getattr(L, name)
@@ -436,6 +438,22 @@ class GpuNnue:
                                       d_children.ptr, d_moves.ptr, d_child_out.ptr, cap, C.byref(total),
                                       stream))
         return total.value
+
+    def expand2_device(self, d_parents, n, mode, out, stream=None, slot=0):
+        """Depth 2 (gn_expand2_device).  out: DeviceBuffers po, off, ch (child boards), mv, co,
+        goff, gmv, gco, plus caps cap / gcap.  Returns (children, grandchildren); with
+        E_CAPACITY the counts needed are in the exception's .need."""
+        t, g = C.c_size_t(), C.c_size_t()
+        p = lambda k: out[k].ptr if out.get(k) is not None else None
+        rc = lib().gn_expand2_device(self.h, slot, d_parents.ptr, n, mode, p("po"), p("off"), p("ch"), p("mv"),
+                                     p("co"), out.get("cap", 0), p("goff"), p("gmv"), p("gco"), out.get("gcap", 0),
+                                     C.byref(t), C.byref(g), stream)
+        if rc == E_CAPACITY:
+            e = GnError(rc, (lib().gn_last_error() or b"").decode(errors="replace"))
+            e.need = (t.value, g.value)
+            raise e
+        _check(rc)
+        return t.value, g.value
 
 
 def move_to_uci(m: int) -> str:

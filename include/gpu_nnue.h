@@ -87,6 +87,11 @@ extern "C" {
                                          refreshes.  Results are identical either way.    */
 
 /* read-only statistics (gn_get_option) */
+#define GN_STAT_PLAN_NS 101           /* the last gn_time_expand_device's planned big net
+                                         (max over devices, per iteration, nanoseconds):
+                                         plan_kernel (lists, tiles, PSQT) ...            */
+#define GN_STAT_STREAM_NS 102         /* ... and stream_eval_kernel (row stream + layer
+                                         stack), the expansion's dominant kernel         */
 #define GN_STAT_CHAIN_FALLBACKS 100   /* blocks of the last chained expansion (per device,
                                          summed) that found their carry / king-cache slot
                                          still in use after a bounded wait and ran
@@ -316,6 +321,15 @@ GN_API int gn_expand_device(gn_ctx *ctx, int device_slot, const gn_board *d_pare
  * nets the row stream's own count (bias, carry and king-cache rows included:
  * GN_OPT_CHAIN, GN_OPT_KING_CACHE), else parent refreshes + child deltas /
  * king-move refreshes; 0 when not incremental. */
+/* Depth 2 (grandchildren): gn_expand_device, then every child's legal children
+ * evaluated incrementally from the child's accumulator (a sibling block refreshes each
+ * child from its predecessor through the king cache).  d_goffsets: total + 1 offsets of
+ * each child's grandchildren in d_gmoves / d_grand_out (gcap entries); grandchild boards
+ * are not returned.  GN_E_CAPACITY: *total / *gtotal hold the counts needed. */
+GN_API int gn_expand2_device(gn_ctx *ctx, int device_slot, const gn_board *d_parents, size_t n, int mode,
+                             gn_eval *d_parent_out, uint32_t *d_offsets, gn_board *d_children, uint16_t *d_moves,
+                             gn_eval *d_child_out, size_t cap, uint32_t *d_goffsets, uint16_t *d_gmoves,
+                             gn_eval *d_grand_out, size_t gcap, size_t *total, size_t *gtotal, void *stream);
 GN_API int gn_time_expand_device(gn_ctx *ctx, int device_slot, const gn_board *d_parents, size_t n, int mode,
                                  int iters, float *ms_total, size_t *total, float *stage_ms, uint64_t *ft_rows,
                                  gn_eval *d_parent_out, uint32_t *d_offsets, uint16_t *d_moves,

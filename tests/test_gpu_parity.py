@@ -552,3 +552,79 @@ def test_nets_from_asset_archive(gpu_ctx, synth_big_path, synth_small_path, tmp_
     with pytest.raises(G.GnError) as e:
         G.GpuNnue(archive=str(q), big_member="nn-000000000000.nnue")
     assert e.value.code == G.E_FORMAT
+
+
+def _expand2(ctx, d_b, n, mode):
+    """gn_expand2_device with buffers sized by its own E_CAPACITY replies."""
+    from fishnet_amd import gpu_nnue as G
+    out = {"po": ctx.alloc(n * 16), "off": ctx.alloc((n + 1) * 4), "cap": 0, "gcap": 0}
+    for _ in range(3):
+        try:
+            t, g = ctx.expand2_device(d_b, n, mode, out)
+            return t, g, out
+        except G.GnError as e:
+            if e.code != G.E_CAPACITY:
+                raise
+            t, g = e.need
+            if t > out["cap"]:
+                out.update(cap=t, ch=ctx.alloc(max(t, 1) * 32), mv=ctx.alloc(max(t, 1) * 2),
+                           co=ctx.alloc(max(t, 1) * 16), goff=ctx.alloc((t + 1) * 4))
+            if g > out["gcap"]:
+                out.update(gcap=g, gmv=ctx.alloc(max(g, 1) * 2), gco=ctx.alloc(max(g, 1) * 16))
+    raise AssertionError("sizing did not converge")
+
+
+@pytest.mark.parametrize("mode", [1, 0])
+def test_grandchildren_vs_depth1_and_oracle(gpu_ctx, oracle_nets, oracle_lib, mode):
+    """Depth 2 (gn_expand2_device): level 1 equals gn_expand_device; every grandchild
+    equals a depth-1 expansion of its parent (the children as a parent batch, king cache
+    off: refresh-started parents); sampled children's grandchildren equal the oracle's."""
+    from fishnet_amd import gpu_nnue as G
+    games, plies = 3, 80
+    n0 = games * (plies + 1)
+    fens = special_fens()
+    d_g = gpu_ctx.alloc(n0 * 32)
+    gpu_ctx.random_games_device(0x5EED0077, 0, games, plies, d_g)
+    gpu_ctx.synchronize()
+    boards = np.concatenate([d_g.download(G.BOARD_DTYPE, n0), G.pack_fens(fens)[0]])
+    n = len(boards)
+    d_b = gpu_ctx.alloc(n * 32)
+    d_b.upload(boards)
+    t, g, out = _expand2(gpu_ctx, d_b, n, mode)
+    assert t > 0 and g > 20 * t
+    po, off = out["po"].download(G.EVAL_DTYPE, n), out["off"].download(np.uint32, n + 1)
+    mv, co = out["mv"].download(np.uint16, t), out["co"].download(G.EVAL_DTYPE, t)
+    goff = out["goff"].download(np.uint32, t + 1)
+    gmv, gco = out["gmv"].download(np.uint16, g), out["gco"].download(G.EVAL_DTYPE, g)
+    # level 1 == gn_expand_device
+    b1 = {k: gpu_ctx.alloc(sz) for k, sz in (("po", n * 16), ("off", (n + 1) * 4), ("ch", t * 32), ("mv", t * 2),
+                                              ("co", t * 16))}
+    assert gpu_ctx.expand_device(d_b, n, mode, b1["po"], b1["off"], b1["ch"], b1["mv"], b1["co"], t) == t
+    assert np.array_equal(b1["po"].download(G.EVAL_DTYPE, n), po)
+    assert np.array_equal(b1["co"].download(G.EVAL_DTYPE, t), co)
+    # level 2 == depth 1 of the children with refresh-started parents (no chain, no cache)
+    b2 = {k: gpu_ctx.alloc(sz) for k, sz in (("po", t * 16), ("off", (t + 1) * 4), ("ch", g * 32), ("mv", g * 2),
+                                              ("co", g * 16))}
+    try:
+        gpu_ctx.set_option(G.OPT_CHAIN, 1)
+        gpu_ctx.set_option(G.OPT_KING_CACHE, 0)
+        assert gpu_ctx.expand_device(out["ch"], t, mode, b2["po"], b2["off"], b2["ch"], b2["mv"], b2["co"], g) == g
+    finally:
+        gpu_ctx.set_option(G.OPT_CHAIN, 81)
+        gpu_ctx.set_option(G.OPT_KING_CACHE, 1)
+    assert np.array_equal(b2["po"].download(G.EVAL_DTYPE, t), co)
+    assert np.array_equal(b2["off"].download(np.uint32, t + 1), goff)
+    assert np.array_equal(b2["mv"].download(np.uint16, g), gmv)
+    assert np.array_equal(b2["co"].download(G.EVAL_DTYPE, g), gco)
+    # sampled children against the oracle
+    big, small = oracle_nets
+    children = out["ch"].download(G.BOARD_DTYPE, t)
+    rng = np.random.default_rng(7)
+    for j in np.unique(np.concatenate([rng.choice(t, size=min(200, t), replace=False), np.arange(40)])):
+        fen = G.board_to_fen(children[j])
+        p_exp, m_exp, k_exp = oracle_lib.expand_eval(big, small, fen, mode)
+        assert tuple(co[j]) == p_exp, fen
+        lo, hi = int(goff[j]), int(goff[j + 1])
+        assert {int(m): tuple(x) for m, x in zip(gmv[lo:hi], gco[lo:hi])} == \
+               {int(m): tuple(x) for m, x in zip(m_exp, k_exp)}, fen
+

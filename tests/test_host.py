@@ -171,3 +171,34 @@ def test_archive_read_zstd_and_ar_variants(tmp_path):
     trunc.write_bytes(A.zstd(A.ar_bytes(members))[:-7])
     with pytest.raises(G.GnError):
         G.archive_read(str(trunc), "odd")
+
+
+def test_rust_sys_crate_matches_header():
+    """rust/gpu-nnue-sys/src/lib.rs mirrors include/gpu_nnue.h: every GN_API function with
+    the same argument count, every GN_ constant with the same value, every struct with the
+    same fields in order (cargo is not in the image; this keeps the binding honest)."""
+    import re
+    hdr = open(os.path.join(ROOT, "include", "gpu_nnue.h")).read()
+    rs = open(os.path.join(ROOT, "rust", "gpu-nnue-sys", "src", "lib.rs")).read()
+    nocomment = re.sub(r"/\*.*?\*/", "", hdr, flags=re.S)
+    nocomment = re.sub(r"//[^\n]*", "", nocomment)
+
+    def nargs(params):
+        params = params.strip()
+        return 0 if params in ("", "void") else params.count(",") + 1
+
+    c_funcs = {m.group(1): nargs(m.group(2))
+               for m in re.finditer(r"GN_API\s+[\w\s\*]+?\b(gn_\w+)\s*\(([^)]*)\)", nocomment)}
+    r_funcs = {m.group(1): nargs(m.group(2)) for m in re.finditer(r"pub fn (gn_\w+)\s*\(([^)]*)\)", rs)}
+    assert c_funcs and c_funcs == r_funcs
+    c_consts = {m.group(1): int(m.group(2).rstrip("u").strip("()"))
+                for m in re.finditer(r"#define (GN_(?:OK|E_\w+|MODE_\w+|OPT_\w+|STAT_\w+|FLAG_\w+|ABI_VERSION))\s+"
+                                     r"(\(?-?\d+\)?u?)", hdr)}
+    r_consts = {m.group(1): int(m.group(2)) for m in re.finditer(r"pub const (GN_\w+): \w+ = (-?\d+);", rs)}
+    assert c_consts == r_consts
+    for st in ("gn_eval", "gn_board", "gn_eval_params", "gn_game"):
+        cb = re.search(r"typedef struct %s \{(.*?)\} %s;" % (st, st), nocomment, re.S).group(1)
+        cf = [re.sub(r"\[.*", "", d.split()[-1]).lstrip("*") for d in cb.split(";") if d.strip()]
+        rb = re.search(r"pub struct %s \{(.*?)\n\}" % st, rs, re.S).group(1)
+        rf = re.findall(r"pub (\w+):", rb)
+        assert cf == rf, (st, cf, rf)
