@@ -211,7 +211,8 @@ struct Dev {
   // planned expansion (stream.hip): per-parent entry bounds and their scan, the entry
   // lists, tile descriptors, the scratch-slot pool and the error word
   DevBuf<uint64_t> ebound, eoff;
-  DevBuf<uint32_t> ent, pool, perr;
+  DevBuf<uint64_t> ent;           // the planned expansion's row entries (stream.hip)
+  DevBuf<uint32_t> pool, perr;
   DevBuf<TileDesc> tiles;
   DevBuf<uint32_t> btiles; // tiles per block of the planned expansion
   DevBuf<uint16_t> bkeys, bkeys2; // block_order scratch
@@ -321,7 +322,7 @@ static int upload_net(Dev &d, int which, const HostNet &h) {
   for (size_t r = 0; r < (size_t)FT_ROWS; ++r)
     for (int b = 0; b < PSQT_BUCKETS; ++b)
       memcpy(&psqt[(size_t)b * FT_ROWS + r], h.ft.data() + r * RS + 2 * (size_t)h.L1 + 4 * b, 4);
-  const size_t sz[9] = {((size_t)FT_ROWS + 4 * (size_t)carry + 128 * (size_t)carry) * RS, h.bias.size() * 2, h.w0.size(), h.b0.size() * 4,
+  const size_t sz[9] = {((size_t)FT_ROWS + 4 * (size_t)carry + 128 * (size_t)carry + (carry ? 1 : 0)) * RS, h.bias.size() * 2, h.w0.size(), h.b0.size() * 4,
                         h.w1.size(), h.b1.size() * 4, h.w2.size(), h.b2.size() * 4, psqt.size() * 4};
   const void *src[9] = {h.ft.data(), h.bias.data(), h.w0.data(), h.b0.data(),
                         h.w1.data(), h.b1.data(), h.w2.data(), h.b2.data(), psqt.data()};
@@ -332,6 +333,7 @@ static int upload_net(Dev &d, int which, const HostNet &h) {
   for (int i = 0; i < 9; ++i)
     HIP_TRY(hipMemcpy(m + off[i], src[i], i == 0 ? (size_t)FT_ROWS * RS : sz[i], hipMemcpyHostToDevice));
   if (carry) HIP_TRY(hipMemset(m + off[0] + (size_t)FT_ROWS * RS, 0, 4 * (size_t)carry * RS));
+  if (carry) HIP_TRY(hipMemset(m + off[0] + (size_t)ZERO_ROW * RS, 0, RS)); // the zero row
   NetDevice &n = d.net[which];
   n.L1 = h.L1;
   n.row_stride = (uint32_t)RS;

@@ -71,7 +71,7 @@ static_assert(sizeof(TileDesc) == 160, "TileDesc is 160 bytes");
 hipError_t launch_plan_stream(const NetDevice &net, const gn_board *parents, size_t n, const uint64_t *offsets,
                               const ChildDelta *deltas, const uint8_t *need_parent, const uint8_t *need_child,
                               int2 *out_parent, int2 *out_child, int swz, const uint8_t *next_slot, int chain_k,
-                              int kc, const uint64_t *eoff, uint32_t *ent, TileDesc *tiles, uint32_t *btiles,
+                              int kc, const uint64_t *eoff, uint64_t *ent, TileDesc *tiles, uint32_t *btiles,
                               uint32_t *pool, uint32_t *err, unsigned long long *rows_out, size_t b0, size_t b1,
                               const uint32_t *order, hipEvent_t mid, hipStream_t s);
 // GN_MODE_FULL preparation: need_small = valid && |simple_eval| > threshold,

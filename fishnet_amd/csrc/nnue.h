@@ -40,6 +40,10 @@ constexpr int SCR_ROWS = 130;
 constexpr int POOL_PER_XCD = 256;
 constexpr int SCR_SLOTS = 8 * POOL_PER_XCD;
 static_assert(SCR_ROWS * SCR_SLOTS <= 132 * CARRY_SLOTS, "scratch slots fit the rows behind the FT rows");
+// One row of zeros after all of those (never written): the row a store-only stream entry
+// loads, so that its multiplier may carry the store's target row (stream.hip).
+constexpr int ZERO_ROW = FT_ROWS + 132 * CARRY_SLOTS;
+static_assert(ZERO_ROW < (1 << 19), "the zero row fits the 19-bit row field");
 constexpr int PSQT_BUCKETS = 8;
 constexpr int LAYER_STACKS = 8;
 constexpr uint32_t NNUE_VERSION = 0x7AF32F20u;

@@ -30,6 +30,14 @@
 //   [27] side (0: the perspective to move)   [28] PAR_E (the parent slot: its accumulator
 //   becomes pacc)   [29] NXT (store the slot's accumulator to this list's carry row)
 //   [30] SCR   [31] KST (store the slot's accumulator to the row of this entry)
+// The plan kernel builds entries in that form and stores each as the stream kernel's
+// pre-decoded u64 (enc64): lo = the row's byte offset (scratch rows: from the first scratch
+// row, the workgroup adds its slot's offset), hi = [15:0] the 16-bit multiplier of the row
+// (1 add, 0xFFFF subtract, 0 no-op: ZERO | SUB entries; a store-only KST entry loads the
+// zero row and has its target scratch row here), [16] PRE (an init before the
+// entry), [18:17] the init kind, [19] LAST, [23:20] slot, [24] side, [25] PAR_E, [26] NXT,
+// [27] KST, [31] SCR; so the stream's common entry is a multiply-add with hi as its scalar
+// operand and two bit tests.
 // Lists are padded per tile to a multiple of 4 with no-op entries (ZERO | SUB) so every
 // ring step issues the same loads.  The ring issues a row load 4 entries before it
 // consumes it, so an entry that loads a scratch row sits at least 4 entries after the
@@ -39,15 +47,11 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <type_traits>
+
 #include "device_util.h"
 #include "kernels.h"
 
-#ifndef GN_CONSUME_MAD
-#define GN_CONSUME_MAD 1
-#endif
-#ifndef GN_ASM_RING
-#define GN_ASM_RING 1 // with GN_CONSUME_MAD: 257 ms vs 273 ms (compiler waits: a vmcnt(0) at the first entry of each revolution)
-#endif
 #ifndef GN_PLAN_WPE
 #define GN_PLAN_WPE 4 // 128 VGPRs, no spills: 4 latency-bound plan waves per SIMD instead of 3
 #endif
@@ -72,6 +76,28 @@ constexpr uint32_t ROW = (1u << 19) - 1, SUB = 1u << 19, I_ZERO = 1u << 20, I_PA
                    INIT = 3u << 20, LAST = 1u << 22, SLOT_SH = 23, SIDE_SH = 27, PAR_E = 1u << 28, NXT = 1u << 29,
                    SCR = 1u << 30, KST = 1u << 31;
 constexpr uint32_t PAD = (uint32_t)FT_BIAS_ROW | I_ZERO | SUB;
+// pre-decoded form (see the header)
+constexpr uint32_t H_PRE = 1u << 16, H_INIT_SH = 17, H_LAST = 1u << 19, H_SLOT_SH = 20, H_SIDE_SH = 24,
+                   H_PAR_E = 1u << 25, H_NXT = 1u << 26, H_KST = 1u << 27, H_SCR = 1u << 31;
+template <int L1>
+__device__ __forceinline__ uint64_t enc64(uint32_t e) {
+  constexpr uint32_t RS = 2 * L1 + 32;
+  const uint32_t row = e & ROW, init = (e >> 20) & 3, sub = e & SUB;
+  const bool keep = init == 1 && sub; // ZERO | SUB: no init, no row (padding, store-only entries)
+  // a store-only KST entry loads the zero row and carries its target (a scratch row) as its
+  // multiplier: the store's offset is then known without the entry's lo word
+  const bool kst = (e & KST) != 0;
+  const uint32_t lo = kst ? (uint32_t)ZERO_ROW * RS : ((e & SCR) ? (uint32_t)FT_ROWS + row : row) * RS;
+  uint32_t hi = kst ? row : keep ? 0u : sub ? 0xFFFFu : 1u;
+  if (!keep && init) hi |= H_PRE | init << H_INIT_SH;
+  hi |= (e & LAST) ? H_LAST : 0u;
+  hi |= ((e >> SLOT_SH) & 15) << H_SLOT_SH | ((e >> SIDE_SH) & 1) << H_SIDE_SH;
+  hi |= (e & PAR_E) ? H_PAR_E : 0u;
+  hi |= (e & NXT) ? H_NXT : 0u;
+  hi |= (e & KST) ? H_KST : 0u;
+  hi |= (e & SCR) && !kst ? H_SCR : 0u;
+  return (uint64_t)hi << 32 | lo;
+}
 __device__ __forceinline__ uint32_t tmpl(int slot, int side) {
   return (uint32_t)slot << SLOT_SH | (uint32_t)side << SIDE_SH;
 }
@@ -88,7 +114,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
     plan_kernel(NetDevice net, const gn_board *__restrict__ parents, const uint64_t *__restrict__ offsets,
                 const ChildDelta *__restrict__ deltas, const uint8_t *__restrict__ need_parent,
                 const uint8_t *__restrict__ need_child, const uint8_t *__restrict__ next_slot, uint32_t np, uint32_t K,
-                uint32_t b0, uint32_t b1, int kc, const uint64_t *__restrict__ eoff, uint32_t *__restrict__ ent, TileDesc *__restrict__ tiles,
+                uint32_t b0, uint32_t b1, int kc, const uint64_t *__restrict__ eoff, uint64_t *__restrict__ ent, TileDesc *__restrict__ tiles,
                 uint32_t *__restrict__ btiles, unsigned long long *__restrict__ rows_out, uint32_t *__restrict__ err) {
   using namespace ps;
   __shared__ uint32_t ksnap[4][128][8]; // per wave: placement (64 nibbles) of each king-cache row
@@ -105,13 +131,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
   const uint32_t pbeg = blk * K, pend = pbeg + K < np ? pbeg + K : np;
   const uint64_t us_b = pbeg + offsets[pbeg];
   const uint64_t rbeg = eoff[pbeg] + 16ull * blk, rend = eoff[pend] + 16ull * (blk + 1);
-  uint32_t *E0 = ent + rbeg, *E1 = ent + rend - 1;
+  uint64_t *E0 = ent + rbeg, *E1 = ent + rend - 1;
   // a block's tiles: <= ceil(slots / 16) + one bucket cut per parent (a parent's own slots hold
   // <= 2 buckets, so a tile is cut at most once per parent), hence this base
   TileDesc *T = tiles + us_b / 16 + (uint64_t)(K + 2) * blk;
   auto put = [&](int g, uint32_t i, uint32_t v) {
-    if (g) E1[-(int64_t)i] = v;
-    else E0[i] = v;
+    if (g) E1[-(int64_t)i] = enc64<L1>(v);
+    else E0[i] = enc64<L1>(v);
   };
   for (int i = lane; i < 128; i += 64) kstate[w][i] = 0;
   uint16_t(*prow)[32] = prow_s[w];
@@ -405,9 +431,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
         const int32_t ps_sum = wave_sum(row >= 0 ? psqt((uint32_t)row, cb) : 0);
         if (lane == 0) T[tile_k].psq[tl][hh != st] = ps_sum;
         const uint32_t tw = tmpl(tl, hh != st);
-        const bool kuse = kc && (sq23 & 0xFFFF) == 64; // not castling
+        bool kuse = kc && (sq23 & 0xFFFF) == 64; // not castling
         const int kci = 64 * hh + kt;
         const int kst = kuse ? kstate[w][kci] : 0;
+        // a cache row, once stored, stays with the list that stored it: the other list's
+        // waves are not ordered with that list's stores inside a tile, so a second list
+        // storing or loading the row could race with them
+        const int own = (kst & 1) ? (kst >> 1) & 1 : -1;
+        if (nxl && own >= 0 && own != hh) kuse = false; // the next parent's slot must be in list hh
         bool hit = false;
         uint64_t bs = 0, ba = 0;
         int spc = 0;
@@ -419,7 +450,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
           const int nd = popcnt(bs) + popcnt(ba);
           hit = nd < cn && (!nxl || ((kst >> 1) & 1) == hh);
         }
-        const int g = hit ? (kst >> 1) & 1 : nxl ? hh : (len0 <= len1 ? 0 : 1);
+        const int g = hit ? own : nxl ? hh : kuse && own >= 0 ? own : (len0 <= len1 ? 0 : 1);
         if (hit) pad_to(g, g ? safe1 : safe0); // the cache row load after the list's last scratch store
         const uint32_t base = g ? len1 : len0;
         const uint32_t L = LAST | (nxl ? NXT : 0u);
@@ -476,7 +507,7 @@ template <int L1>
 __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_EXPAND_WPE)))
     stream_eval_kernel(NetDevice net, const uint64_t *__restrict__ offsets, uint32_t np, uint32_t K, uint32_t b0,
                        uint32_t b1, int swz,
-                       const uint64_t *__restrict__ eoff, const uint32_t *__restrict__ ent,
+                       const uint64_t *__restrict__ eoff, const uint64_t *__restrict__ ent,
                        const TileDesc *__restrict__ tiles, const uint32_t *__restrict__ btiles,
                        const uint32_t *__restrict__ order, int2 *__restrict__ out_parent, int2 *__restrict__ out_child,
                        uint32_t *__restrict__ pool, int use_scr, uint32_t *__restrict__ err, int ablate) {
@@ -494,7 +525,7 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int hu = __builtin_amdgcn_readfirstlane((tid / G) & 1);
   const __amdgpu_buffer_rsrc_t ftr = __builtin_amdgcn_make_buffer_rsrc(
-      (void *)net.ft, 0, (int)(((size_t)FT_ROWS + (size_t)SCR_ROWS * SCR_SLOTS) * RS), 0x00020000);
+      (void *)net.ft, 0, (int)(((size_t)ZERO_ROW + 1) * RS), 0x00020000);
   for (int i = tid; i < 512; i += NT) (&acc0[0][0])[i] = 0;
   // this launch evaluates blocks [b0, b1); with swz, XCD x (= dispatch index mod 8) takes
   // the x-th contiguous eighth of them (a block's king-sorted neighbours share its L2)
@@ -546,6 +577,10 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
     scr = (uint32_t)FT_ROWS + (uint32_t)SCR_ROWS * my_slot;
   }
 
+  // the stream and the tile loop are compiled once per perspective group (HU = hu): the
+  // list's direction and the group's carry row are then constants of the code
+  auto run_group = [&](auto hu_c) {
+  constexpr int HU = decltype(hu_c)::value;
   // ---- per-thread stream state: ONE continuous pipeline per group over the block's list.
   // Entries arrive through scalar loads (their own counter, lgkmcnt), 4 at a time and two
   // groups of 4 ahead, so waiting for an entry never waits for the row loads in flight;
@@ -553,124 +588,86 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
   // (the next tile's first rows are in flight during this tile's layer stack).
   ushort8 pacc_lo = {}, pacc_hi = {}, base_lo = {}, base_hi = {};
   ushort8 rlo[4], rhi[4];
-  uint32_t er[4];
+  uint32_t eh[4]; // hi words of the entries in flight
   uint32_t bq = 0; // buckets done (acc0 / in1 / fwd buffer parity)
-  typedef uint32_t u4e __attribute__((ext_vector_type(4), aligned(4)));
-  typedef const __attribute__((address_space(4))) u4e cu4e;
-  typedef const __attribute__((address_space(4))) uint32_t cu32;
-  cu32 *EL = (cu32 *)(hu ? ent + rend : ent + rbeg);
-  // entries i .. i + 3 of this group's list by one s_load_dwordx4 (list 1 is stored
-  // downward: its 4 entries arrive reversed, see ent4)
-  auto group = [&](uint32_t i) -> u4e { return *(cu4e *)(hu ? EL - 4 - i : EL + i); };
-  auto ent4 = [&](const u4e v, int r) -> uint32_t { return hu ? v[3 - r] : v[r]; };
+  typedef uint32_t u8e __attribute__((ext_vector_type(8), aligned(8)));
+  typedef const __attribute__((address_space(4))) u8e cu8e;
+  typedef const __attribute__((address_space(4))) uint64_t cu64;
+  cu64 *EL = (cu64 *)(HU ? ent + rend : ent + rbeg);
+  // entries i .. i + 3 of this group's list by one s_load_dwordx8 (list 1 is stored
+  // downward: its 4 entries arrive reversed, see elo / ehi)
+  auto group = [&](uint32_t i) -> u8e { return *(cu8e *)(HU ? EL - 4 - i : EL + i); };
+  auto elo = [&](const u8e v, int r) -> uint32_t { return HU ? v[2 * (3 - r)] : v[2 * r]; };
+  auto ehi = [&](const u8e v, int r) -> uint32_t { return HU ? v[2 * (3 - r) + 1] : v[2 * r + 1]; };
   int tl0 = tid;
   asm volatile("" : "+v"(tl0));
   const int jt = tl0 % G;
   const uint32_t j16 = 16 * jt;
-#if GN_ASM_RING
   typedef int sq4 __attribute__((ext_vector_type(4)));
   const uint64_t ftp = (uint64_t)(uintptr_t)net.ft;
   const sq4 rsq = {__builtin_amdgcn_readfirstlane((int)(uint32_t)ftp),
                    __builtin_amdgcn_readfirstlane((int)(uint32_t)(ftp >> 32) & 0xFFFF),
-                   (int)(((size_t)FT_ROWS + (size_t)SCR_ROWS * SCR_SLOTS) * RS), 0x00020000};
+                   (int)(((size_t)ZERO_ROW + 1) * RS), 0x00020000};
+  const uint32_t scr_off = (scr - (uint32_t)FT_ROWS) * RS; // this slot's rows from the first scratch row
+  auto offset = [&](uint32_t lo, uint32_t h) -> uint32_t {
+#ifdef GN_ABLATE_ROWS
+    (void)lo, (void)h;
+    return (uint32_t)FT_BIAS_ROW * RS; // timing diagnostics build only: every row from L1 / L2
+#else
+    return lo + ((uint32_t)((int32_t)h >> 31) & scr_off);
 #endif
-  auto issue = [&](int r, uint32_t e) {
-    er[r] = e;
-    uint32_t row = (e & SCR) ? scr + (e & ROW) : (e & ROW);
-    if (e & KST) row = FT_BIAS_ROW; // a store-only entry: load the (L1-resident) bias row
-    if (ablate & 2) row = FT_BIAS_ROW; // timing diagnostics only: every row from L1 / L2
-#if GN_ASM_RING
+  };
+  auto issue = [&](int r, uint32_t lo, uint32_t h) {
+    eh[r] = h;
     // the ring's loads are invisible to the compiler's wait insertion (which, merging the
     // paths of the entry kinds at the loop head, waits for far more of the ring than an entry
     // needs); consume() waits for exactly its own row: see ring_wait
     asm volatile("buffer_load_dwordx4 %0, %2, %3, %4 offen\n\t"
                  "buffer_load_dwordx4 %1, %2, %3, %4 offen offset:%5"
                  : "=&v"(rlo[r]), "=&v"(rhi[r])
-                 : "v"(j16), "s"(rsq), "s"(row * RS), "n"(L1));
-#else
-    rlo[r] = __builtin_bit_cast(ushort8, __builtin_amdgcn_raw_buffer_load_b128(ftr, j16, row * RS, 0));
-    rhi[r] = __builtin_bit_cast(ushort8, __builtin_amdgcn_raw_buffer_load_b128(ftr, j16 + L1, row * RS, 0));
-#endif
+                 : "v"(j16), "s"(rsq), "s"(offset(lo, h)), "n"(L1));
   };
   // before entry r is consumed: its two loads are the oldest of the 8 in flight (the 3 later
   // entries of the last revolution and the earlier ones of this one were issued since); any
   // other memory operation in between (a drained store, the layer stack's loads) only makes
   // vmcnt(6) wait for more.  The "+v" ties the row registers to the wait: no use before it.
-  auto ring_wait = [&](int r) {
-#if GN_ASM_RING
-    asm volatile("s_waitcnt vmcnt(6)" : "+v"(rlo[r]), "+v"(rhi[r]));
-#else
-    (void)r;
-#endif
-  };
+  auto ring_wait = [&](int r) { asm volatile("s_waitcnt vmcnt(6)" : "+v"(rlo[r]), "+v"(rhi[r])); };
   ushort8 lo = {}, hi = {};
   auto consume = [&](int r) {
     ring_wait(r);
-    const uint32_t e = er[r];
-#ifdef GN_ABL_SIMPLE // timing diagnostics only (wrong results): no entry-kind branches
-    lo += rlo[r], hi += rhi[r];
-    if (e & LAST) *reinterpret_cast<uint2 *>(xt + ((e >> SLOT_SH) & 15) * XS + ((e >> SIDE_SH) & 1) * (L1 / 2) + 8 * jt) = transform8(lo, hi);
-    return;
-#endif
-#if GN_CONSUME_MAD
-    // every kind of entry is one 16-bit multiply-add per dword: acc = src + sg * row with
-    // sg = +1, -1 (SUB) or 0 (a no-op: ZERO | SUB), src = acc, or 0 / the parent / the
-    // sibling base at the entry that starts a slot (wrapping int16, as the accumulators)
-    const bool nop = (e & (INIT | SUB)) == (I_ZERO | SUB);
-    const uint32_t init = nop ? 0u : (e & INIT);
-    const unsigned short sg = nop ? (unsigned short)0 : (e & SUB) ? (unsigned short)0xFFFF : (unsigned short)1;
-    if (init) {
-      const ushort8 z = {};
-      lo = init == I_PACC ? pacc_lo : init == I_BASE ? base_lo : z;
-      hi = init == I_PACC ? pacc_hi : init == I_BASE ? base_hi : z;
+    const uint32_t h = eh[r];
+    // every entry is one 16-bit multiply-add per dword, acc = src + sg * row, its multiplier
+    // sg (1, 0xFFFF = -1, 0) the low half of h as the instruction's scalar operand; src is
+    // the accumulator, or (PRE) 0 / the parent / the sibling base at a slot's first entry
+    // (wrapping int16, as the accumulators)
+    if (h & H_PRE) {
+      const uint32_t init = (h >> H_INIT_SH) & 3;
+      asm volatile("");
+      if (init == 2) lo = pacc_lo, hi = pacc_hi;
+      else if (init == 3) lo = base_lo, hi = base_hi;
+      else lo = ushort8{}, hi = ushort8{};
     }
+    const unsigned short sg = (unsigned short)h;
     lo = rlo[r] * sg + lo, hi = rhi[r] * sg + hi;
-    if (init == I_PACC) {
+    if ((h & (H_PRE | 3u << H_INIT_SH)) == (H_PRE | 2u << H_INIT_SH)) {
       asm volatile("");
       base_lo = lo, base_hi = hi;
     }
-#else
-    const uint32_t init = e & INIT;
-    // scalar branches; the empty asm keeps the compiler from if-converting them into
-    // selects over every alternative
-    if (init == I_ZERO) {
-      asm volatile("");
-      if (!(e & SUB)) lo = rlo[r], hi = rhi[r];
-    } else if (init == I_PACC) {
-      asm volatile("");
-      lo = pacc_lo - rlo[r], hi = pacc_hi - rhi[r];
-      base_lo = lo, base_hi = hi;
-    } else if (init == I_BASE) {
-      if (e & SUB) {
-        asm volatile("");
-        lo = base_lo - rlo[r], hi = base_hi - rhi[r];
-      } else {
-        asm volatile("");
-        lo = base_lo + rlo[r], hi = base_hi + rhi[r];
-      }
-    } else if (e & SUB) {
-      asm volatile("");
-      lo -= rlo[r], hi -= rhi[r];
-    } else {
-      asm volatile("");
-      lo += rlo[r], hi += rhi[r];
-    }
-#endif
-    if (e & LAST) {
-      const int sl = (e >> SLOT_SH) & 15, side = (e >> SIDE_SH) & 1;
+    if (h & H_LAST) {
+      const int sl = (h >> H_SLOT_SH) & 15, side = (h >> H_SIDE_SH) & 1;
       *reinterpret_cast<uint2 *>(xt + sl * XS + side * (L1 / 2) + 8 * jt) = transform8(lo, hi);
-      if (e & PAR_E) {
+      if (h & H_PAR_E) {
         asm volatile("");
         pacc_lo = lo, pacc_hi = hi;
       }
-      if (e & (KST | NXT)) { // accumulator stores: king-cache row and / or this list's carry row
+      if (h & (H_KST | H_NXT)) { // accumulator stores: king-cache row and / or this list's carry row
         asm volatile("");
-        uint32_t so = (scr + (uint32_t)hu) * RS;
-        if (e & KST) so = (scr + (e & ROW)) * RS;
-        for (int rep = (e & KST) && (e & NXT) ? 2 : 1; rep; --rep) {
+        const uint32_t carry = (scr + (uint32_t)HU) * RS;
+        uint32_t so = (h & H_KST) ? (scr + (h & 0xFFFFu)) * RS : carry;
+        for (int rep = (h & H_KST) && (h & H_NXT) ? 2 : 1; rep; --rep) {
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(int4v, lo), ftr, j16, so, 0);
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(int4v, hi), ftr, j16 + L1, so, 0);
-          so = (scr + (uint32_t)hu) * RS;
+          so = carry;
         }
         // drain here (vmcnt(0)): with a store pending, loads and stores would be counted out of
         // order and every later wait of the ring would become vmcnt(0); stores are rare
@@ -679,10 +676,11 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
     }
   };
   uint32_t pos = 0; // the group of 4 entries whose rows are in flight starts here
-  u4e gp = group(4); // the entries whose rows the next revolution issues (prefetched)
+  u8e gp = group(4); // the entries whose rows the next revolution issues (prefetched)
   {
-    const u4e g0 = group(0);
-    issue(0, ent4(g0, 0)), issue(1, ent4(g0, 1)), issue(2, ent4(g0, 2)), issue(3, ent4(g0, 3));
+    const u8e g0 = group(0);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) issue(r, elo(g0, r), ehi(g0, r));
   }
 
   unsigned long long sp_s = 0, sp_w = 0, sp_l = 0, sp_m = 0, sp_n = 0;
@@ -698,7 +696,7 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
       sp_e0 = a0, sp_e1 = a1;
     }
 #endif
-    const uint32_t e_end = __builtin_amdgcn_readfirstlane(D->e_end[hu]);
+    const uint32_t e_end = __builtin_amdgcn_readfirstlane(D->e_end[HU]);
     const uint32_t p_first = __builtin_amdgcn_readfirstlane(D->p_first);
     const uint32_t first = __builtin_amdgcn_readfirstlane(D->first);
     uint32_t mw[4];
@@ -715,12 +713,12 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
       // (lgkmcnt(0): the prefetch of the previous revolution), take this revolution's entries,
       // and only then prefetch the next group, which nothing uses before the next revolution
       __builtin_amdgcn_s_waitcnt(0xC07F);
-      const u4e gw = gp;
+      const u8e gw = gp;
       gp = group(pos + 8);
-      consume(0), issue(0, ent4(gw, 0));
-      consume(1), issue(1, ent4(gw, 1));
-      consume(2), issue(2, ent4(gw, 2));
-      consume(3), issue(3, ent4(gw, 3));
+      consume(0), issue(0, elo(gw, 0), ehi(gw, 0));
+      consume(1), issue(1, elo(gw, 1), ehi(gw, 1));
+      consume(2), issue(2, elo(gw, 2), ehi(gw, 2));
+      consume(3), issue(3, elo(gw, 3), ehi(gw, 3));
       pos += 4;
     }
     asm volatile("" ::: "memory");
@@ -822,9 +820,6 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
             }
           }
         }
-#if !GN_ASM_RING
-        __builtin_amdgcn_s_waitcnt(0x0F70); // no store pending into the compiler-tracked ring
-#endif
       }
       ++bq;
     }
@@ -838,6 +833,9 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
 #else
   (void)sp_s, (void)sp_w, (void)sp_l, (void)sp_m, (void)sp_n, (void)sp_e0, (void)sp_e1;
 #endif
+  };
+  if (hu) run_group(std::integral_constant<int, 1>{});
+  else run_group(std::integral_constant<int, 0>{});
   if (use_scr) { // every wave's stores are complete before the slot goes back to the pool
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -850,7 +848,7 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
 hipError_t launch_plan_stream(const NetDevice &net, const gn_board *parents, size_t n, const uint64_t *offsets,
                               const ChildDelta *deltas, const uint8_t *need_parent, const uint8_t *need_child,
                               int2 *out_parent, int2 *out_child, int swz, const uint8_t *next_slot, int chain_k,
-                              int kc, const uint64_t *eoff, uint32_t *ent, TileDesc *tiles, uint32_t *btiles,
+                              int kc, const uint64_t *eoff, uint64_t *ent, TileDesc *tiles, uint32_t *btiles,
                               uint32_t *pool, uint32_t *err, unsigned long long *rows_out, size_t b0, size_t b1,
                               const uint32_t *order, hipEvent_t mid, hipStream_t s) {
   if (!n || b1 <= b0) return hipSuccess;

@@ -10,7 +10,7 @@ cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 timeout -k 10 400 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err || { tail -20 $OUT/bench.err; exit 1; }
 cat $OUT/bench.json
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- \
-    python bench.py --no-cpu-baseline --check 0 > $OUT/trace.log 2>&1 || { tail -20 $OUT/trace.log; exit 1; }
+    python bench.py --no-cpu-baseline --no-secondary --check 0 > $OUT/trace.log 2>&1 || { tail -20 $OUT/trace.log; exit 1; }
 echo "trace done"
 for wl in ${WLS:-expand big16m small1m}; do
   ARGS="--workload $wl --steps 1 --warmup 0 --no-cpu-baseline --no-secondary --check 0"
