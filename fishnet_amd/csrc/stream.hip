@@ -751,7 +751,7 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
         // (batches of FB k-steps: the next tile's rows stay in flight in registers meanwhile)
         constexpr int FB = 2;
 #pragma unroll
-        for (int k0 = 0; k0 < KPW; k0 += FB) {
+        for (int k0 = 0; k0 < KPW && !(ablate & 16); k0 += FB) { // (16: timing diagnostics, no fc_0)
           int4v wv[FB], av[FB];
 #pragma unroll
           for (int j = 0; j < FB; ++j) wv[j] = *reinterpret_cast<const int4v *>(wb + 64 * (k0 + j));
@@ -764,7 +764,7 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
         for (int i = 0; i < 4; ++i) atomicAdd(&acc0[buf][(4 * kg + i) * 16 + row], acc[i]);
       }
       __syncthreads();
-      if (wave == (int)(bq % NW)) { // fc_0 activations, fc_1, fc_2, outputs of bucket b
+      if (wave == (int)(bq % NW) && !(ablate & 8)) { // fc_0 activations, fc_1, fc_2, outputs of bucket b (8: diagnostics)
         const int32_t bias0 = net.b0[b * 16 + row];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
