@@ -38,8 +38,7 @@
 // entry), [18:17] the init kind, [19] LAST, [23:20] slot, [24] side, [25] PAR_E, [26] NXT,
 // [27] KST, [31] SCR; so the stream's common entry is a multiply-add with hi as its scalar
 // operand and two bit tests.
-// Lists are padded per tile to a multiple of 4 with no-op entries (ZERO | SUB) so every
-// ring step issues the same loads.  The ring issues a row load 4 entries before it
+// The ring issues a row load 4 entries before it
 // consumes it, so an entry that loads a scratch row sits at least 4 entries after the
 // last store to scratch in its list (no-op entries are inserted when needed): the load
 // is then issued after the store, by the same lanes.  The ring runs across tiles.
@@ -155,13 +154,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
   };
 
   auto flush = [&]() {
-    // pad both lists of the tile to a multiple of 4 with no-op entries
-    if (lane < 3) {
-      if (len0 + lane < ((len0 + 3) & ~3u)) put(0, len0 + lane, PAD);
-      if (len1 + lane < ((len1 + 3) & ~3u)) put(1, len1 + lane, PAD);
-    }
-    fpads += (((len0 + 3) & ~3u) - len0) + (((len1 + 3) & ~3u) - len1);
-    len0 = (len0 + 3) & ~3u, len1 = (len1 + 3) & ~3u;
+    // (the lists need no padding at a tile's end: the stream enters and leaves its ring
+    // revolutions at any entry)
     TileDesc *d = T + tile_k;
     if (lane >= t_fill && lane < 16) d->meta[lane] = 0;
     if (lane == 0) d->e_end[0] = len0, d->e_end[1] = len1, d->p_first = p_first, d->first = t_first;
@@ -675,8 +669,9 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
       }
     }
   };
-  uint32_t pos = 0; // the group of 4 entries whose rows are in flight starts here
+  uint32_t pos = 0; // the next entry to consume: entries pos .. pos + 3 have their rows in flight
   u8e gp = group(4); // the entries whose rows the next revolution issues (prefetched)
+  u8e gw;            // ... and this revolution's
   {
     const u8e g0 = group(0);
 #pragma unroll
@@ -703,23 +698,26 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
 #pragma unroll
     for (int i = 0; i < 4; ++i)
       mw[i] = (uint32_t)__builtin_amdgcn_readfirstlane((int)reinterpret_cast<const uint32_t *>(D->meta)[i]);
-    // ---- the row stream of this group's list segment [pos, e_end) (a multiple of 4): a
-    // counted loop of its own (the empty asm keeps it from being fused with the tile loop,
-    // which would merge its wait counts with the layer stack's)
-    const uint32_t nrev = (e_end - pos) >> 2;
+    // ---- the row stream of this group's list segment [pos, e_end): ring slot r holds entry i
+    // with i % 4 == r, so a tile may begin and end anywhere in a revolution of 4 entries (a
+    // revolution starts at a multiple of 4: it waits for its prefetched group of entries,
+    // whose rows it issues, and prefetches the next); every step is guarded by uniform tests
 #pragma unroll 1
-    for (uint32_t t = 0; t < nrev; ++t) {
-      // scalar loads complete out of order, so any use waits for all of them: wait once here
-      // (lgkmcnt(0): the prefetch of the previous revolution), take this revolution's entries,
-      // and only then prefetch the next group, which nothing uses before the next revolution
-      __builtin_amdgcn_s_waitcnt(0xC07F);
-      const u8e gw = gp;
-      gp = group(pos + 8);
-      consume(0), issue(0, elo(gw, 0), ehi(gw, 0));
-      consume(1), issue(1, elo(gw, 1), ehi(gw, 1));
-      consume(2), issue(2, elo(gw, 2), ehi(gw, 2));
-      consume(3), issue(3, elo(gw, 3), ehi(gw, 3));
-      pos += 4;
+    while (pos < e_end) {
+      const uint32_t r0 = pos & 3;
+      if (r0 == 0) {
+        // scalar loads complete out of order, so any use waits for all of them: wait once
+        // here (lgkmcnt(0): the prefetch of the previous revolution), take this revolution's
+        // entries, and only then prefetch the next group, which nothing uses before the next
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        gw = gp;
+        gp = group(pos + 8);
+        consume(0), issue(0, elo(gw, 0), ehi(gw, 0));
+        ++pos;
+      }
+      if (r0 <= 1 && pos < e_end) consume(1), issue(1, elo(gw, 1), ehi(gw, 1)), ++pos;
+      if (r0 <= 2 && pos < e_end) consume(2), issue(2, elo(gw, 2), ehi(gw, 2)), ++pos;
+      if (pos < e_end) consume(3), issue(3, elo(gw, 3), ehi(gw, 3)), ++pos;
     }
     asm volatile("" ::: "memory");
     const unsigned long long t1 = SP_T();
@@ -765,7 +763,16 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
       }
       __syncthreads();
       if (wave == (int)(bq % NW) && !(ablate & 8)) { // fc_0 activations, fc_1, fc_2, outputs of bucket b (8: diagnostics)
+        // the finishing step's scalar weights and the tile's PSQT first (one wait for memory)
         const int32_t bias0 = net.b0[b * 16 + row];
+        const int32_t b1l = net.b1[b * 32 + row], b1h = net.b1[b * 32 + 16 + row];
+        const int32_t w2l = net.w2[b * 32 + row], w2h = net.w2[b * 32 + 16 + row];
+        const int32_t b2v = net.b2[b];
+        int2 pq[4] = {};
+        if (row == 0) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) pq[i] = *reinterpret_cast<const int2 *>(D->psq[4 * kg + i]);
+        }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int pos = 4 * kg + i;
@@ -792,8 +799,6 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
         }
         const int4v cl = __builtin_amdgcn_mfma_i32_16x16x64_i8(a1, wl, zero, 0, 0, 0);
         const int4v ch = __builtin_amdgcn_mfma_i32_16x16x64_i8(a1, wh, zero, 0, 0, 0);
-        const int32_t b1l = net.b1[b * 32 + row], b1h = net.b1[b * 32 + 16 + row];
-        const int32_t w2l = net.w2[b * 32 + row], w2h = net.w2[b * 32 + 16 + row];
         int32_t part[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -805,14 +810,13 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
 #pragma unroll
           for (int i = 0; i < 4; ++i) part[i] = wadd(part[i], __shfl_xor(part[i], off, 16));
         if (row == 0) {
-          const int32_t b2v = net.b2[b];
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const int pos = 4 * kg + i;
             const uint32_t m = (mw[pos >> 2] >> (8 * (pos & 3))) & 0xFF;
             if ((m & 1) && (int)((m >> 1) & 7) == b) {
               const int32_t positional = wadd(wadd(b2v, part[i]), fwd[buf][pos]);
-              const int32_t psqt = (int32_t)((uint32_t)D->psq[pos][0] - (uint32_t)D->psq[pos][1]) / 2;
+              const int32_t psqt = (int32_t)((uint32_t)pq[i].x - (uint32_t)pq[i].y) / 2;
               const int2 val = make_int2(psqt / 16, positional / 16);
               const uint32_t P = p_first + (uint32_t)__builtin_popcount(pm & ((2u << pos) - 1)) - (pm & 1);
               if ((pm >> pos) & 1) out_parent[P] = val;
