@@ -58,8 +58,9 @@ struct TileDesc {
   uint32_t first;
   uint8_t meta[16];
   int32_t psq[16][2];
+  int16_t adj[16]; // a child slot's output index minus its position (the chained walk's reorder)
 };
-static_assert(sizeof(TileDesc) == 160, "TileDesc is 160 bytes");
+static_assert(sizeof(TileDesc) == 192, "TileDesc is 192 bytes");
 // Tiles of a block start at tiles + (pbeg + offsets[pbeg]) / 16 + (K + 2) * block (btiles[block]
 // of them), entries at ent + eoff[pbeg] + 16 * block (list 0 upward, list 1 downward from
 // the region's end, eoff = exclusive scan of write_children's per-parent entry bounds).

@@ -9,35 +9,35 @@
 //                       two lists of row entries (one per absolute perspective) and a
 //                       descriptor per 16-slot tile, in HBM.  Every decision that is
 //                       sequential inside a block is made here: the sibling cache, the
-//                       chain carry (parent p + 1 starts from parent p's child that is
-//                       its position), the king cache (Stockfish's AccumulatorCaches
-//                       analog: a king-move refresh starts from the accumulator the
-//                       block last computed for that perspective and king square, plus
-//                       the placement difference), the list balance, and every PSQT
-//                       sum (PSQT never enters the row stream).
+//                       chain (parent p + 1 starts from parent p's child that is its
+//                       position: that child is evaluated last among its siblings and its
+//                       accumulators become the parent accumulators), the king cache
+//                       (Stockfish's AccumulatorCaches analog: a king-move refresh starts
+//                       from the accumulator the block last computed for that perspective
+//                       and king square, plus the placement difference), the list balance,
+//                       and every PSQT sum (PSQT never enters the row stream).
 //   stream_eval_kernel  one workgroup per block: each perspective group of waves walks
 //                       its list with a 4-deep register ring of row loads, transforms at
 //                       each slot's last entry into the LDS tile, and after each tile
 //                       all waves run fc_0 as int8 MFMAs; one wave per bucket finishes
 //                       fc_1 / fc_2 and writes the outputs while the others stream on.
 //
-// Entry (u32), shared by the two kernels:
-//   [18:0] row: an FT row, or (SCR) a row of the workgroup's scratch slot: 0 / 1 the
-//          carry row of perspective 0 / 1, 2 + 64 h + ksq the king-cache row of (h, ksq)
+// Entry (u32), as the plan kernel builds it:
+//   [18:0] row: an FT row, the zero row, or (SCR) a row of the workgroup's scratch slot
+//          (2 + 64 h + ksq: the king-cache row of (h, ksq))
 //   [19] SUB   [21:20] init before this entry: 0 none, 1 ZERO (lo = row; with SUB: keep,
 //          a store-only entry), 2 PACC (lo = parent - row, saved as the sibling base),
 //          3 BASE (lo = base +- row)   [22] LAST entry of its slot   [26:23] slot in tile
-//   [27] side (0: the perspective to move)   [28] PAR_E (the parent slot: its accumulator
-//   becomes pacc)   [29] NXT (store the slot's accumulator to this list's carry row)
-//   [30] SCR   [31] KST (store the slot's accumulator to the row of this entry)
-// The plan kernel builds entries in that form and stores each as the stream kernel's
-// pre-decoded u64 (enc64): lo = the row's byte offset (scratch rows: from the first scratch
-// row, the workgroup adds its slot's offset), hi = [15:0] the 16-bit multiplier of the row
-// (1 add, 0xFFFF subtract, 0 no-op: ZERO | SUB entries; a store-only KST entry loads the
-// zero row and has its target scratch row here), [16] PRE (an init before the
-// entry), [18:17] the init kind, [19] LAST, [23:20] slot, [24] side, [25] PAR_E, [26] NXT,
-// [27] KST, [31] SCR; so the stream's common entry is a multiply-add with hi as its scalar
-// operand and two bit tests.
+//   [27] side (0: the perspective to move)   [28] PAR_E (the slot's accumulator becomes
+//   pacc: a parent, or the child that is the next parent)   [30] SCR   [31] KST (store
+//   the slot's accumulator to the row of this entry)
+// The plan kernel stores each entry as the stream kernel's pre-decoded u64 (enc64):
+// lo = the row's byte offset (scratch rows: from the first scratch row, the workgroup
+// adds its slot's offset), hi = [15:0] the 16-bit multiplier of the row (1 add, 0xFFFF
+// subtract, 0 no-op: ZERO | SUB entries; a store-only KST entry loads the zero row and
+// has its target scratch row here), [16] PRE (an init before the entry), [18:17] the init
+// kind, [19] LAST, [23:20] slot, [24] side, [25] PAR_E, [27] KST, [31] SCR; so the
+// stream's common entry is a multiply-add with hi as its scalar operand and two bit tests.
 // The ring issues a row load 4 entries before it
 // consumes it, so an entry that loads a scratch row sits at least 4 entries after the
 // last store to scratch in its list (no-op entries are inserted when needed): the load
@@ -72,12 +72,12 @@ __device__ unsigned long long gn_sp[8]; // [0] stream [1] barrier wait [2] layer
 namespace gn {
 namespace ps {
 constexpr uint32_t ROW = (1u << 19) - 1, SUB = 1u << 19, I_ZERO = 1u << 20, I_PACC = 2u << 20, I_BASE = 3u << 20,
-                   INIT = 3u << 20, LAST = 1u << 22, SLOT_SH = 23, SIDE_SH = 27, PAR_E = 1u << 28, NXT = 1u << 29,
+                   INIT = 3u << 20, LAST = 1u << 22, SLOT_SH = 23, SIDE_SH = 27, PAR_E = 1u << 28,
                    SCR = 1u << 30, KST = 1u << 31;
 constexpr uint32_t PAD = (uint32_t)FT_BIAS_ROW | I_ZERO | SUB;
 // pre-decoded form (see the header)
 constexpr uint32_t H_PRE = 1u << 16, H_INIT_SH = 17, H_LAST = 1u << 19, H_SLOT_SH = 20, H_SIDE_SH = 24,
-                   H_PAR_E = 1u << 25, H_NXT = 1u << 26, H_KST = 1u << 27, H_SCR = 1u << 31;
+                   H_PAR_E = 1u << 25, H_KST = 1u << 27, H_SCR = 1u << 31;
 template <int L1>
 __device__ __forceinline__ uint64_t enc64(uint32_t e) {
   constexpr uint32_t RS = 2 * L1 + 32;
@@ -92,7 +92,6 @@ __device__ __forceinline__ uint64_t enc64(uint32_t e) {
   hi |= (e & LAST) ? H_LAST : 0u;
   hi |= ((e >> SLOT_SH) & 15) << H_SLOT_SH | ((e >> SIDE_SH) & 1) << H_SIDE_SH;
   hi |= (e & PAR_E) ? H_PAR_E : 0u;
-  hi |= (e & NXT) ? H_NXT : 0u;
   hi |= (e & KST) ? H_KST : 0u;
   hi |= (e & SCR) && !kst ? H_SCR : 0u;
   return (uint64_t)hi << 32 | lo;
@@ -193,6 +192,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
       }
       carried = nxq > 0;
     }
+    // the child that is the next parent is evaluated last among its siblings (its accumulators
+    // then become the parent accumulators the next parent starts from): processing position q
+    // (1..nch) takes child ci(q), the others keep their order
+    auto child_of = [&](int q) -> int {
+      const int c = q - 1;
+      return nxq > 0 && c >= nxq - 1 ? (c < nch - 1 ? c + 1 : nxq - 1) : c;
+    };
+    const int nxpos = nxq > 0 ? nch : -1;
     int ckey0 = -1, ckey1 = -1; // sibling keys carried across this parent's segments
     // ---- a refreshed parent starts from the king cache when the block last computed an
     // accumulator for this perspective and king square (Stockfish's AccumulatorCaches for
@@ -239,8 +246,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
         if (q == 0) {
           vld = need_parent ? need_parent[p] : 1;
           cst = stm, cnt = P, kinds = 3 | 3 << 2;
-        } else if ((vld = need_child ? need_child[off + q - 1] : 1)) {
-          const uint32_t *src = reinterpret_cast<const uint32_t *>(deltas + off + q - 1);
+        } else if ((vld = need_child ? need_child[off + child_of(q)] : 1)) {
+          const uint32_t *src = reinterpret_cast<const uint32_t *>(deltas + off + child_of(q));
           w0 = src[0], w1 = src[1], w2 = src[2], w3 = src[3];
           const uint32_t meta = src[4];
           cst = (meta >> 10) & 1;
@@ -286,8 +293,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
       if (km1) ckey1 = __builtin_amdgcn_readlane(key1, 63 - __builtin_clzll(km1));
       // ---- entries of the parent and of delta perspectives (prefix sums over the lanes)
       if (live && q0 == 0) { // the parent loads the carry / cache rows: after their stores
-        if (have || pnd[0] >= 0) pad_to(0, safe0);
-        if (have || pnd[1] >= 0) pad_to(1, safe1);
+        if (pnd[0] >= 0) pad_to(0, safe0);
+        if (pnd[1] >= 0) pad_to(1, safe1);
       }
       const bool ref0 = (kinds & 3) == 2, ref1 = (kinds >> 2) == 2;
       int d0 = 0, d1 = 0;
@@ -308,7 +315,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
       }
       const uint32_t exc = inc - c, tot = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
       const uint32_t t0w = tmpl(t, cst != 0), t1w = tmpl(t, cst != 1);
-      const bool nx = q == nxq;
+      const bool nx = q == nxpos;
       if (in && live) {
         auto delta = [&](int g, uint32_t at, uint32_t lo2, uint32_t hi2, int s, int n, bool hit, uint32_t tw,
                          uint32_t L) {
@@ -327,12 +334,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
             if (n > 3) put(g, at + 2, r3 | tw | L);
           }
         };
-        if ((kinds & 3) == 1) delta(0, len0 + (exc & 0xFFFF), w0, w1, s0, n0, hit0, t0w, LAST | (nx ? NXT : 0u));
-        if ((kinds >> 2) == 1) delta(1, len1 + (exc >> 16), w2, w3, s1, n1, hit1, t1w, LAST | (nx ? NXT : 0u));
+        if ((kinds & 3) == 1) delta(0, len0 + (exc & 0xFFFF), w0, w1, s0, n0, hit0, t0w, LAST | (nx ? PAR_E : 0u));
+        if ((kinds >> 2) == 1) delta(1, len1 + (exc >> 16), w2, w3, s1, n1, hit1, t1w, LAST | (nx ? PAR_E : 0u));
         if (kinds == 15) {
-          if (have) { // the parent from the carry rows: one entry per list
-            put(0, len0 + (exc & 0xFFFF), SCR | 0u | t0w | I_ZERO | PAR_E | LAST);
-            put(1, len1 + (exc >> 16), SCR | 1u | t1w | I_ZERO | PAR_E | LAST);
+          if (have) { // the parent is its predecessor's last child: pacc, one entry per list
+            put(0, len0 + (exc & 0xFFFF), (uint32_t)ZERO_ROW | t0w | I_PACC | SUB | PAR_E | LAST);
+            put(1, len1 + (exc >> 16), (uint32_t)ZERO_ROW | t1w | I_PACC | SUB | PAR_E | LAST);
           } else { // bias entry or the cache row; the rest follows (below, lane = square / row)
             put(0, len0 + (exc & 0xFFFF),
                 (pnd[0] >= 0 ? SCR | (uint32_t)(2 + pkq[0]) : (uint32_t)FT_BIAS_ROW) | t0w | I_ZERO | PAR_E);
@@ -359,6 +366,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
         }
       }
       if (in) T[tile_k].meta[t] = (uint8_t)((live && vld ? 1 : 0) | bk << 1 | (q == 0 ? 16 : 0) | cst << 5);
+      if (in) T[tile_k].adj[t] = (int16_t)(q == 0 ? 0 : child_of(q) - (q - 1));
       // the parent's rows (lane = row) after its bias entry (the parent is lane 0 of its segment)
       if (live && q0 == 0 && !have) {
         const uint64_t lt2 = (1ull << lane) - 1;
@@ -395,17 +403,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
         }
         ps::wave_sync();
       }
-      { // a delta child that is the next parent stores its carry rows at its last entry
-        const uint64_t nxm = __ballot(in && live && nx);
-        if (nxm) {
-          const int l = __builtin_ctzll(nxm);
-          const uint32_t e0 = (uint32_t)__builtin_amdgcn_readlane((int)(inc & 0xFFFF), l);
-          const uint32_t e1 = (uint32_t)__builtin_amdgcn_readlane((int)(inc >> 16), l);
-          const int kd = __builtin_amdgcn_readlane(kinds, l);
-          if ((kd & 3) == 1) safe0 = len0 + e0 - 1 + 4; // inclusive prefix: last entry at inc - 1
-          if ((kd >> 2) == 1) safe1 = len1 + e1 - 1 + 4;
-        }
-      }
       len0 += tot & 0xFFFF, len1 += tot >> 16;
       rows += (tot & 0xFFFF) + (tot >> 16);
       // ---- king-move refreshes, one job per slot in slot order, lane = square
@@ -415,7 +412,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
         jm &= jm - 1;
         const int hh = __builtin_amdgcn_readlane((int)ref1, l), st = __builtin_amdgcn_readlane(cst, l);
         const int cn = __builtin_amdgcn_readlane(cnt, l), tl = t_fill + l;
-        const bool nxl = q0 + l == nxq;
+        const bool nxl = q0 + l == nxpos;
         const uint32_t sq01 = (uint32_t)__builtin_amdgcn_readlane((int)(hh ? w2 : w0), l),
                        sq23 = (uint32_t)__builtin_amdgcn_readlane((int)(hh ? w3 : w1), l);
         const int kt = (int)(sq01 >> 16);
@@ -447,7 +444,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
         const int g = hit ? own : nxl ? hh : kuse && own >= 0 ? own : (len0 <= len1 ? 0 : 1);
         if (hit) pad_to(g, g ? safe1 : safe0); // the cache row load after the list's last scratch store
         const uint32_t base = g ? len1 : len0;
-        const uint32_t L = LAST | (nxl ? NXT : 0u);
+        const uint32_t L = LAST | (nxl ? PAR_E : 0u);
         const uint32_t krow = SCR | (uint32_t)(2 + kci);
         int ne;
         if (hit) {
@@ -475,7 +472,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
           if (lane == 0) kstate[w][kci] = (uint8_t)(1 | g << 1);
           ps::wave_sync();
         }
-        if (kuse || nxl) { // this slot's last entry stores to scratch
+        if (kuse) { // this slot's last entry stores to scratch
           uint32_t &sf = g ? safe1 : safe0;
           sf = base + (uint32_t)ne - 1 + 4;
         }
@@ -654,15 +651,11 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
         asm volatile("");
         pacc_lo = lo, pacc_hi = hi;
       }
-      if (h & (H_KST | H_NXT)) { // accumulator stores: king-cache row and / or this list's carry row
+      if (h & H_KST) { // the accumulator to its king-cache row
         asm volatile("");
-        const uint32_t carry = (scr + (uint32_t)HU) * RS;
-        uint32_t so = (h & H_KST) ? (scr + (h & 0xFFFFu)) * RS : carry;
-        for (int rep = (h & H_KST) && (h & H_NXT) ? 2 : 1; rep; --rep) {
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(int4v, lo), ftr, j16, so, 0);
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(int4v, hi), ftr, j16 + L1, so, 0);
-          so = carry;
-        }
+        const uint32_t so = (scr + (h & 0xFFFFu)) * RS;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(int4v, lo), ftr, j16, so, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(int4v, hi), ftr, j16 + L1, so, 0);
         // drain here (vmcnt(0)): with a store pending, loads and stores would be counted out of
         // order and every later wait of the ring would become vmcnt(0); stores are rare
         __builtin_amdgcn_s_waitcnt(0x0F70);
@@ -769,9 +762,10 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
         const int32_t w2l = net.w2[b * 32 + row], w2h = net.w2[b * 32 + 16 + row];
         const int32_t b2v = net.b2[b];
         int2 pq[4] = {};
+        int adj[4] = {};
         if (row == 0) {
 #pragma unroll
-          for (int i = 0; i < 4; ++i) pq[i] = *reinterpret_cast<const int2 *>(D->psq[4 * kg + i]);
+          for (int i = 0; i < 4; ++i) pq[i] = *reinterpret_cast<const int2 *>(D->psq[4 * kg + i]), adj[i] = D->adj[4 * kg + i];
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -820,7 +814,7 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
               const int2 val = make_int2(psqt / 16, positional / 16);
               const uint32_t P = p_first + (uint32_t)__builtin_popcount(pm & ((2u << pos) - 1)) - (pm & 1);
               if ((pm >> pos) & 1) out_parent[P] = val;
-              else out_child[u0 + pos - P - 1] = val;
+              else out_child[u0 + pos - P - 1 + adj[i]] = val;
             }
           }
         }
@@ -858,7 +852,7 @@ hipError_t launch_plan_stream(const NetDevice &net, const gn_board *parents, siz
   if (!n || b1 <= b0) return hipSuccess;
   if (n >= 0x80000000ull) return hipErrorInvalidValue; // 32-bit parent indices in the kernels
   const uint32_t K = chain_k > 1 && next_slot ? (uint32_t)chain_k : 1u;
-  const int scr = K > 1 || kc; // carry rows or king cache in use
+  const int scr = K > 1 && kc; // the king cache's rows (the chained walk itself needs no scratch)
   if (b1 > (n + K - 1) / K) return hipErrorInvalidValue;
   const uint32_t nb = (uint32_t)(b1 - b0), B0 = (uint32_t)b0, B1 = (uint32_t)b1;
   const unsigned pg = (nb + 3) / 4, g = swz ? 8 * ((nb + 7) / 8) : nb;
