@@ -656,9 +656,10 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
         const uint32_t so = (scr + (h & 0xFFFFu)) * RS;
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(int4v, lo), ftr, j16, so, 0);
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(int4v, hi), ftr, j16 + L1, so, 0);
-        // drain here (vmcnt(0)): with a store pending, loads and stores would be counted out of
-        // order and every later wait of the ring would become vmcnt(0); stores are rare
-        __builtin_amdgcn_s_waitcnt(0x0F70);
+        // no drain: the ring's vmcnt(6) still covers an entry's own loads with these two stores
+        // outstanding (loads complete in order, so >= 2 of the >= 4 completions it waits for are
+        // that entry's loads), and a later load of the row is issued after the store in program
+        // order by the same lanes (the plan keeps it >= 4 entries behind)
       }
     }
   };
