@@ -508,7 +508,10 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
   constexpr uint32_t RS = 2 * L1 + 32;
   static_assert(G % 64 == 0 && KS % NW == 0 && KPW % 2 == 0, "geometry");
   __shared__ __attribute__((aligned(16))) uint8_t xt[TILE * XS];
-  __shared__ int32_t acc0[2][256];
+  // fc_0 partial sums [position][output], rows padded to 20 dwords: the 4 lane groups of an
+  // atomic (kg) then fall on different banks (a 16-dword row put all 4 on the same bank)
+  constexpr int AS = 20;
+  __shared__ int32_t acc0[2][16 * AS];
   __shared__ __attribute__((aligned(16))) uint8_t in1[2][TILE][32];
   __shared__ int32_t fwd[2][TILE];
   __shared__ uint32_t sslot;
@@ -517,7 +520,7 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
   const int hu = __builtin_amdgcn_readfirstlane((tid / G) & 1);
   const __amdgpu_buffer_rsrc_t ftr = __builtin_amdgcn_make_buffer_rsrc(
       (void *)net.ft, 0, (int)(((size_t)ZERO_ROW + 1) * RS), 0x00020000);
-  for (int i = tid; i < 512; i += NT) (&acc0[0][0])[i] = 0;
+  for (int i = tid; i < 2 * 16 * AS; i += NT) (&acc0[0][0])[i] = 0;
   // this launch evaluates blocks [b0, b1); with swz, XCD x (= dispatch index mod 8) takes
   // the x-th contiguous eighth of them (a block's king-sorted neighbours share its L2)
   const uint32_t nblk = b1 - b0;
@@ -753,7 +756,7 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
           for (int j = 0; j < FB; ++j) acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(av[j], wv[j], acc, 0, 0, 0);
         }
 #pragma unroll
-        for (int i = 0; i < 4; ++i) atomicAdd(&acc0[buf][(4 * kg + i) * 16 + row], acc[i]);
+        for (int i = 0; i < 4; ++i) atomicAdd(&acc0[buf][(4 * kg + i) * AS + row], acc[i]);
       }
       __syncthreads();
       if (wave == (int)(bq % NW) && !(ablate & 8)) { // fc_0 activations, fc_1, fc_2, outputs of bucket b (8: diagnostics)
@@ -771,7 +774,7 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int pos = 4 * kg + i;
-          const int32_t vv = wadd(acc0[buf][pos * 16 + row], bias0);
+          const int32_t vv = wadd(acc0[buf][pos * AS + row], bias0);
           if (row < 15) {
             const long long s2 = ((long long)vv * vv) >> 19;
             in1[buf][pos][row] = (uint8_t)(s2 < 127 ? s2 : 127);
@@ -784,7 +787,7 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
         }
         ps::wave_sync();
 #pragma unroll
-        for (int i = 0; i < 4; ++i) acc0[buf][(4 * kg + i) * 16 + row] = 0; // free for bucket bq + 2
+        for (int i = 0; i < 4; ++i) acc0[buf][(4 * kg + i) * AS + row] = 0; // free for bucket bq + 2
         const int4v zero = {0, 0, 0, 0};
         int4v wl = zero, wh = zero, a1 = zero;
         if (kg < 2) {
