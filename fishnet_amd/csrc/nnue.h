@@ -33,9 +33,10 @@ constexpr int CARRY_ROW0 = FT_ROWS;
 constexpr int KC_ROW0 = CARRY_ROW0 + 4 * CARRY_SLOTS;
 static_assert(KC_ROW0 + 128 * CARRY_SLOTS <= (1 << 19), "carry and king-cache rows must fit the 19-bit row field");
 // The planned expansion (stream.hip) gives each running workgroup a scratch slot of
-// SCR_ROWS rows from a pool of POOL_PER_XCD slots per XCD: 2 carry rows (one per
-// perspective) and 128 king-cache rows (perspective x king square).  The slots occupy
-// the same rows behind the FT rows as the carry / king-cache rows above.
+// SCR_ROWS rows from a pool of POOL_PER_XCD slots per XCD: rows 2 + 64 h + ksq are the
+// king-cache rows (perspective x king square); rows 0 and 1 are unused since its chained
+// walk carries the next parent in registers.  The slots occupy the same rows behind the
+// FT rows as the carry / king-cache rows above.
 constexpr int SCR_ROWS = 130;
 constexpr int POOL_PER_XCD = 256;
 constexpr int SCR_SLOTS = 8 * POOL_PER_XCD;
