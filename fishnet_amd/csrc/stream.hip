@@ -54,8 +54,18 @@
 #ifndef GN_PLAN_WPE
 #define GN_PLAN_WPE 4 // 128 VGPRs, no spills: 4 latency-bound plan waves per SIMD instead of 3
 #endif
+#ifndef GN_RING
+#define GN_RING 4 // row-ring depth of the stream (entries in flight per wave); 4 or 8
+#endif
 #ifndef GN_EXPAND_WPE
-#define GN_EXPAND_WPE 5
+#define GN_EXPAND_WPE (GN_RING == 4 ? 5 : 4)
+#endif
+#define GN_STR2(x) #x
+#define GN_STR(x) GN_STR2(x)
+#if GN_RING == 4
+#define GN_RING_WAIT 6 // the 3 later entries' 2 loads each
+#else
+#define GN_RING_WAIT 14
 #endif
 
 #ifdef GN_STREAM_PROF
@@ -398,7 +408,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
             if ((lane & 7) == 0) ksnap[w][kci][lane >> 3] = x;
             if (lane == 0) kstate[w][kci] = (uint8_t)(1 | hh << 1);
             uint32_t &sf = hh ? safe1 : safe0;
-            sf = b0 + (uint32_t)(pnd[hh] >= 0 ? pnd[hh] : P) + 4; // the store's index + 4
+            sf = b0 + (uint32_t)(pnd[hh] >= 0 ? pnd[hh] : P) + GN_RING; // the store's index + ring depth
           }
         }
         ps::wave_sync();
@@ -474,7 +484,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
         }
         if (kuse) { // this slot's last entry stores to scratch
           uint32_t &sf = g ? safe1 : safe0;
-          sf = base + (uint32_t)ne - 1 + 4;
+          sf = base + (uint32_t)ne - 1 + GN_RING;
         }
         if (g) len1 += (uint32_t)ne;
         else len0 += (uint32_t)ne;
@@ -581,18 +591,20 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
   // rows are loaded one group of 4 ahead of consumption, also across tile boundaries
   // (the next tile's first rows are in flight during this tile's layer stack).
   ushort8 pacc_lo = {}, pacc_hi = {}, base_lo = {}, base_hi = {};
-  ushort8 rlo[4], rhi[4];
-  uint32_t eh[4]; // hi words of the entries in flight
+  constexpr int RD = GN_RING;
+  static_assert(RD == 4 || RD == 8, "ring depth");
+  ushort8 rlo[RD], rhi[RD];
+  uint32_t eh[RD]; // hi words of the entries in flight
   uint32_t bq = 0; // buckets done (acc0 / in1 / fwd buffer parity)
-  typedef uint32_t u8e __attribute__((ext_vector_type(8), aligned(8)));
+  typedef uint32_t u8e __attribute__((ext_vector_type(2 * RD), aligned(8)));
   typedef const __attribute__((address_space(4))) u8e cu8e;
   typedef const __attribute__((address_space(4))) uint64_t cu64;
   cu64 *EL = (cu64 *)(HU ? ent + rend : ent + rbeg);
   // entries i .. i + 3 of this group's list by one s_load_dwordx8 (list 1 is stored
   // downward: its 4 entries arrive reversed, see elo / ehi)
-  auto group = [&](uint32_t i) -> u8e { return *(cu8e *)(HU ? EL - 4 - i : EL + i); };
-  auto elo = [&](const u8e v, int r) -> uint32_t { return HU ? v[2 * (3 - r)] : v[2 * r]; };
-  auto ehi = [&](const u8e v, int r) -> uint32_t { return HU ? v[2 * (3 - r) + 1] : v[2 * r + 1]; };
+  auto group = [&](uint32_t i) -> u8e { return *(cu8e *)(HU ? EL - RD - i : EL + i); };
+  auto elo = [&](const u8e v, int r) -> uint32_t { return HU ? v[2 * (RD - 1 - r)] : v[2 * r]; };
+  auto ehi = [&](const u8e v, int r) -> uint32_t { return HU ? v[2 * (RD - 1 - r) + 1] : v[2 * r + 1]; };
   int tl0 = tid;
   asm volatile("" : "+v"(tl0));
   const int jt = tl0 % G;
@@ -625,7 +637,9 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
   // entries of the last revolution and the earlier ones of this one were issued since); any
   // other memory operation in between (a drained store, the layer stack's loads) only makes
   // vmcnt(6) wait for more.  The "+v" ties the row registers to the wait: no use before it.
-  auto ring_wait = [&](int r) { asm volatile("s_waitcnt vmcnt(6)" : "+v"(rlo[r]), "+v"(rhi[r])); };
+  auto ring_wait = [&](int r) {
+    asm volatile("s_waitcnt vmcnt(" GN_STR(GN_RING_WAIT) ")" : "+v"(rlo[r]), "+v"(rhi[r]));
+  };
   ushort8 lo = {}, hi = {};
   auto consume = [&](int r) {
     ring_wait(r);
@@ -667,12 +681,12 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
     }
   };
   uint32_t pos = 0; // the next entry to consume: entries pos .. pos + 3 have their rows in flight
-  u8e gp = group(4); // the entries whose rows the next revolution issues (prefetched)
+  u8e gp = group(RD); // the entries whose rows the next revolution issues (prefetched)
   u8e gw;            // ... and this revolution's
   {
     const u8e g0 = group(0);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) issue(r, elo(g0, r), ehi(g0, r));
+    for (int r = 0; r < RD; ++r) issue(r, elo(g0, r), ehi(g0, r));
   }
 
   unsigned long long sp_s = 0, sp_w = 0, sp_l = 0, sp_m = 0, sp_n = 0;
@@ -701,20 +715,20 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
     // whose rows it issues, and prefetches the next); every step is guarded by uniform tests
 #pragma unroll 1
     while (pos < e_end) {
-      const uint32_t r0 = pos & 3;
+      const uint32_t r0 = pos & (RD - 1);
       if (r0 == 0) {
         // scalar loads complete out of order, so any use waits for all of them: wait once
         // here (lgkmcnt(0): the prefetch of the previous revolution), take this revolution's
         // entries, and only then prefetch the next group, which nothing uses before the next
         __builtin_amdgcn_s_waitcnt(0xC07F);
         gw = gp;
-        gp = group(pos + 8);
+        gp = group(pos + 2 * RD);
         consume(0), issue(0, elo(gw, 0), ehi(gw, 0));
         ++pos;
       }
-      if (r0 <= 1 && pos < e_end) consume(1), issue(1, elo(gw, 1), ehi(gw, 1)), ++pos;
-      if (r0 <= 2 && pos < e_end) consume(2), issue(2, elo(gw, 2), ehi(gw, 2)), ++pos;
-      if (pos < e_end) consume(3), issue(3, elo(gw, 3), ehi(gw, 3)), ++pos;
+#pragma unroll
+      for (int r = 1; r < RD; ++r)
+        if (r0 <= (uint32_t)r && pos < e_end) consume(r), issue(r, elo(gw, r), ehi(gw, r)), ++pos;
     }
     asm volatile("" ::: "memory");
     const unsigned long long t1 = SP_T();
@@ -861,12 +875,14 @@ hipError_t launch_plan_stream(const NetDevice &net, const gn_board *parents, siz
   const uint32_t nb = (uint32_t)(b1 - b0), B0 = (uint32_t)b0, B1 = (uint32_t)b1;
   const unsigned pg = (nb + 3) / 4, g = swz ? 8 * ((nb + 7) / 8) : nb;
   static const int ablate = getenv("GN_ABLATE") ? atoi(getenv("GN_ABLATE")) : 0; // timing diagnostics only
+  // timing diagnostics only: extra dynamic LDS per workgroup (fewer workgroups per CU)
+  static const size_t lds_pad = getenv("GN_STREAM_LDS_PAD") ? (size_t)atoi(getenv("GN_STREAM_LDS_PAD")) : 0;
   if (net.L1 == 3072) {
     hipLaunchKernelGGL((plan_kernel<3072>), dim3(pg), dim3(256), 0, s, net, parents, offsets, deltas, need_parent,
                        need_child, K > 1 ? next_slot : nullptr, (uint32_t)n, K, B0, B1, K > 1 ? kc : 0, eoff, ent,
                        tiles, btiles, rows_out, err);
     if (mid) (void)hipEventRecord(mid, s);
-    hipLaunchKernelGGL((stream_eval_kernel<3072>), dim3(g), dim3(384), 0, s, net, offsets, (uint32_t)n, K, B0, B1,
+    hipLaunchKernelGGL((stream_eval_kernel<3072>), dim3(g), dim3(384), lds_pad, s, net, offsets, (uint32_t)n, K, B0, B1,
                        swz, eoff, ent, tiles, btiles, order, out_parent, out_child, pool, scr, err, ablate);
   } else if (net.L1 == 1024) {
     hipLaunchKernelGGL((plan_kernel<1024>), dim3(pg), dim3(256), 0, s, net, parents, offsets, deltas, need_parent,
