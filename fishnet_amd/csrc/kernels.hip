@@ -1822,11 +1822,14 @@ hipError_t king_sort(const gn_board *boards, size_t n, uint64_t *keys, uint32_t 
 // XCD swizzle gives it a contiguous eighth of this order) gather from the same king-bucket
 // slices of the FT and share the XCD's L2.  keys: uint16 (wk << 6 | bk; 4095: invalid).
 __global__ void block_keys_kernel(const gn_board *__restrict__ parents, size_t n, uint32_t K, uint32_t nblk,
-                                  uint16_t *__restrict__ keys, uint32_t *__restrict__ idx) {
+                                  uint16_t *__restrict__ keys, uint32_t *__restrict__ idx, int mode) {
   const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= nblk) return;
   const size_t pb = (size_t)b * K, pe = pb + K < n ? pb + K : n;
-  const gn_board p = parents[pb + (pe - pb) / 2];
+  // which parent keys the block (diagnostics: GN_BLOCK_KEY 1 first, 2 three quarters, 3 one quarter)
+  const size_t at = mode == 1 ? pb : mode == 2 ? pb + 3 * (pe - pb) / 4 : mode == 3 ? pb + (pe - pb) / 4
+                                                                                    : pb + (pe - pb) / 2;
+  const gn_board p = parents[at];
   uint64_t wlo, whi;
   piece_words(p, wlo, whi);
   uint64_t o = p.occ;
@@ -1837,14 +1840,16 @@ __global__ void block_keys_kernel(const gn_board *__restrict__ parents, size_t n
     if (pc == make_piece(WHITE, KING)) wk = sq;
     if (pc == make_piece(BLACK, KING)) bk = sq;
   }
-  keys[b] = (uint16_t)(wk << 6 | bk);
+  keys[b] = (uint16_t)(mode == 4 ? bk << 6 | wk : wk << 6 | bk);
   idx[b] = b;
 }
 
 hipError_t block_order(const gn_board *parents, size_t n, uint32_t K, uint32_t nblk, uint16_t *keys, uint32_t *idx,
                        uint16_t *keys_out, uint32_t *order, void *&temp, size_t &temp_bytes, hipStream_t s) {
   if (!nblk) return hipSuccess;
-  hipLaunchKernelGGL(block_keys_kernel, dim3(blocks_for(nblk, 256)), dim3(256), 0, s, parents, n, K, nblk, keys, idx);
+  static const int mode = getenv("GN_BLOCK_KEY") ? atoi(getenv("GN_BLOCK_KEY")) : 0; // diagnostics
+  hipLaunchKernelGGL(block_keys_kernel, dim3(blocks_for(nblk, 256)), dim3(256), 0, s, parents, n, K, nblk, keys, idx,
+                     mode);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   size_t need = 0;
