@@ -196,6 +196,7 @@ struct Dev {
   DevBuf<uint32_t> off32;
   DevBuf<uint16_t> moves, moves_tmp; // moves_tmp: when the caller keeps no moves
   DevBuf<uint32_t> owner;             // parent of each child (write_children scratch)
+  DevBuf<Board> unpacked;             // the parents unpacked once (write_children scratch)
   DevBuf<ChildDelta> deltas;
   DevBuf<uint64_t> kkeys, kkeys2; // king-sort keys
   DevBuf<uint32_t> kidx, kperm;   // king-sort permutation
@@ -365,7 +366,7 @@ static void destroy(gn_ctx *ctx) {
     d.io_boards.release(), d.frontier[0].release(), d.frontier[1].release();
     d.io_out.release(), d.io_out2.release(), d.counts.release(), d.offsets.release();
     d.off32.release(), d.moves.release(), d.sum.release(), d.deltas.release();
-    d.moves_tmp.release(), d.owner.release();
+    d.moves_tmp.release(), d.owner.release(), d.unpacked.release();
     d.p_osm.release(), d.p_obg.release(), d.p_nsm.release(), d.p_nbg.release();
     if (d.scan_tmp) (void)hipFree(d.scan_tmp);
     if (d.sort_tmp) (void)hipFree(d.sort_tmp);
@@ -633,6 +634,7 @@ static int generate_children(Dev &d, const gn_board *parents, size_t n, gn_board
   }
   if (want_deltas) HIP_TRY(d.deltas.ensure(std::max<size_t>(t, 1)));
   HIP_TRY(d.owner.ensure(std::max<size_t>(t, 1)));
+  HIP_TRY(d.unpacked.ensure(std::max<size_t>(n, 1)));
   if (!moves) {
     HIP_TRY(d.moves_tmp.ensure(std::max<size_t>(t, 1)));
     moves = d.moves_tmp.p;
@@ -643,7 +645,7 @@ static int generate_children(Dev &d, const gn_board *parents, size_t n, gn_board
   } else if (t) {
     HIP_TRY(launch_write_children(parents, n, d.tables, d.offsets.p, 0, t, children, moves, d.owner.p,
                                   want_deltas ? d.deltas.p : nullptr, d.chain_k > 1 ? d.nslot.p : nullptr, d.chain_k,
-                                  rows, s));
+                                  rows, s, d.unpacked.p));
   }
   if (ev) HIP_TRY(hipEventRecord(ev[2], s));
   return GN_OK;
@@ -738,7 +740,7 @@ static int expand_evaluate(gn_ctx *ctx, Dev &d, const gn_board *parents, size_t 
           HIP_TRY(launch_write_children(parents + pa, pb - pa, d.tables, off + pa, d.cbound[c],
                                         d.cbound[c + 1] - d.cbound[c], d.dw_children, d.dw_moves, d.owner.p,
                                         d.deltas.p, d.chain_k > 1 ? d.nslot.p + pa : nullptr, d.chain_k, d.dw_rows,
-                                        sc));
+                                        sc, d.unpacked.p + pa));
         HIP_TRY(launch_plan_stream(d.net[BIG], parents, n, off, dl, f ? d.p_nbg.p : nullptr, f ? d.nbg.p : nullptr,
                                    d.p_obg.p, d.obg.p, ctx->swizzle & 1, d.chain_k > 1 ? d.nslot.p : nullptr,
                                    d.chain_k, ctx->king_cache ? 1 : 0, d.eoff.p, d.ent.p, d.tiles.p, d.btiles.p,

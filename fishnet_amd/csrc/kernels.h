@@ -93,10 +93,12 @@ hipError_t launch_count_children(const gn_board *boards, size_t n, const Tables 
 // children of every board at offsets[i] (exclusive prefix sums of counts): their moves,
 // owning board (owner, scratch) and, for children [c0, c0 + nc) (all children of these
 // boards), the child boards, deltas and chained-walk links.  moves / owner: required.
+// unpacked (optional, n entries): the boards unpacked once by the per-board pass, so that the
+// per-child pass reads its parent instead of unpacking it again.
 hipError_t launch_write_children(const gn_board *boards, size_t n, const Tables *tables, const uint64_t *offsets,
                                  size_t c0, size_t nc, gn_board *children, uint16_t *moves, uint32_t *owner,
                                  ChildDelta *deltas, uint8_t *next_slot, int chain_k, unsigned long long *rows,
-                                 hipStream_t s);
+                                 hipStream_t s, Board *unpacked = nullptr);
 // sum of legal-move counts over all boards into *total (added; caller zeroes)
 hipError_t launch_count_sum(const gn_board *boards, size_t n, const Tables *tables,
                             unsigned long long *total, hipStream_t s);

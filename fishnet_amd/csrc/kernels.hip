@@ -1548,7 +1548,7 @@ __device__ __forceinline__ bool same_placement(const gn_board &a, const gn_board
 __global__ void child_moves_kernel(const gn_board *__restrict__ boards, size_t n, const Tables *__restrict__ tables,
                                    const uint64_t *__restrict__ offsets, uint16_t *__restrict__ moves,
                                    uint32_t *__restrict__ owner, uint8_t *__restrict__ next_slot,
-                                   unsigned long long *__restrict__ rows) {
+                                   unsigned long long *__restrict__ rows, Board *__restrict__ unpacked) {
   __shared__ Tables T;
   load_tables(T, tables);
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1556,6 +1556,7 @@ __global__ void child_moves_kernel(const gn_board *__restrict__ boards, size_t n
   if (next_slot) next_slot[i] = 255; // child_boards_kernel overwrites it on a match
   Board B;
   if (!unpack(boards[i], B)) return;
+  if (unpacked) unpacked[i] = B; // for child_boards_kernel (a valid board has children only)
   uint64_t k = offsets[i];
   gen_legal(B, T, [&](uint16_t m) {
     moves[k] = m;
@@ -1571,13 +1572,15 @@ __global__ void child_boards_kernel(const gn_board *__restrict__ boards, size_t 
                                     const uint64_t *__restrict__ offsets, size_t c0, size_t nc,
                                     const uint16_t *__restrict__ moves, const uint32_t *__restrict__ owner,
                                     gn_board *__restrict__ children, ChildDelta *__restrict__ deltas,
-                                    uint8_t *__restrict__ next_slot, int chain_k, unsigned long long *__restrict__ rows) {
+                                    uint8_t *__restrict__ next_slot, int chain_k, unsigned long long *__restrict__ rows,
+                                    const Board *__restrict__ unpacked) {
   const size_t c = c0 + (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   unsigned long long nr = 0;
   if (c < c0 + nc) {
     const uint32_t i = owner[c];
     Board B;
-    unpack(boards[i], B); // valid: an invalid parent has no children
+    if (unpacked) B = unpacked[i]; // the siblings share it (one cache line run per parent)
+    else unpack(boards[i], B);     // valid: an invalid parent has no children
     Dirty d;
     const Board C = do_move(B, moves[c], &d);
     gn_board pb;
@@ -1749,14 +1752,14 @@ hipError_t launch_count_children(const gn_board *boards, size_t n, const Tables 
 hipError_t launch_write_children(const gn_board *boards, size_t n, const Tables *tables, const uint64_t *offsets,
                                  size_t c0, size_t nc, gn_board *children, uint16_t *moves, uint32_t *owner,
                                  ChildDelta *deltas, uint8_t *next_slot, int chain_k, unsigned long long *rows,
-                                 hipStream_t s) {
+                                 hipStream_t s, Board *unpacked) {
   if (!n) return hipSuccess;
   if (!moves || !owner) return hipErrorInvalidValue;
   hipLaunchKernelGGL(child_moves_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, boards, n, tables, offsets, moves,
-                     owner, next_slot, rows);
+                     owner, next_slot, rows, unpacked);
   if (nc)
     hipLaunchKernelGGL(child_boards_kernel, dim3(blocks_for(nc, 256)), dim3(256), 0, s, boards, n, offsets, c0, nc,
-                       moves, owner, children, deltas, next_slot, chain_k, rows);
+                       moves, owner, children, deltas, next_slot, chain_k, rows, unpacked);
   return hipGetLastError();
 }
 
