@@ -197,6 +197,7 @@ struct Dev {
   DevBuf<uint16_t> moves, moves_tmp; // moves_tmp: when the caller keeps no moves
   DevBuf<uint32_t> owner;             // parent of each child (write_children scratch)
   DevBuf<Board> unpacked;             // the parents unpacked once (write_children scratch)
+  const uint16_t *child_moves = nullptr; // the last generate_children's moves (finalize reads them)
   DevBuf<ChildDelta> deltas;
   DevBuf<uint64_t> kkeys, kkeys2; // king-sort keys
   DevBuf<uint32_t> kidx, kperm;   // king-sort permutation
@@ -562,8 +563,12 @@ static int finalize_range(gn_ctx *ctx, Dev &d, const gn_board *parents, const gn
                           hipStream_t s) {
   auto o = [](auto *p, size_t k) { return p ? p + k : p; };
   const gn_eval_params &P = ctx->P;
+  // children from their parents as write_children unpacked them (owner is relative to the
+  // range's first parent when the pipeline wrote the children range by range)
+  const bool fast = d.child_moves != nullptr;
   HIP_TRY(launch_finalize(children + ca, cb - ca, mode, o(d.osm.p, ca), o(d.obg.p, ca), o(d.nsm.p, ca), o(d.nbg.p, ca),
-                          P, d.tables, child_out + ca, s));
+                          P, d.tables, child_out + ca, s, fast ? d.owner.p + ca : nullptr,
+                          fast ? d.child_moves + ca : nullptr, fast ? d.unpacked.p + (d.defer_write ? pa : 0) : nullptr));
   if (parent_out)
     HIP_TRY(launch_finalize(parents + pa, pb - pa, mode, o(d.p_osm.p, pa), o(d.p_obg.p, pa), o(d.p_nsm.p, pa),
                             o(d.p_nbg.p, pa), P, d.tables, parent_out + pa, s));
@@ -639,6 +644,7 @@ static int generate_children(Dev &d, const gn_board *parents, size_t n, gn_board
     HIP_TRY(d.moves_tmp.ensure(std::max<size_t>(t, 1)));
     moves = d.moves_tmp.p;
   }
+  d.child_moves = moves;
   if (d.planned && defer && t && expand_chunks((n + d.chain_k - 1) / std::max(1, d.chain_k)) > 1) {
     // expand_evaluate writes the children range by range, in its pipeline
     d.defer_write = true, d.dw_children = children, d.dw_moves = moves, d.dw_rows = rows;

@@ -83,9 +83,13 @@ hipError_t launch_classify(const gn_board *boards, size_t n, const gn_eval_param
 hipError_t launch_reeval(const int2 *out_small, const uint8_t *need_small, size_t n, const gn_eval_params &P,
                          uint8_t *need_big, hipStream_t s);
 // Eval::evaluate epilogue -> gn_eval (flags incl. IN_CHECK / BAD_FEN).
+// owner / moves / unpacked (optional, children only): board i is unpacked[owner[i]] after
+// moves[i] (the parents write_children unpacked), instead of unpacking boards[i].
 hipError_t launch_finalize(const gn_board *boards, size_t n, int mode, const int2 *out_small,
                            const int2 *out_big, const uint8_t *need_small, const uint8_t *need_big,
-                           const gn_eval_params &P, const Tables *tables, gn_eval *out, hipStream_t s);
+                           const gn_eval_params &P, const Tables *tables, gn_eval *out, hipStream_t s,
+                           const uint32_t *owner = nullptr, const uint16_t *moves = nullptr,
+                           const Board *unpacked = nullptr);
 // legal-move counts per board (invalid boards: 0); ebound (optional): per parent an
 // upper bound of the planned expansion's list entries (stream.hip)
 hipError_t launch_count_children(const gn_board *boards, size_t n, const Tables *tables, uint64_t *counts,

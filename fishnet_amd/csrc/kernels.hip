@@ -1439,14 +1439,18 @@ __global__ void reeval_kernel(const int2 *__restrict__ out_small, const uint8_t 
 __global__ void finalize_kernel(const gn_board *__restrict__ boards, size_t n, int mode,
                                 const int2 *__restrict__ out_small, const int2 *__restrict__ out_big,
                                 const uint8_t *__restrict__ need_small, const uint8_t *__restrict__ need_big,
-                                gn_eval_params P, const Tables *__restrict__ tables, gn_eval *__restrict__ out) {
+                                gn_eval_params P, const Tables *__restrict__ tables, gn_eval *__restrict__ out,
+                                const uint32_t *__restrict__ owner, const uint16_t *__restrict__ moves,
+                                const Board *__restrict__ unpacked) {
   __shared__ Tables T;
   load_tables(T, tables);
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   Board B;
   gn_eval e = {0, 0, 0, 0};
-  if (!unpack(boards[i], B)) {
+  if (unpacked) {
+    B = do_move(unpacked[owner[i]], moves[i], nullptr); // a legal child of a valid parent
+  } else if (!unpack(boards[i], B)) {
     e.flags = GN_FLAG_BAD_FEN;
     out[i] = e;
     return;
@@ -1498,10 +1502,11 @@ hipError_t launch_reeval(const int2 *out_small, const uint8_t *need_small, size_
 
 hipError_t launch_finalize(const gn_board *boards, size_t n, int mode, const int2 *out_small, const int2 *out_big,
                            const uint8_t *need_small, const uint8_t *need_big, const gn_eval_params &P,
-                           const Tables *tables, gn_eval *out, hipStream_t s) {
+                           const Tables *tables, gn_eval *out, hipStream_t s, const uint32_t *owner,
+                           const uint16_t *moves, const Board *unpacked) {
   if (!n) return hipSuccess;
   hipLaunchKernelGGL(finalize_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, boards, n, mode, out_small, out_big,
-                     need_small, need_big, P, tables, out);
+                     need_small, need_big, P, tables, out, owner, moves, unpacked);
   return hipGetLastError();
 }
 
