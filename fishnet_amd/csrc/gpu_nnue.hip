@@ -633,7 +633,10 @@ static int generate_children(Dev &d, const gn_board *parents, size_t n, gn_board
   if ((children_or_null || moves) && t > cap) // caller-owned child buffers hold cap entries
     return fail(GN_E_CAPACITY, "%zu children exceed capacity %zu", (size_t)t, cap);
   gn_board *children = children_or_null;
-  if (!children) {
+  // the planned big-net path reads no child board after this (finalize makes each child from
+  // its unpacked parent and move): library-internal boards are then not written at all
+  const bool skip_boards = !children_or_null && d.planned && defer;
+  if (!children && !skip_boards) {
     HIP_TRY(d.frontier[1].ensure(std::max<size_t>(t, 1)));
     children = d.frontier[1].p;
   }

@@ -1588,9 +1588,12 @@ __global__ void child_boards_kernel(const gn_board *__restrict__ boards, size_t 
     else unpack(boards[i], B);     // valid: an invalid parent has no children
     Dirty d;
     const Board C = do_move(B, moves[c], &d);
+    // the packed child: stored when the caller keeps the boards (children != NULL), and
+    // compared with the next board when its occupancy matches (the chained walk's link)
+    const bool link = next_slot && (size_t)i + 1 < n && C.byType[0] == boards[i + 1].occ;
     gn_board pb;
-    pack(C, pb);
-    children[c] = pb;
+    if (children || link) pack(C, pb);
+    if (children) children[c] = pb;
     if (deltas) deltas[c] = make_child_delta(B, C, d);
     // per child either the delta rows or a refresh of the perspective whose king moved
     nr = d.king_moved ? popcnt(C.byType[0]) + d.n_rem + d.n_add : 2 * (d.n_rem + d.n_add);
@@ -1598,7 +1601,7 @@ __global__ void child_boards_kernel(const gn_board *__restrict__ boards, size_t 
     // no two legal moves give one placement); the chained walk then starts parent i + 1
     // from that child's accumulators, gathering one carry row per perspective instead of
     // its refresh
-    if (next_slot && (size_t)i + 1 < n) {
+    if (link) {
       const gn_board nb = boards[i + 1];
       if (same_placement(pb, nb)) {
         next_slot[i] = (uint8_t)(c - offsets[i]);
