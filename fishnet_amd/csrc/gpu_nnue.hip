@@ -58,7 +58,7 @@ const Tables &host_tables() {
 struct HostNet {
   int L1 = 0;
   uint32_t hash = 0;
-  std::vector<uint8_t> ft;    // [22528][2*L1 + 32]
+  std::vector<uint8_t> ft;    // [22528][ft_row_stride(L1)]
   std::vector<int16_t> bias;  // [L1], doubled
   std::vector<int8_t> w0, w1, w2;
   std::vector<int32_t> b0, b1, b2;
@@ -121,7 +121,7 @@ static int parse_net(const uint8_t *data, size_t len, HostNet &h) {
   if (l1 != 3072 && l1 != 1024 && l1 != 128) return fail(GN_E_FORMAT, "unsupported L1 width %d", l1);
   h.L1 = l1;
   h.hash = hash;
-  const size_t RS = 2 * (size_t)l1 + 32;
+  const size_t RS = ft_row_stride((uint32_t)l1);
   h.ft.assign((size_t)FT_ROWS * RS, 0);
   h.bias.resize(l1);
   uint8_t *ft = h.ft.data();
@@ -315,7 +315,7 @@ static gn_eval_params default_params() {
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 static int upload_net(Dev &d, int which, const HostNet &h) {
-  const size_t RS = 2 * (size_t)h.L1 + 32;
+  const size_t RS = ft_row_stride((uint32_t)h.L1);
   size_t off[9], o = 0;
   const int carry = h.L1 == 128 ? 0 : CARRY_SLOTS; // the chained walk's scratch rows
   // the PSQT weights once more as [bucket][row] (721 KB: L2-resident for the plan kernel's

@@ -174,7 +174,7 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR) __attribute__((amdgpu_wav
   constexpr int NW = NT / 64;
   constexpr int TILE = 16;
   constexpr int XS = L1 + 16; // padded LDS row: conflict-free ds_read_b128 across 16 rows
-  constexpr uint32_t RS = 2 * L1 + 32;
+  constexpr uint32_t RS = ft_row_stride(L1);
   static_assert(NT % 64 == 0 && TILE % PAR == 0, "geometry");
 
   // LDS: big net 53.2 KB -> 3 workgroups (18 waves) per CU.  The feature list
@@ -387,7 +387,7 @@ template <int L1, bool U>
 __device__ __forceinline__ void run_rows(const uint8_t *__restrict__ ft, uint32_t j16, const uint16_t *rr, int k,
                                          int ns, int n, bool psl, uint32_t psb, bool save, ushort8 &base_lo,
                                          ushort8 &base_hi, ushort8 &lo, ushort8 &hi, uint32_t &ps) {
-  constexpr uint32_t RS = 2 * L1 + 32;
+  constexpr uint32_t RS = ft_row_stride(L1);
 #pragma unroll 1
   for (; k < n; k += 4) {
     ushort8 a0, a1, a2, a3, b0, b1, b2, b3;
@@ -437,7 +437,7 @@ __device__ __forceinline__ void run_rows_u(const uint8_t *__restrict__ ft, uint3
                                            uint32_t r01, uint32_t r23, int k, int ns, int n, bool psl, uint32_t psb,
                                            bool save, ushort8 &base_lo, ushort8 &base_hi, ushort8 &lo, ushort8 &hi,
                                            uint32_t &ps, int lane) {
-  constexpr uint32_t RS = 2 * L1 + 32;
+  constexpr uint32_t RS = ft_row_stride(L1);
   const uint32_t rl = n > 4 && lane < n ? rr[lane] : 0u;
   auto off = [&](int e) -> uint32_t {
     uint32_t v = e == 0 ? (r01 & 0xFFFF) : e == 1 ? (r01 >> 16) : e == 2 ? (r23 & 0xFFFF) : e == 3 ? (r23 >> 16) : 0u;
@@ -513,7 +513,7 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR) __attribute__((amdgpu_wav
   constexpr int NW = NT / 64;
   constexpr int TILE = 16;
   constexpr int XS = L1 + 16;
-  constexpr uint32_t RS = 2 * L1 + 32;
+  constexpr uint32_t RS = ft_row_stride(L1);
   constexpr int ROWS_BYTES = TILE * 2 * 32 * 2;
   constexpr int SCRATCH = ROWS_BYTES > LS_SCRATCH ? ROWS_BYTES : LS_SCRATCH;
   constexpr int PACC = PAR > 1 ? 2 * L1 : 8; // shared parent accumulators (small net only)
@@ -834,7 +834,7 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
   constexpr int NW = NT / 64;
   constexpr int TILE = 16;
   constexpr int XS = L1 + 16;
-  constexpr uint32_t RS = 2 * L1 + 32;
+  constexpr uint32_t RS = ft_row_stride(L1);
   constexpr int CAP = 256;         // row entries per list and tile
   constexpr int FILL = CAP - 8;    // content limit: padding to 4 + 4 run-ahead entries
   constexpr int NLS = NW >= 4 ? 2 : 1; // layer-stack waves: the last NLS waves

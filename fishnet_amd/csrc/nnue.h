@@ -2,10 +2,11 @@
 // libgpu_nnue, shared between the host loader and the kernels.
 //
 // HBM layout of one network (all arrays 256-B aligned):
-//   ft      [22528 + 1][RS] bytes, RS = 2*L1 + 32: one feature's row is the L1
-//           int16 feature-transformer weights (doubled at load, as Stockfish
-//           scale_weights does) followed by its 8 int32 PSQT weights, so one
-//           gathered feature = one contiguous row (6,176 B big / 288 B small).
+//   ft      [22528 + 1][RS] bytes, RS = 2*L1 + 32 rounded up to 128: one feature's
+//           row is the L1 int16 feature-transformer weights (doubled at load, as
+//           Stockfish scale_weights does) followed by its 8 int32 PSQT weights, so
+//           one gathered feature = one contiguous row (6,272 B big / 384 B small;
+//           the 128-B start keeps the L1 weights on 48 whole lines, not 49).
 //           Row FT_BIAS_ROW (the extra last row) is the bias with zero PSQT, so
 //           a refresh is "zero + bias row + feature rows" in one row stream.
 //   bias    [L1] int16 (doubled)
@@ -23,6 +24,12 @@ namespace gn {
 constexpr int FT_INPUTS = 22528;
 constexpr int FT_BIAS_ROW = FT_INPUTS; // see the layout above
 constexpr int FT_ROWS = FT_INPUTS + 1;
+// FT row stride in bytes: 2*L1 + 32 rounded up to GN_ROW_ALIGN (a 128-B multiple keeps a
+// row's L1 weights on whole 128-B lines)
+#ifndef GN_ROW_ALIGN
+#define GN_ROW_ALIGN 128
+#endif
+constexpr uint32_t ft_row_stride(uint32_t l1) { return (2 * l1 + 32 + GN_ROW_ALIGN - 1) / GN_ROW_ALIGN * GN_ROW_ALIGN; }
 // Big nets: CARRY_SLOTS x 4 scratch rows follow the FT rows in the same allocation
 // (the expansion's chained walk, kernels.hip expand_stream): slot = dispatch index
 // mod CARRY_SLOTS, rows = parity of the parent x perspective.  Row indices stay

@@ -90,7 +90,7 @@ constexpr uint32_t H_PRE = 1u << 16, H_INIT_SH = 17, H_LAST = 1u << 19, H_SLOT_S
                    H_PAR_E = 1u << 25, H_KST = 1u << 27, H_SCR = 1u << 31;
 template <int L1>
 __device__ __forceinline__ uint64_t enc64(uint32_t e) {
-  constexpr uint32_t RS = 2 * L1 + 32;
+  constexpr uint32_t RS = ft_row_stride(L1);
   const uint32_t row = e & ROW, init = (e >> 20) & 3, sub = e & SUB;
   const bool keep = init == 1 && sub; // ZERO | SUB: no init, no row (padding, store-only entries)
   // a store-only KST entry loads the zero row and carries its target (a scratch row) as its
@@ -515,7 +515,7 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
   using namespace ps;
   constexpr int G = L1 / 16; // threads per perspective group (whole waves)
   constexpr int NT = 2 * G, NW = NT / 64, TILE = 16, XS = L1 + 16, KS = L1 / 64, KPW = KS / NW;
-  constexpr uint32_t RS = 2 * L1 + 32;
+  constexpr uint32_t RS = ft_row_stride(L1);
   static_assert(G % 64 == 0 && KS % NW == 0 && KPW % 2 == 0, "geometry");
   __shared__ __attribute__((aligned(16))) uint8_t xt[TILE * XS];
   // fc_0 partial sums [position][output], rows padded to 20 dwords: the 4 lane groups of an
