@@ -203,7 +203,7 @@ class Ctx:
 def run_eval(c: Ctx, wl: dict, n: int, steps: int, warmup: int, max_plies: int, check: int):
     """Full-refresh batch evaluation of n device-resident positions per GPU."""
     G, nn, mode = c.G, c.nn, wl["mode"]
-    d_b, d_o = nn.alloc(n * 32), nn.alloc(n * 16)
+    d_b, d_o = nn.alloc(n * 32), nn.alloc(n * G.EVAL_SIZE)
     t = time.perf_counter()
     first, _ = c.shard(n)
     nn.random_positions_device(SEED, first, n, max_plies, d_b)
@@ -218,7 +218,7 @@ def run_eval(c: Ctx, wl: dict, n: int, steps: int, warmup: int, max_plies: int, 
     c.barrier_sync()
     wall = c.comm.max(time.perf_counter() - t0)
     out, boards = d_o.download(G.EVAL_DTYPE, n), d_b.download(G.BOARD_DTYPE, n)
-    checksum = nn.checksum_device(d_o, n * 16)
+    checksum = nn.checksum_device(d_o, n * G.EVAL_SIZE)
     d_b.free(), d_o.free()
     pieces = popcounts(boards["occ"])
     alg = rows * (2 * wl["l1"] + 4) + n * 40
@@ -249,8 +249,8 @@ def run_expand(c: Ctx, wl: dict, games: int, steps: int, warmup: int, check: int
     gen_s = time.perf_counter() - t
     # one untimed expansion sizes the output buffers (and warms up); then W warmup steps
     _, total, _, _ = nn.time_expand_device(d_p, n, mode, 1)
-    out = {"po": nn.alloc(n * 16), "off": nn.alloc((n + 1) * 4), "mv": nn.alloc(max(total, 1) * 2),
-           "co": nn.alloc(max(total, 1) * 16), "cap": total}
+    out = {"po": nn.alloc(n * G.EVAL_SIZE), "off": nn.alloc((n + 1) * 4), "mv": nn.alloc(max(total, 1) * 2),
+           "co": nn.alloc(max(total, 1) * G.EVAL_SIZE), "cap": total}
     if warmup:
         nn.time_expand_device(d_p, n, mode, warmup, outputs=out)
     c.barrier_sync()
@@ -263,7 +263,7 @@ def run_expand(c: Ctx, wl: dict, games: int, steps: int, warmup: int, check: int
     # timed region): the roofline's dominant kernel is stream_eval_kernel alone
     plan_ms, stream_ms = nn.get_option(G.STAT_PLAN_NS) / 1e6, nn.get_option(G.STAT_STREAM_NS) / 1e6
     parents = d_p.download(G.BOARD_DTYPE, n)
-    sums = (nn.checksum_device(out["po"], n * 16), nn.checksum_device(out["co"], children * 16),
+    sums = (nn.checksum_device(out["po"], n * G.EVAL_SIZE), nn.checksum_device(out["co"], children * G.EVAL_SIZE),
             nn.checksum_device(out["mv"], children * 2), nn.checksum_device(out["off"], (n + 1) * 4))
     planned = stream_ms > 0
     r = dict(value=c.world * (n + children) * steps / wall, wall=wall, stage=stage,
@@ -308,7 +308,7 @@ def run_expand(c: Ctx, wl: dict, games: int, steps: int, warmup: int, check: int
         finally:
             nn.set_option(G.OPT_CHAIN, opts[0])
             nn.set_option(G.OPT_KING_CACHE, opts[1])
-        ref = (nn.checksum_device(out["po"], n * 16), nn.checksum_device(out["co"], t2 * 16),
+        ref = (nn.checksum_device(out["po"], n * G.EVAL_SIZE), nn.checksum_device(out["co"], t2 * G.EVAL_SIZE),
                nn.checksum_device(out["mv"], t2 * 2), nn.checksum_device(out["off"], (n + 1) * 4))
         ver["vs_plain_path"] = {"equal": bool(ref == sums and t2 == children), "parents": n, "children": children,
                                 "checksum_timed": f"{sums[0] ^ sums[1]:016x}",
@@ -330,7 +330,7 @@ def run_expand2(c: Ctx, games: int, mode: int, steps: int, check: int):
     first, _ = c.shard(games)
     nn.random_games_device(SEED + 2, first, games, PLIES, d_p)
     nn.synchronize()
-    out = {"po": nn.alloc(n * 16), "off": nn.alloc((n + 1) * 4), "cap": 0, "gcap": 0}
+    out = {"po": nn.alloc(n * G.EVAL_SIZE), "off": nn.alloc((n + 1) * 4), "cap": 0, "gcap": 0}
     for _ in range(3):  # sized by the library's own capacity replies (also the warmup)
         try:
             t, g = nn.expand2_device(d_p, n, mode, out)
@@ -340,9 +340,9 @@ def run_expand2(c: Ctx, games: int, mode: int, steps: int, check: int):
                 raise
             t, g = e.need
             if t > out["cap"]:
-                out.update(cap=t, ch=nn.alloc(t * 32), mv=nn.alloc(t * 2), co=nn.alloc(t * 16), goff=nn.alloc((t + 1) * 4))
+                out.update(cap=t, ch=nn.alloc(t * 32), mv=nn.alloc(t * 2), co=nn.alloc(t * G.EVAL_SIZE), goff=nn.alloc((t + 1) * 4))
             if g > out["gcap"]:
-                out.update(gcap=g, gmv=nn.alloc(max(g, 1) * 2), gco=nn.alloc(max(g, 1) * 16))
+                out.update(gcap=g, gmv=nn.alloc(max(g, 1) * 2), gco=nn.alloc(max(g, 1) * G.EVAL_SIZE))
     c.barrier_sync()
     t0 = time.perf_counter()
     for _ in range(steps):
@@ -368,7 +368,9 @@ def run_expand2(c: Ctx, games: int, mode: int, steps: int, check: int):
             mv = out["gmv"].download(np.uint16, hi - lo, offset=lo)
             ev = out["gco"].download(G.EVAL_DTYPE, hi - lo, offset=lo)
             p_exp, m_exp, k_exp = O.expand_eval(big, small, fens[k], mode, incremental=True)
-            return int(tuple(co[j]) != p_exp or dict(zip(mv.tolist(), map(tuple, ev.tolist()))) !=
+            # (co[j] is a child record, p_exp the same position scored: compare the static part)
+            static = lambda t: tuple(t)[:4] + (int(tuple(t)[5]) & 15,)
+            return int(static(co[j]) != static(p_exp) or dict(zip(mv.tolist(), map(tuple, ev.tolist()))) !=
                        dict(zip(m_exp, map(tuple, k_exp.tolist())))), hi - lo
 
         with cf.ThreadPoolExecutor(host_threads()) as ex:

@@ -15,6 +15,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "../../include/gpu_nnue.h"
 
 #define GN_HD __host__ __device__ __forceinline__
@@ -259,6 +261,21 @@ GN_HD int move_to(uint16_t m) { return m & 63; }
 GN_HD int move_type(uint16_t m) { return m >> 14; }
 GN_HD int move_promo(uint16_t m) { return ((m >> 12) & 3) + KNIGHT; }
 
+// emit(m) of gen_legal returns void, or bool: true stops the generation (any_legal)
+template <class F>
+GN_HD bool emit_stop(F &emit, uint16_t m) {
+  if constexpr (std::is_void<decltype(emit(m))>::value) {
+    emit(m);
+    return false;
+  } else {
+    return emit(m);
+  }
+}
+#define GN_EMIT(m)                                                                                  \
+  do {                                                                                              \
+    if (emit_stop(emit, (m))) return;                                                               \
+  } while (0)
+
 // Legal move generator.  emit(uint16_t move) is called once per legal move,
 // in a fixed order (king, knights, sliders, pawns, castling).
 template <class F>
@@ -272,7 +289,7 @@ GN_HD void gen_legal(const Board &B, const Tables &T, F &&emit) {
     Bitboard tg = T.king[ksq] & ~ours, occ_nok = occ ^ sqbb(ksq);
     while (tg) {
       int to = pop_lsb(tg);
-      if (!(attackers_to(B, T, to, occ_nok) & theirs)) emit(make_move(ksq, to));
+      if (!(attackers_to(B, T, to, occ_nok) & theirs)) GN_EMIT(make_move(ksq, to));
     }
   }
   if (checkers & (checkers - 1)) return; // double check: king moves only
@@ -294,7 +311,7 @@ GN_HD void gen_legal(const Board &B, const Tables &T, F &&emit) {
     while (pcs) {
       int from = pop_lsb(pcs);
       Bitboard tg = T.knight[from] & target;
-      while (tg) emit(make_move(from, pop_lsb(tg)));
+      while (tg) GN_EMIT(make_move(from, pop_lsb(tg)));
     }
   }
   // sliders
@@ -307,7 +324,7 @@ GN_HD void gen_legal(const Board &B, const Tables &T, F &&emit) {
       if (f & (B.byType[BISHOP] | B.byType[QUEEN])) att |= bishop_attacks(T, from, occ);
       att &= target;
       if (pinned & f) att &= line_through(T, ksq, from);
-      while (att) emit(make_move(from, pop_lsb(att)));
+      while (att) GN_EMIT(make_move(from, pop_lsb(att)));
     }
   }
   // pawns
@@ -330,12 +347,12 @@ GN_HD void gen_legal(const Board &B, const Tables &T, F &&emit) {
       while (tg) {
         int to = pop_lsb(tg);
         if (sqbb(to) & last) {
-          emit(make_move(from, to, MT_PROMOTION, QUEEN));
-          emit(make_move(from, to, MT_PROMOTION, ROOK));
-          emit(make_move(from, to, MT_PROMOTION, BISHOP));
-          emit(make_move(from, to, MT_PROMOTION, KNIGHT));
+          GN_EMIT(make_move(from, to, MT_PROMOTION, QUEEN));
+          GN_EMIT(make_move(from, to, MT_PROMOTION, ROOK));
+          GN_EMIT(make_move(from, to, MT_PROMOTION, BISHOP));
+          GN_EMIT(make_move(from, to, MT_PROMOTION, KNIGHT));
         } else
-          emit(make_move(from, to));
+          GN_EMIT(make_move(from, to));
       }
       if (B.ep != SQ_NONE && (T.pawn[us][from] & sqbb(B.ep))) {
         // full simulation: removes both pawns, adds ours on ep, recomputes attackers
@@ -346,7 +363,7 @@ GN_HD void gen_legal(const Board &B, const Tables &T, F &&emit) {
                         (bishop_attacks(T, ksq, occ2) & (B.byType[BISHOP] | B.byType[QUEEN])) |
                         (T.knight[ksq] & B.byType[KNIGHT]) | (T.pawn[us][ksq] & B.byType[PAWN])) &
                        th2;
-        if (!att) emit(make_move(from, B.ep, MT_EN_PASSANT));
+        if (!att) GN_EMIT(make_move(from, B.ep, MT_EN_PASSANT));
       }
     }
   }
@@ -369,7 +386,7 @@ GN_HD void gen_legal(const Board &B, const Tables &T, F &&emit) {
                      (bishop_attacks(T, kto, occ2) & (B.byType[BISHOP] | B.byType[QUEEN]))) &
                     theirs;
       if (sl) continue;
-      emit(make_move(ksq, rsq, MT_CASTLING));
+      GN_EMIT(make_move(ksq, rsq, MT_CASTLING));
     }
   }
 }
@@ -479,6 +496,16 @@ GN_HD Board start_position() {
   B.castle_rook[0] = 7, B.castle_rook[1] = 0, B.castle_rook[2] = 63, B.castle_rook[3] = 56;
   B.rule50 = 0, B.fullmove = 1;
   return B;
+}
+
+// any legal move (stalemate / checkmate detection): stops at the first one
+GN_HD bool any_legal(const Board &B, const Tables &T) {
+  bool any = false;
+  gen_legal(B, T, [&](uint16_t) {
+    any = true;
+    return true;
+  });
+  return any;
 }
 
 GN_HD int count_legal(const Board &B, const Tables &T) {

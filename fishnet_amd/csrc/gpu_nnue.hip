@@ -239,6 +239,20 @@ struct Dev {
   uint16_t *dw_moves = nullptr;
   unsigned long long *dw_rows = nullptr;
   float plan_ms = 0, stream_ms = 0; // the last timed planned expansion (GN_STAT_PLAN_NS / _STREAM_NS)
+  // the score rule's two levels of in-check replies (resolve_scores): selection, the selected
+  // positions, their replies and the replies' records / rule values
+  struct ScoreLevel {
+    DevBuf<uint64_t> sel, pos, counts, offsets;
+    DevBuf<uint32_t> idx, owner;
+    DevBuf<gn_board> boards, children;
+    DevBuf<uint16_t> moves;
+    DevBuf<gn_eval> ce;
+    DevBuf<int32_t> sv;
+    void release() {
+      sel.release(), pos.release(), counts.release(), offsets.release(), idx.release(), owner.release();
+      boards.release(), children.release(), moves.release(), ce.release(), sv.release();
+    }
+  } lv[2];
   static constexpr size_t MAX_CHUNKS = 4;
   uint64_t cbound[MAX_CHUNKS + 1] = {}; // children offsets at the range boundaries
   std::mutex mu;
@@ -375,6 +389,7 @@ static void destroy(gn_ctx *ctx) {
     d.nslot.release(), d.tickets.release(), d.ksnap.release();
     d.ebound.release(), d.eoff.release(), d.ent.release(), d.pool.release(), d.perr.release(), d.tiles.release(), d.btiles.release();
     d.bkeys.release(), d.bkeys2.release(), d.bidx.release(), d.border.release();
+    d.lv[0].release(), d.lv[1].release();
     for (int i = 0; i < 2; ++i) {
       if (d.aux[i]) (void)hipStreamSynchronize(d.aux[i]), (void)hipStreamDestroy(d.aux[i]);
       if (d.join[i]) (void)hipEventDestroy(d.join[i]);
@@ -457,8 +472,11 @@ struct KernelTimes {
 
 // Launch sequence of one evaluation.  ev (optional) = 5 events recorded between
 // the stages [classify(+)] [small net (+reeval)] [big net] [finalize].
+// score: the records are positions (the score rule's static part; resolve_scores does the
+// in-check ones) rather than child records; counts (optional): their legal-move counts.
 static int evaluate_on(gn_ctx *ctx, Dev &d, const gn_board *b, size_t n, int mode, gn_eval *out, hipStream_t s,
-                       hipEvent_t *ev, unsigned long long *rows_out = nullptr) {
+                       hipEvent_t *ev, unsigned long long *rows_out = nullptr, int score = 1,
+                       const uint64_t *counts = nullptr) {
   if (mode < GN_MODE_FULL || mode > GN_MODE_SMALL) return fail(GN_E_INVALID, "bad mode %d", mode);
   if ((mode != GN_MODE_SMALL && !d.has[BIG]) || (mode != GN_MODE_BIG && !d.has[SMALL]))
     return fail(GN_E_NONET, "mode %d needs a network that is not loaded", mode);
@@ -495,7 +513,7 @@ static int evaluate_on(gn_ctx *ctx, Dev &d, const gn_board *b, size_t n, int mod
     HIP_TRY(launch_eval_net(d.net[BIG], b, mode == GN_MODE_FULL ? d.nbg.p : nullptr, n, d.obg.p, perm, swz, s,
                             rows_out));
   HIP_TRY(mark(3));
-  HIP_TRY(launch_finalize(b, n, mode, d.osm.p, d.obg.p, d.nsm.p, d.nbg.p, P, d.tables, out, s));
+  HIP_TRY(launch_finalize(b, n, mode, d.osm.p, d.obg.p, d.nsm.p, d.nbg.p, P, d.tables, out, s, score, counts));
   HIP_TRY(mark(4));
   return GN_OK;
 }
@@ -558,20 +576,22 @@ static size_t expand_chunks(size_t nblk) {
 }
 
 // finalize of parents [pa, pb) and children [ca, cb) (their net outputs in the Dev buffers)
+// (score_parents: the parents are positions with the score rule; the children are child records)
 static int finalize_range(gn_ctx *ctx, Dev &d, const gn_board *parents, const gn_board *children, int mode,
                           gn_eval *parent_out, gn_eval *child_out, size_t pa, size_t pb, size_t ca, size_t cb,
-                          hipStream_t s) {
+                          hipStream_t s, bool score_parents) {
   auto o = [](auto *p, size_t k) { return p ? p + k : p; };
   const gn_eval_params &P = ctx->P;
   // children from their parents as write_children unpacked them (owner is relative to the
   // range's first parent when the pipeline wrote the children range by range)
   const bool fast = d.child_moves != nullptr;
   HIP_TRY(launch_finalize(children + ca, cb - ca, mode, o(d.osm.p, ca), o(d.obg.p, ca), o(d.nsm.p, ca), o(d.nbg.p, ca),
-                          P, d.tables, child_out + ca, s, fast ? d.owner.p + ca : nullptr,
+                          P, d.tables, child_out + ca, s, 0, nullptr, fast ? d.owner.p + ca : nullptr,
                           fast ? d.child_moves + ca : nullptr, fast ? d.unpacked.p + (d.defer_write ? pa : 0) : nullptr));
-  if (parent_out)
+  if (parent_out) // the parents' legal-move counts are generate_children's
     HIP_TRY(launch_finalize(parents + pa, pb - pa, mode, o(d.p_osm.p, pa), o(d.p_obg.p, pa), o(d.p_nsm.p, pa),
-                            o(d.p_nbg.p, pa), P, d.tables, parent_out + pa, s));
+                            o(d.p_nbg.p, pa), P, d.tables, parent_out + pa, s, score_parents ? 1 : 0,
+                            d.counts.p + pa));
   return GN_OK;
 }
 
@@ -666,18 +686,22 @@ static int generate_children(Dev &d, const gn_board *parents, size_t n, gn_board
 // ev (optional) gets 5 events: after classify, after the small net (+reeval),
 // after the big net, after finalize, and (planned path) between its plan and stream
 // kernels (recorded before the pipeline when it runs in several ranges).
+// score_parents: the parents are positions (the score rule's static part; callers run
+// resolve_scores on them) rather than child records (depth 2's level 2).
 static int expand_evaluate(gn_ctx *ctx, Dev &d, const gn_board *parents, size_t n, const gn_board *children,
                            size_t total, int mode, gn_eval *parent_out, gn_eval *child_out, hipStream_t s,
-                           hipEvent_t *ev, unsigned long long *rows_out = nullptr) {
+                           hipEvent_t *ev, unsigned long long *rows_out = nullptr, bool score_parents = true) {
   if (mode < GN_MODE_FULL || mode > GN_MODE_SMALL) return fail(GN_E_INVALID, "bad mode %d", mode);
   if ((mode != GN_MODE_SMALL && !d.has[BIG]) || (mode != GN_MODE_BIG && !d.has[SMALL]))
     return fail(GN_E_NONET, "mode %d needs a network that is not loaded", mode);
   if (!ctx->incremental) {
     if (total) {
-      int rc = evaluate_on(ctx, d, children, total, mode, child_out, s, nullptr);
+      int rc = evaluate_on(ctx, d, children, total, mode, child_out, s, nullptr, nullptr, 0);
       if (rc) return rc;
     }
-    return parent_out ? evaluate_on(ctx, d, parents, n, mode, parent_out, s, nullptr) : GN_OK;
+    return parent_out ? evaluate_on(ctx, d, parents, n, mode, parent_out, s, nullptr, nullptr, score_parents ? 1 : 0,
+                                    d.counts.p)
+                      : GN_OK;
   }
   const size_t nt = std::max<size_t>(total, 1);
   if (mode != GN_MODE_BIG) {
@@ -756,7 +780,7 @@ static int expand_evaluate(gn_ctx *ctx, Dev &d, const gn_board *parents, size_t 
                                    d.pool.p, d.perr.p, rows_out, b0, b1, order, mid, sc));
         if (C > 1) { // this range's finalize (after the join when not pipelined)
           int rc = finalize_range(ctx, d, parents, children, mode, parent_out, child_out, pa, pb, d.cbound[c],
-                                  d.cbound[c + 1], sc);
+                                  d.cbound[c + 1], sc, score_parents);
           if (rc) return rc;
         }
         return GN_OK;
@@ -790,10 +814,58 @@ static int expand_evaluate(gn_ctx *ctx, Dev &d, const gn_board *parents, size_t 
   }
   HIP_TRY(mark(2));
   if (!piped) {
-    int rc = finalize_range(ctx, d, parents, children, mode, parent_out, child_out, 0, n, 0, total, s);
+    int rc = finalize_range(ctx, d, parents, children, mode, parent_out, child_out, 0, n, 0, total, s, score_parents);
     if (rc) return rc;
   }
   HIP_TRY(mark(3));
+  return GN_OK;
+}
+
+// ---------------------------------------------------------- score rule ---
+// The in-check part of the score rule (include/gpu_nnue.h, gn_eval.score): for every scored
+// position of out[0, n) in check with a legal move (finalize set the rest), its legal
+// replies are generated and evaluated as positions on the device, the replies in check
+// are resolved one level down (depth 2 -> 1; at depth 0 a reply keeps its static value),
+// and score_reduce_kernel takes the negamax over them.  sv_out (optional): the positions'
+// rule values for the level above.  Synchronous (the selection's and the replies' counts
+// size the next launches); a batch without such positions costs one select + scan.
+// Stockfish has no static evaluation in check (Eval::evaluate asserts !checkers) and
+// always prints a score from its search; fishnet requires one for every analysed
+// position (/root/reference/src/stockfish.rs:366-368, src/ipc.rs:56).
+static int resolve_scores(gn_ctx *ctx, Dev &d, const gn_board *boards, size_t n, int mode, gn_eval *out,
+                          int32_t *sv_out, hipStream_t s, int depth = 2) {
+  if (!n || depth <= 0 || !out) return GN_OK;
+  Dev::ScoreLevel &L = d.lv[2 - depth];
+  HIP_TRY(L.sel.ensure(n + 1));
+  HIP_TRY(L.pos.ensure(n + 1));
+  HIP_TRY(launch_score_select(out, n, L.sel.p, s));
+  HIP_TRY(exclusive_scan_u64(L.sel.p, L.pos.p, n + 1, d.scan_tmp, d.scan_bytes, s));
+  uint64_t m = 0;
+  HIP_TRY(hipMemcpyAsync(&m, L.pos.p + n, sizeof(m), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  if (!m) return GN_OK;
+  HIP_TRY(L.idx.ensure(m));
+  HIP_TRY(L.boards.ensure(m));
+  HIP_TRY(L.counts.ensure(m + 1));
+  HIP_TRY(L.offsets.ensure(m + 1));
+  HIP_TRY(launch_score_gather(boards, L.sel.p, L.pos.p, n, L.idx.p, L.boards.p, s));
+  HIP_TRY(hipMemsetAsync(L.counts.p + m, 0, sizeof(uint64_t), s));
+  HIP_TRY(launch_count_children(L.boards.p, m, d.tables, L.counts.p, s));
+  HIP_TRY(exclusive_scan_u64(L.counts.p, L.offsets.p, m + 1, d.scan_tmp, d.scan_bytes, s));
+  uint64_t t = 0;
+  HIP_TRY(hipMemcpyAsync(&t, L.offsets.p + m, sizeof(t), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  HIP_TRY(L.moves.ensure(std::max<uint64_t>(t, 1)));
+  HIP_TRY(L.owner.ensure(std::max<uint64_t>(t, 1)));
+  HIP_TRY(L.children.ensure(std::max<uint64_t>(t, 1)));
+  HIP_TRY(L.ce.ensure(std::max<uint64_t>(t, 1)));
+  HIP_TRY(L.sv.ensure(std::max<uint64_t>(t, 1)));
+  HIP_TRY(launch_write_children(L.boards.p, m, d.tables, L.offsets.p, 0, t, L.children.p, L.moves.p, L.owner.p,
+                                nullptr, nullptr, 1, nullptr, s));
+  int rc = evaluate_on(ctx, d, L.children.p, t, mode, L.ce.p, s, nullptr);
+  if (rc) return rc;
+  if ((rc = resolve_scores(ctx, d, L.children.p, t, mode, L.ce.p, L.sv.p, s, depth - 1)) != GN_OK) return rc;
+  HIP_TRY(launch_score_reduce(L.boards.p, m, L.idx.p, L.offsets.p, L.moves.p, L.ce.p, L.sv.p, ctx->P, out, sv_out, s));
   return GN_OK;
 }
 
@@ -863,6 +935,7 @@ static int evaluate_boards_host(gn_ctx *ctx, const gn_board *boards, size_t n, i
       HIP_TRY(hipMemcpyAsync(d.io_boards.p, boards + lo, (hi - lo) * sizeof(gn_board), hipMemcpyHostToDevice,
                              d.stream));
       int r = evaluate_on(ctx, d, d.io_boards.p, hi - lo, mode, d.io_out.p, d.stream, nullptr);
+      if (!r) r = resolve_scores(ctx, d, d.io_boards.p, hi - lo, mode, d.io_out.p, nullptr, d.stream);
       if (r) return r;
       HIP_TRY(hipMemcpyAsync(out + lo, d.io_out.p, (hi - lo) * sizeof(gn_eval), hipMemcpyDeviceToHost, d.stream));
       HIP_TRY(hipStreamSynchronize(d.stream));
@@ -962,6 +1035,7 @@ static int expand_boards_host(gn_ctx *ctx, const gn_board *boards, size_t n, int
       HIP_TRY(d.io_out.ensure(m));
       HIP_TRY(d.io_out2.ensure(std::max<size_t>(t, 1)));
       r = expand_evaluate(ctx, d, d.io_boards.p, m, d.frontier[1].p, t, mode, d.io_out.p, d.io_out2.p, s, nullptr);
+      if (!r) r = resolve_scores(ctx, d, d.io_boards.p, m, mode, d.io_out.p, nullptr, s);
       if (r) return r;
       if (t) {
         HIP_TRY(hipMemcpyAsync(child_out + base[k], d.io_out2.p, t * sizeof(gn_eval), hipMemcpyDeviceToHost, s));
@@ -1135,7 +1209,7 @@ int gn_evaluate_games(gn_ctx *ctx, const gn_game *games, size_t n_games, int mod
       for (size_t k = 0; k < rep[i].boards.size(); ++k) {
         const size_t at = position_offsets[i] + k;
         if (rep[i].skip[k]) {
-          position_out[at] = gn_eval{0, 0, 0, 0, (uint16_t)GN_FLAG_SKIPPED};
+          position_out[at] = gn_eval{0, 0, 0, 0, 0, (uint16_t)(GN_FLAG_SKIPPED | GN_FLAG_NO_SCORE), 0};
         } else {
           ev.push_back(rep[i].boards[k]);
           where.push_back((uint32_t)at);
@@ -1344,6 +1418,9 @@ int gn_set_eval_params(gn_ctx *ctx, const gn_eval_params *p) {
       p->wdl_material_anchor == 0)
     return fail(GN_E_INVALID, "zero divisor in eval params");
   if (p->wdl_material_min > p->wdl_material_max) return fail(GN_E_INVALID, "wdl material range is empty");
+  if (p->value_clamp < 0 || p->value_clamp >= VALUE_MATE_IN_MAX_PLY)
+    return fail(GN_E_INVALID, "value_clamp must be in [0, %d) (static values stay below mate scores)",
+                (int)VALUE_MATE_IN_MAX_PLY);
   ctx->P = *p;
   return GN_OK;
 }
@@ -1423,7 +1500,8 @@ int gn_evaluate_device(gn_ctx *ctx, int device_slot, const gn_board *d_boards, s
   hipStream_t s = stream ? (hipStream_t)stream : d->stream;
   SeqGuard sg(*d, s);
   HIP_TRY(sg.e);
-  return evaluate_on(ctx, *d, d_boards, n, mode, d_out, s, nullptr);
+  int rc = evaluate_on(ctx, *d, d_boards, n, mode, d_out, s, nullptr);
+  return rc ? rc : resolve_scores(ctx, *d, d_boards, n, mode, d_out, nullptr, s);
 }
 
 int gn_time_evaluate_device(gn_ctx *ctx, int device_slot, const gn_board *d_boards, size_t n, int mode,
@@ -1451,9 +1529,11 @@ int gn_time_evaluate_device(gn_ctx *ctx, int device_slot, const gn_board *d_boar
     HIP_TRY(hipMemsetAsync(d->sum.p, 0, sizeof(unsigned long long), d->stream));
   }
   hipError_t he = hipEventRecord(ev[0], d->stream);
-  for (int it = 0; it < iters && rc == GN_OK && he == hipSuccess; ++it)
+  for (int it = 0; it < iters && rc == GN_OK && he == hipSuccess; ++it) {
     rc = evaluate_on(ctx, *d, d_boards, n, mode, d_out, d->stream, per_kernel_ms ? &ev[2 + 5 * it] : nullptr,
                      ft_rows && it == 0 ? d->sum.p : nullptr);
+    if (rc == GN_OK) rc = resolve_scores(ctx, *d, d_boards, n, mode, d_out, nullptr, d->stream);
+  }
   if (rc == GN_OK && he == hipSuccess) he = hipEventRecord(ev[1], d->stream);
   if (rc == GN_OK && he == hipSuccess) he = hipEventSynchronize(ev[1]);
   if (rc == GN_OK && he == hipSuccess) he = hipEventElapsedTime(ms_total, ev[0], ev[1]);
@@ -1587,6 +1667,7 @@ int gn_expand_device(gn_ctx *ctx, int device_slot, const gn_board *d_parents, si
     return rc;
   }
   rc = expand_evaluate(ctx, *d, d_parents, n, d_children, t, mode, d_parent_out, d_child_out, s, nullptr);
+  if (!rc) rc = resolve_scores(ctx, *d, d_parents, n, mode, d_parent_out, nullptr, s);
   if (rc) return rc;
   HIP_TRY(hipStreamSynchronize(s));
   return check_plan(*d, s);
@@ -1634,6 +1715,7 @@ int gn_expand2_device(gn_ctx *ctx, int device_slot, const gn_board *d_parents, s
   if (rc) return rc;
   HIP_TRY(hipStreamSynchronize(s));
   if ((rc = check_plan(*d, s)) != GN_OK) return rc;
+  if ((rc = resolve_scores(ctx, *d, d_parents, n, mode, d_parent_out, nullptr, s)) != GN_OK) return rc;
   if (!t) {
     HIP_TRY(hipMemsetAsync(d_goffsets, 0, sizeof(uint32_t), s));
     HIP_TRY(hipStreamSynchronize(s));
@@ -1656,7 +1738,9 @@ int gn_expand2_device(gn_ctx *ctx, int device_slot, const gn_board *d_parents, s
     return rc;
   }
   HIP_TRY(d->io_out.ensure(t));
-  rc = expand_evaluate(ctx, *d, d_children, t, d->frontier[1].p, g, mode, d->io_out.p, d_grand_out, s, nullptr);
+  // (the children as parents are child records here too: compared with level 1's below)
+  rc = expand_evaluate(ctx, *d, d_children, t, d->frontier[1].p, g, mode, d->io_out.p, d_grand_out, s, nullptr,
+                       nullptr, false);
   if (rc) return rc;
   // the children evaluated twice (level 1 as children, level 2 as parents) must agree
   HIP_TRY(d->sum.ensure(2));
@@ -1681,9 +1765,9 @@ int gn_time_expand_device(gn_ctx *ctx, int device_slot, const gn_board *d_parent
   hipStream_t s = d->stream;
   SeqGuard sg(*d, s);
   HIP_TRY(sg.e);
-  // start, [count+scan], [total read], [write], [classify], [small], [big], [finalize], and
-  // the planned big net's plan -> stream boundary
-  const int NE = 9;
+  // start, [count+scan], [total read], [write], [classify], [small], [big], [finalize], the
+  // planned big net's plan -> stream boundary, and [score rule] (ends at e[9])
+  const int NE = 10;
   std::vector<hipEvent_t> ev((size_t)iters * NE + 2, nullptr);
   auto cleanup = [&] {
     for (auto &e : ev)
@@ -1716,22 +1800,26 @@ int gn_time_expand_device(gn_ctx *ctx, int device_slot, const gn_board *d_parent
     }
     HIP_TRY(d->io_out.ensure(n));
     HIP_TRY(d->io_out2.ensure(std::max<size_t>(t, 1)));
-    rc = expand_evaluate(ctx, *d, d_parents, n, d->frontier[1].p, t, mode, d_parent_out ? d_parent_out : d->io_out.p,
+    gn_eval *po = d_parent_out ? d_parent_out : d->io_out.p;
+    rc = expand_evaluate(ctx, *d, d_parents, n, d->frontier[1].p, t, mode, po,
                          d_child_out ? d_child_out : d->io_out2.p, s, e + 4, it == 0 ? d->sum.p + 1 : nullptr);
+    if (rc == GN_OK) rc = resolve_scores(ctx, *d, d_parents, n, mode, po, nullptr, s);
+    if (rc == GN_OK) he = hipEventRecord(e[9], s);
   }
   if (rc == GN_OK && he == hipSuccess && d_offsets) he = launch_offsets_u32(d->offsets.p, n + 1, d_offsets, s);
   if (rc == GN_OK && he == hipSuccess) he = hipEventRecord(ev[1], s);
   if (rc == GN_OK && he == hipSuccess) he = hipEventSynchronize(ev[1]);
   if (rc == GN_OK && he == hipSuccess) he = hipEventElapsedTime(ms_total, ev[0], ev[1]);
   if (rc == GN_OK && he == hipSuccess && stage_ms) {
-    float acc[7] = {0, 0, 0, 0, 0, 0, 0};
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (int it = 0; it < iters && he == hipSuccess; ++it)
-      for (int k = 0; k < 7 && he == hipSuccess; ++k) {
+      for (int k = 0; k < 8 && he == hipSuccess; ++k) {
         float ms = 0;
-        he = hipEventElapsedTime(&ms, ev[2 + (size_t)NE * it + k], ev[2 + (size_t)NE * it + k + 1]);
+        const size_t o = 2 + (size_t)NE * it;
+        he = hipEventElapsedTime(&ms, ev[o + k], ev[o + (k < 7 ? k + 1 : 9)]);
         acc[k] += ms;
       }
-    for (int k = 0; k < 7; ++k) stage_ms[k] = acc[k] / (float)iters;
+    for (int k = 0; k < 8; ++k) stage_ms[k] = acc[k] / (float)iters;
   }
   if (rc == GN_OK && he == hipSuccess && d->planned) { // the big net's two kernels apart
     float pl = 0, st = 0;

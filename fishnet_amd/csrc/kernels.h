@@ -83,13 +83,27 @@ hipError_t launch_classify(const gn_board *boards, size_t n, const gn_eval_param
 hipError_t launch_reeval(const int2 *out_small, const uint8_t *need_small, size_t n, const gn_eval_params &P,
                          uint8_t *need_big, hipStream_t s);
 // Eval::evaluate epilogue -> gn_eval (flags incl. IN_CHECK / BAD_FEN).
+// score: 0 child records (GN_FLAG_NO_SCORE); 1 positions: the score rule's static part
+// (mate 0 / cp 0 without a legal move, from counts[i] when given, else found here; final_cp
+// otherwise, which resolve_scores replaces for the in-check ones).
 // owner / moves / unpacked (optional, children only): board i is unpacked[owner[i]] after
 // moves[i] (the parents write_children unpacked), instead of unpacking boards[i].
 hipError_t launch_finalize(const gn_board *boards, size_t n, int mode, const int2 *out_small,
                            const int2 *out_big, const uint8_t *need_small, const uint8_t *need_big,
                            const gn_eval_params &P, const Tables *tables, gn_eval *out, hipStream_t s,
-                           const uint32_t *owner = nullptr, const uint16_t *moves = nullptr,
-                           const Board *unpacked = nullptr);
+                           int score, const uint64_t *counts = nullptr, const uint32_t *owner = nullptr,
+                           const uint16_t *moves = nullptr, const Board *unpacked = nullptr);
+// The score rule's in-check positions (include/gpu_nnue.h gn_eval.score): select (sel[n + 1],
+// 1 for a scored position in check with a legal move), gather (idx / boards of the selected,
+// pos = exclusive scan of sel), reduce (max over each selected position's replies
+// [off[j], off[j + 1]) of moves / records ce, csv = the replies' own rule values where
+// GN_FLAG_SEARCHED; writes score / flags / best_move of out[idx[j]] and sv[idx[j]] if sv).
+hipError_t launch_score_select(const gn_eval *out, size_t n, uint64_t *sel, hipStream_t s);
+hipError_t launch_score_gather(const gn_board *boards, const uint64_t *sel, const uint64_t *pos, size_t n,
+                               uint32_t *idx, gn_board *sb, hipStream_t s);
+hipError_t launch_score_reduce(const gn_board *sb, size_t m, const uint32_t *idx, const uint64_t *off,
+                               const uint16_t *moves, const gn_eval *ce, const int32_t *csv, const gn_eval_params &P,
+                               gn_eval *out, int32_t *sv, hipStream_t s);
 // legal-move counts per board (invalid boards: 0); ebound (optional): per parent an
 // upper bound of the planned expansion's list entries (stream.hip)
 hipError_t launch_count_children(const gn_board *boards, size_t n, const Tables *tables, uint64_t *counts,

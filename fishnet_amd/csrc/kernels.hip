@@ -1441,17 +1441,17 @@ __global__ void finalize_kernel(const gn_board *__restrict__ boards, size_t n, i
                                 const uint8_t *__restrict__ need_small, const uint8_t *__restrict__ need_big,
                                 gn_eval_params P, const Tables *__restrict__ tables, gn_eval *__restrict__ out,
                                 const uint32_t *__restrict__ owner, const uint16_t *__restrict__ moves,
-                                const Board *__restrict__ unpacked) {
+                                const Board *__restrict__ unpacked, int score, const uint64_t *__restrict__ counts) {
   __shared__ Tables T;
   load_tables(T, tables);
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   Board B;
-  gn_eval e = {0, 0, 0, 0};
+  gn_eval e = {0, 0, 0, 0, 0, 0, 0};
   if (unpacked) {
     B = do_move(unpacked[owner[i]], moves[i], nullptr); // a legal child of a valid parent
   } else if (!unpack(boards[i], B)) {
-    e.flags = GN_FLAG_BAD_FEN;
+    e.flags = GN_FLAG_BAD_FEN | GN_FLAG_NO_SCORE;
     out[i] = e;
     return;
   }
@@ -1478,10 +1478,74 @@ __global__ void finalize_kernel(const gn_board *__restrict__ boards, size_t n, i
   v = wadd(v, -(wmul(v, (int32_t)B.rule50) / P.rule50_div));
   v = clampi(v, -P.value_clamp, P.value_clamp);
   if (small) flags |= GN_FLAG_SMALLNET;
-  if (in_check(B, T)) flags |= GN_FLAG_IN_CHECK;
-  e.psqt = o.x, e.positional = o.y, e.final_v = v, e.flags = (uint16_t)flags;
+  const bool check = in_check(B, T);
+  if (check) flags |= GN_FLAG_IN_CHECK;
+  e.psqt = o.x, e.positional = o.y, e.final_v = v;
   e.final_cp = wdl_to_cp(v, wdl_material(B, P), P);
+  // the score rule's static part (include/gpu_nnue.h); in-check positions with legal moves
+  // keep final_cp until score_reduce_kernel replaces it
+  if (!score) {
+    flags |= GN_FLAG_NO_SCORE; // a child record
+  } else if (counts ? counts[i] == 0 : !any_legal(B, T)) {
+    flags |= GN_FLAG_NO_MOVES | (check ? GN_FLAG_MATE : 0u); // mate 0 / cp 0
+  } else {
+    e.score = e.final_cp;
+  }
+  e.flags = (uint16_t)flags;
   out[i] = e;
+}
+
+// ---- the score rule's in-check positions (gpu_nnue.hip resolve_scores) ------------------
+// sel[i] = 1 for a scored position in check with a legal move; sel[n] = 0 (the scan's end)
+__global__ void score_select_kernel(const gn_eval *__restrict__ out, size_t n, uint64_t *__restrict__ sel) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i > n) return;
+  uint64_t v = 0;
+  if (i < n) {
+    const uint32_t f = out[i].flags;
+    v = (f & GN_FLAG_IN_CHECK) && !(f & (GN_FLAG_NO_MOVES | GN_FLAG_NO_SCORE | GN_FLAG_BAD_FEN));
+  }
+  sel[i] = v;
+}
+
+// the selected positions, compacted: idx[k] = i, sb[k] = boards[i] for k = pos[i]
+__global__ void score_gather_kernel(const gn_board *__restrict__ boards, const uint64_t *__restrict__ sel,
+                                    const uint64_t *__restrict__ pos, size_t n, uint32_t *__restrict__ idx,
+                                    gn_board *__restrict__ sb) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || !sel[i]) return;
+  const uint64_t k = pos[i];
+  idx[k] = (uint32_t)i;
+  sb[k] = boards[i];
+}
+
+// value = max over the replies c of negate_ply(rule_value(c)) (ties: the smaller move), then
+// score / flags / best_move of selected position j; sv (optional) receives the value for
+// the level above
+__global__ void score_reduce_kernel(const gn_board *__restrict__ sb, size_t m, const uint32_t *__restrict__ idx,
+                                    const uint64_t *__restrict__ off, const uint16_t *__restrict__ moves,
+                                    const gn_eval *__restrict__ ce, const int32_t *__restrict__ csv,
+                                    gn_eval_params P, gn_eval *__restrict__ out, int32_t *__restrict__ sv) {
+  const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= m) return;
+  int32_t best = INT32_MIN;
+  uint32_t bm = 0xFFFFu;
+  for (uint64_t c = off[j]; c < off[j + 1]; ++c) {
+    const gn_eval r = ce[c];
+    const int32_t v = negate_ply(rule_value(r.flags, r.final_v, csv[c]));
+    const uint32_t mv = moves[c];
+    if (v > best || (v == best && mv < bm)) best = v, bm = mv;
+  }
+  Board B;
+  unpack(sb[j], B);
+  const uint32_t i = idx[j];
+  gn_eval e = out[i];
+  uint32_t fl = (e.flags | GN_FLAG_SEARCHED) & ~GN_FLAG_MATE;
+  e.score = rule_score(best, wdl_material(B, P), P, fl);
+  e.flags = (uint16_t)fl;
+  e.best_move = (uint16_t)bm;
+  out[i] = e;
+  if (sv) sv[i] = best;
 }
 
 static inline unsigned blocks_for(size_t n, int bs) { return (unsigned)((n + bs - 1) / bs); }
@@ -1502,11 +1566,32 @@ hipError_t launch_reeval(const int2 *out_small, const uint8_t *need_small, size_
 
 hipError_t launch_finalize(const gn_board *boards, size_t n, int mode, const int2 *out_small, const int2 *out_big,
                            const uint8_t *need_small, const uint8_t *need_big, const gn_eval_params &P,
-                           const Tables *tables, gn_eval *out, hipStream_t s, const uint32_t *owner,
-                           const uint16_t *moves, const Board *unpacked) {
+                           const Tables *tables, gn_eval *out, hipStream_t s, int score, const uint64_t *counts,
+                           const uint32_t *owner, const uint16_t *moves, const Board *unpacked) {
   if (!n) return hipSuccess;
   hipLaunchKernelGGL(finalize_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, boards, n, mode, out_small, out_big,
-                     need_small, need_big, P, tables, out, owner, moves, unpacked);
+                     need_small, need_big, P, tables, out, owner, moves, unpacked, score, counts);
+  return hipGetLastError();
+}
+
+hipError_t launch_score_select(const gn_eval *out, size_t n, uint64_t *sel, hipStream_t s) {
+  hipLaunchKernelGGL(score_select_kernel, dim3(blocks_for(n + 1, 256)), dim3(256), 0, s, out, n, sel);
+  return hipGetLastError();
+}
+
+hipError_t launch_score_gather(const gn_board *boards, const uint64_t *sel, const uint64_t *pos, size_t n,
+                               uint32_t *idx, gn_board *sb, hipStream_t s) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(score_gather_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, boards, sel, pos, n, idx, sb);
+  return hipGetLastError();
+}
+
+hipError_t launch_score_reduce(const gn_board *sb, size_t m, const uint32_t *idx, const uint64_t *off,
+                               const uint16_t *moves, const gn_eval *ce, const int32_t *csv, const gn_eval_params &P,
+                               gn_eval *out, int32_t *sv, hipStream_t s) {
+  if (!m) return hipSuccess;
+  hipLaunchKernelGGL(score_reduce_kernel, dim3(blocks_for(m, 256)), dim3(256), 0, s, sb, m, idx, off, moves, ce, csv,
+                     P, out, sv);
   return hipGetLastError();
 }
 

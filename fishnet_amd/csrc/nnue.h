@@ -163,21 +163,48 @@ GN_HD int packed_features(const gn_board &p, uint16_t *rows_white, uint16_t *row
 // a = p_a(m) of the win-rate model, m = clamp(material, lo, hi) / anchor, and
 // cp = round(100 * v / a).  Evaluated in double in Stockfish's operation order
 // with contraction off (Stockfish's gcc -std=c++17 build does not fuse), rounded
-// half away from zero as std::round; saturated to int16 (see gn_eval).
+// half away from zero as std::round; saturated to int32 (0 for a non-finite quotient).
 GN_HD int wdl_material(const Board &B, const gn_eval_params &P) {
   int m = 0;
 #pragma unroll
   for (int pt = PAWN; pt <= QUEEN; ++pt) m += P.wdl_piece_weight[pt - 1] * popcnt(B.byType[pt]);
   return m;
 }
-GN_HD int16_t wdl_to_cp(int32_t v, int material, const gn_eval_params &P) {
+GN_HD int32_t wdl_to_cp(int32_t v, int material, const gn_eval_params &P) {
 #pragma clang fp contract(off)
   const int lo = P.wdl_material_min, hi = P.wdl_material_max;
   const int mc = material < lo ? lo : material > hi ? hi : material;
   const double m = (double)mc / (double)P.wdl_material_anchor;
   const double a = ((P.wdl_a[0] * m + P.wdl_a[1]) * m + P.wdl_a[2]) * m + P.wdl_a[3];
   const double cp = round((double)(100 * (int64_t)v) / a);
-  return (int16_t)(cp > 32767.0 ? 32767 : cp < -32767.0 ? -32767 : (int)cp);
+  if (!(cp == cp)) return 0;
+  return cp > 2147483647.0 ? 2147483647 : cp < -2147483647.0 ? -2147483647 : (int32_t)cp;
+}
+
+// ---- the score rule (gn_eval.score, include/gpu_nnue.h) --------------------------------
+// Values in Stockfish's units: VALUE_MATE - ply for a mate ply plies away, static
+// evaluations clamped below VALUE_MATE_IN_MAX_PLY (gn_eval_params.value_clamp).
+constexpr int32_t VALUE_MATE = 32000, VALUE_MATE_IN_MAX_PLY = 32000 - 246;
+// The value a record contributes to its parent's in-check rule (its side-to-move POV);
+// `searched` is its own rule value when GN_FLAG_SEARCHED is set.
+GN_HD int32_t rule_value(uint32_t flags, int32_t final_v, int32_t searched) {
+  if (flags & GN_FLAG_NO_MOVES) return (flags & GN_FLAG_IN_CHECK) ? -VALUE_MATE : 0;
+  return (flags & GN_FLAG_SEARCHED) ? searched : final_v;
+}
+// A reply's value seen from the position before it: negated, mates one ply further away.
+GN_HD int32_t negate_ply(int32_t v) {
+  v = -v;
+  return v >= VALUE_MATE_IN_MAX_PLY ? v - 1 : v <= -VALUE_MATE_IN_MAX_PLY ? v + 1 : v;
+}
+// score / GN_FLAG_MATE of a rule value, as Stockfish's UCI `score` prints it
+// (mate (ply + 1) / 2 when mating, -ply / 2 when mated; else cp by to_cp).
+GN_HD int32_t rule_score(int32_t v, int material, const gn_eval_params &P, uint32_t &flags) {
+  if (v >= VALUE_MATE_IN_MAX_PLY || v <= -VALUE_MATE_IN_MAX_PLY) {
+    const int32_t ply = VALUE_MATE - (v > 0 ? v : -v);
+    flags |= GN_FLAG_MATE;
+    return v > 0 ? (ply + 1) / 2 : -ply / 2;
+  }
+  return wdl_to_cp(v, material, P);
 }
 
 // 32-bit hashes stored in .nnue files

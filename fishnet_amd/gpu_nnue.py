@@ -20,15 +20,19 @@ LIB_PATH = os.environ.get("GPU_NNUE_LIB", os.path.join(HERE, "lib", "libgpu_nnue
 
 MODE_FULL, MODE_BIG, MODE_SMALL = 0, 1, 2
 FLAG_IN_CHECK, FLAG_SMALLNET, FLAG_BAD_FEN, FLAG_REEVAL, FLAG_SKIPPED = 1, 2, 4, 8, 16
+FLAG_MATE, FLAG_NO_SCORE, FLAG_SEARCHED, FLAG_NO_MOVES = 32, 64, 128, 256
 ERRORS = {-1: "INVALID", -2: "IO", -3: "FORMAT", -4: "HIP", -5: "NOMEM", -6: "CAPACITY",
           -7: "NODEVICE", -8: "NONET", -9: "ILLEGAL_MOVE"}
 E_INVALID, E_IO, E_FORMAT, E_CAPACITY, E_ILLEGAL_MOVE = -1, -2, -3, -6, -9
 
-EVAL_DTYPE = np.dtype([("psqt", "<i4"), ("positional", "<i4"), ("final_v", "<i4"), ("final_cp", "<i2"),
-                       ("flags", "<u2")])
+# gn_eval (ABI v3): the static evaluation, and the score fishnet posts (gpu_nnue.h)
+EVAL_DTYPE = np.dtype([("psqt", "<i4"), ("positional", "<i4"), ("final_v", "<i4"), ("final_cp", "<i4"),
+                       ("score", "<i4"), ("flags", "<u2"), ("best_move", "<u2")])
 BOARD_DTYPE = np.dtype([("occ", "<u8"), ("pc", "u1", (16,)), ("stm_ep", "u1"), ("reserved", "u1"),
                         ("castle", "<u2"), ("rule50", "<u2"), ("fullmove", "<u2")])
-assert EVAL_DTYPE.itemsize == 16 and BOARD_DTYPE.itemsize == 32
+EVAL_SIZE, BOARD_SIZE = EVAL_DTYPE.itemsize, BOARD_DTYPE.itemsize
+assert EVAL_SIZE == 24 and BOARD_SIZE == 32
+ABI_VERSION = 3
 
 EXPORTS = ["gn_load_net", "gn_load_net_memory", "gn_free", "gn_last_error", "gn_abi_version",
            "gn_get_eval_params", "gn_set_eval_params", "gn_net_info", "gn_evaluate_batch",
@@ -41,7 +45,8 @@ EXPORTS = ["gn_load_net", "gn_load_net_memory", "gn_free", "gn_last_error", "gn_
            "gn_boards_to_fens", "gn_load_net_archive", "gn_archive_read", "gn_expand2_device"]
 OPT_INCREMENTAL_CHILDREN, OPT_XCD_SWIZZLE, OPT_KING_SORT, OPT_CHAIN, OPT_KING_CACHE = 1, 2, 3, 4, 5
 STAT_CHAIN_FALLBACKS, STAT_PLAN_NS, STAT_STREAM_NS = 100, 101, 102
-EXPAND_STAGES = ["count_scan", "total_readback", "write_children", "classify", "small_net", "big_net", "finalize"]
+EXPAND_STAGES = ["count_scan", "total_readback", "write_children", "classify", "small_net", "big_net", "finalize",
+                 "score"]
 
 
 class GnError(RuntimeError):
@@ -138,6 +143,8 @@ def lib():
         f.restype = i32
     L.gn_free.restype = None
     L.gn_last_error.restype = C.c_char_p
+    if L.gn_abi_version() != ABI_VERSION:
+        raise ImportError(f"{LIB_PATH} has ABI {L.gn_abi_version()}, this module expects {ABI_VERSION}: rebuild it")
     _lib = L
     return L
 
@@ -404,7 +411,7 @@ class GpuNnue:
         """outputs: optional dict of DeviceBuffers po (parents), off (u32 offsets), mv (moves), co (children)
         plus cap; they receive the timed expansion's results."""
         ms, total, rows = C.c_float(), C.c_size_t(), C.c_uint64()
-        st = (C.c_float * 7)()
+        st = (C.c_float * len(EXPAND_STAGES))()
         o = outputs or {}
         ptr = lambda k: o[k].ptr if k in o else None
         _check(lib().gn_time_expand_device(self.h, slot, d_parents.ptr, n, mode, iters, C.byref(ms),

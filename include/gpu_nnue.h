@@ -30,8 +30,11 @@ extern "C" {
 #endif
 
 /* v2: gn_eval carries final_cp (UCIEngine::to_cp) and 16-bit flags; gn_eval_params
- * carries the win-rate model; expansion shards over every device of the context. */
-#define GN_ABI_VERSION 2
+ * carries the win-rate model; expansion shards over every device of the context.
+ * v3: gn_eval is 24 bytes: final_cp is int32 and every evaluated position carries the
+ * score fishnet posts (score, GN_FLAG_MATE / GN_FLAG_SEARCHED / GN_FLAG_NO_MOVES,
+ * best_move): checkmate, stalemate and in-check positions included. */
+#define GN_ABI_VERSION 3
 
 #if defined(__GNUC__)
 #define GN_API __attribute__((visibility("default")))
@@ -105,21 +108,43 @@ extern "C" {
 #define GN_FLAG_BAD_FEN 4u  /* unparsable / unsupported position; values are 0     */
 #define GN_FLAG_REEVAL 8u   /* small net was run, then the big net re-evaluated   */
 #define GN_FLAG_SKIPPED 16u /* listed in skipPositions: not evaluated, values 0    */
+#define GN_FLAG_MATE 32u    /* score is a mate distance (UCI `score mate <score>`)  */
+#define GN_FLAG_NO_SCORE 64u /* no score: skipped / bad position, or a child record */
+#define GN_FLAG_SEARCHED 128u /* score from the in-check rule over the legal replies
+                                 (best_move set), not from the static evaluation   */
+#define GN_FLAG_NO_MOVES 256u /* no legal move: checkmate (with IN_CHECK) or stalemate */
 
 /* One result.  psqt/positional are Network::evaluate's NetworkOutput (already
  * divided by OutputScale = 16) of the net that produced final_v; final_v is
  * Eval::evaluate(pos, optimism = 0) in internal Value units; final_cp is
  * final_v in centipawns as Stockfish prints it (UCIEngine::to_cp: the win-rate
- * model's a(material), round(100 * v / a)), i.e. the `score cp` fishnet parses
- * (/root/reference/src/stockfish.rs:419-427) and posts; all side-to-move POV.
- * |final_cp| <= 100 * value_clamp / min a < 2^15 for the default parameters;
- * it saturates at +-32767 for parameters that would exceed it. */
+ * model's a(material), round(100 * v / a)); all side-to-move POV.
+ *
+ * score is what fishnet posts for the position: the `score cp X` / `score mate N` a
+ * Stockfish `go` prints and stockfish.rs:419-431 parses; fishnet requires one for
+ * every analysed position (stockfish.rs:366-368, ipc.rs:56 `expect("got score")`).
+ * The rule, for every position a call is given (batch, game and parent positions):
+ *   - no legal move: checkmate -> `mate 0` (GN_FLAG_MATE, score 0), stalemate -> `cp 0`
+ *     (what Stockfish prints at depth 0); GN_FLAG_NO_MOVES;
+ *   - not in check: score = final_cp (the static evaluation);
+ *   - in check with legal moves (Stockfish has no static eval there): a check extension,
+ *     value(p, d) = max over legal replies c of -value(c, d - 1) from d = 2, where a reply
+ *     with no legal move is mated (-VALUE_MATE = -32000) or stalemated (0), a reply not in
+ *     check -- or any reply at d = 0 -- takes its static final_v, and mate values move one
+ *     ply toward zero per level (VALUE_MATE - ply); ties go to the smaller move encoding.
+ *     score = `mate (ply + 1) / 2` / `mate -ply / 2` for |value| >= 31754
+ *     (VALUE_MATE_IN_MAX_PLY), else to_cp(value) with this position's material;
+ *     GN_FLAG_SEARCHED, best_move = the reply (Stockfish encoding).
+ * Child and grandchild records of the expansion calls carry GN_FLAG_NO_SCORE (score 0):
+ * they are search data, not positions fishnet posts. */
 typedef struct gn_eval {
   int32_t psqt;
   int32_t positional;
   int32_t final_v;
-  int16_t final_cp;
+  int32_t final_cp;
+  int32_t score;
   uint16_t flags;
+  uint16_t best_move;
 } gn_eval;
 
 /* Packed position, 32 bytes, the device input format.
@@ -310,13 +335,13 @@ GN_API int gn_expand_device(gn_ctx *ctx, int device_slot, const gn_board *d_pare
                      uint16_t *d_moves, gn_eval *d_child_out, size_t cap, size_t *total, void *stream);
 /* Time `iters` complete expansions of device-resident parents (child count +
  * scan + child generation with deltas + evaluation of parents and children in
- * `mode`).  Outputs go to the caller's device buffers when given (d_parent_out[n],
+ * `mode` + the parents' score rule).  Outputs go to the caller's device buffers when given (d_parent_out[n],
  * d_offsets[n + 1], d_moves[cap], d_child_out[cap]; GN_E_CAPACITY when the
  * children exceed cap), else to library-owned buffers; every iteration writes the
  * same values, so after the call they hold the timed expansion's results.
  * *total = children per expansion;
- * stage_ms (optional, length 7) = average ms of [count+scan, total read-back,
- * write children, classify, small net, big net, finalize]; ft_rows (optional)
+ * stage_ms (optional, length 8) = average ms of [count+scan, total read-back,
+ * write children, classify, small net, big net, finalize, score rule]; ft_rows (optional)
  * = feature-transformer rows one incremental expansion gathers: for the big
  * nets the row stream's own count (bias, carry and king-cache rows included:
  * GN_OPT_CHAIN, GN_OPT_KING_CACHE), else parent refreshes + child deltas /

@@ -744,7 +744,7 @@ static void material(const pos_t *p, int *pawns, int npm[2]) {
  *   m = clamp(material, 17, 78) / 58.0,
  *   a = ((as[0] m + as[1]) m + as[2]) m + as[3],
  *   cp = round(100 * v / a). */
-static int16_t to_cp(const pos_t *p, int32_t v) {
+static int32_t to_cp(const pos_t *p, int32_t v) {
   static const int W[7] = {0, 1, 3, 3, 5, 9, 0};
   static const double as[4] = {-37.45051876, 121.19101539, -132.78783573, 420.70576692};
   int material = 0;
@@ -752,10 +752,7 @@ static int16_t to_cp(const pos_t *p, int32_t v) {
     if (p->b[sq]) material += W[TYPE_OF(p->b[sq])];
   double m = (double)(material < 17 ? 17 : material > 78 ? 78 : material) / 58.0;
   double a = (((as[0] * m + as[1]) * m + as[2]) * m) + as[3];
-  double cp = round((double)(100 * (long long)v) / a);
-  if (cp > 32767.0) cp = 32767.0;
-  if (cp < -32767.0) cp = -32767.0;
-  return (int16_t)cp;
+  return (int32_t)round((double)(100 * (long long)v) / a);
 }
 
 /* Where a position's accumulators come from: a full refresh (src == NULL), or an
@@ -811,15 +808,84 @@ static void evaluate(const or_net *big, const or_net *small, const pos_t *p, int
   evaluate_src(big, small, p, mode, out, NULL);
 }
 
+/* ---- the score rule (gpu_nnue.h at gn_eval): what fishnet posts per position --------
+ * value(p, d): no legal move -> -32000 (mated) / 0 (stalemate); not in check, or d = 0 ->
+ * the static final_v; in check -> max over the legal replies c of -value(c, d - 1), a mate
+ * value moving one ply toward zero per level; ties to the smaller move encoding.  Written
+ * as a plain recursion over this oracle's own movegen (the product batches the levels). */
+#define OR_VALUE_MATE 32000
+#define OR_MATE_IN_MAX_PLY (32000 - 246)
+
+static int32_t negate_ply(int32_t v) {
+  v = -v;
+  if (v >= OR_MATE_IN_MAX_PLY) return v - 1;
+  if (v <= -OR_MATE_IN_MAX_PLY) return v + 1;
+  return v;
+}
+
+/* rec (optional): p's static record; best: the chosen reply when p was searched */
+static int32_t rule_value(const or_net *big, const or_net *small, const pos_t *p, int mode, int depth, or_eval *rec,
+                          int *nmoves, uint16_t *best) {
+  or_eval tmp;
+  uint16_t mv[256];
+  if (!rec) rec = &tmp;
+  evaluate(big, small, p, mode, rec);
+  const int n = gen_legal(p, mv), check = in_check(p);
+  if (nmoves) *nmoves = n;
+  if (!n) return check ? -OR_VALUE_MATE : 0;
+  if (!check || depth == 0) return rec->final_v;
+  int32_t bv = INT32_MIN;
+  uint16_t bm = 0xFFFF;
+  for (int i = 0; i < n; ++i) {
+    pos_t q;
+    do_move(p, mv[i], &q);
+    const int32_t v = negate_ply(rule_value(big, small, &q, mode, depth - 1, NULL, NULL, NULL));
+    if (v > bv || (v == bv && mv[i] < bm)) bv = v, bm = mv[i];
+  }
+  if (best) *best = bm;
+  return bv;
+}
+
+/* a position's record: the static evaluation plus its score */
+static void evaluate_position(const or_net *big, const or_net *small, const pos_t *p, int mode, or_eval *out) {
+  int n = 0;
+  uint16_t bm = 0;
+  const int32_t v = rule_value(big, small, p, mode, 2, out, &n, &bm);
+  uint32_t fl = out->flags;
+  out->score = 0, out->best_move = 0;
+  if (!n) {
+    fl |= OR_FLAG_NO_MOVES | ((fl & OR_FLAG_IN_CHECK) ? OR_FLAG_MATE : 0u); /* mate 0 / cp 0 */
+  } else if (!(fl & OR_FLAG_IN_CHECK)) {
+    out->score = out->final_cp;
+  } else {
+    fl |= OR_FLAG_SEARCHED;
+    out->best_move = bm;
+    if (v >= OR_MATE_IN_MAX_PLY || v <= -OR_MATE_IN_MAX_PLY) {
+      const int32_t ply = OR_VALUE_MATE - (v > 0 ? v : -v);
+      fl |= OR_FLAG_MATE;
+      out->score = v > 0 ? (ply + 1) / 2 : -ply / 2;
+    } else {
+      out->score = to_cp(p, v);
+    }
+  }
+  out->flags = (uint16_t)fl;
+}
+
+/* a child record of an expansion: no score */
+static void as_child(or_eval *e) {
+  e->score = 0, e->best_move = 0;
+  e->flags |= OR_FLAG_NO_SCORE;
+}
+
 int or_eval_fen(const or_net *big, const or_net *small, const char *fen, int mode, or_eval *out) {
   pos_t p;
   memset(out, 0, sizeof(*out));
   if (parse_fen(fen, &p)) {
-    out->flags = OR_FLAG_BAD_FEN;
+    out->flags = OR_FLAG_BAD_FEN | OR_FLAG_NO_SCORE;
     return -1;
   }
   if ((mode != OR_MODE_SMALL && !big) || (mode != OR_MODE_BIG && !small)) return -2;
-  evaluate(big, small, &p, mode, out);
+  evaluate_position(big, small, &p, mode, out);
   return 0;
 }
 
@@ -893,10 +959,10 @@ int or_expand_eval(const or_net *big, const or_net *small, const char *fen, int 
   uint16_t mv[256];
   if (parse_fen(fen, &p)) {
     memset(parent, 0, sizeof(*parent));
-    parent->flags = OR_FLAG_BAD_FEN;
+    parent->flags = OR_FLAG_BAD_FEN | OR_FLAG_NO_SCORE;
     return -1;
   }
-  evaluate(big, small, &p, mode, parent);
+  evaluate_position(big, small, &p, mode, parent);
   int n = gen_legal(&p, mv);
   if (n > cap) return -2;
   for (int i = 0; i < n; ++i) {
@@ -904,6 +970,7 @@ int or_expand_eval(const or_net *big, const or_net *small, const char *fen, int 
     do_move(&p, mv[i], &q);
     moves[i] = mv[i];
     evaluate(big, small, &q, mode, &children[i]);
+    as_child(&children[i]);
   }
   return n;
 }
@@ -918,11 +985,11 @@ int or_expand_eval_inc(const or_net *big, const or_net *small, const char *fen, 
   uint16_t mv[256];
   if (parse_fen(fen, &p)) {
     memset(parent, 0, sizeof(*parent));
-    parent->flags = OR_FLAG_BAD_FEN;
+    parent->flags = OR_FLAG_BAD_FEN | OR_FLAG_NO_SCORE;
     return -1;
   }
   acc_src_t src = {&p, {&pa[0], &pa[1]}, {0, 0}, &ca};
-  evaluate(big, small, &p, mode, parent);
+  evaluate_position(big, small, &p, mode, parent);
   int n = gen_legal(&p, mv);
   if (n > cap) return -2;
   for (int i = 0; i < n; ++i) {
@@ -930,6 +997,7 @@ int or_expand_eval_inc(const or_net *big, const or_net *small, const char *fen, 
     do_move(&p, mv[i], &q);
     moves[i] = mv[i];
     evaluate_src(big, small, &q, mode, &children[i], &src);
+    as_child(&children[i]);
   }
   return n;
 }

@@ -38,13 +38,23 @@ extern "C" {
 #define OR_FLAG_SMALLNET 2u
 #define OR_FLAG_BAD_FEN 4u
 #define OR_FLAG_REEVAL 8u
+#define OR_FLAG_MATE 32u     /* score is a mate distance                            */
+#define OR_FLAG_NO_SCORE 64u /* no score (bad FEN, or a child record)               */
+#define OR_FLAG_SEARCHED 128u /* score from the in-check rule, best_move set        */
+#define OR_FLAG_NO_MOVES 256u /* no legal move (checkmate / stalemate)              */
 
+/* Mirror of gn_eval (ABI v3).  score: the score fishnet posts, by the rule gpu_nnue.h
+ * states at gn_eval (restated in or_score below from that text and from what the
+ * reference requires: a `score cp|mate` for every analysed position,
+ * /root/reference/src/stockfish.rs:366-368, src/ipc.rs:56). */
 typedef struct {
   int32_t psqt;       /* NetworkOutput.psqt of the net that produced final  */
   int32_t positional; /* NetworkOutput.positional of that net               */
   int32_t final_v;    /* Eval::evaluate(optimism = 0), side-to-move POV     */
-  int16_t final_cp;   /* UCIEngine::to_cp(final_v): the printed centipawns  */
+  int32_t final_cp;   /* UCIEngine::to_cp(final_v): the printed centipawns  */
+  int32_t score;      /* cp, or moves to mate with OR_FLAG_MATE              */
   uint16_t flags;
+  uint16_t best_move; /* the in-check rule's reply (Stockfish encoding)     */
 } or_eval;
 
 typedef struct or_net or_net;
@@ -59,7 +69,8 @@ uint32_t or_net_hash(const or_net *net);
 /* expected network hash for a given L1 width (FT hash ^ architecture hash) */
 uint32_t or_expected_hash(int l1, uint32_t *ft_hash, uint32_t *arch_hash);
 
-/* evaluate one FEN.  big or small may be NULL when the mode does not need it. */
+/* evaluate one FEN (a position: the score rule applies).  big or small may be NULL when
+ * the mode does not need it. */
 int or_eval_fen(const or_net *big, const or_net *small, const char *fen, int mode, or_eval *out);
 /* evaluate a batch with `threads` POSIX threads (threads <= 0: 1) */
 int or_eval_fens(const or_net *big, const or_net *small, const char *const *fens, size_t n,
@@ -79,7 +90,8 @@ int or_normalize_fen(const char *fen, char *out, int cap);
 uint64_t or_perft(const char *fen, int depth); /* UINT64_MAX on a bad FEN */
 
 /* parent + every legal child evaluated (children in Stockfish movegen order is
- * NOT promised; moves[] reports the order used).  Returns the child count, or
+ * NOT promised; moves[] reports the order used).  The parent is a position (scored),
+ * the children are child records (OR_FLAG_NO_SCORE).  Returns the child count, or
  * negative on error / cap overflow. */
 int or_expand_eval(const or_net *big, const or_net *small, const char *fen, int mode,
                    or_eval *parent, uint16_t *moves, or_eval *children, int cap);

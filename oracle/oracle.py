@@ -20,15 +20,21 @@ NATIVE_LIB_PATH = os.path.join(HERE, "_build", "liboracle_native.so")
 
 MODE_FULL, MODE_BIG, MODE_SMALL = 0, 1, 2
 FLAG_IN_CHECK, FLAG_SMALLNET, FLAG_BAD_FEN, FLAG_REEVAL = 1, 2, 4, 8
+FLAG_MATE, FLAG_NO_SCORE, FLAG_SEARCHED, FLAG_NO_MOVES = 32, 64, 128, 256
 
 
 class OrEval(C.Structure):
-    _fields_ = [("psqt", C.c_int32), ("positional", C.c_int32),
-                ("final_v", C.c_int32), ("final_cp", C.c_int16), ("flags", C.c_uint16)]
+    _fields_ = [("psqt", C.c_int32), ("positional", C.c_int32), ("final_v", C.c_int32),
+                ("final_cp", C.c_int32), ("score", C.c_int32), ("flags", C.c_uint16), ("best_move", C.c_uint16)]
 
 
-EVAL_DTYPE = np.dtype([("psqt", "<i4"), ("positional", "<i4"),
-                       ("final_v", "<i4"), ("final_cp", "<i2"), ("flags", "<u2")])
+EVAL_DTYPE = np.dtype([("psqt", "<i4"), ("positional", "<i4"), ("final_v", "<i4"), ("final_cp", "<i4"),
+                       ("score", "<i4"), ("flags", "<u2"), ("best_move", "<u2")])
+assert EVAL_DTYPE.itemsize == C.sizeof(OrEval) == 24
+
+
+def _tup(e):
+    return (e.psqt, e.positional, e.final_v, e.final_cp, e.score, e.flags, e.best_move)
 
 _lib = None
 
@@ -121,7 +127,7 @@ def _h(net):
 def eval_fen(big, small, fen, mode=MODE_FULL):
     out = OrEval()
     lib().or_eval_fen(_h(big), _h(small), fen.encode(), mode, C.byref(out))
-    return (out.psqt, out.positional, out.final_v, out.final_cp, out.flags)
+    return _tup(out)
 
 
 def eval_fens(big, small, fens, mode=MODE_FULL, threads=1):
@@ -192,8 +198,7 @@ def expand_eval(big, small, fen, mode=MODE_FULL, incremental=False):
     n = f(_h(big), _h(small), fen.encode(), mode, C.byref(parent), moves, kids.ctypes.data, 256)
     if n < 0:
         raise ValueError("bad fen")
-    return ((parent.psqt, parent.positional, parent.final_v, parent.final_cp, parent.flags),
-            list(moves[:n]), kids[:n].copy())
+    return _tup(parent), list(moves[:n]), kids[:n].copy()
 
 
 def expand_eval_batch(big, small, fens, mode=MODE_FULL, incremental=True, threads=1, keep_children=False):

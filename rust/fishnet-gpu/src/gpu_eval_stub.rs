@@ -2,13 +2,22 @@
 //! same `go_multiple(Chunk) -> Result<Vec<PositionResponse>, ChunkFailed>` signature, so
 //! the worker's `tokio::select!` (src/main.rs:267-303) can call either.  Goes into
 //! fishnet's src/stockfish.rs (or a sibling module) beside StockfishStub.
+//!
+//! Every response carries a score, as Stockfish's `go` always prints one
+//! (stockfish.rs:366-368 rejects a response without one, and the queue's
+//! `PositionResponse::to_best` does `expect("got score")`, src/ipc.rs:56): the library
+//! scores every position it is given (include/gpu_nnue.h at gn_eval): checkmate
+//! `mate 0`, stalemate `cp 0`, a position in check by its in-check rule over the legal
+//! replies (depth 1, the reply as best move and pv), else the static evaluation's `cp`.
+//! This stub only maps those fields; a record without a score (a position the library
+//! refuses) fails the chunk like an engine error, never the queue.
 use std::{num::NonZeroU8, sync::Arc, time::Duration};
 
 use shakmaty::{fen::Fen, uci::UciMove, CastlingMode, Chess, EnPassantMode, Position as _};
 
 use crate::{
     api::Score,
-    gpu_nnue::GpuNnue,
+    gpu_nnue::{move_to_uci, GpuEval, GpuNnue},
     ipc::{Chunk, ChunkFailed, Matrix, Position, PositionResponse},
 };
 use gpu_nnue_sys as sys;
@@ -28,6 +37,18 @@ fn replay_to_fen(pos: &Position) -> Option<Fen> {
     Some(Fen::from_position(board, EnPassantMode::Legal))
 }
 
+/// The score Stockfish would print for the record (`score cp` / `score mate`), or None for a
+/// record the library could not score.
+pub fn score_of(e: &GpuEval) -> Option<Score> {
+    if e.flags & sys::GN_FLAG_NO_SCORE != 0 {
+        None
+    } else if e.flags & sys::GN_FLAG_MATE != 0 {
+        Some(Score::Mate(i64::from(e.score)))
+    } else {
+        Some(Score::Cp(i64::from(e.score)))
+    }
+}
+
 impl GpuEvalStub {
     pub fn new(nnue: Arc<GpuNnue>) -> GpuEvalStub {
         GpuEvalStub { nnue }
@@ -45,32 +66,37 @@ impl GpuEvalStub {
             .await
             .map_err(|_| ChunkFailed { batch_id })?
             .map_err(|_| ChunkFailed { batch_id })?; // GN_E_* -> ChunkFailed (the existing drop path)
-        Ok(chunk
+        chunk
             .positions
             .into_iter()
             .zip(evals)
             .map(|(pos, e)| {
+                // (positions with skip = true are the previous-position dummies the queue adds for
+                // hash warm-up, position_index None: scored like any other, their responses are
+                // dropped by QueueState::handle_position_responses, queue.rs:201-206)
+                let score = score_of(&e).ok_or(ChunkFailed { batch_id })?;
+                let searched = e.flags & sys::GN_FLAG_SEARCHED != 0;
+                let depth: u8 = if searched { 1 } else { 0 };
                 let mut scores = Matrix::new();
-                if pos.skip {
-                    // skipPositions: no score, as the UCI path leaves them
-                } else if e.flags & (sys::GN_FLAG_IN_CHECK | sys::GN_FLAG_BAD_FEN) == 0 {
-                    // static eval, no search: the centipawns Stockfish prints (UCIEngine::to_cp),
-                    // i.e. what stockfish.rs:419-427 parses from `score cp`
-                    scores.set(NonZeroU8::MIN, 0, Score::Cp(i64::from(e.final_cp)));
+                scores.set(NonZeroU8::MIN, depth, score);
+                let mut pvs = Matrix::new();
+                let best_move: Option<UciMove> = searched.then(|| move_to_uci(e.best_move));
+                if let Some(m) = &best_move {
+                    pvs.set(NonZeroU8::MIN, depth, vec![m.clone()]);
                 }
-                PositionResponse {
+                Ok(PositionResponse {
                     work: pos.work,
                     position_index: pos.position_index,
                     url: pos.url,
                     scores,
-                    pvs: Matrix::new(),
-                    best_move: None::<UciMove>,
-                    depth: 0,
+                    pvs,
+                    best_move,
+                    depth,
                     nodes: 1,
                     time: Duration::ZERO,
                     nps: None,
-                }
+                })
             })
-            .collect())
+            .collect()
     }
 }

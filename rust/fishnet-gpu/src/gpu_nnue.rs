@@ -17,7 +17,7 @@ use std::{
 };
 
 use gpu_nnue_sys as sys;
-use shakmaty::fen::Fen;
+use shakmaty::{fen::Fen, uci::UciMove, Role, Square};
 
 pub use sys::gn_eval as GpuEval;
 
@@ -97,7 +97,8 @@ impl GpuNnue {
     }
 
     /// evaluate_batch(&[Fen]) -> (psqt, positional, final_v, final_cp) per position,
-    /// side-to-move POV; final_cp is the `score cp` Stockfish would print.
+    /// side-to-move POV, plus the score fishnet posts (score / GN_FLAG_MATE / best_move:
+    /// checkmate, stalemate and checks included, include/gpu_nnue.h at gn_eval).
     pub fn evaluate_batch(&self, fens: &[Fen]) -> Result<Vec<GpuEval>, GpuError> {
         let owned: Vec<CString> = fens.iter().map(|f| CString::new(f.to_string()).unwrap()).collect();
         let ptrs: Vec<*const std::os::raw::c_char> = owned.iter().map(|c| c.as_ptr()).collect();
@@ -152,6 +153,17 @@ impl GpuNnue {
             r.children.truncate(nc);
             return Ok(r);
         }
+    }
+}
+
+/// A move in Stockfish's 16-bit encoding (gn_eval.best_move, child_moves) as the Chess960 UCI
+/// fishnet runs its engines with (castling = king takes rook, stockfish.rs:200).
+pub fn move_to_uci(m: u16) -> UciMove {
+    const PROMO: [Role; 4] = [Role::Knight, Role::Bishop, Role::Rook, Role::Queen];
+    UciMove::Normal {
+        from: Square::new(u32::from((m >> 6) & 63)),
+        to: Square::new(u32::from(m & 63)),
+        promotion: (m >> 14 == 1).then(|| PROMO[usize::from((m >> 12) & 3)]),
     }
 }
 

@@ -1,4 +1,4 @@
-//! gpu-nnue-sys — raw FFI of libgpu_nnue.so, 1:1 with `include/gpu_nnue.h` (ABI v2).
+//! gpu-nnue-sys — raw FFI of libgpu_nnue.so, 1:1 with `include/gpu_nnue.h` (ABI v3).
 //!
 //! fishnet's `src/main.rs:1` forbids unsafe code in the binary crate, so the FFI lives in
 //! this separate crate; the safe wrapper is `fishnet-gpu/src/gpu_nnue.rs`.  Every item here
@@ -8,7 +8,7 @@
 #![allow(non_camel_case_types)]
 use std::os::raw::{c_char, c_int, c_void};
 
-pub const GN_ABI_VERSION: c_int = 2;
+pub const GN_ABI_VERSION: c_int = 3;
 
 // return codes
 pub const GN_OK: c_int = 0;
@@ -44,17 +44,25 @@ pub const GN_FLAG_SMALLNET: u16 = 2;
 pub const GN_FLAG_BAD_FEN: u16 = 4;
 pub const GN_FLAG_REEVAL: u16 = 8;
 pub const GN_FLAG_SKIPPED: u16 = 16;
+pub const GN_FLAG_MATE: u16 = 32;
+pub const GN_FLAG_NO_SCORE: u16 = 64;
+pub const GN_FLAG_SEARCHED: u16 = 128;
+pub const GN_FLAG_NO_MOVES: u16 = 256;
 
 /// One result: NetworkOutput (psqt, positional) of the net that produced final_v,
-/// Eval::evaluate (internal units) and UCIEngine::to_cp (the `score cp` fishnet posts).
+/// Eval::evaluate (internal units), UCIEngine::to_cp, and the score fishnet posts for the
+/// position (`score cp` / `score mate` with GN_FLAG_MATE; the in-check rule's reply in
+/// best_move with GN_FLAG_SEARCHED; see the header at gn_eval).
 #[repr(C)]
 #[derive(Clone, Copy, Default, Debug, PartialEq, Eq)]
 pub struct gn_eval {
     pub psqt: i32,
     pub positional: i32,
     pub final_v: i32,
-    pub final_cp: i16,
+    pub final_cp: i32,
+    pub score: i32,
     pub flags: u16,
+    pub best_move: u16,
 }
 
 /// Packed position (32 bytes), the device input format.

@@ -148,7 +148,7 @@ def test_evaluate_games_vs_oracle(gpu_ctx, oracle_nets, oracle_lib, mode):
         got = o["evals"]
         for i in range(len(fens)):
             if i in skip:
-                assert tuple(got[i]) == (0, 0, 0, 0, G.FLAG_SKIPPED)
+                assert tuple(got[i]) == (0, 0, 0, 0, 0, G.FLAG_SKIPPED | G.FLAG_NO_SCORE, 0)
             else:
                 assert tuple(got[i]) == tuple(exp[i]), (fens[i], got[i], exp[i])
 
@@ -170,3 +170,49 @@ def test_evaluate_games_with_children_vs_oracle(gpu_ctx, oracle_nets, oracle_lib
             p_exp, m_exp, k_exp = oracle_lib.expand_eval(big, small, fen, 0)
             assert tuple(o["evals"][i]) == tuple(p_exp)
             assert dict(zip(cm.tolist(), map(tuple, ce.tolist()))) == dict(zip(m_exp, map(tuple, k_exp.tolist())))
+
+
+# games whose lines run into check, checkmate and stalemate
+FOOLS_MATE = "f2f3 e7e5 g2g4 d8h4"
+LOYD_STALEMATE = "e2e3 a7a5 d1h5 a8a6 h5a5 h7h5 h2h4 a6h6 a5c7 f7f6 c7d7 e8f7 d7b7 d8d3 b7b8 d3h7 b8c8 f7g6 c8e6"
+
+
+def uci_score(G, rec):
+    """The score GpuEvalStub posts for a record (rust/fishnet-gpu/src/gpu_eval_stub.rs): None
+    only for a record without one (skipped / bad position)."""
+    if rec["flags"] & G.FLAG_NO_SCORE:
+        return None
+    return ("mate" if rec["flags"] & G.FLAG_MATE else "cp", int(rec["score"]))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("children", [False, True])
+def test_every_game_position_scored(gpu_ctx, oracle_nets, oracle_lib, children):
+    """a8: every non-skipped position of a lichess batch gets the score fishnet
+    posts, checkmate -> mate 0, stalemate -> cp 0, checks by the in-check rule; equal to the
+    oracle's records, with and without children."""
+    from fishnet_amd import gpu_nnue as G
+    big, small = oracle_nets
+    rng = random.Random(2024)
+    games = [(START, FOOLS_MATE, []), (START, OPERA, [5]), (START, LOYD_STALEMATE, [0]),
+             (START, _random_game(oracle_lib, rng, START, 120), [])]
+    out = gpu_ctx.evaluate_games(games, 0, children=children)
+    seen = set()
+    for (root, moves, skip), o in zip(games, out):
+        assert o["status"] == 0
+        fens, _ = oracle_lib.replay_game(root, moves)
+        exp = oracle_lib.eval_fens(big, small, fens, 0)
+        for i, fen in enumerate(fens):
+            got = o["evals"][i]
+            if i in skip:
+                assert uci_score(G, got) is None
+                continue
+            assert tuple(got) == tuple(exp[i]), fen
+            s = uci_score(G, got)
+            assert s is not None, fen
+            if got["flags"] & G.FLAG_NO_MOVES:
+                seen.add("mate0" if s == ("mate", 0) else "stalemate" if s == ("cp", 0) else "?")
+            elif got["flags"] & G.FLAG_IN_CHECK:
+                assert got["flags"] & G.FLAG_SEARCHED and got["best_move"]
+                seen.add("check")
+    assert seen == {"mate0", "stalemate", "check"}

@@ -25,6 +25,16 @@ def random_fens(n, seed, max_plies=160):
     return [G.board_to_fen(b) for b in boards]
 
 
+STATIC = ["psqt", "positional", "final_v", "final_cp"]
+
+
+def static_part(rec):
+    """The static evaluation of a record (a child record and the same position's scored record
+    agree on it; the score fields differ by design, gpu_nnue.h at gn_eval)."""
+    r = np.asarray(rec)
+    return [tuple(int(x) for x in t) for t in r[STATIC].tolist()], (r["flags"] & 15).tolist()
+
+
 def _cmp(got, exp, fens):
     bad = np.nonzero(got != exp)[0]
     if len(bad):
@@ -58,6 +68,30 @@ def test_golden_vectors(gpu_ctx):
         fens = [r[0] for r in rows]
         exp = np.array([tuple(r[1:]) for r in rows], dtype=gpu_ctx.evaluate_batch([], mode).dtype)
         _cmp(gpu_ctx.evaluate_batch(fens, mode), exp, fens)
+
+
+def test_score_fixture_all_modes(gpu_ctx, oracle_nets, oracle_lib):
+    """The score rule (gpu_nnue.h at gn_eval) on checkmates, stalemates and in-check positions
+    whose replies are static, in check (searched one level down) or mating / mated: the
+    committed oracle records, the live oracle, and the same positions as expansion parents."""
+    from fishnet_amd import gpu_nnue as G
+    g = json.load(open(os.path.join(HERE, "golden", "score_fens.json")))
+    big, small = oracle_nets
+    for name, mode in (("full", 0), ("big", 1), ("small", 2)):
+        rows = g["results"][name]
+        fens = [r[0] for r in rows]
+        exp = np.array([tuple(r[1:]) for r in rows], dtype=G.EVAL_DTYPE)
+        _cmp(oracle_lib.eval_fens(big, small, fens, mode), exp, fens)
+        _cmp(gpu_ctx.evaluate_batch(fens, mode), exp, fens)
+        parents, offs, moves, kids = gpu_ctx.expand_and_evaluate(fens, mode)
+        _cmp(parents, exp, fens)
+        assert (kids["flags"] & G.FLAG_NO_SCORE).all() and not kids["score"].any()
+        searched = (exp["flags"] & G.FLAG_SEARCHED) != 0
+        assert searched.sum() >= 30 and (exp["flags"] & G.FLAG_NO_MOVES != 0).sum() >= 20
+    d_b, d_o = gpu_ctx.alloc(len(fens) * 32), gpu_ctx.alloc(len(fens) * G.EVAL_SIZE)
+    d_b.upload(G.pack_fens(fens)[0])
+    gpu_ctx.evaluate_device(d_b, len(fens), 2, d_o)  # the device API runs the rule too
+    _cmp(d_o.download(G.EVAL_DTYPE, len(fens)), exp, fens)
 
 
 def test_bad_fens_flagged(gpu_ctx):
@@ -118,8 +152,8 @@ def test_big_stress_net_chained_king_cache():
     ctx.random_games_device(0x5EED0000 + 99, 0, games, plies, d_b)
     ctx.synchronize()
     cap = 60 * n
-    bufs = {k: ctx.alloc(sz) for k, sz in (("po", n * 16), ("off", (n + 1) * 4), ("ch", cap * 32),
-                                              ("mv", cap * 2), ("co", cap * 16))}
+    bufs = {k: ctx.alloc(sz) for k, sz in (("po", n * G.EVAL_SIZE), ("off", (n + 1) * 4), ("ch", cap * 32),
+                                              ("mv", cap * 2), ("co", cap * G.EVAL_SIZE))}
 
     def run(k, kc):
         ctx.set_option(G.OPT_CHAIN, k)
@@ -139,7 +173,7 @@ def test_device_api_matches_host_api(gpu_ctx):
     boards = G.random_positions(42, 1000, 4099, 160)
     fens = [G.board_to_fen(b) for b in boards]
     d_b = gpu_ctx.alloc(boards.nbytes)
-    d_o = gpu_ctx.alloc(len(boards) * 16)
+    d_o = gpu_ctx.alloc(len(boards) * G.EVAL_SIZE)
     d_b.upload(boards)
     for mode in (0, 1, 2):
         gpu_ctx.evaluate_device(d_b, len(boards), mode, d_o)
@@ -207,8 +241,8 @@ def test_expand_device_matches_host(gpu_ctx):
     fens = [G.board_to_fen(b) for b in boards]
     hp, hoffs, hmoves, hkids = gpu_ctx.expand_and_evaluate(fens, 0)
     n, cap = len(boards), int(hoffs[-1])
-    bufs = {k: gpu_ctx.alloc(sz) for k, sz in (("b", n * 32), ("po", n * 16), ("off", (n + 1) * 4),
-                                                  ("ch", cap * 32), ("mv", cap * 2), ("co", cap * 16))}
+    bufs = {k: gpu_ctx.alloc(sz) for k, sz in (("b", n * 32), ("po", n * G.EVAL_SIZE), ("off", (n + 1) * 4),
+                                                  ("ch", cap * 32), ("mv", cap * 2), ("co", cap * G.EVAL_SIZE))}
     bufs["b"].upload(boards)
     total = gpu_ctx.expand_device(bufs["b"], n, 0, bufs["po"], bufs["off"], bufs["ch"], bufs["mv"], bufs["co"], cap)
     assert total == cap
@@ -254,7 +288,7 @@ def test_locality_options_do_not_change_results(gpu_ctx, swz, ksort):
     from fishnet_amd import gpu_nnue as G
     boards = G.random_positions(3, 0, 5003, 160)
     boards[17] = np.zeros(1, dtype=G.BOARD_DTYPE)  # an invalid board mixed in
-    d_b, d_o = gpu_ctx.alloc(boards.nbytes), gpu_ctx.alloc(len(boards) * 16)
+    d_b, d_o = gpu_ctx.alloc(boards.nbytes), gpu_ctx.alloc(len(boards) * G.EVAL_SIZE)
     d_b.upload(boards)
     ref = {}
     for mode in (0, 1, 2):
@@ -293,8 +327,8 @@ def test_chained_walk_matches_refresh_and_oracle(gpu_ctx, oracle_nets, oracle_li
     gpu_ctx.synchronize()
     boards = d_b.download(G.BOARD_DTYPE, n)
     cap = 60 * n
-    bufs = {k: gpu_ctx.alloc(sz) for k, sz in (("po", n * 16), ("off", (n + 1) * 4), ("ch", cap * 32),
-                                                  ("mv", cap * 2), ("co", cap * 16))}
+    bufs = {k: gpu_ctx.alloc(sz) for k, sz in (("po", n * G.EVAL_SIZE), ("off", (n + 1) * 4), ("ch", cap * 32),
+                                                  ("mv", cap * 2), ("co", cap * G.EVAL_SIZE))}
 
     def run(k):
         gpu_ctx.set_option(G.OPT_CHAIN, k)
@@ -369,8 +403,8 @@ def test_chained_walk_at_bench_scale(gpu_ctx, oracle_nets, oracle_lib):
     gpu_ctx.random_games_device(0x5EED0000 + 4200, 0, games, plies, d_b)
     gpu_ctx.synchronize()
     _, total, _, _ = gpu_ctx.time_expand_device(d_b, n, 1, 1)
-    out = {"po": gpu_ctx.alloc(n * 16), "off": gpu_ctx.alloc((n + 1) * 4), "mv": gpu_ctx.alloc(total * 2),
-           "co": gpu_ctx.alloc(total * 16), "cap": total}
+    out = {"po": gpu_ctx.alloc(n * G.EVAL_SIZE), "off": gpu_ctx.alloc((n + 1) * 4), "mv": gpu_ctx.alloc(total * 2),
+           "co": gpu_ctx.alloc(total * G.EVAL_SIZE), "cap": total}
 
     def run(k, kc):
         gpu_ctx.set_option(G.OPT_CHAIN, k)
@@ -378,7 +412,7 @@ def test_chained_walk_at_bench_scale(gpu_ctx, oracle_nets, oracle_lib):
         _, t, _, rows = gpu_ctx.time_expand_device(d_b, n, 1, 1, outputs=out)
         assert t == total
         return tuple(gpu_ctx.checksum_device(out[b], nb) for b, nb in
-                     (("po", n * 16), ("off", (n + 1) * 4), ("mv", t * 2), ("co", t * 16))), rows
+                     (("po", n * G.EVAL_SIZE), ("off", (n + 1) * 4), ("mv", t * 2), ("co", t * G.EVAL_SIZE))), rows
 
     try:
         plain, rows_plain = run(1, 0)
@@ -411,7 +445,7 @@ def test_small_net_one_million_vs_oracle(gpu_ctx, oracle_nets, oracle_lib):
     against the multithreaded oracle."""
     from fishnet_amd import gpu_nnue as G
     n = 1 << 20
-    d_b, d_o = gpu_ctx.alloc(n * 32), gpu_ctx.alloc(n * 16)
+    d_b, d_o = gpu_ctx.alloc(n * 32), gpu_ctx.alloc(n * G.EVAL_SIZE)
     gpu_ctx.random_positions_device(0x5EED0000, 0, n, 160, d_b)
     gpu_ctx.evaluate_device(d_b, n, G.MODE_SMALL, d_o)
     gpu_ctx.synchronize()
@@ -464,7 +498,7 @@ def test_caller_stream_and_context_stream_do_not_race(gpu_ctx):
     import ctypes
     from fishnet_amd import gpu_nnue as G
     n = 1 << 18
-    bufs = [(gpu_ctx.alloc(n * 32), gpu_ctx.alloc(n * 16)) for _ in range(2)]
+    bufs = [(gpu_ctx.alloc(n * 32), gpu_ctx.alloc(n * G.EVAL_SIZE)) for _ in range(2)]
     for k, (d_b, _) in enumerate(bufs):
         gpu_ctx.random_positions_device(100 + k, 0, n, 160, d_b)
     exp = []
@@ -557,7 +591,7 @@ def test_nets_from_asset_archive(gpu_ctx, synth_big_path, synth_small_path, tmp_
 def _expand2(ctx, d_b, n, mode):
     """gn_expand2_device with buffers sized by its own E_CAPACITY replies."""
     from fishnet_amd import gpu_nnue as G
-    out = {"po": ctx.alloc(n * 16), "off": ctx.alloc((n + 1) * 4), "cap": 0, "gcap": 0}
+    out = {"po": ctx.alloc(n * G.EVAL_SIZE), "off": ctx.alloc((n + 1) * 4), "cap": 0, "gcap": 0}
     for _ in range(3):
         try:
             t, g = ctx.expand2_device(d_b, n, mode, out)
@@ -568,9 +602,9 @@ def _expand2(ctx, d_b, n, mode):
             t, g = e.need
             if t > out["cap"]:
                 out.update(cap=t, ch=ctx.alloc(max(t, 1) * 32), mv=ctx.alloc(max(t, 1) * 2),
-                           co=ctx.alloc(max(t, 1) * 16), goff=ctx.alloc((t + 1) * 4))
+                           co=ctx.alloc(max(t, 1) * G.EVAL_SIZE), goff=ctx.alloc((t + 1) * 4))
             if g > out["gcap"]:
-                out.update(gcap=g, gmv=ctx.alloc(max(g, 1) * 2), gco=ctx.alloc(max(g, 1) * 16))
+                out.update(gcap=g, gmv=ctx.alloc(max(g, 1) * 2), gco=ctx.alloc(max(g, 1) * G.EVAL_SIZE))
     raise AssertionError("sizing did not converge")
 
 
@@ -597,14 +631,14 @@ def test_grandchildren_vs_depth1_and_oracle(gpu_ctx, oracle_nets, oracle_lib, mo
     goff = out["goff"].download(np.uint32, t + 1)
     gmv, gco = out["gmv"].download(np.uint16, g), out["gco"].download(G.EVAL_DTYPE, g)
     # level 1 == gn_expand_device
-    b1 = {k: gpu_ctx.alloc(sz) for k, sz in (("po", n * 16), ("off", (n + 1) * 4), ("ch", t * 32), ("mv", t * 2),
-                                              ("co", t * 16))}
+    b1 = {k: gpu_ctx.alloc(sz) for k, sz in (("po", n * G.EVAL_SIZE), ("off", (n + 1) * 4), ("ch", t * 32), ("mv", t * 2),
+                                              ("co", t * G.EVAL_SIZE))}
     assert gpu_ctx.expand_device(d_b, n, mode, b1["po"], b1["off"], b1["ch"], b1["mv"], b1["co"], t) == t
     assert np.array_equal(b1["po"].download(G.EVAL_DTYPE, n), po)
     assert np.array_equal(b1["co"].download(G.EVAL_DTYPE, t), co)
     # level 2 == depth 1 of the children with refresh-started parents (no chain, no cache)
-    b2 = {k: gpu_ctx.alloc(sz) for k, sz in (("po", t * 16), ("off", (t + 1) * 4), ("ch", g * 32), ("mv", g * 2),
-                                              ("co", g * 16))}
+    b2 = {k: gpu_ctx.alloc(sz) for k, sz in (("po", t * G.EVAL_SIZE), ("off", (t + 1) * 4), ("ch", g * 32), ("mv", g * 2),
+                                              ("co", g * G.EVAL_SIZE))}
     try:
         gpu_ctx.set_option(G.OPT_CHAIN, 1)
         gpu_ctx.set_option(G.OPT_KING_CACHE, 0)
@@ -612,7 +646,7 @@ def test_grandchildren_vs_depth1_and_oracle(gpu_ctx, oracle_nets, oracle_lib, mo
     finally:
         gpu_ctx.set_option(G.OPT_CHAIN, 81)
         gpu_ctx.set_option(G.OPT_KING_CACHE, 1)
-    assert np.array_equal(b2["po"].download(G.EVAL_DTYPE, t), co)
+    assert static_part(b2["po"].download(G.EVAL_DTYPE, t)) == static_part(co)  # scored positions vs child records
     assert np.array_equal(b2["off"].download(np.uint32, t + 1), goff)
     assert np.array_equal(b2["mv"].download(np.uint16, g), gmv)
     assert np.array_equal(b2["co"].download(G.EVAL_DTYPE, g), gco)
@@ -623,7 +657,8 @@ def test_grandchildren_vs_depth1_and_oracle(gpu_ctx, oracle_nets, oracle_lib, mo
     for j in np.unique(np.concatenate([rng.choice(t, size=min(200, t), replace=False), np.arange(40)])):
         fen = G.board_to_fen(children[j])
         p_exp, m_exp, k_exp = oracle_lib.expand_eval(big, small, fen, mode)
-        assert tuple(co[j]) == p_exp, fen
+        assert static_part(co[j:j + 1]) == static_part(np.array([p_exp], dtype=G.EVAL_DTYPE)), fen
+        assert co[j]["flags"] & G.FLAG_NO_SCORE
         lo, hi = int(goff[j]), int(goff[j + 1])
         assert {int(m): tuple(x) for m, x in zip(gmv[lo:hi], gco[lo:hi])} == \
                {int(m): tuple(x) for m, x in zip(m_exp, k_exp)}, fen

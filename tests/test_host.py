@@ -28,11 +28,11 @@ def test_library_exports_every_header_symbol(G):
     for s in syms:
         assert hasattr(lib, s), s
     assert sorted(G.EXPORTS) == syms
-    assert lib.gn_abi_version() == 2
+    assert lib.gn_abi_version() == G.ABI_VERSION == 3
 
 
 def test_structs_match_header(G):
-    assert G.BOARD_DTYPE.itemsize == 32 and G.EVAL_DTYPE.itemsize == 16
+    assert G.BOARD_DTYPE.itemsize == 32 and G.EVAL_DTYPE.itemsize == 24
     p = G.default_eval_params()
     assert (p.small_net_threshold, p.psqt_weight, p.positional_weight, p.reeval_threshold) == (962, 125, 131, 236)
     assert (p.complexity_div_big, p.material_pawn_big, p.material_base, p.rule50_div) == (18000, 535, 77777, 212)
@@ -65,7 +65,7 @@ def test_random_positions_deterministic_and_legal(G, oracle_lib):
     for brd in a:
         fen = G.board_to_fen(brd)
         assert oracle_lib.normalize_fen(fen) == fen
-        assert oracle_lib.eval_fen(None, None, fen, 3)[-1] & oracle_lib.FLAG_BAD_FEN == 0
+        assert oracle_lib.eval_fen(None, None, fen, 3)[5] & oracle_lib.FLAG_BAD_FEN == 0
         assert len(oracle_lib.legal_moves(fen)) > 0 or True
 
 

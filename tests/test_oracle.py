@@ -77,8 +77,8 @@ def test_goldens_regenerate_identically(oracle_lib, oracle_nets, synth_big_path,
 
 def test_goldens_cover_every_branch():
     g = json.load(open(os.path.join(HERE, "golden", "eval_goldens.json")))
-    assert g["columns"][-1] == "flags"
-    flags = [r[-1] for r in g["results"]["full"]]
+    fi = g["columns"].index("flags")
+    flags = [r[fi] for r in g["results"]["full"]]
     assert any(f & 1 for f in flags) and any(f & 2 for f in flags) and any(f & 8 for f in flags)
     assert any(f & 10 == 0 for f in flags)
 
@@ -248,3 +248,81 @@ def test_oracle_under_sanitizers(oracle_lib, tmp_path):
         assert (n, s) == (len(kids), int(kids["final_v"].astype(np.int64).sum())), fen
         assert p2 == oracle_lib.perft(fen, 2), fen
     assert lines[len(fens) - 1] == "bad"
+
+
+# ---- the score rule (include/gpu_nnue.h at gn_eval; tests/golden/score_fens.json) -------
+def _score_doc():
+    return json.load(open(os.path.join(HERE, "golden", "score_fens.json")))
+
+
+def test_score_goldens_regenerate_identically(oracle_lib, oracle_nets, synth_big_path, synth_small_path):
+    g = _score_doc()
+    sha = lambda p: hashlib.sha256(open(p, "rb").read()).hexdigest()
+    assert g["nets"]["big"]["sha256"] == sha(synth_big_path)
+    assert g["nets"]["small"]["sha256"] == sha(synth_small_path)
+    big, small = oracle_nets
+    for name, mode in (("full", 0), ("big", 1), ("small", 2)):
+        rows = g["results"][name]
+        got = oracle_lib.eval_fens(big, small, [r[0] for r in rows], mode, threads=4)
+        assert [list(map(int, r)) for r in got.tolist()] == [r[1:] for r in rows]
+
+
+def test_score_categories_mean_what_they_say(oracle_lib):
+    """Each fixture category has the score fishnet would post: mate 0 / cp 0 without a legal
+    move, a searched cp or mate in check, best_move a legal reply."""
+    O = oracle_lib
+    g = _score_doc()
+    cats, cols = g["categories"], g["columns"]
+    rec = {r[0]: dict(zip(cols[1:], r[1:])) for r in g["results"]["full"]}
+    assert {k for k, v in cats.items() if v} == {"mate0", "stalemate", "searched_d1", "searched_d2", "mate+", "mate-"}
+    for k, fens in cats.items():
+        for fen in fens:
+            r = rec[fen]
+            moves = O.legal_moves(fen)
+            if k in ("mate0", "stalemate"):
+                assert not moves and r["flags"] & O.FLAG_NO_MOVES and r["score"] == 0 and r["best_move"] == 0
+                assert bool(r["flags"] & O.FLAG_MATE) == (k == "mate0") == bool(r["flags"] & O.FLAG_IN_CHECK)
+            else:
+                assert moves and r["flags"] & O.FLAG_IN_CHECK and r["flags"] & O.FLAG_SEARCHED
+                assert r["best_move"] in moves
+                assert bool(r["flags"] & O.FLAG_MATE) == k.startswith("mate")
+                if k == "mate+":
+                    assert r["score"] >= 1
+                if k == "mate-":
+                    assert r["score"] <= -1
+
+
+def py_rule_value(O, small, fen, depth):
+    """Second restatement of the rule (negamax over oracle primitives, in Python)."""
+    e = O.eval_fen(None, small, fen, O.MODE_SMALL)
+    moves = O.legal_moves(fen)
+    check = e[5] & O.FLAG_IN_CHECK
+    if not moves:
+        return (-32000 if check else 0), None
+    if not check or depth == 0:
+        return e[2], None
+    best = None
+    for m in sorted(moves):  # ties: the smaller move encoding (strict > keeps the first)
+        v = -py_rule_value(O, small, O.child_fen(fen, m), depth - 1)[0]
+        v = v - 1 if v >= 31754 else v + 1 if v <= -31754 else v
+        if best is None or v > best[0]:
+            best = (v, m)
+    return best
+
+
+def test_score_rule_restated_in_python(oracle_lib, oracle_nets):
+    O = oracle_lib
+    _, small = oracle_nets
+    g = _score_doc()
+    cols = g["columns"]
+    for row in g["results"]["small"]:
+        r = dict(zip(cols[1:], row[1:]))
+        if not r["flags"] & O.FLAG_SEARCHED:
+            continue
+        v, m = py_rule_value(O, small, row[0], 2)
+        assert m == r["best_move"], row[0]
+        if r["flags"] & O.FLAG_MATE:
+            ply = 32000 - abs(v)
+            assert r["score"] == ((ply + 1) // 2 if v > 0 else -(ply // 2)), row[0]
+        else:
+            assert r["score"] == py_to_cp(v, row[0]), row[0]
