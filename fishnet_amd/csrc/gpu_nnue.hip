@@ -215,12 +215,13 @@ struct Dev {
   DevBuf<uint64_t> ebound, eoff;
   DevBuf<uint64_t> ent;           // the planned expansion's row entries (stream.hip)
   DevBuf<uint32_t> pool, perr;
+  DevBuf<unsigned long long> pstat; // no-op entries the last planned expansion's plan inserted (GN_SCR_GAP)
   DevBuf<TileDesc> tiles;
   DevBuf<uint32_t> btiles; // tiles per block of the planned expansion
   DevBuf<uint16_t> bkeys, bkeys2; // block_order scratch
   DevBuf<uint32_t> bidx, border;  // block_order: identity, then the order
   uint64_t etot = 0;        // eoff[n] of the current expansion
-  bool planned = false;     // the last expansion ran the planned kernels (perr is meaningful)
+  bool planned = false;     // the last expansion runs the planned kernels (perr is meaningful)
   void *scan_tmp = nullptr;
   size_t scan_bytes = 0;
   // Cross-stream ordering of the library-owned scratch above: every launch sequence
@@ -228,16 +229,6 @@ struct Dev {
   // caller stream and return while their kernels are still queued).
   hipEvent_t done = nullptr;
   hipStream_t done_on = nullptr;
-  // The planned expansion runs as a pipeline of block ranges on two library streams
-  // (range c + 1's child generation and plan overlap range c's row stream); the caller's
-  // stream forks to them at go and joins them at join[].
-  hipStream_t aux[2] = {nullptr, nullptr};
-  hipEvent_t go = nullptr, join[2] = {nullptr, nullptr};
-  // generate_children(defer = true): write_children is left to the pipeline
-  bool defer_write = false;
-  gn_board *dw_children = nullptr;
-  uint16_t *dw_moves = nullptr;
-  unsigned long long *dw_rows = nullptr;
   float plan_ms = 0, stream_ms = 0; // the last timed planned expansion (GN_STAT_PLAN_NS / _STREAM_NS)
   // the score rule's two levels of in-check replies (resolve_scores): selection, the selected
   // positions, their replies and the replies' records / rule values
@@ -253,8 +244,6 @@ struct Dev {
       boards.release(), children.release(), moves.release(), ce.release(), sv.release();
     }
   } lv[2];
-  static constexpr size_t MAX_CHUNKS = 4;
-  uint64_t cbound[MAX_CHUNKS + 1] = {}; // children offsets at the range boundaries
   std::mutex mu;
 };
 
@@ -388,13 +377,9 @@ static void destroy(gn_ctx *ctx) {
     d.kkeys.release(), d.kkeys2.release(), d.kidx.release(), d.kperm.release();
     d.nslot.release(), d.tickets.release(), d.ksnap.release();
     d.ebound.release(), d.eoff.release(), d.ent.release(), d.pool.release(), d.perr.release(), d.tiles.release(), d.btiles.release();
+    d.pstat.release();
     d.bkeys.release(), d.bkeys2.release(), d.bidx.release(), d.border.release();
     d.lv[0].release(), d.lv[1].release();
-    for (int i = 0; i < 2; ++i) {
-      if (d.aux[i]) (void)hipStreamSynchronize(d.aux[i]), (void)hipStreamDestroy(d.aux[i]);
-      if (d.join[i]) (void)hipEventDestroy(d.join[i]);
-    }
-    if (d.go) (void)hipEventDestroy(d.go);
     if (d.done) (void)hipEventDestroy(d.done);
     if (d.stream) (void)hipStreamDestroy(d.stream);
   }
@@ -435,11 +420,6 @@ static int create(const uint8_t *big, size_t big_len, const uint8_t *small, size
     HIP_TRY(hipSetDevice(id));
     HIP_TRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
     HIP_TRY(hipEventCreateWithFlags(&d.done, hipEventDisableTiming));
-    HIP_TRY(hipEventCreateWithFlags(&d.go, hipEventDisableTiming));
-    for (int i = 0; i < 2; ++i) {
-      HIP_TRY(hipStreamCreateWithFlags(&d.aux[i], hipStreamNonBlocking));
-      HIP_TRY(hipEventCreateWithFlags(&d.join[i], hipEventDisableTiming));
-    }
     HIP_TRY(hipMalloc(&d.tables, sizeof(Tables)));
     HIP_TRY(hipMemcpy(d.tables, &host_tables(), sizeof(Tables), hipMemcpyHostToDevice));
     for (int w = 0; w < 2; ++w)
@@ -556,42 +536,32 @@ static int chain_len(const gn_ctx *ctx, Dev &d, size_t n) {
   return (int)k;
 }
 
-// The big net's expansion runs planned (stream.hip) unless GN_STREAM=old selects the
-// round-1 single-kernel expand_stream (A/B timing); both give identical results.
-static bool plan_path(const gn_ctx *ctx, const Dev &d) {
+// The big net's expansion (modes FULL / BIG) runs planned (stream.hip) unless GN_STREAM=old
+// selects the round-1 single-kernel expand_stream (A/B timing); both give identical results.
+// (Round 2's pipeline of block ranges on two streams, range c + 1's child generation and plan
+// under range c's row stream, took the same time as the serial order, 296 vs 259 + 19 + 15.5
+// + 5 ms: the overlapped kernels slow the row stream by what they add; it was removed.)
+static bool plan_path(const gn_ctx *ctx, const Dev &d, int mode) {
   static const bool old = getenv("GN_STREAM") && !strcmp(getenv("GN_STREAM"), "old");
   static const bool legacy = getenv("GN_EXPAND_LEGACY") && atoi(getenv("GN_EXPAND_LEGACY"));
-  return !old && !legacy && ctx->incremental && d.has[BIG] && (d.net[BIG].L1 == 3072 || d.net[BIG].L1 == 1024);
+  return !old && !legacy && mode != GN_MODE_SMALL && ctx->incremental && d.has[BIG] &&
+         (d.net[BIG].L1 == 3072 || d.net[BIG].L1 == 1024);
 }
 
-// Block ranges of the planned expansion's pipeline (expand_evaluate), GN_EXPAND_CHUNKS
-// (<= 4; default 1).  Measured on the 49,152-game line: 4 ranges on two streams take the
-// same 296 ms as the serial 259 ms stream + 19 ms plan + 15.5 ms children + 5 ms finalize,
-// the overlapped kernels slowing the row stream by what they add (they share its CUs and
-// its L2), so the serial order is the default; the pipeline stays for A/B runs.
-static size_t expand_chunks(size_t nblk) {
-  static const int env = getenv("GN_EXPAND_CHUNKS") ? atoi(getenv("GN_EXPAND_CHUNKS")) : 1;
-  const size_t c = env > 0 ? (size_t)env : 1;
-  return std::max<size_t>(1, std::min<size_t>(std::min<size_t>(c, Dev::MAX_CHUNKS), std::max<size_t>(nblk, 1)));
-}
-
-// finalize of parents [pa, pb) and children [ca, cb) (their net outputs in the Dev buffers)
+// finalize of the n parents and total children (their net outputs in the Dev buffers)
 // (score_parents: the parents are positions with the score rule; the children are child records)
-static int finalize_range(gn_ctx *ctx, Dev &d, const gn_board *parents, const gn_board *children, int mode,
-                          gn_eval *parent_out, gn_eval *child_out, size_t pa, size_t pb, size_t ca, size_t cb,
-                          hipStream_t s, bool score_parents) {
-  auto o = [](auto *p, size_t k) { return p ? p + k : p; };
+static int finalize_all(gn_ctx *ctx, Dev &d, const gn_board *parents, const gn_board *children, int mode,
+                        gn_eval *parent_out, gn_eval *child_out, size_t n, size_t total, hipStream_t s,
+                        bool score_parents) {
   const gn_eval_params &P = ctx->P;
-  // children from their parents as write_children unpacked them (owner is relative to the
-  // range's first parent when the pipeline wrote the children range by range)
+  // children from their parents as write_children unpacked them
   const bool fast = d.child_moves != nullptr;
-  HIP_TRY(launch_finalize(children + ca, cb - ca, mode, o(d.osm.p, ca), o(d.obg.p, ca), o(d.nsm.p, ca), o(d.nbg.p, ca),
-                          P, d.tables, child_out + ca, s, 0, nullptr, fast ? d.owner.p + ca : nullptr,
-                          fast ? d.child_moves + ca : nullptr, fast ? d.unpacked.p + (d.defer_write ? pa : 0) : nullptr));
+  HIP_TRY(launch_finalize(children, total, mode, d.osm.p, d.obg.p, d.nsm.p, d.nbg.p, P, d.tables, child_out, s, 0,
+                          nullptr, fast ? d.owner.p : nullptr, fast ? d.child_moves : nullptr,
+                          fast ? d.unpacked.p : nullptr));
   if (parent_out) // the parents' legal-move counts are generate_children's
-    HIP_TRY(launch_finalize(parents + pa, pb - pa, mode, o(d.p_osm.p, pa), o(d.p_obg.p, pa), o(d.p_nsm.p, pa),
-                            o(d.p_nbg.p, pa), P, d.tables, parent_out + pa, s, score_parents ? 1 : 0,
-                            d.counts.p + pa));
+    HIP_TRY(launch_finalize(parents, n, mode, d.p_osm.p, d.p_obg.p, d.p_nsm.p, d.p_nbg.p, P, d.tables, parent_out, s,
+                            score_parents ? 1 : 0, d.counts.p));
   return GN_OK;
 }
 
@@ -609,13 +579,20 @@ static hipError_t count_children(Dev &d, const gn_board *parents, size_t n, hipS
   return hipSuccess;
 }
 
+// skip_internal: the planned big-net path reads no child board after this (finalize makes each
+// child from its unpacked parent and move), so library-internal child boards are not written.
 static int generate_children(Dev &d, const gn_board *parents, size_t n, gn_board *children_or_null, size_t cap,
                              uint16_t *moves, bool want_deltas, size_t *total, hipStream_t s, hipEvent_t *ev,
                              unsigned long long *rows = nullptr, int chain_k = 1, bool plan = false,
-                             bool defer = false) {
+                             bool skip_internal = false) {
   d.chain_k = want_deltas ? chain_k : 1;
   d.planned = want_deltas && plan;
-  d.defer_write = false;
+  if (d.planned) { // a stale error bit of an earlier expansion must not fail this one
+    HIP_TRY(d.perr.ensure(1));
+    HIP_TRY(d.pstat.ensure(1));
+    HIP_TRY(hipMemsetAsync(d.perr.p, 0, sizeof(uint32_t), s));
+    HIP_TRY(hipMemsetAsync(d.pstat.p, 0, sizeof(unsigned long long), s));
+  }
   if (d.chain_k > 1) {
     HIP_TRY(d.nslot.ensure(n));
     HIP_TRY(d.tickets.ensure(CARRY_SLOTS + 1));
@@ -636,26 +613,13 @@ static int generate_children(Dev &d, const gn_board *parents, size_t n, gn_board
   uint64_t t = 0;
   HIP_TRY(hipMemcpyAsync(&t, d.offsets.p + n, sizeof(t), hipMemcpyDeviceToHost, s));
   if (d.planned) HIP_TRY(hipMemcpyAsync(&d.etot, d.eoff.p + n, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
-  if (d.planned) { // children offsets at the pipeline's range boundaries (expand_evaluate)
-    const size_t K = (size_t)std::max(1, d.chain_k), nblk = (n + K - 1) / K, C = expand_chunks(nblk);
-    d.cbound[0] = 0;
-    for (size_t c = 1; c < C; ++c)
-      HIP_TRY(hipMemcpyAsync(&d.cbound[c], d.offsets.p + std::min(nblk * c / C * K, n), sizeof(uint64_t),
-                             hipMemcpyDeviceToHost, s));
-  }
   HIP_TRY(hipStreamSynchronize(s));
   *total = (size_t)t;
-  if (d.planned) {
-    const size_t K = (size_t)std::max(1, d.chain_k), nblk = (n + K - 1) / K;
-    d.cbound[expand_chunks(nblk)] = t;
-  }
   if (ev) HIP_TRY(hipEventRecord(ev[1], s));
   if ((children_or_null || moves) && t > cap) // caller-owned child buffers hold cap entries
     return fail(GN_E_CAPACITY, "%zu children exceed capacity %zu", (size_t)t, cap);
   gn_board *children = children_or_null;
-  // the planned big-net path reads no child board after this (finalize makes each child from
-  // its unpacked parent and move): library-internal boards are then not written at all
-  const bool skip_boards = !children_or_null && d.planned && defer;
+  const bool skip_boards = !children_or_null && d.planned && skip_internal;
   if (!children && !skip_boards) {
     HIP_TRY(d.frontier[1].ensure(std::max<size_t>(t, 1)));
     children = d.frontier[1].p;
@@ -668,10 +632,7 @@ static int generate_children(Dev &d, const gn_board *parents, size_t n, gn_board
     moves = d.moves_tmp.p;
   }
   d.child_moves = moves;
-  if (d.planned && defer && t && expand_chunks((n + d.chain_k - 1) / std::max(1, d.chain_k)) > 1) {
-    // expand_evaluate writes the children range by range, in its pipeline
-    d.defer_write = true, d.dw_children = children, d.dw_moves = moves, d.dw_rows = rows;
-  } else if (t) {
+  if (t) {
     HIP_TRY(launch_write_children(parents, n, d.tables, d.offsets.p, 0, t, children, moves, d.owner.p,
                                   want_deltas ? d.deltas.p : nullptr, d.chain_k > 1 ? d.nslot.p : nullptr, d.chain_k,
                                   rows, s, d.unpacked.p));
@@ -684,8 +645,7 @@ static int generate_children(Dev &d, const gn_board *parents, size_t n, gn_board
 // expand_eval kernels (one workgroup per parent, children from the parent
 // accumulators); otherwise every child is a full refresh (evaluate_on).
 // ev (optional) gets 5 events: after classify, after the small net (+reeval),
-// after the big net, after finalize, and (planned path) between its plan and stream
-// kernels (recorded before the pipeline when it runs in several ranges).
+// after the big net, after finalize, and (planned path) between its plan and stream kernels.
 // score_parents: the parents are positions (the score rule's static part; callers run
 // resolve_scores on them) rather than child records (depth 2's level 2).
 static int expand_evaluate(gn_ctx *ctx, Dev &d, const gn_board *parents, size_t n, const gn_board *children,
@@ -720,8 +680,6 @@ static int expand_evaluate(gn_ctx *ctx, Dev &d, const gn_board *parents, size_t 
   }
   auto mark = [&](int k) -> hipError_t { return ev ? hipEventRecord(ev[k], s) : hipSuccess; };
   const gn_eval_params &P = ctx->P;
-  bool piped = false;       // finalize ran inside the big net's pipeline
-  hipEvent_t mid = nullptr; // recorded between the plan and stream kernels (timing)
   const uint64_t *off = d.offsets.p;
   const ChildDelta *dl = d.deltas.p;
   if (mode == GN_MODE_FULL) {
@@ -748,17 +706,11 @@ static int expand_evaluate(gn_ctx *ctx, Dev &d, const gn_board *parents, size_t 
       HIP_TRY(d.tiles.ensure((n + total) / 16 + (K + 2) * nblk + 2));
       HIP_TRY(d.btiles.ensure(nblk + 1));
       HIP_TRY(d.pool.ensure(64));
-      HIP_TRY(d.perr.ensure(1));
-      HIP_TRY(hipMemsetAsync(d.perr.p, 0, sizeof(uint32_t), s));
       HIP_TRY(hipMemsetAsync(d.pool.p, 0, 64 * sizeof(uint32_t), s));
-      // block ranges as a pipeline: range c's row stream (memory-bound, the whole GPU)
-      // overlaps range c + 1's child generation and plan (latency-bound) and range c - 1's
-      // finalize; results do not depend on the split (every index is absolute)
-      const size_t C = expand_chunks(nblk);
-      // XCD-local block order (one range only: a range's order must stay inside it)
+      // XCD-local block order
       static const bool bsort = !getenv("GN_BLOCK_SORT") || atoi(getenv("GN_BLOCK_SORT"));
       const uint32_t *order = nullptr;
-      if (bsort && C == 1 && ctx->king_sort && nblk > 1) {
+      if (bsort && ctx->king_sort && nblk > 1) {
         HIP_TRY(d.bkeys.ensure(nblk));
         HIP_TRY(d.bkeys2.ensure(nblk));
         HIP_TRY(d.bidx.ensure(nblk));
@@ -767,44 +719,10 @@ static int expand_evaluate(gn_ctx *ctx, Dev &d, const gn_board *parents, size_t 
                             d.sort_tmp, d.sort_bytes, s));
         order = d.border.p;
       }
-      auto run = [&](size_t c, hipStream_t sc) -> int {
-        const size_t b0 = nblk * c / C, b1 = nblk * (c + 1) / C, pa = b0 * K, pb = std::min(b1 * K, n);
-        if (d.defer_write)
-          HIP_TRY(launch_write_children(parents + pa, pb - pa, d.tables, off + pa, d.cbound[c],
-                                        d.cbound[c + 1] - d.cbound[c], d.dw_children, d.dw_moves, d.owner.p,
-                                        d.deltas.p, d.chain_k > 1 ? d.nslot.p + pa : nullptr, d.chain_k, d.dw_rows,
-                                        sc, d.unpacked.p + pa));
-        HIP_TRY(launch_plan_stream(d.net[BIG], parents, n, off, dl, f ? d.p_nbg.p : nullptr, f ? d.nbg.p : nullptr,
-                                   d.p_obg.p, d.obg.p, ctx->swizzle & 1, d.chain_k > 1 ? d.nslot.p : nullptr,
-                                   d.chain_k, ctx->king_cache ? 1 : 0, d.eoff.p, d.ent.p, d.tiles.p, d.btiles.p,
-                                   d.pool.p, d.perr.p, rows_out, b0, b1, order, mid, sc));
-        if (C > 1) { // this range's finalize (after the join when not pipelined)
-          int rc = finalize_range(ctx, d, parents, children, mode, parent_out, child_out, pa, pb, d.cbound[c],
-                                  d.cbound[c + 1], sc, score_parents);
-          if (rc) return rc;
-        }
-        return GN_OK;
-      };
-      mid = ev ? ev[4] : nullptr;
-      if (C == 1 && !d.defer_write) {
-        int rc = run(0, s);
-        if (rc) return rc;
-      } else {
-        if (mid) HIP_TRY(hipEventRecord(mid, s));
-        mid = nullptr;
-        HIP_TRY(hipEventRecord(d.go, s));
-        for (int i = 0; i < 2; ++i) HIP_TRY(hipStreamWaitEvent(d.aux[i], d.go, 0));
-        for (size_t c = 0; c < C; ++c) {
-          int rc = run(c, d.aux[c & 1]);
-          if (rc) return rc;
-        }
-        for (int i = 0; i < 2; ++i) {
-          HIP_TRY(hipEventRecord(d.join[i], d.aux[i]));
-          HIP_TRY(hipStreamWaitEvent(s, d.join[i], 0));
-        }
-        d.defer_write = false;
-        if (C > 1) piped = true;
-      }
+      HIP_TRY(launch_plan_stream(d.net[BIG], parents, n, off, dl, f ? d.p_nbg.p : nullptr, f ? d.nbg.p : nullptr,
+                                 d.p_obg.p, d.obg.p, ctx->swizzle & 1, d.chain_k > 1 ? d.nslot.p : nullptr, d.chain_k,
+                                 ctx->king_cache ? 1 : 0, d.eoff.p, d.ent.p, d.tiles.p, d.btiles.p, d.pool.p, d.perr.p,
+                                 rows_out, d.pstat.p, 0, nblk, order, ev ? ev[4] : nullptr, s));
     } else {
       HIP_TRY(launch_expand_net(d.net[BIG], parents, n, off, children, dl, f ? d.p_nbg.p : nullptr,
                                 f ? d.nbg.p : nullptr, d.p_obg.p, d.obg.p, ctx->swizzle & 1,
@@ -813,10 +731,8 @@ static int expand_evaluate(gn_ctx *ctx, Dev &d, const gn_board *parents, size_t 
     }
   }
   HIP_TRY(mark(2));
-  if (!piped) {
-    int rc = finalize_range(ctx, d, parents, children, mode, parent_out, child_out, 0, n, 0, total, s, score_parents);
-    if (rc) return rc;
-  }
+  int rc = finalize_all(ctx, d, parents, children, mode, parent_out, child_out, n, total, s, score_parents);
+  if (rc) return rc;
   HIP_TRY(mark(3));
   return GN_OK;
 }
@@ -832,8 +748,15 @@ static int expand_evaluate(gn_ctx *ctx, Dev &d, const gn_board *parents, size_t 
 // Stockfish has no static evaluation in check (Eval::evaluate asserts !checkers) and
 // always prints a score from its search; fishnet requires one for every analysed
 // position (/root/reference/src/stockfish.rs:366-368, src/ipc.rs:56).
+// replies (optional, an expansion's parents): every position's legal replies are already
+// evaluated (child records / moves at d.offsets, the parents unpacked in d.unpacked); they are
+// reused instead of generated and evaluated again.
+struct Replies {
+  const gn_eval *rec;
+  const uint16_t *moves;
+};
 static int resolve_scores(gn_ctx *ctx, Dev &d, const gn_board *boards, size_t n, int mode, gn_eval *out,
-                          int32_t *sv_out, hipStream_t s, int depth = 2) {
+                          int32_t *sv_out, hipStream_t s, int depth = 2, const Replies *replies = nullptr) {
   if (!n || depth <= 0 || !out) return GN_OK;
   Dev::ScoreLevel &L = d.lv[2 - depth];
   HIP_TRY(L.sel.ensure(n + 1));
@@ -849,6 +772,21 @@ static int resolve_scores(gn_ctx *ctx, Dev &d, const gn_board *boards, size_t n,
   HIP_TRY(L.counts.ensure(m + 1));
   HIP_TRY(L.offsets.ensure(m + 1));
   HIP_TRY(launch_score_gather(boards, L.sel.p, L.pos.p, n, L.idx.p, L.boards.p, s));
+  if (replies) {
+    uint64_t t = 0;
+    HIP_TRY(launch_score_replies(L.idx.p, m, d.offsets.p, L.counts.p, L.offsets.p, d.scan_tmp, d.scan_bytes, &t, s));
+    HIP_TRY(L.moves.ensure(std::max<uint64_t>(t, 1)));
+    HIP_TRY(L.children.ensure(std::max<uint64_t>(t, 1)));
+    HIP_TRY(L.ce.ensure(std::max<uint64_t>(t, 1)));
+    HIP_TRY(L.sv.ensure(std::max<uint64_t>(t, 1)));
+    HIP_TRY(launch_score_replies_fill(L.idx.p, m, d.offsets.p, L.offsets.p, replies->rec, replies->moves, d.unpacked.p,
+                                      d.tables, L.ce.p, L.children.p, L.moves.p, s));
+    int rc = resolve_scores(ctx, d, L.children.p, t, mode, L.ce.p, L.sv.p, s, depth - 1);
+    if (rc) return rc;
+    HIP_TRY(launch_score_reduce(L.boards.p, m, L.idx.p, L.offsets.p, L.moves.p, L.ce.p, L.sv.p, ctx->P, out, sv_out,
+                                s));
+    return GN_OK;
+  }
   HIP_TRY(hipMemsetAsync(L.counts.p + m, 0, sizeof(uint64_t), s));
   HIP_TRY(launch_count_children(L.boards.p, m, d.tables, L.counts.p, s));
   HIP_TRY(exclusive_scan_u64(L.counts.p, L.offsets.p, m + 1, d.scan_tmp, d.scan_bytes, s));
@@ -1029,13 +967,14 @@ static int expand_boards_host(gn_ctx *ctx, const gn_board *boards, size_t n, int
       HIP_TRY(d.moves.ensure(std::max<size_t>(tk, 1)));
       size_t t = 0;
       int r = generate_children(d, d.io_boards.p, m, nullptr, d.moves.cap, d.moves.p, ctx->incremental, &t, s, nullptr,
-                                nullptr, chain_len(ctx, d, m), plan_path(ctx, d), mode == GN_MODE_BIG);
+                                nullptr, chain_len(ctx, d, m), plan_path(ctx, d, mode), mode == GN_MODE_BIG);
       if (r) return r;
       if (t != tk) return fail(GN_E_HIP, "child count changed between passes (%zu != %zu)", t, tk);
       HIP_TRY(d.io_out.ensure(m));
       HIP_TRY(d.io_out2.ensure(std::max<size_t>(t, 1)));
       r = expand_evaluate(ctx, d, d.io_boards.p, m, d.frontier[1].p, t, mode, d.io_out.p, d.io_out2.p, s, nullptr);
-      if (!r) r = resolve_scores(ctx, d, d.io_boards.p, m, mode, d.io_out.p, nullptr, s);
+      const Replies rp{d.io_out2.p, d.moves.p}; // the replies this expansion evaluated
+      if (!r) r = resolve_scores(ctx, d, d.io_boards.p, m, mode, d.io_out.p, nullptr, s, 2, &rp);
       if (r) return r;
       if (t) {
         HIP_TRY(hipMemcpyAsync(child_out + base[k], d.io_out2.p, t * sizeof(gn_eval), hipMemcpyDeviceToHost, s));
@@ -1658,7 +1597,7 @@ int gn_expand_device(gn_ctx *ctx, int device_slot, const gn_board *d_parents, si
   if (!d_children || !d_moves || !d_child_out) return fail(GN_E_INVALID, "NULL child buffer");
   size_t t = 0;
   int rc = generate_children(*d, d_parents, n, d_children, cap, d_moves, ctx->incremental, &t, s, nullptr, nullptr,
-                             chain_len(ctx, *d, n), plan_path(ctx, *d), mode == GN_MODE_BIG);
+                             chain_len(ctx, *d, n), plan_path(ctx, *d, mode), mode == GN_MODE_BIG);
   *total = t;
   if (t > 0xFFFFFFFFull) return fail(GN_E_CAPACITY, "%zu children exceed 32-bit offsets", t);
   HIP_TRY(launch_offsets_u32(d->offsets.p, n + 1, d_offsets, s));
@@ -1667,7 +1606,8 @@ int gn_expand_device(gn_ctx *ctx, int device_slot, const gn_board *d_parents, si
     return rc;
   }
   rc = expand_evaluate(ctx, *d, d_parents, n, d_children, t, mode, d_parent_out, d_child_out, s, nullptr);
-  if (!rc) rc = resolve_scores(ctx, *d, d_parents, n, mode, d_parent_out, nullptr, s);
+  const Replies rp{d_child_out, d_moves}; // the replies this expansion evaluated
+  if (!rc) rc = resolve_scores(ctx, *d, d_parents, n, mode, d_parent_out, nullptr, s, 2, &rp);
   if (rc) return rc;
   HIP_TRY(hipStreamSynchronize(s));
   return check_plan(*d, s);
@@ -1703,7 +1643,7 @@ int gn_expand2_device(gn_ctx *ctx, int device_slot, const gn_board *d_parents, s
   }
   // level 1
   int rc = generate_children(*d, d_parents, n, d_children, cap, d_moves, ctx->incremental, &t, s, nullptr, nullptr,
-                             chain_len(ctx, *d, n), plan_path(ctx, *d), mode == GN_MODE_BIG);
+                             chain_len(ctx, *d, n), plan_path(ctx, *d, mode), mode == GN_MODE_BIG);
   *total = t;
   if (t > 0xFFFFFFFFull) return fail(GN_E_CAPACITY, "%zu children exceed 32-bit offsets", t);
   HIP_TRY(launch_offsets_u32(d->offsets.p, n + 1, d_offsets, s));
@@ -1715,7 +1655,8 @@ int gn_expand2_device(gn_ctx *ctx, int device_slot, const gn_board *d_parents, s
   if (rc) return rc;
   HIP_TRY(hipStreamSynchronize(s));
   if ((rc = check_plan(*d, s)) != GN_OK) return rc;
-  if ((rc = resolve_scores(ctx, *d, d_parents, n, mode, d_parent_out, nullptr, s)) != GN_OK) return rc;
+  const Replies rp{d_child_out, d_moves}; // level 1's replies
+  if ((rc = resolve_scores(ctx, *d, d_parents, n, mode, d_parent_out, nullptr, s, 2, &rp)) != GN_OK) return rc;
   if (!t) {
     HIP_TRY(hipMemsetAsync(d_goffsets, 0, sizeof(uint32_t), s));
     HIP_TRY(hipStreamSynchronize(s));
@@ -1729,7 +1670,7 @@ int gn_expand2_device(gn_ctx *ctx, int device_slot, const gn_board *d_parents, s
     return g ? fail(GN_E_CAPACITY, "%zu grandchildren exceed capacity %zu", g, gcap) : GN_OK;
   }
   rc = generate_children(*d, d_children, t, nullptr, gcap, d_gmoves, ctx->incremental, &g, s, nullptr, nullptr,
-                         chain_len(ctx, *d, t), plan_path(ctx, *d), mode == GN_MODE_BIG);
+                         chain_len(ctx, *d, t), plan_path(ctx, *d, mode), mode == GN_MODE_BIG);
   *gtotal = g;
   if (g > 0xFFFFFFFFull) return fail(GN_E_CAPACITY, "%zu grandchildren exceed 32-bit offsets", g);
   HIP_TRY(launch_offsets_u32(d->offsets.p, t + 1, d_goffsets, s));
@@ -1789,7 +1730,7 @@ int gn_time_expand_device(gn_ctx *ctx, int device_slot, const gn_board *d_parent
     if (he != hipSuccess) break;
     // rows by write_children's formula only when no planned row stream counts them (a
     // per-wave atomic over every child would sit in the timed region)
-    const bool planned = plan_path(ctx, *d);
+    const bool planned = plan_path(ctx, *d, mode);
     rc = generate_children(*d, d_parents, n, nullptr, cap, d_moves, ctx->incremental, &t, s, e + 1,
                            it == 0 && !planned ? d->sum.p : nullptr, chain_len(ctx, *d, n), planned,
                            mode == GN_MODE_BIG);
@@ -1803,7 +1744,8 @@ int gn_time_expand_device(gn_ctx *ctx, int device_slot, const gn_board *d_parent
     gn_eval *po = d_parent_out ? d_parent_out : d->io_out.p;
     rc = expand_evaluate(ctx, *d, d_parents, n, d->frontier[1].p, t, mode, po,
                          d_child_out ? d_child_out : d->io_out2.p, s, e + 4, it == 0 ? d->sum.p + 1 : nullptr);
-    if (rc == GN_OK) rc = resolve_scores(ctx, *d, d_parents, n, mode, po, nullptr, s);
+    const Replies rp{d_child_out ? d_child_out : d->io_out2.p, d->child_moves}; // this expansion's replies
+    if (rc == GN_OK) rc = resolve_scores(ctx, *d, d_parents, n, mode, po, nullptr, s, 2, &rp);
     if (rc == GN_OK) he = hipEventRecord(e[9], s);
   }
   if (rc == GN_OK && he == hipSuccess && d_offsets) he = launch_offsets_u32(d->offsets.p, n + 1, d_offsets, s);
@@ -1923,6 +1865,21 @@ int gn_get_option(const gn_ctx *ctx, int option, int64_t *value) {
     float m = 0;
     for (auto &dp : ctx->devs) m = std::max(m, option == GN_STAT_PLAN_NS ? dp->plan_ms : dp->stream_ms);
     *value = (int64_t)((double)m * 1e6);
+    return GN_OK;
+  }
+  case GN_STAT_SCRATCH_PADS: { // read-only: the last planned expansion's GN_SCR_GAP no-op entries, summed
+    int64_t sum = 0;
+    for (auto &dp : ctx->devs) {
+      Dev &d = *dp;
+      std::lock_guard<std::mutex> lk(d.mu);
+      if (!d.pstat.p) continue;
+      HIP_TRY(hipSetDevice(d.id));
+      if (d.done_on) HIP_TRY(hipEventSynchronize(d.done));
+      unsigned long long v = 0;
+      HIP_TRY(hipMemcpy(&v, d.pstat.p, sizeof(v), hipMemcpyDeviceToHost));
+      sum += (int64_t)v;
+    }
+    *value = sum;
     return GN_OK;
   }
   case GN_STAT_CHAIN_FALLBACKS: { // read-only: blocks of the last chained expansion per device, summed

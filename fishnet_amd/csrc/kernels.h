@@ -6,6 +6,20 @@
 
 #include "nnue.h"
 
+// Row-ring depth of the planned expansion's stream (stream.hip: entries in flight per wave,
+// 4 or 8), and the least distance, in entries of one list, from a king-cache store to a later
+// load of that row: the store is issued while consuming entry j, the ring then waits
+// vmcnt(2 * RD - 2) before each entry, which retires the store (vmcnt counts loads and stores
+// together in issue order, MI355X_MICROARCH.md "s_waitcnt vmcnt(N)") at entry j + RD - 1,
+// whose ring slot then issues entry j + 2 * RD - 1's loads.  A load at that distance or more
+// is therefore issued after the store has completed, with no drain and no reliance on how
+// the memory pipeline orders one wave's store and load to one address.  The plan pads the
+// lists to keep it and asserts it (error bit 4).
+#ifndef GN_RING
+#define GN_RING 4
+#endif
+#define GN_SCR_GAP (2 * GN_RING - 1)
+
 namespace gn {
 
 // NetworkOutput {psqt / 16, positional / 16} for every position whose
@@ -66,15 +80,18 @@ static_assert(sizeof(TileDesc) == 192, "TileDesc is 192 bytes");
 // the region's end, eoff = exclusive scan of write_children's per-parent entry bounds).
 // One call plans and evaluates blocks [b0, b1) of the n parents (every index absolute, so
 // block ranges can run as a pipeline on different streams).  pool: 64 words, zeroed by the
-// caller before the first range; err: bit 0 entry overflow, bit 1 no scratch slot.
-// rows_out: += FT rows the stream gathers (bias, carry and king-cache rows included).
+// caller before the first range; err: bit 0 entry overflow, bit 1 no scratch slot, bit 2 a
+// king-cache load closer than GN_SCR_GAP entries to its list's last store to scratch.
+// rows_out: += FT rows the stream gathers (bias, carry and king-cache rows included);
+// pads_out (optional): += no-op entries the plan inserted to keep GN_SCR_GAP.
 // order: block order of the stream (block_order) or NULL; mid: recorded between the kernels.
 hipError_t launch_plan_stream(const NetDevice &net, const gn_board *parents, size_t n, const uint64_t *offsets,
                               const ChildDelta *deltas, const uint8_t *need_parent, const uint8_t *need_child,
                               int2 *out_parent, int2 *out_child, int swz, const uint8_t *next_slot, int chain_k,
                               int kc, const uint64_t *eoff, uint64_t *ent, TileDesc *tiles, uint32_t *btiles,
-                              uint32_t *pool, uint32_t *err, unsigned long long *rows_out, size_t b0, size_t b1,
-                              const uint32_t *order, hipEvent_t mid, hipStream_t s);
+                              uint32_t *pool, uint32_t *err, unsigned long long *rows_out,
+                              unsigned long long *pads_out, size_t b0, size_t b1, const uint32_t *order,
+                              hipEvent_t mid, hipStream_t s);
 // GN_MODE_FULL preparation: need_small = valid && |simple_eval| > threshold,
 // need_big = valid && !need_small.
 hipError_t launch_classify(const gn_board *boards, size_t n, const gn_eval_params &P, uint8_t *need_small,
@@ -101,6 +118,16 @@ hipError_t launch_finalize(const gn_board *boards, size_t n, int mode, const int
 hipError_t launch_score_select(const gn_eval *out, size_t n, uint64_t *sel, hipStream_t s);
 hipError_t launch_score_gather(const gn_board *boards, const uint64_t *sel, const uint64_t *pos, size_t n,
                                uint32_t *idx, gn_board *sb, hipStream_t s);
+// Replies already evaluated by an expansion (records rec / moves at [off[i], off[i + 1]) of
+// parent i, the parents unpacked by write_children): compact offsets coff (m + 1, scan of
+// counts; *total_host = coff[m], synchronous), then (_fill) ce / cb / cm = the selected
+// parents' replies as positions of the rule (records with their static score part, boards,
+// moves).
+hipError_t launch_score_replies(const uint32_t *idx, size_t m, const uint64_t *off, uint64_t *counts,
+                                uint64_t *coff, void *&temp, size_t &temp_bytes, uint64_t *total_host, hipStream_t s);
+hipError_t launch_score_replies_fill(const uint32_t *idx, size_t m, const uint64_t *off, const uint64_t *coff,
+                                     const gn_eval *rec, const uint16_t *moves, const Board *unpacked,
+                                     const Tables *tables, gn_eval *ce, gn_board *cb, uint16_t *cm, hipStream_t s);
 hipError_t launch_score_reduce(const gn_board *sb, size_t m, const uint32_t *idx, const uint64_t *off,
                                const uint16_t *moves, const gn_eval *ce, const int32_t *csv, const gn_eval_params &P,
                                gn_eval *out, int32_t *sv, hipStream_t s);

@@ -1519,6 +1519,46 @@ __global__ void score_gather_kernel(const gn_board *__restrict__ boards, const u
   sb[k] = boards[i];
 }
 
+// An expansion's selected parents (idx) already have every reply evaluated (records rec,
+// moves, [off[i], off[i + 1]) per parent i): their reply counts for the compaction's scan ...
+__global__ void score_counts_kernel(const uint32_t *__restrict__ idx, size_t m, const uint64_t *__restrict__ off,
+                                    uint64_t *__restrict__ counts) {
+  const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < m) counts[k] = off[idx[k] + 1] - off[idx[k]];
+  else if (k == m) counts[m] = 0;
+}
+
+// ... and the replies as positions of the rule (compacted at coff[k]): their records with the
+// static score part (any legal move? as finalize does for positions), boards and moves.
+__global__ void score_replies_kernel(const uint32_t *__restrict__ idx, size_t m, const uint64_t *__restrict__ off,
+                                     const uint64_t *__restrict__ coff, const gn_eval *__restrict__ rec,
+                                     const uint16_t *__restrict__ moves, const Board *__restrict__ unpacked,
+                                     const Tables *__restrict__ tables, gn_eval *__restrict__ ce,
+                                     gn_board *__restrict__ cb, uint16_t *__restrict__ cm) {
+  __shared__ Tables T;
+  load_tables(T, tables);
+  const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= m) return;
+  const uint32_t i = idx[k];
+  const Board P = unpacked[i];
+  uint64_t d = coff[k];
+  for (uint64_t c = off[i]; c < off[i + 1]; ++c, ++d) {
+    const uint16_t mv = moves[c];
+    const Board B = do_move(P, mv, nullptr);
+    gn_eval e = rec[c];
+    uint32_t f = e.flags & ~GN_FLAG_NO_SCORE;
+    e.score = 0;
+    if (!any_legal(B, T)) f |= GN_FLAG_NO_MOVES | ((f & GN_FLAG_IN_CHECK) ? GN_FLAG_MATE : 0u);
+    else e.score = e.final_cp;
+    e.flags = (uint16_t)f;
+    ce[d] = e;
+    gn_board pb;
+    pack(B, pb);
+    cb[d] = pb;
+    cm[d] = mv;
+  }
+}
+
 // value = max over the replies c of negate_ply(rule_value(c)) (ties: the smaller move), then
 // score / flags / best_move of selected position j; sv (optional) receives the value for
 // the level above
@@ -1586,6 +1626,25 @@ hipError_t launch_score_gather(const gn_board *boards, const uint64_t *sel, cons
   return hipGetLastError();
 }
 
+hipError_t launch_score_replies(const uint32_t *idx, size_t m, const uint64_t *off, uint64_t *counts,
+                                uint64_t *coff, void *&temp, size_t &temp_bytes, uint64_t *total_host, hipStream_t s) {
+  hipError_t e;
+  hipLaunchKernelGGL(score_counts_kernel, dim3(blocks_for(m + 1, 256)), dim3(256), 0, s, idx, m, off, counts);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  if ((e = exclusive_scan_u64(counts, coff, m + 1, temp, temp_bytes, s)) != hipSuccess) return e;
+  if ((e = hipMemcpyAsync(total_host, coff + m, sizeof(uint64_t), hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+  return hipStreamSynchronize(s);
+}
+
+hipError_t launch_score_replies_fill(const uint32_t *idx, size_t m, const uint64_t *off, const uint64_t *coff,
+                                     const gn_eval *rec, const uint16_t *moves, const Board *unpacked,
+                                     const Tables *tables, gn_eval *ce, gn_board *cb, uint16_t *cm, hipStream_t s) {
+  if (!m) return hipSuccess;
+  hipLaunchKernelGGL(score_replies_kernel, dim3(blocks_for(m, 256)), dim3(256), 0, s, idx, m, off, coff, rec, moves,
+                     unpacked, tables, ce, cb, cm);
+  return hipGetLastError();
+}
+
 hipError_t launch_score_reduce(const gn_board *sb, size_t m, const uint32_t *idx, const uint64_t *off,
                                const uint16_t *moves, const gn_eval *ce, const int32_t *csv, const gn_eval_params &P,
                                gn_eval *out, int32_t *sv, hipStream_t s) {
@@ -1614,12 +1673,14 @@ __global__ void count_children_kernel(const gn_board *__restrict__ boards, size_
   counts[i] = c;
   if (ebound) { // planned-expansion entries of this parent (stream.hip), bounded: its refresh
     // (bias + P rows + the cache store per list, or the cache row + <= P differences + the
-    // store) or its carry entries, after <= 4 no-ops per list; per child
+    // store) or its carry entries, after <= GN_SCR_GAP no-ops per list; per child
     // <= 4 delta entries per list, or for a king move a refresh (bias + <= P rows + the
-    // cache store, after <= 4 no-ops) + the other perspective's <= 4; per-tile padding
-    // (<= 3 per list per tile the parent touches)
+    // cache store, after <= GN_SCR_GAP no-ops) + the other perspective's <= 4; per-tile
+    // padding (<= 3 per list per tile the parent touches)
     const uint64_t P = popcnt(B.byType[0]);
-    ebound[i] = c || P ? 2 * (P + 2) + 8 + 8 * (c - kmoves) + (P + 10) * kmoves + 6 * ((c + 1) / 16 + 2) : 0;
+    ebound[i] = c || P ? 2 * (P + 2) + 2 * GN_SCR_GAP + 8 * (c - kmoves) + (P + 6 + GN_SCR_GAP) * kmoves +
+                             6 * ((c + 1) / 16 + 2)
+                       : 0;
   }
 }
 

@@ -39,9 +39,10 @@
 // kind, [19] LAST, [23:20] slot, [24] side, [25] PAR_E, [27] KST, [31] SCR; so the
 // stream's common entry is a multiply-add with hi as its scalar operand and two bit tests.
 // The ring issues a row load 4 entries before it
-// consumes it, so an entry that loads a scratch row sits at least 4 entries after the
-// last store to scratch in its list (no-op entries are inserted when needed): the load
-// is then issued after the store, by the same lanes.  The ring runs across tiles.
+// consumes it, so an entry that loads a scratch row sits at least GN_SCR_GAP = 7 entries
+// after the last store to scratch in its list (no-op entries are inserted when needed): the
+// ring's own vmcnt waits have then retired the store before the load issues (kernels.h).
+// The ring runs across tiles.
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -53,9 +54,6 @@
 
 #ifndef GN_PLAN_WPE
 #define GN_PLAN_WPE 4 // 128 VGPRs, no spills: 4 latency-bound plan waves per SIMD instead of 3
-#endif
-#ifndef GN_RING
-#define GN_RING 4 // row-ring depth of the stream (entries in flight per wave); 4 or 8
 #endif
 #ifndef GN_EXPAND_WPE
 #define GN_EXPAND_WPE (GN_RING == 4 ? 5 : 4)
@@ -123,7 +121,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
                 const ChildDelta *__restrict__ deltas, const uint8_t *__restrict__ need_parent,
                 const uint8_t *__restrict__ need_child, const uint8_t *__restrict__ next_slot, uint32_t np, uint32_t K,
                 uint32_t b0, uint32_t b1, int kc, const uint64_t *__restrict__ eoff, uint64_t *__restrict__ ent, TileDesc *__restrict__ tiles,
-                uint32_t *__restrict__ btiles, unsigned long long *__restrict__ rows_out, uint32_t *__restrict__ err) {
+                uint32_t *__restrict__ btiles, unsigned long long *__restrict__ rows_out,
+                unsigned long long *__restrict__ pads_out, uint32_t *__restrict__ err) {
   using namespace ps;
   __shared__ uint32_t ksnap[4][128][8]; // per wave: placement (64 nibbles) of each king-cache row
   __shared__ uint8_t kstate[4][128];    // bit 0: row holds an accumulator, bit 1: the list that stored it
@@ -140,17 +139,25 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
   const uint64_t us_b = pbeg + offsets[pbeg];
   const uint64_t rbeg = eoff[pbeg] + 16ull * blk, rend = eoff[pend] + 16ull * (blk + 1);
   uint64_t *E0 = ent + rbeg, *E1 = ent + rend - 1;
+  const uint64_t rtot = rend - rbeg; // the block's entry region (both lists)
+  uint32_t bad = 0;                  // this lane's error bits (reported once per wave)
   // a block's tiles: <= ceil(slots / 16) + one bucket cut per parent (a parent's own slots hold
   // <= 2 buckets, so a tile is cut at most once per parent), hence this base
   TileDesc *T = tiles + us_b / 16 + (uint64_t)(K + 2) * blk;
+  uint32_t safe0 = 0, safe1 = 0; // first index of each list at which a scratch row may be loaded
   auto put = [&](int g, uint32_t i, uint32_t v) {
+    if (i >= rtot) { // never past the block's region (the final check reports the overflow)
+      bad |= 1u;
+      return;
+    }
+    // a scratch-row load must sit GN_SCR_GAP entries after the list's last scratch store
+    if ((v & SCR) && !(v & KST) && i < (g ? safe1 : safe0)) bad |= 4u;
     if (g) E1[-(int64_t)i] = enc64<L1>(v);
     else E0[i] = enc64<L1>(v);
   };
   for (int i = lane; i < 128; i += 64) kstate[w][i] = 0;
   uint16_t(*prow)[32] = prow_s[w];
   uint32_t len0 = 0, len1 = 0, tile_k = 0, p_first = pbeg, u_fill = 0, t_first = 0, tile_bm = 0;
-  uint32_t safe0 = 0, safe1 = 0; // first index of each list at which a scratch row may be loaded
   int t_fill = 0, carried = 0;
   unsigned long long rows = 0, pads = 0, fpads = 0;
   auto pad_to = [&](int g, uint32_t target) { // no-op entries up to target (lane-parallel, < 64)
@@ -408,7 +415,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
             if ((lane & 7) == 0) ksnap[w][kci][lane >> 3] = x;
             if (lane == 0) kstate[w][kci] = (uint8_t)(1 | hh << 1);
             uint32_t &sf = hh ? safe1 : safe0;
-            sf = b0 + (uint32_t)(pnd[hh] >= 0 ? pnd[hh] : P) + GN_RING; // the store's index + ring depth
+            sf = b0 + (uint32_t)(pnd[hh] >= 0 ? pnd[hh] : P) + GN_SCR_GAP; // the store's index + the gap
           }
         }
         ps::wave_sync();
@@ -484,7 +491,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
         }
         if (kuse) { // this slot's last entry stores to scratch
           uint32_t &sf = g ? safe1 : safe0;
-          sf = base + (uint32_t)ne - 1 + GN_RING;
+          sf = base + (uint32_t)ne - 1 + GN_SCR_GAP;
         }
         if (g) len1 += (uint32_t)ne;
         else len0 += (uint32_t)ne;
@@ -495,9 +502,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
   }
   if (t_fill) flush();
   if (lane == 0) btiles[blk] = tile_k;
+  // error bits: 1 entries beyond the block's region (eoff under-counted), 4 a scratch-row load
+  // closer than GN_SCR_GAP to its list's last scratch store; neither can happen by construction
+  const uint32_t werr = __ballot(bad & 1u) ? 1u : 0u, werr4 = __ballot(bad & 4u) ? 4u : 0u;
   if (lane == 0) {
-    if ((uint64_t)len0 + len1 > rend - rbeg) atomicOr(err, 1u); // cannot happen: eoff bounds the entries
+    if ((uint64_t)len0 + len1 > rtot || werr) atomicOr(err, 1u);
+    if (werr4) atomicOr(err, 4u);
     if (rows_out) atomicAdd(rows_out, rows);
+    if (pads_out && pads) atomicAdd(pads_out, pads);
     SP_ADD(6, pads), SP_ADD(7, fpads);
   }
   (void)pads, (void)fpads;
@@ -865,8 +877,9 @@ hipError_t launch_plan_stream(const NetDevice &net, const gn_board *parents, siz
                               const ChildDelta *deltas, const uint8_t *need_parent, const uint8_t *need_child,
                               int2 *out_parent, int2 *out_child, int swz, const uint8_t *next_slot, int chain_k,
                               int kc, const uint64_t *eoff, uint64_t *ent, TileDesc *tiles, uint32_t *btiles,
-                              uint32_t *pool, uint32_t *err, unsigned long long *rows_out, size_t b0, size_t b1,
-                              const uint32_t *order, hipEvent_t mid, hipStream_t s) {
+                              uint32_t *pool, uint32_t *err, unsigned long long *rows_out,
+                              unsigned long long *pads_out, size_t b0, size_t b1, const uint32_t *order,
+                              hipEvent_t mid, hipStream_t s) {
   if (!n || b1 <= b0) return hipSuccess;
   if (n >= 0x80000000ull) return hipErrorInvalidValue; // 32-bit parent indices in the kernels
   const uint32_t K = chain_k > 1 && next_slot ? (uint32_t)chain_k : 1u;
@@ -880,14 +893,14 @@ hipError_t launch_plan_stream(const NetDevice &net, const gn_board *parents, siz
   if (net.L1 == 3072) {
     hipLaunchKernelGGL((plan_kernel<3072>), dim3(pg), dim3(256), 0, s, net, parents, offsets, deltas, need_parent,
                        need_child, K > 1 ? next_slot : nullptr, (uint32_t)n, K, B0, B1, K > 1 ? kc : 0, eoff, ent,
-                       tiles, btiles, rows_out, err);
+                       tiles, btiles, rows_out, pads_out, err);
     if (mid) (void)hipEventRecord(mid, s);
     hipLaunchKernelGGL((stream_eval_kernel<3072>), dim3(g), dim3(384), lds_pad, s, net, offsets, (uint32_t)n, K, B0, B1,
                        swz, eoff, ent, tiles, btiles, order, out_parent, out_child, pool, scr, err, ablate);
   } else if (net.L1 == 1024) {
     hipLaunchKernelGGL((plan_kernel<1024>), dim3(pg), dim3(256), 0, s, net, parents, offsets, deltas, need_parent,
                        need_child, K > 1 ? next_slot : nullptr, (uint32_t)n, K, B0, B1, K > 1 ? kc : 0, eoff, ent,
-                       tiles, btiles, rows_out, err);
+                       tiles, btiles, rows_out, pads_out, err);
     if (mid) (void)hipEventRecord(mid, s);
     hipLaunchKernelGGL((stream_eval_kernel<1024>), dim3(g), dim3(128), 0, s, net, offsets, (uint32_t)n, K, B0, B1,
                        swz, eoff, ent, tiles, btiles, order, out_parent, out_child, pool, scr, err, ablate);

@@ -44,7 +44,7 @@ EXPORTS = ["gn_load_net", "gn_load_net_memory", "gn_free", "gn_last_error", "gn_
            "gn_net_sha256", "gn_partition", "gn_checksum_device",
            "gn_boards_to_fens", "gn_load_net_archive", "gn_archive_read", "gn_expand2_device"]
 OPT_INCREMENTAL_CHILDREN, OPT_XCD_SWIZZLE, OPT_KING_SORT, OPT_CHAIN, OPT_KING_CACHE = 1, 2, 3, 4, 5
-STAT_CHAIN_FALLBACKS, STAT_PLAN_NS, STAT_STREAM_NS = 100, 101, 102
+STAT_CHAIN_FALLBACKS, STAT_PLAN_NS, STAT_STREAM_NS, STAT_SCRATCH_PADS = 100, 101, 102, 103
 EXPAND_STAGES = ["count_scan", "total_readback", "write_children", "classify", "small_net", "big_net", "finalize",
                  "score"]
 

@@ -95,6 +95,11 @@ extern "C" {
                                          plan_kernel (lists, tiles, PSQT) ...            */
 #define GN_STAT_STREAM_NS 102         /* ... and stream_eval_kernel (row stream + layer
                                          stack), the expansion's dominant kernel         */
+#define GN_STAT_SCRATCH_PADS 103      /* no-op entries the last planned expansion inserted
+                                         (per device, summed) so that every king-cache load
+                                         sits >= 2 * ring depth - 1 list entries after the
+                                         list's last king-cache store (the store has then
+                                         completed when the load issues)                 */
 #define GN_STAT_CHAIN_FALLBACKS 100   /* blocks of the last chained expansion (per device,
                                          summed) that found their carry / king-cache slot
                                          still in use after a bounded wait and ran

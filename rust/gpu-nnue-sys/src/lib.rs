@@ -37,6 +37,7 @@ pub const GN_OPT_KING_CACHE: c_int = 5;
 pub const GN_STAT_CHAIN_FALLBACKS: c_int = 100;
 pub const GN_STAT_PLAN_NS: c_int = 101;
 pub const GN_STAT_STREAM_NS: c_int = 102;
+pub const GN_STAT_SCRATCH_PADS: c_int = 103;
 
 // per-position flags
 pub const GN_FLAG_IN_CHECK: u16 = 1;

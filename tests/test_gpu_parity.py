@@ -663,3 +663,88 @@ def test_grandchildren_vs_depth1_and_oracle(gpu_ctx, oracle_nets, oracle_lib, mo
         assert {int(m): tuple(x) for m, x in zip(gmv[lo:hi], gco[lo:hi])} == \
                {int(m): tuple(x) for m, x in zip(m_exp, k_exp)}, fen
 
+
+
+def _expand_runner(ctx, d_b, n, cap, mode=1):
+    """expand_device with the given chain / king-cache options into fresh buffers."""
+    from fishnet_amd import gpu_nnue as G
+    bufs = {k: ctx.alloc(sz) for k, sz in (("po", n * G.EVAL_SIZE), ("off", (n + 1) * 4), ("ch", cap * 32),
+                                              ("mv", cap * 2), ("co", cap * G.EVAL_SIZE))}
+
+    def run(k, kc, inc=1):
+        ctx.set_option(G.OPT_CHAIN, k)
+        ctx.set_option(G.OPT_KING_CACHE, kc)
+        ctx.set_option(G.OPT_INCREMENTAL_CHILDREN, inc)
+        try:
+            t = ctx.expand_device(d_b, n, mode, bufs["po"], bufs["off"], bufs["ch"], bufs["mv"], bufs["co"], cap)
+        finally:
+            ctx.set_option(G.OPT_CHAIN, 81)
+            ctx.set_option(G.OPT_KING_CACHE, 1)
+            ctx.set_option(G.OPT_INCREMENTAL_CHILDREN, 1)
+        return (bufs["po"].download(G.EVAL_DTYPE, n), bufs["off"].download(np.uint32, n + 1),
+                bufs["mv"].download(np.uint16, t), bufs["co"].download(G.EVAL_DTYPE, t))
+    return run
+
+
+def _check_vs_oracle(oracle_lib, big, fens, res, mode=1):
+    parents, offs, moves, kids = res
+    for i, fen in enumerate(fens):
+        p_exp, m_exp, k_exp = oracle_lib.expand_eval(big, None, fen, mode)
+        assert tuple(parents[i]) == p_exp, fen
+        lo, hi = int(offs[i]), int(offs[i + 1])
+        assert {int(m): tuple(x) for m, x in zip(moves[lo:hi], kids[lo:hi])} == \
+               {int(m): tuple(x) for m, x in zip(m_exp, k_exp)}, fen
+
+
+@pytest.mark.parametrize("stress", [False, True])
+def test_l1_1024_planned_expansion(oracle_lib, stress):
+    """the planned path is the default for L1 = 1024 nets too (plan_kernel<1024> +
+    stream_eval_kernel<1024>: 2 waves of 128 threads, the rotating finishing wave, 8 k-steps per
+    wave, 2,176-B rows).  Chained walk and king cache on and off and the full-refresh path give
+    identical results, and the first games equal the oracle, on a normal and an int16-wrap net."""
+    from fishnet_amd import gpu_nnue as G, synthnet
+    p = synthnet.cached_synth_net(1024, 5, stress=stress)
+    ctx = G.GpuNnue(p, None)
+    try:
+        assert ctx.net_info()["big_l1"] == 1024
+        games, plies = 30, 80
+        n = games * (plies + 1)
+        d_b = ctx.alloc(n * 32)
+        ctx.random_games_device(0x5EED1024, 0, games, plies, d_b)
+        ctx.synchronize()
+        run = _expand_runner(ctx, d_b, n, 60 * n)
+        ref = run(1, 0, inc=0)  # every position a full refresh (eval_net<1024>)
+        for k, kc in ((1, 0), (-81, 1), (-81, 0), (-5, 1), (81, 1)):
+            got = run(k, kc)
+            assert all(np.array_equal(a, b) for a, b in zip(ref, got)), (k, kc)
+        on = oracle_lib.Net(p)
+        fens = [G.board_to_fen(b) for b in d_b.download(G.BOARD_DTYPE, 2 * (plies + 1))]
+        _check_vs_oracle(oracle_lib, on, fens, ref)
+    finally:
+        ctx.close()
+
+
+def test_king_cache_reload_at_minimum_gap(gpu_ctx, oracle_nets, oracle_lib):
+    """a king-cache row reloaded right after its store.  Kings shuffling
+    e1-e2 / e8-e7 make every parent and every king-move child hit the rows the previous
+    positions stored; the plan pads each such reload to exactly GN_SCR_GAP list entries behind
+    the store (GN_STAT_SCRATCH_PADS > 0: the minimum distance occurred), the plan's error word
+    (bit 2: a reload closer than that; checked after every planned expansion) stays clear, and
+    the results equal the refresh path and the oracle."""
+    from fishnet_amd import gpu_nnue as G
+    shuffle = "e2e4 e7e5 " + " ".join(["e1e2 e8e7 e2e1 e7e8"] * 19) + " e1e2 e8e7"
+    start = "rnbqkbnr/pppppppp/8/8/8/8/PPPPPPPP/RNBQKBNR w KQkq - 0 1"
+    fens, _ = oracle_lib.replay_game(start, shuffle)
+    assert len(fens) == 81
+    boards = np.tile(G.pack_fens(fens)[0], 24)
+    n = len(boards)
+    d_b = gpu_ctx.alloc(n * 32)
+    d_b.upload(boards)
+    run = _expand_runner(gpu_ctx, d_b, n, 40 * n)
+    ref = run(1, 0)
+    got = run(-81, 1)
+    pads = gpu_ctx.get_option(G.STAT_SCRATCH_PADS)
+    assert pads > 0
+    assert all(np.array_equal(a, b) for a, b in zip(ref, got))
+    big, _ = oracle_nets
+    _check_vs_oracle(oracle_lib, big, fens, tuple(x[:81] if i == 0 else x for i, x in enumerate(got)))
