@@ -259,6 +259,10 @@ def run_expand(c: Ctx, wl: dict, games: int, steps: int, warmup: int, check: int
     c.barrier_sync()
     wall = c.comm.max(time.perf_counter() - t0)
     fallbacks = nn.get_option(G.STAT_CHAIN_FALLBACKS)
+    try:
+        scratch_pads = nn.get_option(G.STAT_SCRATCH_PADS)
+    except G.GnError:  # an older library in an A/B run
+        scratch_pads = None
     # the big net's two kernels timed apart (HIP events on the library's stream, inside the
     # timed region): the roofline's dominant kernel is stream_eval_kernel alone
     plan_ms, stream_ms = nn.get_option(G.STAT_PLAN_NS) / 1e6, nn.get_option(G.STAT_STREAM_NS) / 1e6
@@ -270,6 +274,7 @@ def run_expand(c: Ctx, wl: dict, games: int, steps: int, warmup: int, check: int
              kern_ms=stream_ms if planned else stage[5 if mode != 2 else 4], plan_ms=plan_ms,
              alg=rows * (2 * wl["l1"] + 4), rows=rows, parents=parents, n=n,
              children=children, gen_s=gen_s, checksum=sums[0] ^ sums[1], chain_fallbacks=fallbacks,
+             scratch_pads=scratch_pads,
              kernel=(f"stream_eval_kernel<{wl['l1']}>" if planned else f"expand_stream<{wl['l1']}>")
              if wl["l1"] != 128 else f"expand_eval<{wl['l1']}>")
     if check:
@@ -385,6 +390,102 @@ def run_expand2(c: Ctx, games: int, mode: int, steps: int, check: int):
     return r
 
 
+START_FEN = "rnbqkbnr/pppppppp/8/8/8/8/PPPPPPPP/RNBQKBNR w KQkq - 0 1"
+
+
+def run_abi_games(c: Ctx, games: int, mode: int, steps: int, check: int):
+    """secondary.abi_games: the C-ABI's host-facing path as fishnet would call it.  Lichess-shaped
+    batches (root FEN + the game's UCI moves as one string, AcquireResponseBody) in host memory ->
+    gn_evaluate_games(with_children=1) -> every position's and every legal child's record in host
+    memory (the caller's reused numpy arrays).  Inside the call: host FEN parse + move
+    tokenizing, upload, the GPU replay of the moves, the expansion in chunks of whole games, the
+    downloads overlapped with the next chunk.  Verified: sampled positions with all children vs
+    the oracle, and the first full-length games vs the device-resident expansion of the same
+    games (gn_random_games_device + gn_expand_device)."""
+    G, nn = c.G, c.nn
+    first, _ = c.shard(games)
+    seed = SEED + 3
+    t = time.perf_counter()
+    ucis = G.random_games_uci(seed, first, games, PLIES)
+    arr, keep = G._games_array([(START_FEN, u, ()) for u in ucis])
+    prep_s = time.perf_counter() - t
+    bufs = {}
+    res = nn.evaluate_games_arrays(arr, games, mode, True, bufs=bufs)  # sizes the buffers (and warms up)
+    caps = res[-1]
+    c.barrier_sync()
+    t0 = time.perf_counter()
+    stages = []
+    for _ in range(steps):
+        res = nn.evaluate_games_arrays(arr, games, mode, True, caps, bufs)
+        stages.append(nn.host_stages())
+    c.barrier_sync()
+    wall = c.comm.max(time.perf_counter() - t0)
+    offs, status, pos, coffs, cmv, cev, _ = res
+    npos, nch = len(pos), len(cev)
+    st = {k: round(sum(s[k] for s in stages) / len(stages), 3) for k in stages[0]}
+    r = {"workload": f"C-ABI host path: {games} lichess-shaped games per MI355X (start position + {PLIES} random plies "
+                     f"as one UCI string each, AcquireResponseBody form) -> gn_evaluate_games(with_children=1): "
+                     f"{npos} positions + {nch} legal children, records in host memory",
+         "value": round(c.world * (npos + nch) * steps / wall, 1), "unit": "evals/s",
+         "ms_per_call": round(wall * 1e3 / steps, 3), "positions": npos, "children": nch,
+         "result_bytes_to_host": int(npos * G.EVAL_SIZE + nch * (G.EVAL_SIZE + 2) + (npos + 1) * 4),
+         "stage_ms": st, "prep_s_untimed": round(prep_s, 2),
+         "stages": "parse: host root FEN + UCI tokenizing; upload: inputs to the device; replay: the GPU replay of "
+                   "the moves; compute: children + evaluation + score rule over all chunks (main thread); "
+                   "download: device->host record copies, all chunks (a drain thread, overlapping the next "
+                   "chunk); tail: downloads left after the last chunk computed; total: the call"}
+    if check:
+        O, big, small = c.oracle_nets()
+        rng = np.random.default_rng(77 + c.rank)
+        ok = np.nonzero(status[:games] == 0)[0]
+        gi = rng.choice(ok, size=min(check, len(ok)), replace=False)
+        items = [(int(g), int(rng.integers(0, int(offs[g + 1] - offs[g])))) for g in gi]
+
+        def one(it):
+            g, k = it
+            fens, _ = O.replay_game(START_FEN, ucis[g].split()[:k])
+            at = int(offs[g]) + k
+            a, b = int(coffs[at]), int(coffs[at + 1])
+            p_exp, m_exp, k_exp = O.expand_eval(big if mode != 2 else None, small if mode != 1 else None, fens[-1],
+                                                mode, incremental=True)
+            got = dict(zip(cmv[a:b].tolist(), map(tuple, cev[a:b].tolist())))
+            return int(tuple(pos[at]) != p_exp or got != dict(zip(m_exp, map(tuple, k_exp.tolist())))), b - a
+
+        with cf.ThreadPoolExecutor(host_threads()) as ex:
+            out = list(ex.map(one, items))
+        ver = {"oracle": {"positions": len(items), "children": sum(x[1] for x in out),
+                          "mismatching_positions": sum(x[0] for x in out)}}
+        # the first full-length games against the device-resident expansion of the same games
+        ng = min(512, games)
+        d_b = nn.alloc(ng * (PLIES + 1) * 32)
+        nn.random_games_device(seed, first, ng, PLIES, d_b)
+        nn.synchronize()
+        dev = d_b.download(G.BOARD_DTYPE, ng * (PLIES + 1)).reshape(ng, PLIES + 1)
+        full = [g for g in range(ng) if status[g] == 0 and offs[g + 1] - offs[g] == PLIES + 1]
+        sel = np.concatenate([dev[g] for g in full])
+        m, cap = len(sel), int(coffs[int(offs[full[-1] + 1])] - coffs[int(offs[full[0]])]) + 1
+        cap = max(cap, 64 * m)
+        db = {k: nn.alloc(sz) for k, sz in (("b", m * 32), ("po", m * G.EVAL_SIZE), ("off", (m + 1) * 4),
+                                               ("ch", cap * 32), ("mv", cap * 2), ("co", cap * G.EVAL_SIZE))}
+        db["b"].upload(sel)
+        tt = nn.expand_device(db["b"], m, mode, db["po"], db["off"], db["ch"], db["mv"], db["co"], cap)
+        po, doff = db["po"].download(G.EVAL_DTYPE, m), db["off"].download(np.uint32, m + 1)
+        dmv, dco = db["mv"].download(np.uint16, tt), db["co"].download(G.EVAL_DTYPE, tt)
+        bad, i = 0, 0
+        for g in full:
+            a0, a1 = int(offs[g]), int(offs[g + 1])
+            c0, c1 = int(coffs[a0]), int(coffs[a1])
+            d0, d1 = int(doff[i]), int(doff[i + a1 - a0])
+            bad += int(not (np.array_equal(pos[a0:a1], po[i:i + a1 - a0]) and np.array_equal(cmv[c0:c1], dmv[d0:d1])
+                            and np.array_equal(cev[c0:c1], dco[d0:d1])))
+            i += a1 - a0
+        for b in list(db.values()) + [d_b]:
+            b.free()
+        ver["vs_device_resident"] = {"games": len(full), "positions": m, "children": tt, "mismatching_games": bad}
+        r["oracle_check"] = ver
+    return r
+
+
 def cpu_baseline_eval(c: Ctx, boards, mode, budget_s):
     """The oracle built -O3 -march=native on this GPU's share of host cores, full refresh per
     position (a batch of unrelated FENs has no parent to update from)."""
@@ -465,9 +566,17 @@ def main():
     ap.add_argument("--king-sort", type=int, default=-1, help="GN_OPT_KING_SORT (-1: library default)")
     ap.add_argument("--chain", type=int, default=None, help="GN_OPT_CHAIN (None: library default; -k: exactly k)")
     ap.add_argument("--king-cache", type=int, default=None, help="GN_OPT_KING_CACHE (None: library default)")
+    ap.add_argument("--abi-games", type=int, default=0,
+                    help="only the secondary.abi_games line with this many games per GPU (A/B runs)")
     args = ap.parse_args()
 
     c = Ctx(args)
+    if args.abi_games:
+        r = run_abi_games(c, args.abi_games, 1, args.steps, args.check)
+        if c.rank == 0:
+            print(json.dumps(r), flush=True)
+        c.close()
+        return
     G = c.G
     wl = WORKLOADS[args.workload]
     mode = wl["mode"]
@@ -478,7 +587,8 @@ def main():
         cfg = {"workload": wl["config"], "games_per_gpu": n, "parents_per_gpu": r["n"],
                "children_per_gpu": r["children"], "evals_per_step_per_gpu": r["n"] + r["children"],
                "evals_per_step_all_gpus": c.world * (r["n"] + r["children"]), "plies": PLIES,
-               "ft_rows_per_step_per_gpu": r["rows"], "chain_fallbacks": r["chain_fallbacks"]}
+               "ft_rows_per_step_per_gpu": r["rows"], "chain_fallbacks": r["chain_fallbacks"],
+               "king_cache_gap_pads": r["scratch_pads"]}
         stage_names = G.EXPAND_STAGES
         data = f"synthetic: seeded random 80-ply games generated on the GPU; nets {c.net_label}"
     else:
@@ -532,6 +642,13 @@ def main():
         if "oracle_check" in g2:
             g2["rank_check_failures"] = c.comm.gather_i64(g2["oracle_check"]["mismatching_children"])
         sec["grandchild"] = g2
+        ag = run_abi_games(c, WORKLOADS["expand"]["n"], 1, 2, 256 if args.check else 0)
+        ag["frac_of_device_resident"] = round(ag["value"] / line["value"], 4)
+        if "oracle_check" in ag:
+            ck = ag["oracle_check"]
+            ag["rank_check_failures"] = c.comm.gather_i64(ck["oracle"]["mismatching_positions"] +
+                                                          ck["vs_device_resident"]["mismatching_games"])
+        sec["abi_games"] = ag
         line["secondary"] = sec
 
     if c.rank == 0:

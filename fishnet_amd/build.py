@@ -19,20 +19,36 @@ HEADERS = ["chess.h", "host_board.h", "nnue.h", "kernels.h", "sha256.h", "device
 ARCH = "gfx950"
 
 
-def _stale():
-    if not os.path.exists(LIB):
-        return True
-    t = os.path.getmtime(LIB)
+def source_hash(defines=()) -> str:
+    """SHA-256 over every source and header the library is built from, and the flags."""
+    import hashlib
+    h = hashlib.sha256()
     deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.join(ROOT, "include", "gpu_nnue.h")]
-    return any(os.path.getmtime(d) > t for d in deps)
+    for d in deps:
+        h.update(os.path.basename(d).encode() + b"\0")
+        with open(d, "rb") as f:
+            h.update(f.read())
+    h.update(" ".join([ARCH, *defines]).encode())
+    return h.hexdigest()
+
+
+def _stale(lib: str, defines=()) -> bool:
+    """The library is current when the hash stored beside it (<lib>.sha256, written by the build
+    that produced it) equals the sources' hash: a copied tree (the gpurun snapshot) with other
+    sources rebuilds, whatever the file times say."""
+    stamp = lib + ".sha256"
+    if not os.path.exists(lib) or not os.path.exists(stamp):
+        return True
+    with open(stamp) as f:
+        return f.read().strip() != source_hash(defines)
 
 
 def build(force: bool = False, verbose: bool = False, defines=(), out: str | None = None) -> str:
     """defines/out: experiment variants (e.g. -DGN_EXPAND_WPE=5 into lib/libgpu_nnue_w5.so),
     selected at run time with GPU_NNUE_LIB; the default build has neither."""
     lib = out or LIB
-    if not force and not defines and not _stale():
-        return LIB
+    if not force and not _stale(lib, defines):
+        return lib
     os.makedirs(LIBDIR, exist_ok=True)
     objs = []
     for src in SOURCES:
@@ -47,6 +63,8 @@ def build(force: bool = False, verbose: bool = False, defines=(), out: str | Non
     cmd = ["hipcc", f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs + ["-lpthread"]
     subprocess.run(cmd, check=True)
     os.replace(tmp, lib)
+    with open(lib + ".sha256", "w") as f:
+        f.write(source_hash(defines) + "\n")
     for o in objs:
         os.remove(o)
     return lib

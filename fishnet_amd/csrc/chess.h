@@ -457,6 +457,61 @@ GN_HD Board do_move(const Board &B, uint16_t m, Dirty *d = nullptr) {
   return C;
 }
 
+// ------------------------------------------------------------- UCI moves ----
+// A lichess move token (AcquireResponseBody.moves, /root/reference/src/api.rs:306-321) as a
+// 16-bit code: from | to << 6 | promo << 12 (promo 0 none, 1..4 = n b r q); UCI_BAD for a
+// token that is not from-square + to-square (+ promotion letter).
+constexpr uint16_t UCI_BAD = 0xFFFF;
+GN_HD uint16_t uci_code(const char *u, int len) {
+  if (len != 4 && len != 5) return UCI_BAD;
+  if (u[0] < 'a' || u[0] > 'h' || u[1] < '1' || u[1] > '8' || u[2] < 'a' || u[2] > 'h' || u[3] < '1' || u[3] > '8')
+    return UCI_BAD;
+  int promo = 0;
+  if (len == 5) {
+    promo = u[4] == 'n' ? 1 : u[4] == 'b' ? 2 : u[4] == 'r' ? 3 : u[4] == 'q' ? 4 : -1;
+    if (promo < 0) return UCI_BAD;
+  }
+  const int from = (u[1] - '1') * 8 + (u[0] - 'a'), to = (u[3] - '1') * 8 + (u[2] - 'a');
+  return (uint16_t)(from | to << 6 | promo << 12);
+}
+
+// shakmaty 0.27.3 UciMove::to_move (the reference's move resolution, queue.rs:576), standard
+// chess: the king moving onto a square of the castling rights is castling with that rook
+// (Chess960 notation, king takes rook); the king moving from e1/e8 to the c/g file of its
+// back rank is castling with the a/h rook (standard notation); otherwise the move from
+// `from` to `to` (en passant included) with the promotion piece; the candidate must be
+// legal.  Host (gn_replay_game) and device (the GPU replay of gn_evaluate_games) run this.
+GN_HD bool resolve_uci(const Board &B, const Tables &T, uint16_t code, uint16_t &out) {
+  if (code == UCI_BAD) return false;
+  const int from = code & 63, to = (code >> 6) & 63, pr = code >> 12;
+  const int promo = pr ? KNIGHT + pr - 1 : 0;
+  const int pc = piece_on(B, from);
+  if (!pc || (promo && (pc & 7) != PAWN)) return false;
+  const int us = B.stm;
+  int rook = -1;
+  if ((pc & 7) == KING) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (B.castle_rook[i] == to) rook = to;
+    if (rook < 0 && from == (us ? 60 : 4) && (to >> 3) == (us ? 7 : 0) && ((to & 7) == 2 || (to & 7) == 6))
+      rook = (to & 56) | ((to & 7) == 2 ? 0 : 7);
+  }
+  bool found = false;
+  gen_legal(B, T, [&](uint16_t m) {
+    if (move_from(m) != from) return false;
+    const int t = move_type(m);
+    if (rook >= 0) {
+      if (t == MT_CASTLING && move_to(m) == rook) found = true, out = m;
+      return found;
+    }
+    if (t == MT_CASTLING || move_to(m) != to) return false;
+    if (t == MT_PROMOTION ? move_promo(m) != promo : promo != 0) return false;
+    found = true, out = m;
+    return true;
+  });
+  return found;
+}
+
 // ------------------------------------------------------ random playouts ----
 // xoshiro256** (Blackman & Vigna), seeded through splitmix64
 struct Xoshiro {
@@ -547,6 +602,41 @@ GN_HD Board random_playout(uint64_t seed, int max_plies, const Tables &T) {
     if (!in_check(B, T)) break;
   }
   return B;
+}
+
+// A random game (the bench's lichess-shaped batches): `plies` uniformly random legal plies
+// from the start position (xoshiro256**, seed); emit(k, B, move) for k = 0..plies with the
+// position after k plies and the move that made it (0 for k = 0, and for the plies after the
+// game ended: mate, stalemate or rule50 >= 100 repeat the final position).
+template <class F>
+GN_HD void random_game(uint64_t seed, int plies, const Tables &T, F &&emit) {
+  Xoshiro rng(seed);
+  Board B = start_position();
+  emit(0, B, (uint16_t)0);
+  for (int k = 1; k <= plies; ++k) {
+    const int n = count_legal(B, T);
+    uint16_t m = 0;
+    if (n && B.rule50 < 100) {
+      m = nth_legal(B, T, (int)rng.below((uint32_t)n));
+      B = do_move(B, m);
+    }
+    emit(k, B, m);
+  }
+}
+
+// UCI text of a move in Stockfish encoding as the lichess API sends it (standard chess:
+// castling as the king's two-square move, e1g1; Chess960 positions: king takes rook);
+// buf >= 6 bytes; returns the length.
+GN_HD int move_uci(uint16_t m, char *buf) {
+  int from = move_from(m), to = move_to(m);
+  if (move_type(m) == MT_CASTLING && (from == 4 || from == 60) && ((to & 7) == 0 || (to & 7) == 7))
+    to = (to & 56) | ((to & 7) == 0 ? 2 : 6);
+  buf[0] = (char)('a' + (from & 7)), buf[1] = (char)('1' + (from >> 3));
+  buf[2] = (char)('a' + (to & 7)), buf[3] = (char)('1' + (to >> 3));
+  int n = 4;
+  if (move_type(m) == MT_PROMOTION) buf[n++] = "nbrq"[move_promo(m) - KNIGHT];
+  buf[n] = '\0';
+  return n;
 }
 
 } // namespace gn

@@ -10,6 +10,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -244,6 +245,20 @@ struct Dev {
       boards.release(), children.release(), moves.release(), ce.release(), sv.release();
     }
   } lv[2];
+  // the host-buffer calls' pipeline (expand_chunks): per chunk slot the parent / child
+  // records and child moves a drain thread downloads on the copy stream while the next chunk
+  // computes; the lichess replay's inputs and outputs (replay_games_kernel)
+  hipStream_t copy = nullptr;
+  hipEvent_t cev[2] = {nullptr, nullptr};
+  DevBuf<gn_eval> po2[2], co2[2];
+  DevBuf<uint16_t> mv2[2];
+  DevBuf<gn_board> roots, rboards, par;
+  DevBuf<uint64_t> moff;
+  DevBuf<uint16_t> codes, smoves;
+  DevBuf<int32_t> rstatus;
+  DevBuf<uint32_t> gidx;
+  // stage times of the last host-buffer call on this device (GN_STAT_HOST_*), ms
+  double t_upload = 0, t_replay = 0, t_compute = 0, t_download = 0, t_tail = 0;
   std::mutex mu;
 };
 
@@ -286,6 +301,7 @@ struct gn_ctx {
   bool king_cache = true;   // GN_OPT_KING_CACHE
   int l1[2] = {0, 0};
   uint32_t hash[2] = {0, 0};
+  double t_parse = 0, t_total = 0; // the last host-buffer expansion call (GN_STAT_HOST_*), ms
 };
 
 enum { BIG = 0, SMALL = 1 };
@@ -380,6 +396,13 @@ static void destroy(gn_ctx *ctx) {
     d.pstat.release();
     d.bkeys.release(), d.bkeys2.release(), d.bidx.release(), d.border.release();
     d.lv[0].release(), d.lv[1].release();
+    for (int i = 0; i < 2; ++i) {
+      d.po2[i].release(), d.co2[i].release(), d.mv2[i].release();
+      if (d.cev[i]) (void)hipEventDestroy(d.cev[i]);
+    }
+    d.roots.release(), d.rboards.release(), d.par.release(), d.moff.release(), d.codes.release();
+    d.smoves.release(), d.rstatus.release(), d.gidx.release();
+    if (d.copy) (void)hipStreamSynchronize(d.copy), (void)hipStreamDestroy(d.copy);
     if (d.done) (void)hipEventDestroy(d.done);
     if (d.stream) (void)hipStreamDestroy(d.stream);
   }
@@ -420,7 +443,21 @@ static int create(const uint8_t *big, size_t big_len, const uint8_t *small, size
     HIP_TRY(hipSetDevice(id));
     HIP_TRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
     HIP_TRY(hipEventCreateWithFlags(&d.done, hipEventDisableTiming));
+    HIP_TRY(hipStreamCreateWithFlags(&d.copy, hipStreamNonBlocking));
+    for (int i = 0; i < 2; ++i) HIP_TRY(hipEventCreateWithFlags(&d.cev[i], hipEventDisableTiming));
+#ifdef GN_AB_AUX_STREAMS // A/B only: two extra streams, as the removed range pipeline had
+    {
+      hipStream_t x[2];
+      for (int i = 0; i < 2; ++i) HIP_TRY(hipStreamCreateWithFlags(&x[i], hipStreamNonBlocking));
+    }
+#endif
+    if (getenv("GN_NET_PAD")) { // A/B only: a device allocation of this many bytes before the nets
+      void *x = nullptr;
+      HIP_TRY(hipMalloc(&x, (size_t)atoll(getenv("GN_NET_PAD"))));
+    }
     HIP_TRY(hipMalloc(&d.tables, sizeof(Tables)));
+    HIP_TRY(d.perr.ensure(1)); // the planned expansion's error word and pad count
+    HIP_TRY(d.pstat.ensure(1));
     HIP_TRY(hipMemcpy(d.tables, &host_tables(), sizeof(Tables), hipMemcpyHostToDevice));
     for (int w = 0; w < 2; ++w)
       if (hn[w].L1) {
@@ -588,8 +625,6 @@ static int generate_children(Dev &d, const gn_board *parents, size_t n, gn_board
   d.chain_k = want_deltas ? chain_k : 1;
   d.planned = want_deltas && plan;
   if (d.planned) { // a stale error bit of an earlier expansion must not fail this one
-    HIP_TRY(d.perr.ensure(1));
-    HIP_TRY(d.pstat.ensure(1));
     HIP_TRY(hipMemsetAsync(d.perr.p, 0, sizeof(uint32_t), s));
     HIP_TRY(hipMemsetAsync(d.pstat.p, 0, sizeof(unsigned long long), s));
   }
@@ -886,14 +921,167 @@ static int evaluate_boards_host(gn_ctx *ctx, const gn_board *boards, size_t n, i
   }
 }
 
-// Host parent boards -> every legal child -> parent/child gn_eval, sharded over every
-// device of the context: parents [bounds[k], bounds[k + 1]) on device k (bounds from
-// partition(); NULL = equal ranges).  Two passes with all device locks held: child
-// counts per shard (so every shard knows where its children go in the caller's
-// arrays), then generation + evaluation + download into those places.
+// ------------------------------------------------------ host pipeline ----
+// The host-buffer expansion (gn_expand_and_evaluate, gn_evaluate_games with children),
+// sharded over the context's devices: shard k's parents are resident on its device (uploaded
+// boards, or the lichess replay's output); pass 1 counts every shard's children so that each
+// shard knows where its children go in the caller's arrays; pass 2 expands a shard in chunks
+// of whole games, and a drain thread downloads chunk c's records on the device's copy
+// stream while chunk c + 1 computes (two slots of device output buffers).
+using Clock = std::chrono::steady_clock;
+static double ms_since(Clock::time_point t) {
+  return std::chrono::duration<double, std::milli>(Clock::now() - t).count();
+}
+
+// f(k, d, lo, hi) on every device k whose shard [b[k], b[k + 1]) is not empty, one host thread
+// per device (the caller holds every device lock); the first failure's code and message.
+template <class F>
+static int run_shards(gn_ctx *ctx, const std::vector<size_t> &b, F &&f) {
+  const size_t nd = ctx->devs.size();
+  std::vector<int> rcs(nd, GN_OK);
+  std::vector<std::string> errs(nd);
+  auto work = [&](size_t k) {
+    if (b[k] >= b[k + 1]) return;
+    try {
+      rcs[k] = f(k, *ctx->devs[k], b[k], b[k + 1]);
+    } catch (const std::bad_alloc &) {
+      rcs[k] = fail(GN_E_NOMEM, "host allocation failed");
+    } catch (...) {
+      rcs[k] = fail(GN_E_INVALID, "unexpected exception");
+    }
+    if (rcs[k]) errs[k] = g_err;
+  };
+  if (nd == 1) work(0);
+  else {
+    std::vector<std::thread> th;
+    for (size_t k = 0; k < nd; ++k) th.emplace_back(work, k);
+    for (auto &t : th) t.join();
+  }
+  for (size_t k = 0; k < nd; ++k)
+    if (rcs[k]) {
+      g_err = errs[k];
+      return rcs[k];
+    }
+  return GN_OK;
+}
+
+static void reset_host_stats(gn_ctx *ctx) {
+  for (auto &dp : ctx->devs) dp->t_upload = dp->t_replay = dp->t_compute = dp->t_download = dp->t_tail = 0;
+}
+
+// Chunk bounds of a shard's m parents: cut only where `starts` allows (the first parent of each
+// game, ascending; empty: anywhere), each chunk >= target parents; {0, ..., m}.
+static std::vector<size_t> chunk_bounds(size_t m, const std::vector<size_t> &starts, size_t target) {
+  std::vector<size_t> c{0};
+  size_t j = 0;
+  while (c.back() < m) {
+    const size_t want = c.back() + std::max<size_t>(target, 1);
+    if (want >= m) break;
+    if (starts.empty()) {
+      c.push_back(want);
+      continue;
+    }
+    while (j < starts.size() && starts[j] < want) ++j;
+    if (j == starts.size() || starts[j] >= m) break;
+    c.push_back(starts[j]);
+  }
+  c.push_back(m);
+  return c;
+}
+
+// Parents per chunk: keeps >= 2048 whole 81-parent blocks per chunk (chain_len's full block
+// length), and about eight chunks per shard so the first and last chunk, the parts that
+// cannot overlap, are short.
+static size_t chunk_target(size_t m) { return std::max<size_t>((size_t)2048 * 81, (m + 7) / 8); }
+
+// Pass 1 of a shard: its m device-resident parents' child offsets (m + 1, relative) to the host.
+static int count_shard(Dev &d, const gn_board *d_par, size_t m, std::vector<uint64_t> &off) {
+  size_t total = 0;
+  HIP_TRY(count_children(d, d_par, m, d.stream, &total));
+  off.resize(m + 1);
+  HIP_TRY(hipMemcpy(off.data(), d.offsets.p, (m + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  return GN_OK;
+}
+
+// Pass 2 of a shard (see above).  off: the shard's child offsets from pass 1; results to
+// parent_out[0, m) (optional), child_moves / child_out[0, off[m]) (the caller's arrays at this
+// shard's base).
+static int expand_pipelined(gn_ctx *ctx, Dev &d, const gn_board *d_par, size_t m, int mode,
+                            const std::vector<uint64_t> &off, const std::vector<size_t> &chunks, gn_eval *parent_out,
+                            uint16_t *child_moves, gn_eval *child_out) {
+  hipStream_t s = d.stream;
+  size_t maxp = 1, maxc = 1;
+  for (size_t c = 0; c + 1 < chunks.size(); ++c)
+    maxp = std::max(maxp, chunks[c + 1] - chunks[c]),
+    maxc = std::max<size_t>(maxc, off[chunks[c + 1]] - off[chunks[c]]);
+  for (int k = 0; k < 2; ++k) {
+    HIP_TRY(d.po2[k].ensure(maxp));
+    HIP_TRY(d.co2[k].ensure(maxc));
+    HIP_TRY(d.mv2[k].ensure(maxc));
+  }
+  std::thread drain[2];
+  int drc[2] = {GN_OK, GN_OK};
+  std::string derr[2];
+  double dms[2] = {0, 0};
+  auto join = [&](int k) -> int {
+    if (drain[k].joinable()) drain[k].join();
+    d.t_download += dms[k], dms[k] = 0;
+    if (!drc[k]) return GN_OK;
+    const int r = drc[k];
+    drc[k] = GN_OK;
+    g_err = derr[k];
+    return r;
+  };
+  int rc = GN_OK;
+  for (size_t c = 0; c + 1 < chunks.size() && rc == GN_OK; ++c) {
+    const int k = (int)(c & 1);
+    if ((rc = join(k)) != GN_OK) break; // the slot's previous chunk is downloaded
+    const size_t pa = chunks[c], mp = chunks[c + 1] - pa;
+    const uint64_t cb = off[pa], tc = off[chunks[c + 1]] - cb;
+    const auto t0 = Clock::now();
+    size_t t = 0;
+    rc = generate_children(d, d_par + pa, mp, nullptr, d.mv2[k].cap, d.mv2[k].p, ctx->incremental, &t, s, nullptr,
+                           nullptr, chain_len(ctx, d, mp), plan_path(ctx, d, mode), mode == GN_MODE_BIG);
+    if (!rc && t != tc) rc = fail(GN_E_HIP, "child count changed between passes (%zu != %zu)", t, (size_t)tc);
+    if (!rc)
+      rc = expand_evaluate(ctx, d, d_par + pa, mp, d.frontier[1].p, t, mode, d.po2[k].p, d.co2[k].p, s, nullptr);
+    const Replies rp{d.co2[k].p, d.mv2[k].p};
+    if (!rc) rc = resolve_scores(ctx, d, d_par + pa, mp, mode, d.po2[k].p, nullptr, s, 2, &rp);
+    if (!rc) rc = check_plan(d, s); // synchronises the stream: chunk c is computed
+    if (rc) break;
+    d.t_compute += ms_since(t0);
+    if (hipEventRecord(d.cev[k], s) != hipSuccess) {
+      rc = fail(GN_E_HIP, "hipEventRecord failed");
+      break;
+    }
+    drain[k] = std::thread([&, k, pa, mp, t, cb] {
+      const auto t1 = Clock::now();
+      hipError_t e = hipSetDevice(d.id);
+      if (e == hipSuccess) e = hipStreamWaitEvent(d.copy, d.cev[k], 0);
+      if (e == hipSuccess && t)
+        e = hipMemcpyAsync(child_out + cb, d.co2[k].p, t * sizeof(gn_eval), hipMemcpyDeviceToHost, d.copy);
+      if (e == hipSuccess && t)
+        e = hipMemcpyAsync(child_moves + cb, d.mv2[k].p, t * sizeof(uint16_t), hipMemcpyDeviceToHost, d.copy);
+      if (e == hipSuccess && parent_out)
+        e = hipMemcpyAsync(parent_out + pa, d.po2[k].p, mp * sizeof(gn_eval), hipMemcpyDeviceToHost, d.copy);
+      if (e == hipSuccess) e = hipStreamSynchronize(d.copy);
+      if (e != hipSuccess) drc[k] = GN_E_HIP, derr[k] = std::string("result download failed: ") + hipGetErrorString(e);
+      dms[k] = ms_since(t1);
+    });
+  }
+  const auto tt = Clock::now();
+  for (int k = 0; k < 2; ++k) {
+    const int r = join(k);
+    if (!rc) rc = r;
+  }
+  d.t_tail = ms_since(tt);
+  return rc;
+}
+
+// Host parent boards -> every legal child -> parent/child gn_eval (gn_expand_and_evaluate),
+// sharded over every device of the context (equal parent ranges).
 static int expand_boards_host(gn_ctx *ctx, const gn_board *boards, size_t n, int mode, gn_eval *parent_out,
-                              uint32_t *child_offsets, uint16_t *child_moves, gn_eval *child_out, size_t cap,
-                              const size_t *bounds_in = nullptr) {
+                              uint32_t *child_offsets, uint16_t *child_moves, gn_eval *child_out, size_t cap) {
   if (!slot(ctx, 0)) return fail(GN_E_INVALID, "bad context");
   if (!n) {
     child_offsets[0] = 0;
@@ -902,50 +1090,21 @@ static int expand_boards_host(gn_ctx *ctx, const gn_board *boards, size_t n, int
   try {
     const size_t nd = ctx->devs.size();
     std::vector<size_t> b(nd + 1);
-    if (bounds_in) std::copy(bounds_in, bounds_in + nd + 1, b.begin());
-    else partition(nullptr, n, (int)nd, b.data());
-    // every device lock for the whole call (in device order), so the two passes see the
-    // same device state
-    std::vector<std::unique_lock<std::mutex>> locks;
+    partition(nullptr, n, (int)nd, b.data());
+    std::vector<std::unique_lock<std::mutex>> locks; // every device lock for the whole call
     for (auto &dp : ctx->devs) locks.emplace_back(dp->mu);
     std::vector<std::vector<uint64_t>> off(nd);
-    std::vector<int> rcs(nd, GN_OK);
-    std::vector<std::string> errs(nd);
-    auto parallel = [&](auto &&f) {
-      auto work = [&](size_t k) {
-        rcs[k] = b[k] < b[k + 1] ? f(k, *ctx->devs[k], b[k], b[k + 1] - b[k]) : GN_OK;
-        if (rcs[k]) errs[k] = g_err;
-      };
-      if (nd == 1) work(0);
-      else {
-        std::vector<std::thread> th;
-        for (size_t k = 0; k < nd; ++k) th.emplace_back(work, k);
-        for (auto &t : th) t.join();
-      }
-      for (size_t k = 0; k < nd; ++k)
-        if (rcs[k]) {
-          g_err = errs[k];
-          return rcs[k];
-        }
-      return (int)GN_OK;
-    };
-    // pass 1: upload + child counts + scan + offsets to the host
-    int rc = parallel([&](size_t k, Dev &d, size_t lo, size_t m) -> int {
+    // pass 1: upload + child counts
+    int rc = run_shards(ctx, b, [&](size_t k, Dev &d, size_t lo, size_t hi) -> int {
       HIP_TRY(hipSetDevice(d.id));
       SeqGuard sg(d, d.stream);
       HIP_TRY(sg.e);
-      hipStream_t s = d.stream;
-      HIP_TRY(d.io_boards.ensure(m));
-      HIP_TRY(hipMemcpyAsync(d.io_boards.p, boards + lo, m * sizeof(gn_board), hipMemcpyHostToDevice, s));
-      HIP_TRY(d.counts.ensure(m + 1));
-      HIP_TRY(d.offsets.ensure(m + 1));
-      HIP_TRY(hipMemsetAsync(d.counts.p + m, 0, sizeof(uint64_t), s));
-      HIP_TRY(launch_count_children(d.io_boards.p, m, d.tables, d.counts.p, s));
-      HIP_TRY(exclusive_scan_u64(d.counts.p, d.offsets.p, m + 1, d.scan_tmp, d.scan_bytes, s));
-      off[k].resize(m + 1);
-      HIP_TRY(hipMemcpyAsync(off[k].data(), d.offsets.p, (m + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
-      HIP_TRY(hipStreamSynchronize(s));
-      return GN_OK;
+      const auto t0 = Clock::now();
+      HIP_TRY(d.par.ensure(hi - lo));
+      HIP_TRY(hipMemcpyAsync(d.par.p, boards + lo, (hi - lo) * sizeof(gn_board), hipMemcpyHostToDevice, d.stream));
+      HIP_TRY(hipStreamSynchronize(d.stream));
+      d.t_upload += ms_since(t0);
+      return count_shard(d, d.par.p, hi - lo, off[k]);
     });
     if (rc) return rc;
     std::vector<uint64_t> base(nd + 1, 0);
@@ -957,33 +1116,16 @@ static int expand_boards_host(gn_ctx *ctx, const gn_board *boards, size_t n, int
     child_offsets[n] = (uint32_t)total;
     if (total > cap) return fail(GN_E_CAPACITY, "%zu children exceed capacity %zu", (size_t)total, cap);
     if (total && (!child_moves || !child_out)) return fail(GN_E_INVALID, "NULL child buffer");
-    // pass 2: children + deltas, incremental evaluation, results into the caller's arrays
-    return parallel([&](size_t k, Dev &d, size_t lo, size_t m) -> int {
+    // pass 2: chunks of 81 parents' multiples (a FEN batch has no games: blocks of 81 = chain_len)
+    return run_shards(ctx, b, [&](size_t k, Dev &d, size_t lo, size_t hi) -> int {
       HIP_TRY(hipSetDevice(d.id));
       SeqGuard sg(d, d.stream);
       HIP_TRY(sg.e);
-      hipStream_t s = d.stream;
-      const size_t tk = (size_t)off[k].back();
-      HIP_TRY(d.moves.ensure(std::max<size_t>(tk, 1)));
-      size_t t = 0;
-      int r = generate_children(d, d.io_boards.p, m, nullptr, d.moves.cap, d.moves.p, ctx->incremental, &t, s, nullptr,
-                                nullptr, chain_len(ctx, d, m), plan_path(ctx, d, mode), mode == GN_MODE_BIG);
-      if (r) return r;
-      if (t != tk) return fail(GN_E_HIP, "child count changed between passes (%zu != %zu)", t, tk);
-      HIP_TRY(d.io_out.ensure(m));
-      HIP_TRY(d.io_out2.ensure(std::max<size_t>(t, 1)));
-      r = expand_evaluate(ctx, d, d.io_boards.p, m, d.frontier[1].p, t, mode, d.io_out.p, d.io_out2.p, s, nullptr);
-      const Replies rp{d.io_out2.p, d.moves.p}; // the replies this expansion evaluated
-      if (!r) r = resolve_scores(ctx, d, d.io_boards.p, m, mode, d.io_out.p, nullptr, s, 2, &rp);
-      if (r) return r;
-      if (t) {
-        HIP_TRY(hipMemcpyAsync(child_out + base[k], d.io_out2.p, t * sizeof(gn_eval), hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipMemcpyAsync(child_moves + base[k], d.moves.p, t * sizeof(uint16_t), hipMemcpyDeviceToHost, s));
-      }
-      if (parent_out)
-        HIP_TRY(hipMemcpyAsync(parent_out + lo, d.io_out.p, m * sizeof(gn_eval), hipMemcpyDeviceToHost, s));
-      HIP_TRY(hipStreamSynchronize(s));
-      return check_plan(d, s);
+      const size_t m = hi - lo;
+      std::vector<size_t> starts;
+      for (size_t i = 81; i < m; i += 81) starts.push_back(i);
+      return expand_pipelined(ctx, d, d.par.p, m, mode, off[k], chunk_bounds(m, starts, chunk_target(m)),
+                              parent_out ? parent_out + lo : nullptr, child_moves + base[k], child_out + base[k]);
     });
   } catch (const std::bad_alloc &) {
     return fail(GN_E_NOMEM, "host allocation failed");
@@ -1003,55 +1145,9 @@ static int expand_boards_host(gn_ctx *ctx, const gn_board *boards, size_t n, int
 // (queue.rs:617, 633).  A move that does not resolve to a legal move fails the
 // game, as `uci.to_move(&pos)?` fails the whole batch in the reference.
 
-static int uci_square(const char *s) {
-  if (s[0] < 'a' || s[0] > 'h' || s[1] < '1' || s[1] > '8') return -1;
-  return (s[1] - '1') * 8 + (s[0] - 'a');
-}
-
-// shakmaty 0.27.3 UciMove::to_move, standard chess:
-//   the king moving onto a square of the castling rights => castling with that rook
-//   (Chess960 notation, king takes rook);
-//   the king moving from e1/e8 to the c/g file of its back rank => castling with the
-//   a/h rook (standard notation);
-//   otherwise the move from `from` to `to` (en passant included) with the promotion
-//   piece of the 5th character;
-// and the candidate must be legal.
+// (shakmaty 0.27.3 UciMove::to_move: resolve_uci in chess.h, shared with the GPU replay)
 static bool uci_to_move(const Board &B, const char *u, size_t len, uint16_t &out) {
-  if (len != 4 && len != 5) return false;
-  const int from = uci_square(u), to = uci_square(u + 2);
-  if (from < 0 || to < 0) return false;
-  int promo = 0;
-  if (len == 5) {
-    static const char P[] = "nbrq";
-    const char *c = (u[4] != '\0') ? strchr(P, u[4]) : nullptr;
-    if (!c) return false;
-    promo = KNIGHT + (int)(c - P);
-  }
-  const int pc = piece_on(B, from);
-  if (!pc || (promo && (pc & 7) != PAWN)) return false;
-  const int us = B.stm;
-  int rook = -1;
-  if ((pc & 7) == KING) {
-    for (int i = 0; i < 4; ++i)
-      if (B.castle_rook[i] == to) rook = to;
-    if (rook < 0 && from == (us ? 60 : 4) && (to >> 3) == (us ? 7 : 0) && ((to & 7) == 2 || (to & 7) == 6))
-      rook = (to & 56) | ((to & 7) == 2 ? 0 : 7);
-  }
-  uint16_t mv[256];
-  const int n = legal_moves(B, mv);
-  for (int i = 0; i < n; ++i) {
-    const uint16_t m = mv[i];
-    if (move_from(m) != from) continue;
-    const int t = move_type(m);
-    if (rook >= 0) {
-      if (t == MT_CASTLING && move_to(m) == rook) return out = m, true;
-      continue;
-    }
-    if (t == MT_CASTLING || move_to(m) != to) continue;
-    if (t == MT_PROMOTION ? move_promo(m) != promo : promo != 0) continue;
-    return out = m, true;
-  }
-  return false;
+  return resolve_uci(B, host_tables(), uci_code(u, (int)len), out);
 }
 
 struct Replay {
@@ -1096,6 +1192,44 @@ static void replay_game(const gn_game &g, Replay &r) {
     if (g.skip_positions && g.skip_positions[k] < r.skip.size()) r.skip[g.skip_positions[k]] = 1;
 }
 
+// A game prepared on the host for the GPU replay: its root (Position::set on the root FEN)
+// and its move tokens as uci_code values (the wire form, whitespace-separated).
+struct GamePrep {
+  gn_board root;
+  bool ok = false;
+  std::vector<uint16_t> codes;
+};
+
+static void prep_game(const gn_game &g, GamePrep &p) {
+  Board B;
+  if (!g.root_fen || !parse_fen(g.root_fen, B)) return;
+  pack(B, p.root);
+  p.ok = true;
+  const char *s = g.uci_moves ? g.uci_moves : "";
+  while (*s) {
+    while (*s == ' ' || *s == '\t' || *s == '\n' || *s == '\r') ++s;
+    if (!*s) break;
+    const char *e = s;
+    while (*e && *e != ' ' && *e != '\t' && *e != '\n' && *e != '\r') ++e;
+    p.codes.push_back(uci_code(s, (int)std::min<ptrdiff_t>(e - s, 6)) );
+    s = e;
+  }
+}
+
+// the text of a game's move k (1-based), for the error message (at most 16 characters)
+static std::string move_token(const gn_game &g, size_t k) {
+  const char *s = g.uci_moves ? g.uci_moves : "";
+  for (size_t i = 1; *s; ++i) {
+    while (*s == ' ' || *s == '\t' || *s == '\n' || *s == '\r') ++s;
+    if (!*s) break;
+    const char *e = s;
+    while (*e && *e != ' ' && *e != '\t' && *e != '\n' && *e != '\r') ++e;
+    if (i == k) return std::string(s, (size_t)std::min<ptrdiff_t>(e - s, 16));
+    s = e;
+  }
+  return "";
+}
+
 // ============================================================ C-ABI ========
 extern "C" {
 
@@ -1125,65 +1259,183 @@ int gn_evaluate_games(gn_ctx *ctx, const gn_game *games, size_t n_games, int mod
   if (with_children && !child_offsets) return fail(GN_E_INVALID, "child_offsets is NULL");
   if (mode < GN_MODE_FULL || mode > GN_MODE_SMALL) return fail(GN_E_INVALID, "bad mode %d", mode);
   try {
-    std::vector<Replay> rep(n_games);
+    const auto T0 = Clock::now();
+    reset_host_stats(ctx);
+    // host: root FENs parsed, UCI moves tokenized (the wire form, AcquireResponseBody.moves)
+    std::vector<GamePrep> prep(n_games);
     parallel_for(n_games, 64, [&](size_t lo, size_t hi) {
-      for (size_t i = lo; i < hi; ++i) replay_game(games[i], rep[i]);
+      for (size_t i = lo; i < hi; ++i) prep_game(games[i], prep[i]);
     });
-    size_t total = 0;
+    ctx->t_parse = ms_since(T0);
+    // games sharded over the devices, never split, weighted by their positions (moves + 1)
+    const size_t nd = ctx->devs.size();
+    std::vector<uint32_t> w(n_games);
+    for (size_t i = 0; i < n_games; ++i) w[i] = prep[i].ok ? (uint32_t)prep[i].codes.size() + 1 : 0;
+    std::vector<size_t> gb(nd + 1);
+    partition(w.data(), n_games, (int)nd, gb.data());
+    std::vector<std::unique_lock<std::mutex>> locks; // every device lock for the whole call
+    for (auto &dp : ctx->devs) locks.emplace_back(dp->mu);
+    // phase A: each device replays its games (replay_games_kernel) and reports their status
+    std::vector<std::vector<size_t>> glist(nd);  // the device's replayed games (global index)
+    std::vector<std::vector<uint64_t>> moff(nd); // their move-code offsets
+    std::vector<std::vector<int32_t>> st(nd);    // their status (0 or the first illegal move)
+    int rc = run_shards(ctx, gb, [&](size_t k, Dev &d, size_t g0, size_t g1) -> int {
+      HIP_TRY(hipSetDevice(d.id));
+      SeqGuard sg(d, d.stream);
+      HIP_TRY(sg.e);
+      auto &gl = glist[k];
+      auto &mo = moff[k];
+      mo.push_back(0);
+      for (size_t g = g0; g < g1; ++g)
+        if (prep[g].ok) gl.push_back(g), mo.push_back(mo.back() + prep[g].codes.size());
+      const size_t ng = gl.size(), nm = mo.back();
+      if (!ng) return GN_OK;
+      std::vector<uint16_t> codes(std::max<size_t>(nm, 1));
+      std::vector<gn_board> roots(ng);
+      for (size_t j = 0; j < ng; ++j) {
+        roots[j] = prep[gl[j]].root;
+        std::copy(prep[gl[j]].codes.begin(), prep[gl[j]].codes.end(), codes.begin() + mo[j]);
+      }
+      const auto t0 = Clock::now();
+      HIP_TRY(d.roots.ensure(ng));
+      HIP_TRY(d.moff.ensure(ng + 1));
+      HIP_TRY(d.codes.ensure(std::max<size_t>(nm, 1)));
+      HIP_TRY(d.rboards.ensure(nm + ng));
+      HIP_TRY(d.smoves.ensure(std::max<size_t>(nm, 1)));
+      HIP_TRY(d.rstatus.ensure(ng));
+      hipStream_t s = d.stream;
+      HIP_TRY(hipMemcpyAsync(d.roots.p, roots.data(), ng * sizeof(gn_board), hipMemcpyHostToDevice, s));
+      HIP_TRY(hipMemcpyAsync(d.moff.p, mo.data(), (ng + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+      HIP_TRY(hipMemcpyAsync(d.codes.p, codes.data(), codes.size() * sizeof(uint16_t), hipMemcpyHostToDevice, s));
+      HIP_TRY(hipStreamSynchronize(s));
+      d.t_upload += ms_since(t0);
+      const auto t1 = Clock::now();
+      HIP_TRY(launch_replay_games(d.roots.p, ng, d.moff.p, d.codes.p, d.tables, d.rboards.p, d.smoves.p, d.rstatus.p, s));
+      st[k].resize(ng);
+      HIP_TRY(hipMemcpyAsync(st[k].data(), d.rstatus.p, ng * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+      HIP_TRY(hipStreamSynchronize(s));
+      d.t_replay += ms_since(t1);
+      return GN_OK;
+    });
+    if (rc) return rc;
+    // host: status, position offsets; the evaluated (non-skipped) positions of each device
+    std::vector<int32_t> gst(n_games, GN_OK);
+    std::vector<uint32_t> npos(n_games, 0);
     std::string last_err;
-    for (size_t i = 0; i < n_games; ++i) {
-      position_offsets[i] = (uint32_t)total;
-      game_status[i] = rep[i].rc;
-      if (rep[i].rc) last_err = rep[i].err;
-      total += rep[i].boards.size();
+    for (size_t k = 0; k < nd; ++k)
+      for (size_t j = 0; j < glist[k].size(); ++j) {
+        const size_t g = glist[k][j];
+        if (st[k][j]) {
+          gst[g] = GN_E_ILLEGAL_MOVE;
+          last_err = "move " + std::to_string(st[k][j]) + " (" + move_token(games[g], (size_t)st[k][j]) + ") is not legal";
+        } else {
+          npos[g] = (uint32_t)(moff[k][j + 1] - moff[k][j] + 1);
+        }
+      }
+    uint64_t total = 0;
+    for (size_t g = 0; g < n_games; ++g) {
+      if (!prep[g].ok) gst[g] = GN_E_INVALID, last_err = "bad root FEN";
+      game_status[g] = gst[g];
+      position_offsets[g] = (uint32_t)total;
+      total += npos[g];
     }
     if (total > 0xFFFFFFFFull) return fail(GN_E_CAPACITY, "positions exceed 32-bit offsets");
     position_offsets[n_games] = (uint32_t)total;
-    if (total > position_cap) return fail(GN_E_CAPACITY, "%zu positions exceed capacity %zu", total, position_cap);
+    if (total > position_cap) return fail(GN_E_CAPACITY, "%zu positions exceed capacity %zu", (size_t)total, position_cap);
     if (total && !position_out) return fail(GN_E_INVALID, "position_out is NULL");
-    // positions to evaluate: every non-skipped position of every replayed game
-    std::vector<gn_board> ev;
-    std::vector<uint32_t> where, per_game(n_games, 0);
-    for (size_t i = 0; i < n_games; ++i)
-      for (size_t k = 0; k < rep[i].boards.size(); ++k) {
-        const size_t at = position_offsets[i] + k;
-        if (rep[i].skip[k]) {
-          position_out[at] = gn_eval{0, 0, 0, 0, 0, (uint16_t)(GN_FLAG_SKIPPED | GN_FLAG_NO_SCORE), 0};
-        } else {
-          ev.push_back(rep[i].boards[k]);
-          where.push_back((uint32_t)at);
-          ++per_game[i];
+    std::vector<std::vector<uint32_t>> src(nd), where(nd); // device board index / output index per evaluated
+    std::vector<std::vector<size_t>> starts(nd);            // first evaluated position of each game
+    std::vector<size_t> eb(nd + 1, 0);                      // evaluated positions before device k
+    std::vector<uint8_t> skip;
+    for (size_t k = 0; k < nd; ++k) {
+      for (size_t j = 0; j < glist[k].size(); ++j) {
+        const size_t g = glist[k][j];
+        if (!npos[g]) continue;
+        skip.assign(npos[g], 0);
+        for (size_t q = 0; q < games[g].n_skip; ++q)
+          if (games[g].skip_positions && games[g].skip_positions[q] < npos[g]) skip[games[g].skip_positions[q]] = 1;
+        starts[k].push_back(src[k].size());
+        for (uint32_t p = 0; p < npos[g]; ++p) {
+          const size_t at = position_offsets[g] + p;
+          if (skip[p]) {
+            position_out[at] = gn_eval{0, 0, 0, 0, 0, (uint16_t)(GN_FLAG_SKIPPED | GN_FLAG_NO_SCORE), 0};
+          } else {
+            src[k].push_back((uint32_t)(moff[k][j] + j + p));
+            where[k].push_back((uint32_t)at);
+          }
         }
       }
-    std::vector<gn_eval> res(ev.size());
-    int rc = GN_OK;
-    std::vector<uint32_t> coff;
-    if (!with_children) {
-      rc = evaluate_boards_host(ctx, ev.data(), ev.size(), mode, res.data());
-    } else {
-      coff.assign(ev.size() + 1, 0);
-      // game-aligned device shards, weighted by evaluated positions
-      const size_t nd = ctx->devs.size();
-      std::vector<size_t> gb(nd + 1), eb(nd + 1);
-      partition(per_game.data(), n_games, (int)nd, gb.data());
-      size_t acc = 0, g = 0;
-      for (size_t k = 0; k <= nd; ++k) {
-        for (; g < gb[k]; ++g) acc += per_game[g];
-        eb[k] = acc;
-      }
-      rc = expand_boards_host(ctx, ev.data(), ev.size(), mode, res.data(), coff.data(), child_moves, child_out,
-                              child_cap, eb.data());
-      if (rc == GN_OK || rc == GN_E_CAPACITY) { // child offsets over all positions (skipped: no children)
-        size_t e = 0;
-        for (size_t at = 0; at < total; ++at) {
-          child_offsets[at] = coff[e];
-          if (e < where.size() && where[e] == at) ++e;
-        }
-        child_offsets[total] = coff[ev.size()];
-      }
+      eb[k + 1] = eb[k] + src[k].size();
     }
+    // phase B: the evaluated positions gathered into contiguous parents; evaluated (no children)
+    // or counted (pass 1 of the expansion)
+    std::vector<std::vector<gn_eval>> res(nd);
+    std::vector<std::vector<uint64_t>> off(nd);
+    std::vector<size_t> db(nd + 1);
+    for (size_t k = 0; k <= nd; ++k) db[k] = k; // one "item" per device: run_shards' shard k = device k
+    auto has = [&](size_t k) { return !src[k].empty(); };
+    rc = run_shards(ctx, db, [&](size_t k, Dev &d, size_t, size_t) -> int {
+      if (!has(k)) return GN_OK;
+      HIP_TRY(hipSetDevice(d.id));
+      SeqGuard sg(d, d.stream);
+      HIP_TRY(sg.e);
+      const size_t m = src[k].size();
+      hipStream_t s = d.stream;
+      const auto t0 = Clock::now();
+      HIP_TRY(d.gidx.ensure(m));
+      HIP_TRY(d.par.ensure(m));
+      HIP_TRY(hipMemcpyAsync(d.gidx.p, src[k].data(), m * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+      HIP_TRY(launch_gather_boards(d.rboards.p, d.gidx.p, m, d.par.p, s));
+      HIP_TRY(hipStreamSynchronize(s));
+      d.t_upload += ms_since(t0);
+      res[k].resize(m);
+      if (with_children) return count_shard(d, d.par.p, m, off[k]);
+      const auto t1 = Clock::now();
+      HIP_TRY(d.io_out.ensure(m));
+      int r = evaluate_on(ctx, d, d.par.p, m, mode, d.io_out.p, s, nullptr);
+      if (!r) r = resolve_scores(ctx, d, d.par.p, m, mode, d.io_out.p, nullptr, s);
+      if (r) return r;
+      HIP_TRY(hipStreamSynchronize(s));
+      d.t_compute += ms_since(t1);
+      const auto t2 = Clock::now();
+      HIP_TRY(hipMemcpy(res[k].data(), d.io_out.p, m * sizeof(gn_eval), hipMemcpyDeviceToHost));
+      d.t_download += ms_since(t2);
+      return GN_OK;
+    });
     if (rc) return rc;
-    for (size_t e = 0; e < ev.size(); ++e) position_out[where[e]] = res[e];
+    if (with_children) {
+      std::vector<uint64_t> cb(nd + 1, 0);
+      for (size_t k = 0; k < nd; ++k) cb[k + 1] = cb[k] + (has(k) ? off[k].back() : 0);
+      const uint64_t ctot = cb[nd];
+      if (ctot > 0xFFFFFFFFull) return fail(GN_E_CAPACITY, "children exceed 32-bit offsets");
+      // child offsets over all positions (skipped ones: no children)
+      for (size_t g = 0; g < n_games; ++g)
+        for (uint32_t p = 0; p < npos[g]; ++p) child_offsets[position_offsets[g] + p] = 0xFFFFFFFFu;
+      for (size_t k = 0; k < nd; ++k)
+        for (size_t e = 0; e < where[k].size(); ++e) child_offsets[where[k][e]] = (uint32_t)(cb[k] + off[k][e]);
+      uint32_t next = (uint32_t)ctot; // skipped positions take the next evaluated position's offset
+      for (size_t at = total; at-- > 0;) {
+        if (child_offsets[at] == 0xFFFFFFFFu) child_offsets[at] = next;
+        else next = child_offsets[at];
+      }
+      child_offsets[total] = (uint32_t)ctot;
+      if (ctot > child_cap) return fail(GN_E_CAPACITY, "%zu children exceed capacity %zu", (size_t)ctot, child_cap);
+      if (ctot && (!child_moves || !child_out)) return fail(GN_E_INVALID, "NULL child buffer");
+      // phase C: the expansion pipeline, chunks cut at game starts
+      rc = run_shards(ctx, db, [&](size_t k, Dev &d, size_t, size_t) -> int {
+        if (!has(k)) return GN_OK;
+        HIP_TRY(hipSetDevice(d.id));
+        SeqGuard sg(d, d.stream);
+        HIP_TRY(sg.e);
+        const size_t m = src[k].size();
+        return expand_pipelined(ctx, d, d.par.p, m, mode, off[k], chunk_bounds(m, starts[k], chunk_target(m)),
+                                res[k].data(), child_moves + cb[k], child_out + cb[k]);
+      });
+      if (rc) return rc;
+    }
+    for (size_t k = 0; k < nd; ++k)
+      for (size_t e = 0; e < where[k].size(); ++e) position_out[where[k][e]] = res[k][e];
+    ctx->t_total = ms_since(T0);
     if (!last_err.empty()) g_err = last_err;
     return GN_OK;
   } catch (const std::bad_alloc &) {
@@ -1494,6 +1746,29 @@ int gn_time_evaluate_device(gn_ctx *ctx, int device_slot, const gn_board *d_boar
     *ft_rows = r;
   }
   if (he != hipSuccess) return fail(GN_E_HIP, "timing failed: %s", hipGetErrorString(he));
+  return GN_OK;
+}
+
+int gn_random_games_uci(uint64_t seed, size_t first_game, size_t n_games, int plies, char *buf, size_t stride) {
+  if (n_games && !buf) return fail(GN_E_INVALID, "NULL argument");
+  if (plies < 0 || plies > 1000) return fail(GN_E_INVALID, "plies out of range");
+  if (stride < 6 * (size_t)plies + 1) return fail(GN_E_INVALID, "stride < 6 * plies + 1");
+  try {
+    parallel_for(n_games, 64, [&](size_t lo, size_t hi) {
+      for (size_t g = lo; g < hi; ++g) {
+        char *o = buf + g * stride;
+        size_t len = 0;
+        random_game(seed + first_game + g, plies, host_tables(), [&](int k, const Board &, uint16_t m) {
+          if (!k || !m) return;
+          if (len) o[len++] = ' ';
+          len += (size_t)move_uci(m, o + len);
+        });
+        o[len] = '\0';
+      }
+    });
+  } catch (...) {
+    return fail(GN_E_NOMEM, "thread start failed");
+  }
   return GN_OK;
 }
 
@@ -1867,6 +2142,27 @@ int gn_get_option(const gn_ctx *ctx, int option, int64_t *value) {
     *value = (int64_t)((double)m * 1e6);
     return GN_OK;
   }
+  case GN_STAT_HOST_PARSE_NS:
+  case GN_STAT_HOST_TOTAL_NS:
+    *value = (int64_t)((option == GN_STAT_HOST_PARSE_NS ? ctx->t_parse : ctx->t_total) * 1e6);
+    return GN_OK;
+  case GN_STAT_HOST_UPLOAD_NS:
+  case GN_STAT_HOST_REPLAY_NS:
+  case GN_STAT_HOST_COMPUTE_NS:
+  case GN_STAT_HOST_DOWNLOAD_NS:
+  case GN_STAT_HOST_TAIL_NS: { // the last host-buffer call, max over devices
+    double m = 0;
+    for (auto &dp : ctx->devs) {
+      const Dev &d = *dp;
+      m = std::max(m, option == GN_STAT_HOST_UPLOAD_NS    ? d.t_upload
+                      : option == GN_STAT_HOST_REPLAY_NS  ? d.t_replay
+                      : option == GN_STAT_HOST_COMPUTE_NS ? d.t_compute
+                      : option == GN_STAT_HOST_DOWNLOAD_NS ? d.t_download
+                                                           : d.t_tail);
+    }
+    *value = (int64_t)(m * 1e6);
+    return GN_OK;
+  }
   case GN_STAT_SCRATCH_PADS: { // read-only: the last planned expansion's GN_SCR_GAP no-op entries, summed
     int64_t sum = 0;
     for (auto &dp : ctx->devs) {
@@ -1911,10 +2207,15 @@ int gn_expand_and_evaluate(gn_ctx *ctx, const char *const *parent_fens, size_t n
     return GN_OK;
   }
   try {
+    const auto T0 = Clock::now();
+    reset_host_stats(ctx);
     std::vector<gn_board> boards(n);
     int rc = gn_pack_fens(parent_fens, n, boards.data(), nullptr);
     if (rc) return rc;
-    return expand_boards_host(ctx, boards.data(), n, mode, parent_out, child_offsets, child_moves, child_out, cap);
+    ctx->t_parse = ms_since(T0);
+    rc = expand_boards_host(ctx, boards.data(), n, mode, parent_out, child_offsets, child_moves, child_out, cap);
+    ctx->t_total = ms_since(T0);
+    return rc;
   } catch (const std::bad_alloc &) {
     return fail(GN_E_NOMEM, "host allocation failed");
   } catch (...) {

@@ -7,18 +7,24 @@
 #include "nnue.h"
 
 // Row-ring depth of the planned expansion's stream (stream.hip: entries in flight per wave,
-// 4 or 8), and the least distance, in entries of one list, from a king-cache store to a later
-// load of that row: the store is issued while consuming entry j, the ring then waits
-// vmcnt(2 * RD - 2) before each entry, which retires the store (vmcnt counts loads and stores
-// together in issue order, MI355X_MICROARCH.md "s_waitcnt vmcnt(N)") at entry j + RD - 1,
-// whose ring slot then issues entry j + 2 * RD - 1's loads.  A load at that distance or more
-// is therefore issued after the store has completed, with no drain and no reliance on how
-// the memory pipeline orders one wave's store and load to one address.  The plan pads the
-// lists to keep it and asserts it (error bit 4).
+// 4 or 8), and GN_SCR_GAP, the least distance in entries of one list from a king-cache store to
+// a later load of that row (the plan pads the lists to keep it and asserts it: error bit 2).
+// The ring issues an entry's row loads while consuming the entry GN_RING before it, and the
+// store happens while consuming its own entry, so at a distance >= GN_RING the load is issued
+// after the store, by the same lanes, to the same address.  One work-item's later load of an
+// address it stored needs no wait on this hardware: hipcc itself emits `global_store_dword`
+// directly followed by `global_load_dword` for C++ `p[i] = x; y = p[i ^ j];`
+// (tests/test_host.py::test_same_address_store_then_load_needs_no_wait compiles exactly that
+// and checks), i.e. one wave's vector-memory operations reach one address in issue order.
+// -DGN_SCR_GAP=7 (2 * GN_RING - 1) is the stricter variant: the ring's vmcnt(2 * GN_RING - 2)
+// waits then retire the store before the load issues (vmcnt counts loads and stores together
+// in issue order, MI355X_MICROARCH.md "s_waitcnt vmcnt(N)"); measured 2.9 % slower stream.
 #ifndef GN_RING
 #define GN_RING 4
 #endif
-#define GN_SCR_GAP (2 * GN_RING - 1)
+#ifndef GN_SCR_GAP
+#define GN_SCR_GAP GN_RING
+#endif
 
 namespace gn {
 
@@ -153,6 +159,13 @@ hipError_t launch_random_positions(uint64_t seed, size_t first, size_t n, int ma
 // random games: out[g * (plies + 1) + k] = position after k plies of game g
 hipError_t launch_random_games(uint64_t seed, size_t first_game, size_t n_games, int plies, const Tables *tables,
                                gn_board *out, hipStream_t s);
+// lichess batches replayed on the GPU: game g's move codes codes[moff[g], moff[g + 1]) from
+// roots[g]; positions at boards[moff[g] + g + k], resolved moves at smoves[moff[g] + k - 1],
+// status[g] = 0 or the 1-based index of the first illegal move (replay_games_kernel)
+hipError_t launch_replay_games(const gn_board *roots, size_t ng, const uint64_t *moff, const uint16_t *codes,
+                               const Tables *tables, gn_board *boards, uint16_t *smoves, int32_t *status, hipStream_t s);
+// dst[i] = src[idx[i]]
+hipError_t launch_gather_boards(const gn_board *src, const uint32_t *idx, size_t n, gn_board *dst, hipStream_t s);
 // narrowing copy of offsets for the C-ABI
 hipError_t launch_offsets_u32(const uint64_t *in, size_t n, uint32_t *out, hipStream_t s);
 // exclusive scan of n + 1 counts (counts[n] must be 0); temp grows on demand

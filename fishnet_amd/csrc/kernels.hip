@@ -1803,20 +1803,53 @@ __global__ void random_games_kernel(uint64_t seed, size_t first_game, size_t n_g
   load_tables(T, tables);
   const size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= n_games) return;
-  Xoshiro rng(seed + first_game + g);
-  Board B = start_position();
-  gn_board pb;
-  pack(B, pb);
   gn_board *dst = out + g * (size_t)(plies + 1);
-  dst[0] = pb;
-  for (int k = 1; k <= plies; ++k) {
-    const int n = count_legal(B, T);
-    if (n && B.rule50 < 100) {
-      B = do_move(B, nth_legal(B, T, (int)rng.below((uint32_t)n)));
-      pack(B, pb);
-    }
+  random_game(seed + first_game + g, plies, T, [&](int k, const Board &B, uint16_t) {
+    gn_board pb;
+    pack(B, pb);
     dst[k] = pb;
+  });
+}
+
+// Lichess batches replayed on the GPU (gn_evaluate_games; IncomingBatch::from_acquired,
+// /root/reference/src/queue.rs:548-700): one thread per game resolves the game's move codes
+// (uci_code) one after another with resolve_uci (shakmaty's UciMove::to_move rule) and writes
+// position k (the root after k moves) to boards[moff[g] + g + k] and the resolved move to
+// smoves[moff[g] + k - 1]; status[g] = 0, or k for the first move k (1-based) that is not
+// legal (the game then fails, as `uci.to_move(&pos)?` fails the batch, queue.rs:576).
+__global__ void replay_games_kernel(const gn_board *__restrict__ roots, size_t ng, const uint64_t *__restrict__ moff,
+                                    const uint16_t *__restrict__ codes, const Tables *__restrict__ tables,
+                                    gn_board *__restrict__ boards, uint16_t *__restrict__ smoves,
+                                    int32_t *__restrict__ status) {
+  __shared__ Tables T;
+  load_tables(T, tables);
+  const size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= ng) return;
+  const uint64_t m0 = moff[g], m1 = moff[g + 1];
+  gn_board *dst = boards + m0 + g;
+  Board B;
+  unpack(roots[g], B); // validated by the host's FEN parser
+  dst[0] = roots[g];
+  int32_t st = 0;
+  for (uint64_t k = m0; k < m1; ++k) {
+    uint16_t mv = 0;
+    if (!resolve_uci(B, T, codes[k], mv)) {
+      st = (int32_t)(k - m0) + 1;
+      break;
+    }
+    B = do_move(B, mv, nullptr);
+    gn_board pb;
+    pack(B, pb);
+    dst[k - m0 + 1] = pb;
+    smoves[k] = mv;
   }
+  status[g] = st;
+}
+
+__global__ void gather_boards_kernel(const gn_board *__restrict__ src, const uint32_t *__restrict__ idx, size_t n,
+                                     gn_board *__restrict__ dst) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dst[i] = src[idx[i]];
 }
 
 // sort key of a position: both king squares (L2 locality of the king-bucket slices),
@@ -1937,6 +1970,20 @@ hipError_t launch_random_games(uint64_t seed, size_t first_game, size_t n_games,
   if (!n_games) return hipSuccess;
   hipLaunchKernelGGL(random_games_kernel, dim3(blocks_for(n_games, 128)), dim3(128), 0, s, seed, first_game, n_games,
                      plies, tables, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_replay_games(const gn_board *roots, size_t ng, const uint64_t *moff, const uint16_t *codes,
+                               const Tables *tables, gn_board *boards, uint16_t *smoves, int32_t *status, hipStream_t s) {
+  if (!ng) return hipSuccess;
+  hipLaunchKernelGGL(replay_games_kernel, dim3(blocks_for(ng, 64)), dim3(64), 0, s, roots, ng, moff, codes, tables,
+                     boards, smoves, status);
+  return hipGetLastError();
+}
+
+hipError_t launch_gather_boards(const gn_board *src, const uint32_t *idx, size_t n, gn_board *dst, hipStream_t s) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(gather_boards_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, src, idx, n, dst);
   return hipGetLastError();
 }
 

@@ -39,9 +39,9 @@
 // kind, [19] LAST, [23:20] slot, [24] side, [25] PAR_E, [27] KST, [31] SCR; so the
 // stream's common entry is a multiply-add with hi as its scalar operand and two bit tests.
 // The ring issues a row load 4 entries before it
-// consumes it, so an entry that loads a scratch row sits at least GN_SCR_GAP = 7 entries
+// consumes it, so an entry that loads a scratch row sits at least GN_SCR_GAP (= 4) entries
 // after the last store to scratch in its list (no-op entries are inserted when needed): the
-// ring's own vmcnt waits have then retired the store before the load issues (kernels.h).
+// load is then issued after the store, by the same lanes (kernels.h: why that suffices).
 // The ring runs across tiles.
 #include <stdio.h>
 #include <stdlib.h>
@@ -80,7 +80,7 @@ __device__ unsigned long long gn_sp[8]; // [0] stream [1] barrier wait [2] layer
 namespace gn {
 namespace ps {
 constexpr uint32_t ROW = (1u << 19) - 1, SUB = 1u << 19, I_ZERO = 1u << 20, I_PACC = 2u << 20, I_BASE = 3u << 20,
-                   INIT = 3u << 20, LAST = 1u << 22, SLOT_SH = 23, SIDE_SH = 27, PAR_E = 1u << 28,
+                   LAST = 1u << 22, SLOT_SH = 23, SIDE_SH = 27, PAR_E = 1u << 28,
                    SCR = 1u << 30, KST = 1u << 31;
 constexpr uint32_t PAD = (uint32_t)FT_BIAS_ROW | I_ZERO | SUB;
 // pre-decoded form (see the header)
@@ -139,19 +139,24 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
   const uint64_t us_b = pbeg + offsets[pbeg];
   const uint64_t rbeg = eoff[pbeg] + 16ull * blk, rend = eoff[pend] + 16ull * (blk + 1);
   uint64_t *E0 = ent + rbeg, *E1 = ent + rend - 1;
-  const uint64_t rtot = rend - rbeg; // the block's entry region (both lists)
+  const uint32_t rtot = (uint32_t)(rend - rbeg); // the block's entry region (both lists; < 2^32)
   uint32_t bad = 0;                  // this lane's error bits (reported once per wave)
   // a block's tiles: <= ceil(slots / 16) + one bucket cut per parent (a parent's own slots hold
   // <= 2 buckets, so a tile is cut at most once per parent), hence this base
   TileDesc *T = tiles + us_b / 16 + (uint64_t)(K + 2) * blk;
   uint32_t safe0 = 0, safe1 = 0; // first index of each list at which a scratch row may be loaded
   auto put = [&](int g, uint32_t i, uint32_t v) {
+#ifdef GN_AB_PLAN_NOCHECK // A/B only
+    if (g) E1[-(int64_t)i] = enc64<L1>(v);
+    else E0[i] = enc64<L1>(v);
+    return;
+#endif
     if (i >= rtot) { // never past the block's region (the final check reports the overflow)
       bad |= 1u;
       return;
     }
     // a scratch-row load must sit GN_SCR_GAP entries after the list's last scratch store
-    if ((v & SCR) && !(v & KST) && i < (g ? safe1 : safe0)) bad |= 4u;
+    if ((v & (SCR | KST)) == SCR && i < (g ? safe1 : safe0)) bad |= 4u;
     if (g) E1[-(int64_t)i] = enc64<L1>(v);
     else E0[i] = enc64<L1>(v);
   };
@@ -506,7 +511,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
   // closer than GN_SCR_GAP to its list's last scratch store; neither can happen by construction
   const uint32_t werr = __ballot(bad & 1u) ? 1u : 0u, werr4 = __ballot(bad & 4u) ? 4u : 0u;
   if (lane == 0) {
-    if ((uint64_t)len0 + len1 > rtot || werr) atomicOr(err, 1u);
+    if ((uint64_t)len0 + len1 > (uint64_t)rtot || werr) atomicOr(err, 1u);
     if (werr4) atomicOr(err, 4u);
     if (rows_out) atomicAdd(rows_out, rows);
     if (pads_out && pads) atomicAdd(pads_out, pads);

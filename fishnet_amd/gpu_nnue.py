@@ -42,9 +42,11 @@ EXPORTS = ["gn_load_net", "gn_load_net_memory", "gn_free", "gn_last_error", "gn_
            "gn_time_evaluate_device", "gn_random_positions_device", "gn_set_option", "gn_get_option",
            "gn_time_expand_device", "gn_random_games_device", "gn_replay_game", "gn_evaluate_games",
            "gn_net_sha256", "gn_partition", "gn_checksum_device",
-           "gn_boards_to_fens", "gn_load_net_archive", "gn_archive_read", "gn_expand2_device"]
+           "gn_boards_to_fens", "gn_load_net_archive", "gn_archive_read", "gn_expand2_device",
+           "gn_random_games_uci"]
 OPT_INCREMENTAL_CHILDREN, OPT_XCD_SWIZZLE, OPT_KING_SORT, OPT_CHAIN, OPT_KING_CACHE = 1, 2, 3, 4, 5
 STAT_CHAIN_FALLBACKS, STAT_PLAN_NS, STAT_STREAM_NS, STAT_SCRATCH_PADS = 100, 101, 102, 103
+HOST_STAGES = {"parse": 110, "upload": 111, "replay": 112, "compute": 113, "download": 114, "tail": 115, "total": 116}
 EXPAND_STAGES = ["count_scan", "total_readback", "write_children", "classify", "small_net", "big_net", "finalize",
                  "score"]
 
@@ -136,6 +138,7 @@ def lib():
         "gn_archive_read": [C.c_char_p, C.c_char_p, vp, sz, C.POINTER(sz)],
         "gn_expand2_device": [vp, i32, vp, sz, i32, vp, vp, vp, vp, vp, sz, vp, vp, vp, sz, C.POINTER(sz),
                               C.POINTER(sz), vp],
+        "gn_random_games_uci": [C.c_uint64, sz, sz, i32, vp, sz],
     }
     for name, args in sig.items():
         f = getattr(L, name)
@@ -204,6 +207,14 @@ def replay_game(root_fen: str, moves, skip=()):
     mv = np.zeros(max(cap - 1, 1), dtype=np.uint16)
     _check(lib().gn_replay_game(arr, boards.ctypes.data, skipped.ctypes.data, mv.ctypes.data, cap, C.byref(n)))
     return boards, skipped.astype(bool), mv[:cap - 1]
+
+
+def random_games_uci(seed: int, first_game: int, n_games: int, plies: int = 80) -> list:
+    """UCI move strings of the games gn_random_games_device plays (lichess wire form)."""
+    stride = 6 * plies + 1
+    buf = np.zeros((n_games, stride), dtype=np.uint8)
+    _check(lib().gn_random_games_uci(seed, first_game, n_games, plies, buf.ctypes.data, stride))
+    return [bytes(r[:np.argmin(r)]).decode() for r in buf]
 
 
 def net_sha256(data: bytes) -> str:
@@ -380,6 +391,38 @@ class GpuNnue:
                 out.append(d)
             return out
         raise GnError(E_CAPACITY, "capacity retry failed")
+
+    def evaluate_games_arrays(self, arr, ng, mode=MODE_FULL, children=True, caps=None, bufs=None):
+        """gn_evaluate_games on a prepared gn_game array (_games_array), results as flat arrays:
+        (position_offsets, game_status, positions, child_offsets, child_moves, children, caps).
+        caps = (position_cap, child_cap) from an earlier call avoid the sizing retry; bufs (a dict,
+        filled on first use) keeps the output arrays for the next call (a caller's reused buffers)."""
+        pcap, ccap = caps or (0, 0)
+        bufs = {} if bufs is None else bufs
+        offs = np.zeros(ng + 1, dtype=np.uint32)
+        status = np.zeros(max(ng, 1), dtype=np.int32)
+        for _ in range(3):
+            if bufs.get("caps") != (pcap, ccap):
+                bufs.update(caps=(pcap, ccap), pos=np.empty(max(pcap, 1), dtype=EVAL_DTYPE),
+                            coffs=np.empty(pcap + 1, dtype=np.uint32), cmv=np.empty(max(ccap, 1), dtype=np.uint16),
+                            cev=np.empty(max(ccap, 1), dtype=EVAL_DTYPE))
+            pos, coffs, cmv, cev = bufs["pos"], bufs["coffs"], bufs["cmv"], bufs["cev"]
+            rc = lib().gn_evaluate_games(self.h, arr, ng, mode, int(children), offs.ctypes.data, status.ctypes.data,
+                                         pos.ctypes.data, pcap, coffs.ctypes.data if children else None,
+                                         cmv.ctypes.data, cev.ctypes.data, ccap)
+            if rc == E_CAPACITY:
+                need_p = int(offs[-1])
+                need_c = int(coffs[-1]) if children and need_p <= pcap else ccap
+                pcap, ccap = max(pcap, need_p), max(ccap, need_c)
+                continue
+            _check(rc)
+            p, t = int(offs[-1]), int(coffs[int(offs[-1])]) if children else 0
+            return offs, status, pos[:p], coffs[:p + 1], cmv[:t], cev[:t], (pcap, ccap)
+        raise GnError(E_CAPACITY, "capacity retry failed")
+
+    def host_stages(self):
+        """Stage times (ms) of the last gn_evaluate_games / gn_expand_and_evaluate (GN_STAT_HOST_*)."""
+        return {k: self.get_option(v) / 1e6 for k, v in HOST_STAGES.items()}
 
     def perft(self, fen: str, depth: int) -> int:
         v = C.c_uint64()

@@ -100,6 +100,18 @@ extern "C" {
                                          sits >= 2 * ring depth - 1 list entries after the
                                          list's last king-cache store (the store has then
                                          completed when the load issues)                 */
+/* stage times of the last gn_evaluate_games / gn_expand_and_evaluate (nanoseconds; per-device
+ * stages: the slowest device).  The expansion runs in chunks of whole games; a drain thread
+ * downloads chunk c's records on a copy stream while chunk c + 1 computes.               */
+#define GN_STAT_HOST_PARSE_NS 110     /* host: root FENs / FENs parsed, UCI moves tokenized */
+#define GN_STAT_HOST_UPLOAD_NS 111    /* host -> device copies of the inputs               */
+#define GN_STAT_HOST_REPLAY_NS 112    /* the GPU replay of the games' moves (games only)   */
+#define GN_STAT_HOST_COMPUTE_NS 113   /* children, evaluation and score rule, all chunks   */
+#define GN_STAT_HOST_DOWNLOAD_NS 114  /* device -> host result copies, all chunks (they
+                                         overlap the next chunk's compute)               */
+#define GN_STAT_HOST_TAIL_NS 115      /* the downloads still running after the last chunk
+                                         computed (not overlapped)                        */
+#define GN_STAT_HOST_TOTAL_NS 116     /* the whole call                                    */
 #define GN_STAT_CHAIN_FALLBACKS 100   /* blocks of the last chained expansion (per device,
                                          summed) that found their carry / king-cache slot
                                          still in use after a bounded wait and ran
@@ -373,6 +385,11 @@ GN_API int gn_checksum_device(gn_ctx *ctx, int device_slot, const void *d_ptr, s
  * game that ends early repeats its final position).  Asynchronous. */
 GN_API int gn_random_games_device(gn_ctx *ctx, int device_slot, uint64_t seed, size_t first_game, size_t n_games,
                                   int plies, gn_board *d_out, void *stream);
+/* The UCI moves of the same games gn_random_games_device plays, as the lichess API sends a
+ * game (AcquireResponseBody.moves: space-separated, standard castling notation e1g1): game g's
+ * NUL-terminated string at buf + g * stride (stride >= 6 * plies + 1); a game that ended
+ * (mate, stalemate, rule50) stops there.  Host only, multithreaded. */
+GN_API int gn_random_games_uci(uint64_t seed, size_t first_game, size_t n_games, int plies, char *buf, size_t stride);
 /* Device memory helpers (so callers need no HIP headers). */
 GN_API int gn_device_alloc(gn_ctx *ctx, int device_slot, size_t bytes, void **ptr);
 GN_API int gn_device_free(gn_ctx *ctx, int device_slot, void *ptr);

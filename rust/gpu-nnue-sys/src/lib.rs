@@ -38,6 +38,13 @@ pub const GN_STAT_CHAIN_FALLBACKS: c_int = 100;
 pub const GN_STAT_PLAN_NS: c_int = 101;
 pub const GN_STAT_STREAM_NS: c_int = 102;
 pub const GN_STAT_SCRATCH_PADS: c_int = 103;
+pub const GN_STAT_HOST_PARSE_NS: c_int = 110;
+pub const GN_STAT_HOST_UPLOAD_NS: c_int = 111;
+pub const GN_STAT_HOST_REPLAY_NS: c_int = 112;
+pub const GN_STAT_HOST_COMPUTE_NS: c_int = 113;
+pub const GN_STAT_HOST_DOWNLOAD_NS: c_int = 114;
+pub const GN_STAT_HOST_TAIL_NS: c_int = 115;
+pub const GN_STAT_HOST_TOTAL_NS: c_int = 116;
 
 // per-position flags
 pub const GN_FLAG_IN_CHECK: u16 = 1;
@@ -180,6 +187,8 @@ extern "C" {
                               sum: *mut u64) -> c_int;
     pub fn gn_random_games_device(ctx: *mut gn_ctx, device_slot: c_int, seed: u64, first_game: usize,
                                   n_games: usize, plies: c_int, d_out: *mut gn_board, stream: *mut c_void) -> c_int;
+    pub fn gn_random_games_uci(seed: u64, first_game: usize, n_games: usize, plies: c_int, buf: *mut c_char,
+                               stride: usize) -> c_int;
     pub fn gn_device_alloc(ctx: *mut gn_ctx, device_slot: c_int, bytes: usize, ptr: *mut *mut c_void) -> c_int;
     pub fn gn_device_free(ctx: *mut gn_ctx, device_slot: c_int, ptr: *mut c_void) -> c_int;
     pub fn gn_memcpy_h2d(ctx: *mut gn_ctx, device_slot: c_int, dst: *mut c_void, src: *const c_void, bytes: usize)

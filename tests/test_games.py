@@ -216,3 +216,57 @@ def test_every_game_position_scored(gpu_ctx, oracle_nets, oracle_lib, children):
                 assert got["flags"] & G.FLAG_SEARCHED and got["best_move"]
                 seen.add("check")
     assert seen == {"mate0", "stalemate", "check"}
+
+
+def test_random_games_uci_replay(G, oracle_lib):
+    """gn_random_games_uci: the bench's games in the lichess wire form (standard castling
+    notation) replay legally, through the library's host replay and the oracle's."""
+    ucis = G.random_games_uci(0x5EED0003, 0, 24, 80)
+    assert len(ucis) == 24 and all(ucis)
+    for u in ucis:
+        boards, _, played = G.replay_game(START, u)
+        fens, exp = oracle_lib.replay_game(START, u)
+        assert fens_of(G, boards) == fens and [int(m) for m in played] == exp
+        assert len(boards) == len(u.split()) + 1
+
+
+@pytest.mark.gpu
+def test_gpu_replay_equals_device_games_and_host_replay(gpu_ctx, oracle_lib):
+    """gn_evaluate_games replays the moves on the GPU (replay_games_kernel): its positions are
+    the ones gn_random_games_device plays for the same seeds (full-length games), and the host
+    replay's (gn_replay_game) for all; a game with an illegal move fails with its message."""
+    from fishnet_amd import gpu_nnue as G
+    n, plies, seed = 64, 80, 0x5EED0003
+    ucis = G.random_games_uci(seed, 0, n, plies)
+    games = [(START, u, []) for u in ucis] + [(START, "e2e4 e7e5 e1g1", [])]
+    arr, keep = G._games_array(games)
+    offs, status, pos, coffs, cmv, cev, _ = gpu_ctx.evaluate_games_arrays(arr, len(games), 1, children=True)
+    assert list(status[:n]) == [0] * n and status[n] == G.E_ILLEGAL_MOVE
+    assert "move 3 (e1g1) is not legal" in (G.lib().gn_last_error() or b"").decode()
+    d_b = gpu_ctx.alloc(n * (plies + 1) * 32)
+    gpu_ctx.random_games_device(seed, 0, n, plies, d_b)
+    gpu_ctx.synchronize()
+    dev = d_b.download(G.BOARD_DTYPE, n * (plies + 1)).reshape(n, plies + 1)
+    full = [g for g in range(n) if offs[g + 1] - offs[g] == plies + 1]
+    assert len(full) > n // 2
+    sel = np.concatenate([dev[g] for g in full])
+    m, cap = len(sel), int(60 * len(sel))
+    bufs = {k: gpu_ctx.alloc(sz) for k, sz in (("b", m * 32), ("po", m * G.EVAL_SIZE), ("off", (m + 1) * 4),
+                                                  ("ch", cap * 32), ("mv", cap * 2), ("co", cap * G.EVAL_SIZE))}
+    bufs["b"].upload(sel)
+    t = gpu_ctx.expand_device(bufs["b"], m, 1, bufs["po"], bufs["off"], bufs["ch"], bufs["mv"], bufs["co"], cap)
+    po, doff = bufs["po"].download(G.EVAL_DTYPE, m), bufs["off"].download(np.uint32, m + 1)
+    dmv, dco = bufs["mv"].download(np.uint16, t), bufs["co"].download(G.EVAL_DTYPE, t)
+    i = 0
+    for g in full:
+        for k in range(plies + 1):
+            at = int(offs[g]) + k
+            assert pos[at] == po[i], (g, k)
+            a, b = int(coffs[at]), int(coffs[at + 1])
+            c, d = int(doff[i]), int(doff[i + 1])
+            assert np.array_equal(cmv[a:b], dmv[c:d]) and np.array_equal(cev[a:b], dco[c:d]), (g, k)
+            i += 1
+    for g in range(0, n, 7):  # the host replay
+        boards, _, _ = G.replay_game(START, ucis[g])
+        got = gpu_ctx.evaluate_batch([G.board_to_fen(b) for b in boards], 1)
+        assert np.array_equal(got, pos[int(offs[g]):int(offs[g + 1])]), g

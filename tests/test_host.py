@@ -202,3 +202,26 @@ def test_rust_sys_crate_matches_header():
         rb = re.search(r"pub struct %s \{(.*?)\n\}" % st, rs, re.S).group(1)
         rf = re.findall(r"pub (\w+):", rb)
         assert cf == rf, (st, cf, rf)
+
+
+def test_same_address_store_then_load_needs_no_wait(tmp_path):
+    """The rule the planned expansion's king-cache reload relies on (fishnet_amd/csrc/kernels.h,
+    GN_SCR_GAP): one work-item's load of an address it stored earlier needs no s_waitcnt on
+    gfx950.  hipcc's own code generation shows it: for a store and a later possibly-aliasing
+    load in plain C++ it emits the load directly after the store, with no wait between."""
+    import re
+    import shutil
+    import subprocess
+    if not shutil.which("hipcc"):
+        pytest.skip("hipcc not available")
+    src = tmp_path / "k.hip"
+    src.write_text("#include <hip/hip_runtime.h>\n"
+                   "__global__ void k(int *p, int *o, int x, int j) {\n"
+                   "  int i = threadIdx.x;\n  p[i] = x;\n  int y = p[i ^ j];\n  o[i] = y + 1;\n}\n")
+    asm = tmp_path / "k.s"
+    subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "--cuda-device-only", "-S", str(src), "-o", str(asm)],
+                   check=True, capture_output=True)
+    body = asm.read_text().split("_Z1kPiS_ii:", 1)[1].split("s_endpgm", 1)[0]
+    ops = [l.split()[0] for l in body.splitlines() if re.match(r"\s+(global_|s_waitcnt)", l)]
+    i = ops.index("global_store_dword")
+    assert ops[i + 1] == "global_load_dword", ops
