@@ -247,10 +247,13 @@ def run_expand(c: Ctx, wl: dict, games: int, steps: int, warmup: int, check: int
     nn.random_games_device(SEED, first, games, PLIES, d_p)
     nn.synchronize()
     gen_s = time.perf_counter() - t
-    # one untimed expansion sizes the output buffers (and warms up); then W warmup steps
+    # one untimed expansion sizes the output buffers (and warms up); then W warmup steps.  The
+    # outputs live in torch tensors (device memory the library writes through raw pointers), so
+    # that RCCL can gather them at N > 1
     _, total, _, _ = nn.time_expand_device(d_p, n, mode, 1)
-    out = {"po": nn.alloc(n * G.EVAL_SIZE), "off": nn.alloc((n + 1) * 4), "mv": nn.alloc(max(total, 1) * 2),
-           "co": nn.alloc(max(total, 1) * G.EVAL_SIZE), "cap": total}
+    tb = lambda nb: G.DeviceView(nn, c.torch.empty(max(nb, 1), dtype=c.torch.uint8, device=c.comm.device))
+    out = {"po": tb(n * G.EVAL_SIZE), "off": tb((n + 1) * 4), "mv": tb(max(total, 1) * 2),
+           "co": tb(max(total, 1) * G.EVAL_SIZE), "cap": total}
     if warmup:
         nn.time_expand_device(d_p, n, mode, warmup, outputs=out)
     c.barrier_sync()
@@ -320,9 +323,59 @@ def run_expand(c: Ctx, wl: dict, games: int, steps: int, warmup: int, check: int
                                 "checksum_plain": f"{ref[0] ^ ref[1]:016x}",
                                 "plain_path": "GN_OPT_CHAIN=1, GN_OPT_KING_CACHE=0 (refresh-started parents)"}
         r["oracle_check"] = ver
+    if c.world > 1:
+        r["gather"] = gather_results(c, out, n, children, games, mode, check)
     for b in ("po", "off", "mv", "co"):
         out[b].free()
+    out.clear()
     d_p.free()
+    return r
+
+
+def gather_results(c: Ctx, out, n, children, games, mode, check):
+    """The result gather of DESIGN.md section 6 (N > 1): every rank's parent / child records, child
+    moves and offsets of the timed step to rank 0 over RCCL (torch.distributed gather on the
+    records' device memory), outside the timed region and timed on its own; rank 0 then checks
+    sampled parents of every rank, with all their children, against the oracle."""
+    G, T = c.G, c.torch
+    es = G.EVAL_SIZE
+    parts = (("po", n * es), ("off", (n + 1) * 4), ("mv", children * 2), ("co", children * es))
+    c.barrier_sync()
+    t0 = time.perf_counter()
+    got = {k: c.comm.gather_tensor(out[k].tensor[:nb]) for k, nb in parts}
+    T.cuda.synchronize()
+    c.barrier_sync()
+    ms = c.comm.max(time.perf_counter() - t0) * 1e3
+    nbytes = sum(c.comm.gather_i64(sum(nb for _, nb in parts)))
+    r = {"bytes_all_ranks": nbytes, "ms": round(ms, 2), "GBps_into_rank0": round(nbytes / ms / 1e6, 1),
+         "how": "torch.distributed.gather (RCCL over xGMI) of each rank's gn_eval records, child moves and offsets "
+                "to rank 0's device memory, after the timed steps"}
+    bad = 0
+    if c.rank == 0 and check:
+        O, big, small = c.oracle_nets()
+        bounds = G.partition(games * c.world, c.world)
+        d_b = c.nn.alloc(n * 32)
+        rng = np.random.default_rng(4321)
+        checked = 0
+        for rr in range(c.world):
+            c.nn.random_games_device(SEED, bounds[rr], games, PLIES, d_b)
+            c.nn.synchronize()
+            boards = d_b.download(G.BOARD_DTYPE, n)
+            po = got["po"][rr].cpu().numpy().view(G.EVAL_DTYPE)
+            off = got["off"][rr].cpu().numpy().view(np.uint32)
+            for i in rng.choice(n, size=min(32, n), replace=False):
+                lo, hi = int(off[i]), int(off[i + 1])
+                mv = got["mv"][rr][2 * lo:2 * hi].cpu().numpy().view(np.uint16)
+                ev = got["co"][rr][es * lo:es * hi].cpu().numpy().view(G.EVAL_DTYPE)
+                p_exp, m_exp, k_exp = O.expand_eval(big if mode != 2 else None, small if mode != 1 else None,
+                                                    G.board_to_fen(boards[i]), mode, incremental=True)
+                bad += int(tuple(po[i]) != p_exp or dict(zip(mv.tolist(), map(tuple, ev.tolist()))) !=
+                           dict(zip(m_exp, map(tuple, k_exp.tolist()))))
+                checked += 1
+        d_b.free()
+        r["oracle_check"] = {"parents": checked, "ranks": c.world, "mismatching_parents": bad,
+                             "of": "the gathered records on rank 0"}
+    del got
     return r
 
 
@@ -615,6 +668,9 @@ def main():
     if chk is not None:
         bad = (chk["oracle"]["mismatching_parents"] + (0 if chk["vs_plain_path"]["equal"] else 1)
                if args.workload == "expand" else chk["mismatches"])
+        if "gather" in r:
+            line["gather"] = r["gather"]
+            bad += r["gather"].get("oracle_check", {}).get("mismatching_parents", 0)
         line["oracle_check"] = chk
         line["rank_check_failures"] = c.comm.gather_i64(int(bad))
     line["rank_checksums"] = [f"{x:016x}" for x in c.comm.gather_i64(int(r["checksum"]) & 0x7FFFFFFFFFFFFFFF)]

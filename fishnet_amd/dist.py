@@ -103,6 +103,25 @@ class ShardComm:
             return None
         return [np.frombuffer(o.cpu().numpy().tobytes()[:sz], dtype=arr.dtype) for o, sz in zip(outs, sizes)]
 
+    def gather_tensor(self, t, dst: int = 0):
+        """Gathers a 1-D tensor (device tensors over RCCL, CPU tensors over gloo; the length may
+        differ per rank) to dst: dst gets the list of every rank's tensor, the others None.
+        This is the result gather of DESIGN.md section 6 (gn_eval records, moves, offsets)."""
+        if self.world == 1:
+            return [t]
+        torch, dist = self.torch, self.dist
+        sizes = self.gather_i64(int(t.numel()))
+        pad = max(sizes)
+        if t.numel() < pad:
+            buf = torch.zeros(pad, dtype=t.dtype, device=t.device)
+            buf[:t.numel()] = t
+        else:
+            buf = t.contiguous()
+        outs = [torch.empty(pad, dtype=t.dtype, device=t.device) for _ in range(self.world)] \
+            if self.rank == dst else None
+        dist.gather(buf, outs, dst=dst)
+        return None if outs is None else [o[:n] for o, n in zip(outs, sizes)]
+
     def close(self):
         if self.world > 1 and self.dist.is_initialized():
             self.dist.barrier()

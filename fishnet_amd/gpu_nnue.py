@@ -275,6 +275,19 @@ class DeviceBuffer:
             pass
 
 
+class DeviceView(DeviceBuffer):
+    """Device memory the library does not own (a torch tensor's storage, e.g. for RCCL): the
+    same upload / download / pointer interface as DeviceBuffer; never freed here."""
+
+    def __init__(self, ctx: "GpuNnue", tensor, slot: int = 0):
+        self.ctx, self.slot, self.tensor = ctx, slot, tensor
+        self.nbytes = tensor.numel() * tensor.element_size()
+        self.ptr = C.c_void_p(tensor.data_ptr())
+
+    def free(self):
+        self.ptr = C.c_void_p()
+
+
 def archive_read(path, member):
     """One member of an assets archive (zstd + ar) as bytes (gn_archive_read; CPU only)."""
     size = C.c_size_t()

@@ -53,9 +53,14 @@ def _worker(rank, world, port, q):
         mine = [f for g in games[g0:g1] for f in g]
         evals = O.eval_fens(None, net, mine, O.MODE_SMALL) if mine else np.zeros(0, dtype=O.EVAL_DTYPE)
         gathered = comm.gather_array(evals)
+        # the bench's result gather (gather_tensor: device tensors over RCCL there, CPU tensors
+        # over gloo here): the records as raw bytes, lengths differing per rank
+        import torch
+        tens = comm.gather_tensor(torch.from_numpy(np.ascontiguousarray(evals).view(np.uint8).copy()))
         comm.close()
         q.put((rank, len(got), hashlib.sha256(got).hexdigest(), label, first, count, mx, sums, (g0, g1),
-               None if gathered is None else np.concatenate(gathered).tobytes()))
+               None if gathered is None else np.concatenate(gathered).tobytes(),
+               None if tens is None else b"".join(t.numpy().tobytes() for t in tens)))
     except Exception as e:  # surface the failure to the parent
         q.put((rank, "error", repr(e)))
 
@@ -80,7 +85,7 @@ def test_two_rank_gloo_shards_evaluate():
     assert all(r[1] != "error" for r in res.values()), res
     blob = open(synthnet.cached_synth_net(128, 2), "rb").read()
     for r in (0, 1):
-        _, ln, hsh, label, first, count, mx, sums, _, _ = res[r]
+        _, ln, hsh, label, first, count, mx, sums, _, _, _ = res[r]
         assert ln == len(blob) and hsh == hashlib.sha256(blob).hexdigest() and label == "synthetic"
         assert (first, count) == (1000 * r, 1000)
         assert mx == 2.0 and sums == [1000, 1001]
@@ -89,6 +94,7 @@ def test_two_rank_gloo_shards_evaluate():
     games = _game_fens(O)
     exp = O.eval_fens(None, O.Net(data=blob), [f for g in games for f in g], O.MODE_SMALL)
     assert res[0][9] == exp.tobytes() and res[1][9] is None
+    assert res[0][10] == exp.tobytes() and res[1][10] is None
 
 
 def test_partition_is_game_aligned_and_balanced():

@@ -2,6 +2,7 @@
 (no compute calls on a GPU here)."""
 import os
 import re
+import sys
 
 import numpy as np
 import pytest
@@ -225,3 +226,34 @@ def test_same_address_store_then_load_needs_no_wait(tmp_path):
     ops = [l.split()[0] for l in body.splitlines() if re.match(r"\s+(global_|s_waitcnt)", l)]
     i = ops.index("global_store_dword")
     assert ops[i + 1] == "global_load_dword", ops
+
+
+def test_rust_patches_apply_to_reference(tmp_path):
+    """rust/patches: the compile fixes (src/stats.rs rusqlite /
+    min_user_backlog) and the GPU backend wiring (Cargo.toml feature, --gpu-devices, the worker's
+    GPU branch, whole-batch chunks) are current with their generator and apply cleanly to a
+    copy of the reference tree.  cargo is not in the image, so this is the build check."""
+    import shutil
+    import subprocess
+    ref = "/root/reference"
+    if not os.path.isdir(os.path.join(ref, "src")):
+        pytest.skip("reference tree not present")
+    gen = os.path.join(ROOT, "rust", "patches", "make_patches.py")
+    subprocess.run([sys.executable, gen, "--check", "--reference", ref], check=True)
+    work = tmp_path / "fishnet"
+    shutil.copytree(os.path.join(ref, "src"), work / "src")
+    shutil.copy(os.path.join(ref, "Cargo.toml"), work / "Cargo.toml")
+    for p in sorted(os.listdir(os.path.join(ROOT, "rust", "patches"))):
+        if p.endswith(".patch"):
+            with open(os.path.join(ROOT, "rust", "patches", p)) as f:
+                subprocess.run(["patch", "-p1", "-s", "--no-backup-if-mismatch"], cwd=work, stdin=f, check=True)
+    stats = (work / "src" / "stats.rs").read_text()
+    assert "rusqlite" not in stats and "pub fn min_user_backlog(&self) -> Duration" in stats
+    main = (work / "src" / "main.rs").read_text()
+    assert "#![deny(unsafe_code)]" in main and "gpu_backend::go(nnue, chunk, &tx)" in main
+    assert '#[path = "../gpu/fishnet-gpu/src/gpu_eval_stub.rs"]' in main
+    for f in ("gpu_eval_stub.rs", "gpu_nnue.rs"):  # the files the #[path] modules name exist
+        assert os.path.exists(os.path.join(ROOT, "rust", "fishnet-gpu", "src", f))
+    assert 'gpu = ["dep:gpu-nnue-sys"]' in (work / "Cargo.toml").read_text()
+    assert "pub gpu_devices: Option<GpuDevices>" in (work / "src" / "configure.rs").read_text()
+    assert "prev_and_current.chunks(chunk_len)" in (work / "src" / "queue.rs").read_text()
