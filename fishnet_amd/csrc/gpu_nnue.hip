@@ -335,7 +335,7 @@ static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 static int upload_net(Dev &d, int which, const HostNet &h) {
   const size_t RS = ft_row_stride((uint32_t)h.L1);
-  size_t off[9], o = 0;
+  size_t off[10], o = 0;
   const int carry = h.L1 == 128 ? 0 : CARRY_SLOTS; // the chained walk's scratch rows
   // the PSQT weights once more as [bucket][row] (721 KB: L2-resident for the plan kernel's
   // scattered 4-byte reads, which would otherwise each touch a 6 KB FT row)
@@ -343,15 +343,25 @@ static int upload_net(Dev &d, int which, const HostNet &h) {
   for (size_t r = 0; r < (size_t)FT_ROWS; ++r)
     for (int b = 0; b < PSQT_BUCKETS; ++b)
       memcpy(&psqt[(size_t)b * FT_ROWS + r], h.ft.data() + r * RS + 2 * (size_t)h.L1 + 4 * b, 4);
-  const size_t sz[9] = {((size_t)FT_ROWS + 4 * (size_t)carry + 128 * (size_t)carry + (carry ? 1 : 0)) * RS, h.bias.size() * 2, h.w0.size(), h.b0.size() * 4,
-                        h.w1.size(), h.b1.size() * 4, h.w2.size(), h.b2.size() * 4, psqt.size() * 4};
-  const void *src[9] = {h.ft.data(), h.bias.data(), h.w0.data(), h.b0.data(),
-                        h.w1.data(), h.b1.data(), h.w2.data(), h.b2.data(), psqt.data()};
-  for (int i = 0; i < 9; ++i) off[i] = o, o += align256(sz[i]);
+  // fc_0 weights once more in the MFMA's operand order (stream.hip): per bucket and 64-wide
+  // k-step, lane ln's 16 bytes (output ln & 15, inputs 16 (ln >> 4) .. + 15) at 16 ln, so a
+  // wave's k-step is one contiguous 1 KiB (8 whole lines) instead of 16 pieces of 64 B
+  const int KS = h.L1 / 64;
+  std::vector<int8_t> w0f(h.w0.size());
+  for (int b = 0; b < LAYER_STACKS; ++b)
+    for (int ks = 0; ks < KS; ++ks)
+      for (int ln = 0; ln < 64; ++ln)
+        memcpy(&w0f[(((size_t)b * KS + ks) * 64 + ln) * 16],
+               &h.w0[((size_t)b * 16 + (ln & 15)) * h.L1 + 64 * (size_t)ks + 16 * (ln >> 4)], 16);
+  const size_t sz[10] = {((size_t)FT_ROWS + 4 * (size_t)carry + 128 * (size_t)carry + (carry ? 1 : 0)) * RS, h.bias.size() * 2, h.w0.size(), h.b0.size() * 4,
+                         h.w1.size(), h.b1.size() * 4, h.w2.size(), h.b2.size() * 4, psqt.size() * 4, w0f.size()};
+  const void *src[10] = {h.ft.data(), h.bias.data(), h.w0.data(), h.b0.data(),
+                         h.w1.data(), h.b1.data(), h.w2.data(), h.b2.data(), psqt.data(), w0f.data()};
+  for (int i = 0; i < 10; ++i) off[i] = o, o += align256(sz[i]);
   uint8_t *m = nullptr;
   if (hipMalloc(&m, o) != hipSuccess) return fail(GN_E_NOMEM, "device allocation of %zu bytes failed", o);
   d.net_mem[which] = m;
-  for (int i = 0; i < 9; ++i)
+  for (int i = 0; i < 10; ++i)
     HIP_TRY(hipMemcpy(m + off[i], src[i], i == 0 ? (size_t)FT_ROWS * RS : sz[i], hipMemcpyHostToDevice));
   if (carry) HIP_TRY(hipMemset(m + off[0] + (size_t)FT_ROWS * RS, 0, 4 * (size_t)carry * RS));
   if (carry) HIP_TRY(hipMemset(m + off[0] + (size_t)ZERO_ROW * RS, 0, RS)); // the zero row
@@ -369,6 +379,7 @@ static int upload_net(Dev &d, int which, const HostNet &h) {
   n.w2 = reinterpret_cast<const int8_t *>(m + off[6]);
   n.b2 = reinterpret_cast<const int32_t *>(m + off[7]);
   n.psqt = reinterpret_cast<const int32_t *>(m + off[8]);
+  n.w0f = reinterpret_cast<const int8_t *>(m + off[9]);
   d.has[which] = true;
   return GN_OK;
 }

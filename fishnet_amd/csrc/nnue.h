@@ -14,6 +14,8 @@
 //   w1      [8][32][32] int8             b1 [8][32] int32    (fc_1, cols 30,31 pad)
 //   w2      [8][32] int8                 b2 [8] int32        (fc_2)
 //   psqt    [8 buckets][22528 + 1] int32: the PSQT weights again, bucket-major (L2-sized)
+//   w0f     [8][L1 / 64][64][16] int8: w0 again, one 1 KiB block per 64-wide k-step in the
+//           operand order of v_mfma_i32_16x16x64_i8 (lane l: output l & 15, inputs 16 (l >> 4) ..)
 #pragma once
 #include <stdint.h>
 
@@ -70,6 +72,7 @@ struct NetDevice {
   const int8_t *w2;
   const int32_t *b2;
   const int32_t *psqt; // [PSQT_BUCKETS][FT_ROWS]: the rows' PSQT weights by bucket (a copy)
+  const int8_t *w0f;   // [8][L1 / 64][64 lanes][16]: w0 in the int8 MFMA's operand order (a copy)
 };
 
 // HalfKAv2_hm feature index:

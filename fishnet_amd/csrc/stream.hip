@@ -772,7 +772,8 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
       const int ln = tl & 63, row = ln & 15, kg = ln >> 4;
       {
         const uint8_t *xa = xt + row * XS + kg * 16 + 64 * KPW * wave;
-        const int8_t *wb = net.w0 + ((size_t)b * 16 + row) * L1 + kg * 16 + 64 * KPW * wave;
+        // (w0f: the k-step's 64 lanes x 16 B are one contiguous 1 KiB)
+        const int8_t *wb = net.w0f + (((size_t)b * KS + KPW * wave) * 64 + ln) * 16;
         int4v acc = {0, 0, 0, 0};
         // (batches of FB k-steps: the next tile's rows stay in flight in registers meanwhile)
         constexpr int FB = 2;
@@ -780,7 +781,7 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
         for (int k0 = 0; k0 < KPW && !(ablate & 16); k0 += FB) { // (16: timing diagnostics, no fc_0)
           int4v wv[FB], av[FB];
 #pragma unroll
-          for (int j = 0; j < FB; ++j) wv[j] = *reinterpret_cast<const int4v *>(wb + 64 * (k0 + j));
+          for (int j = 0; j < FB; ++j) wv[j] = *reinterpret_cast<const int4v *>(wb + 1024 * (k0 + j));
 #pragma unroll
           for (int j = 0; j < FB; ++j) av[j] = *reinterpret_cast<const int4v *>(xa + 64 * (k0 + j));
 #pragma unroll
