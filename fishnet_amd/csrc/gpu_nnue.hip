@@ -751,8 +751,8 @@ static int expand_evaluate(gn_ctx *ctx, Dev &d, const gn_board *parents, size_t 
       HIP_TRY(d.ent.ensure(d.etot + 16 * (nblk + 1)));
       HIP_TRY(d.tiles.ensure((n + total) / 16 + (K + 2) * nblk + 2));
       HIP_TRY(d.btiles.ensure(nblk + 1));
-      HIP_TRY(d.pool.ensure(64));
-      HIP_TRY(hipMemsetAsync(d.pool.p, 0, 64 * sizeof(uint32_t), s));
+      HIP_TRY(d.pool.ensure(65)); // 8 XCDs x 8 words of scratch-slot bits, then the block claim counter
+      HIP_TRY(hipMemsetAsync(d.pool.p, 0, 65 * sizeof(uint32_t), s));
       // XCD-local block order
       static const bool bsort = !getenv("GN_BLOCK_SORT") || atoi(getenv("GN_BLOCK_SORT"));
       const uint32_t *order = nullptr;
@@ -766,7 +766,7 @@ static int expand_evaluate(gn_ctx *ctx, Dev &d, const gn_board *parents, size_t 
         order = d.border.p;
       }
       HIP_TRY(launch_plan_stream(d.net[BIG], parents, n, off, dl, f ? d.p_nbg.p : nullptr, f ? d.nbg.p : nullptr,
-                                 d.p_obg.p, d.obg.p, ctx->swizzle & 1, d.chain_k > 1 ? d.nslot.p : nullptr, d.chain_k,
+                                 d.p_obg.p, d.obg.p, (ctx->swizzle >> 2) & 1, d.chain_k > 1 ? d.nslot.p : nullptr, d.chain_k,
                                  ctx->king_cache ? 1 : 0, d.eoff.p, d.ent.p, d.tiles.p, d.btiles.p, d.pool.p, d.perr.p,
                                  rows_out, d.pstat.p, 0, nblk, order, ev ? ev[4] : nullptr, s));
     } else {
@@ -2111,7 +2111,7 @@ int gn_set_option(gn_ctx *ctx, int option, int64_t value) {
     ctx->incremental = value != 0;
     return GN_OK;
   case GN_OPT_XCD_SWIZZLE:
-    ctx->swizzle = (int)(value & 3);
+    ctx->swizzle = (int)(value & 7);
     return GN_OK;
   case GN_OPT_KING_SORT:
     ctx->king_sort = value != 0;

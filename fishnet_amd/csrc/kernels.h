@@ -85,8 +85,8 @@ static_assert(sizeof(TileDesc) == 192, "TileDesc is 192 bytes");
 // of them), entries at ent + eoff[pbeg] + 16 * block (list 0 upward, list 1 downward from
 // the region's end, eoff = exclusive scan of write_children's per-parent entry bounds).
 // One call plans and evaluates blocks [b0, b1) of the n parents (every index absolute, so
-// block ranges can run as a pipeline on different streams).  pool: 64 words, zeroed by the
-// caller before the first range; err: bit 0 entry overflow, bit 1 no scratch slot, bit 2 a
+// block ranges can run as a pipeline on different streams).  pool: 65 words (scratch-slot
+// bits, then the stream's block claim counter), zeroed by the caller before each call; err: bit 0 entry overflow, bit 1 no scratch slot, bit 2 a
 // king-cache load closer than GN_SCR_GAP entries to its list's last store to scratch.
 // rows_out: += FT rows the stream gathers (bias, carry and king-cache rows included);
 // pads_out (optional): += no-op entries the plan inserted to keep GN_SCR_GAP.

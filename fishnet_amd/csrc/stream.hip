@@ -76,6 +76,22 @@ __device__ unsigned long long gn_sp[8]; // [0] stream [1] barrier wait [2] layer
 #define SP_T() 0ull
 #define SP_ADD(k, v) (void)0
 #endif
+#ifdef GN_PLAN_PROF
+// diagnostics build only: plan_kernel cycles (s_memtime) per section, summed over waves:
+// [0] parent setup [1] slot descriptors, lists and PSQT of segments [2] a refreshed parent's
+// rows [3] king-move jobs
+__device__ unsigned long long gn_pp[4];
+#define PP_T() __builtin_amdgcn_s_memtime()
+#define PP_ADD(k, v) atomicAdd(&gn_pp[k], (unsigned long long)(v))
+#else
+#define PP_T() 0ull
+#define PP_ADD(k, v) (void)0
+#endif
+#ifdef GN_XCD_PROF
+// diagnostics build only: per XCD, [x] the last workgroup end and [8 + x] the first start
+// (s_memrealtime, 100 MHz, chip-wide), [16 + x] entries streamed, [24 + x] workgroups
+__device__ unsigned long long gn_xp[32] = {0, 0, 0, 0, 0, 0, 0, 0, ~0ull, ~0ull, ~0ull, ~0ull, ~0ull, ~0ull, ~0ull, ~0ull};
+#endif
 
 namespace gn {
 namespace ps {
@@ -133,6 +149,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
   const __amdgpu_buffer_rsrc_t pst = __builtin_amdgcn_make_buffer_rsrc(
       (void *)net.psqt, 0, (int)((size_t)PSQT_BUCKETS * FT_ROWS * 4), 0x00020000);
   auto psqt = [&](uint32_t row, int bucket) -> int32_t { // bucket-major copy (L2-resident)
+#ifdef GN_AB_PLAN_NOPSQT // timing diagnostics only (wrong PSQT): the plan without its PSQT loads
+    return (int32_t)(row + bucket);
+#endif
     return (int32_t)__builtin_amdgcn_raw_buffer_load_b32(pst, (bucket * (uint32_t)FT_ROWS + row) * 4, 0, 0);
   };
   const uint32_t pbeg = blk * K, pend = pbeg + K < np ? pbeg + K : np;
@@ -163,6 +182,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
   for (int i = lane; i < 128; i += 64) kstate[w][i] = 0;
   uint16_t(*prow)[32] = prow_s[w];
   uint32_t len0 = 0, len1 = 0, tile_k = 0, p_first = pbeg, u_fill = 0, t_first = 0, tile_bm = 0;
+  unsigned long long pp_a = 0, pp_b = 0, pp_c = 0, pp_d = 0; // GN_PLAN_PROF: section cycles
   int t_fill = 0, carried = 0;
   unsigned long long rows = 0, pads = 0, fpads = 0;
   auto pad_to = [&](int g, uint32_t target) { // no-op entries up to target (lane-parallel, < 64)
@@ -184,6 +204,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
   };
 
   for (uint32_t p = pbeg; p < pend; ++p) {
+    unsigned long long pp_t = PP_T();
     const uint64_t off = offsets[p];
     const int nch = (int)(offsets[p + 1] - off), total = 1 + nch;
     const gn_board pb = parents[p];
@@ -257,7 +278,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
       }
     }
 
+    pp_a += PP_T() - pp_t;
     for (int q0 = 0; q0 < total;) {
+      pp_t = PP_T();
       if (t_fill == 0) p_first = p, t_first = u_fill;
       const int cand = 16 - t_fill < total - q0 ? 16 - t_fill : total - q0;
       const int q = q0 + lane, t = t_fill + lane;
@@ -389,6 +412,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
       }
       if (in) T[tile_k].meta[t] = (uint8_t)((live && vld ? 1 : 0) | bk << 1 | (q == 0 ? 16 : 0) | cst << 5);
       if (in) T[tile_k].adj[t] = (int16_t)(q == 0 ? 0 : child_of(q) - (q - 1));
+      pp_b += PP_T() - pp_t, pp_t = PP_T();
       // the parent's rows (lane = row) after its bias entry (the parent is lane 0 of its segment)
       if (live && q0 == 0 && !have) {
         const uint64_t lt2 = (1ull << lane) - 1;
@@ -428,6 +452,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
       len0 += tot & 0xFFFF, len1 += tot >> 16;
       rows += (tot & 0xFFFF) + (tot >> 16);
       // ---- king-move refreshes, one job per slot in slot order, lane = square
+      pp_c += PP_T() - pp_t, pp_t = PP_T();
       uint64_t jm = __ballot(in && live && vld && (ref0 || ref1));
       while (jm) {
         const int l = __builtin_ctzll(jm);
@@ -501,6 +526,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
         if (g) len1 += (uint32_t)ne;
         else len0 += (uint32_t)ne;
       }
+      pp_d += PP_T() - pp_t;
       t_fill += seg, q0 += seg, u_fill += (uint32_t)seg;
       if (t_fill == 16) flush();
     }
@@ -515,6 +541,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
     if (werr4) atomicOr(err, 4u);
     if (rows_out) atomicAdd(rows_out, rows);
     if (pads_out && pads) atomicAdd(pads_out, pads);
+    PP_ADD(0, pp_a), PP_ADD(1, pp_b), PP_ADD(2, pp_c), PP_ADD(3, pp_d);
     SP_ADD(6, pads), SP_ADD(7, fpads);
   }
   (void)pads, (void)fpads;
@@ -528,7 +555,8 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
                        const uint64_t *__restrict__ eoff, const uint64_t *__restrict__ ent,
                        const TileDesc *__restrict__ tiles, const uint32_t *__restrict__ btiles,
                        const uint32_t *__restrict__ order, int2 *__restrict__ out_parent, int2 *__restrict__ out_child,
-                       uint32_t *__restrict__ pool, int use_scr, uint32_t *__restrict__ err, int ablate) {
+                       uint32_t *__restrict__ pool, int use_scr, uint32_t *__restrict__ err, int ablate,
+                       uint32_t *__restrict__ claim) {
   using namespace ps;
   constexpr int G = L1 / 16; // threads per perspective group (whole waves)
   constexpr int NT = 2 * G, NW = NT / 64, TILE = 16, XS = L1 + 16, KS = L1 / 64, KPW = KS / NW;
@@ -541,18 +569,30 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
   __shared__ int32_t acc0[2][16 * AS];
   __shared__ __attribute__((aligned(16))) uint8_t in1[2][TILE][32];
   __shared__ int32_t fwd[2][TILE];
-  __shared__ uint32_t sslot;
+  __shared__ uint32_t sslot, sblk;
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int hu = __builtin_amdgcn_readfirstlane((tid / G) & 1);
   const __amdgpu_buffer_rsrc_t ftr = __builtin_amdgcn_make_buffer_rsrc(
       (void *)net.ft, 0, (int)(((size_t)ZERO_ROW + 1) * RS), 0x00020000);
   for (int i = tid; i < 2 * 16 * AS; i += NT) (&acc0[0][0])[i] = 0;
-  // this launch evaluates blocks [b0, b1); with swz, XCD x (= dispatch index mod 8) takes
-  // the x-th contiguous eighth of them (a block's king-sorted neighbours share its L2)
+  // this launch evaluates blocks [b0, b1).  swz: XCD x (= dispatch index mod 8) takes the x-th
+  // contiguous eighth of them; otherwise (default) every workgroup claims the next block of the
+  // order with one atomic (claim[0], zeroed per launch), so blocks are taken in order wherever
+  // a workgroup slot frees up: XCDs that run faster take more blocks (measured: the even XCDs
+  // of an MI355X finish the static split 2-3 % after the odd ones), and the resident blocks of
+  // every XCD stay neighbours in the king order
+  // The grid has nblk + nblk / 16 + 8 workgroups then: the hardware hands every XCD the same
+  // number of them, so a faster XCD needs spare workgroups to take more blocks, and the ones
+  // left over once every block is claimed end here.
   const uint32_t nblk = b1 - b0;
   const uint32_t vgrid = swz ? 8 * ((nblk + 7) / 8) : nblk;
   uint32_t v = blockIdx.x;
+  if (!swz) {
+    if (tid == 0) sblk = atomicAdd(claim, 1u);
+    __syncthreads();
+    v = sblk;
+  }
   if (v >= vgrid) return;
   uint32_t blk = v;
   if (swz) {
@@ -566,6 +606,9 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
   const uint32_t ntiles = btiles[blk];
   const TileDesc *T = tiles + us_b / 16 + (uint64_t)(K + 2) * blk; // as plan_kernel
   const uint64_t rbeg = eoff[pbeg] + 16ull * blk, rend = eoff[pend] + 16ull * (blk + 1);
+#ifdef GN_XCD_PROF
+  const unsigned long long xp_t0 = __builtin_amdgcn_s_memrealtime();
+#endif
   // ---- scratch slot (carry + king-cache rows) from this XCD's pool: never waits on another
   // workgroup; the pool (POOL_PER_XCD slots) outnumbers the workgroups an XCD holds
   uint32_t scr = 0, my_slot = 0;
@@ -877,6 +920,18 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
       __hip_atomic_fetch_and(pool + 8 * (my_slot / POOL_PER_XCD) + (my_slot % POOL_PER_XCD) / 32,
                              ~(1u << (my_slot % 32)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+#ifdef GN_XCD_PROF
+  if (tid == 0) {
+    uint32_t x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+    x &= 7;
+    const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+    atomicMax(&gn_xp[x], t1);
+    atomicMin(&gn_xp[8 + x], xp_t0);
+    atomicAdd(&gn_xp[16 + x], ntiles ? (unsigned long long)T[ntiles - 1].e_end[0] + T[ntiles - 1].e_end[1] : 0ull);
+    atomicAdd(&gn_xp[24 + x], 1ull);
+  }
+#endif
 }
 
 hipError_t launch_plan_stream(const NetDevice &net, const gn_board *parents, size_t n, const uint64_t *offsets,
@@ -892,7 +947,7 @@ hipError_t launch_plan_stream(const NetDevice &net, const gn_board *parents, siz
   const int scr = K > 1 && kc; // the king cache's rows (the chained walk itself needs no scratch)
   if (b1 > (n + K - 1) / K) return hipErrorInvalidValue;
   const uint32_t nb = (uint32_t)(b1 - b0), B0 = (uint32_t)b0, B1 = (uint32_t)b1;
-  const unsigned pg = (nb + 3) / 4, g = swz ? 8 * ((nb + 7) / 8) : nb;
+  const unsigned pg = (nb + 3) / 4, g = swz ? 8 * ((nb + 7) / 8) : nb + nb / 16 + 8; // (stream_eval_kernel: claims)
   static const int ablate = getenv("GN_ABLATE") ? atoi(getenv("GN_ABLATE")) : 0; // timing diagnostics only
   // timing diagnostics only: extra dynamic LDS per workgroup (fewer workgroups per CU)
   static const size_t lds_pad = getenv("GN_STREAM_LDS_PAD") ? (size_t)atoi(getenv("GN_STREAM_LDS_PAD")) : 0;
@@ -902,17 +957,44 @@ hipError_t launch_plan_stream(const NetDevice &net, const gn_board *parents, siz
                        tiles, btiles, rows_out, pads_out, err);
     if (mid) (void)hipEventRecord(mid, s);
     hipLaunchKernelGGL((stream_eval_kernel<3072>), dim3(g), dim3(384), lds_pad, s, net, offsets, (uint32_t)n, K, B0, B1,
-                       swz, eoff, ent, tiles, btiles, order, out_parent, out_child, pool, scr, err, ablate);
+                       swz, eoff, ent, tiles, btiles, order, out_parent, out_child, pool, scr, err, ablate, pool + 64);
   } else if (net.L1 == 1024) {
     hipLaunchKernelGGL((plan_kernel<1024>), dim3(pg), dim3(256), 0, s, net, parents, offsets, deltas, need_parent,
                        need_child, K > 1 ? next_slot : nullptr, (uint32_t)n, K, B0, B1, K > 1 ? kc : 0, eoff, ent,
                        tiles, btiles, rows_out, pads_out, err);
     if (mid) (void)hipEventRecord(mid, s);
     hipLaunchKernelGGL((stream_eval_kernel<1024>), dim3(g), dim3(128), 0, s, net, offsets, (uint32_t)n, K, B0, B1,
-                       swz, eoff, ent, tiles, btiles, order, out_parent, out_child, pool, scr, err, ablate);
+                       swz, eoff, ent, tiles, btiles, order, out_parent, out_child, pool, scr, err, ablate, pool + 64);
   } else {
     return hipErrorInvalidValue;
   }
+#ifdef GN_PLAN_PROF
+  {
+    unsigned long long c[4];
+    (void)hipStreamSynchronize(s);
+    (void)hipMemcpyFromSymbol(c, HIP_SYMBOL(gn_pp), sizeof(c));
+    fprintf(stderr, "plan prof: wave-cycles setup %llu segments %llu parent rows %llu king jobs %llu\n", c[0], c[1],
+            c[2], c[3]);
+    memset(c, 0, sizeof(c));
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(gn_pp), c, sizeof(c));
+  }
+#endif
+#ifdef GN_XCD_PROF
+  {
+    unsigned long long c[32];
+    (void)hipStreamSynchronize(s);
+    (void)hipMemcpyFromSymbol(c, HIP_SYMBOL(gn_xp), sizeof(c));
+    unsigned long long t0 = ~0ull;
+    for (int x = 0; x < 8; ++x) t0 = c[8 + x] < t0 ? c[8 + x] : t0;
+    fprintf(stderr, "xcd prof:");
+    for (int x = 0; x < 8; ++x)
+      fprintf(stderr, " [%d] end %.2f ms start %.2f ms entries %llu wgs %llu;", x, (c[x] - t0) * 1e-5,
+              (c[8 + x] - t0) * 1e-5, c[16 + x], c[24 + x]);
+    fprintf(stderr, "\n");
+    for (int x = 0; x < 8; ++x) c[x] = 0, c[8 + x] = ~0ull, c[16 + x] = 0, c[24 + x] = 0;
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(gn_xp), c, sizeof(c));
+  }
+#endif
 #ifdef GN_STREAM_PROF
   {
     unsigned long long c[8];

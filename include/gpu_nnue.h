@@ -64,8 +64,11 @@ extern "C" {
 #define GN_OPT_INCREMENTAL_CHILDREN 1 /* 1 (default): children from the parent accumulators
                                          by add/sub deltas; 0: full refresh per child    */
 #define GN_OPT_XCD_SWIZZLE 2          /* bit mask, default 1: each XCD takes a contiguous
-                                         range of parents (bit 0, expansion) / of 16-position
-                                         tiles (bit 1, batch evaluation); 0: dispatch order */
+                                         range of parents (bit 0, small-net expansion) / of
+                                         16-position tiles (bit 1, batch evaluation) / of
+                                         blocks (bit 2, big-net expansion); 0: dispatch order
+                                         (big-net expansion: blocks claimed in order by an
+                                         atomic counter) */
 #define GN_OPT_KING_SORT 3            /* 1 (default): evaluate a batch in (white king, black
                                          king) square order for L2 / Infinity-Cache
                                          locality, then (big net) by 30 home-square bits
@@ -97,9 +100,9 @@ extern "C" {
                                          stack), the expansion's dominant kernel         */
 #define GN_STAT_SCRATCH_PADS 103      /* no-op entries the last planned expansion inserted
                                          (per device, summed) so that every king-cache load
-                                         sits >= 2 * ring depth - 1 list entries after the
-                                         list's last king-cache store (the store has then
-                                         completed when the load issues)                 */
+                                         sits >= ring depth (4) list entries after the
+                                         list's last king-cache store (the load then issues
+                                         after the store, from the same lanes)            */
 /* stage times of the last gn_evaluate_games / gn_expand_and_evaluate (nanoseconds; per-device
  * stages: the slowest device).  The expansion runs in chunks of whole games; a drain thread
  * downloads chunk c's records on a copy stream while chunk c + 1 computes.               */

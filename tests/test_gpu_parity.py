@@ -283,7 +283,7 @@ def test_device_playouts_equal_host_playouts(gpu_ctx):
     assert d.download(G.BOARD_DTYPE, 500).tobytes() == host.tobytes()
 
 
-@pytest.mark.parametrize("swz,ksort", [(0, 0), (3, 0), (0, 1), (3, 1)])
+@pytest.mark.parametrize("swz,ksort", [(0, 0), (7, 0), (0, 1), (7, 1)])
 def test_locality_options_do_not_change_results(gpu_ctx, swz, ksort):
     from fishnet_amd import gpu_nnue as G
     boards = G.random_positions(3, 0, 5003, 160)
@@ -305,7 +305,7 @@ def test_locality_options_do_not_change_results(gpu_ctx, swz, ksort):
         assert ref[0][17]["flags"] & G.FLAG_BAD_FEN
         fens = [G.board_to_fen(b) for b in boards[:200] if b["occ"]]
         _, offs, moves, kids = gpu_ctx.expand_and_evaluate(fens, 1)
-        gpu_ctx.set_option(G.OPT_XCD_SWIZZLE, 3 - swz)
+        gpu_ctx.set_option(G.OPT_XCD_SWIZZLE, 7 - swz)
         _, offs2, moves2, kids2 = gpu_ctx.expand_and_evaluate(fens, 1)
         assert np.array_equal(kids, kids2) and np.array_equal(moves, moves2)
     finally:
