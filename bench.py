@@ -677,9 +677,16 @@ def main():
 
     if c.rank == 0 and not args.no_cpu_baseline:
         if args.workload == "expand":
-            line["cpu_baseline"] = cpu_baseline_expand(c, r["parents"][:1_000_000], mode, args.cpu_seconds)
+            cb = cpu_baseline_expand(c, r["parents"][:1_000_000], mode, args.cpu_seconds)
         else:
-            line["cpu_baseline"] = cpu_baseline_eval(c, r["boards"][:200_000], mode, args.cpu_seconds)
+            cb = cpu_baseline_eval(c, r["boards"][:200_000], mode, args.cpu_seconds)
+        # the whole host beside this GPU's share: not measured (the pool gives one GPU 16 of the
+        # host's CPUs), a linear extrapolation to every logical CPU, an upper bound with SMT
+        ncpu = os.cpu_count() or cb["cores"]
+        cb["whole_host"] = {"value": round(cb["value"] * ncpu / cb["cores"], 1), "unit": cb["unit"], "cores": ncpu,
+                            "how": f"linear extrapolation of the {cb['cores']}-thread measurement to all {ncpu} "
+                                   f"logical CPUs (not measured; an upper bound with SMT)"}
+        line["cpu_baseline"] = cb
 
     if not args.no_secondary and args.workload == "expand":
         sec = {}

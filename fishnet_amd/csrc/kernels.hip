@@ -2044,7 +2044,22 @@ __global__ void block_keys_kernel(const gn_board *__restrict__ parents, size_t n
     if (pc == make_piece(WHITE, KING)) wk = sq;
     if (pc == make_piece(BLACK, KING)) bk = sq;
   }
-  keys[b] = (uint16_t)(mode == 4 ? bk << 6 | wk : wk << 6 | bk);
+  // diagnostics: 4 black-king-major; 5 Morton order of the two king squares; 6 Morton order of
+  // the two perspectives' king buckets (HalfKAv2_hm, nnue.h feature_index)
+  auto morton6 = [](uint32_t a, uint32_t c) {
+    uint32_t r = 0;
+    for (int i = 0; i < 6; ++i) r |= ((a >> i) & 1u) << (2 * i + 1) | ((c >> i) & 1u) << (2 * i);
+    return r;
+  };
+  auto kbucket = [](int ksq, int persp) {
+    const int kf = ksq & 7, rr = (ksq >> 3) ^ (persp ? 7 : 0);
+    return 4 * (7 - rr) + (kf < 4 ? kf : 7 - kf);
+  };
+  uint32_t key = (uint32_t)(wk << 6 | bk);
+  if (mode == 4) key = (uint32_t)(bk << 6 | wk);
+  if (mode == 5) key = morton6((uint32_t)wk, (uint32_t)bk);
+  if (mode == 6) key = morton6((uint32_t)kbucket(wk, 0), (uint32_t)kbucket(bk, 1));
+  keys[b] = (uint16_t)key;
   idx[b] = b;
 }
 

@@ -78,8 +78,8 @@ __device__ unsigned long long gn_sp[8]; // [0] stream [1] barrier wait [2] layer
 #endif
 #ifdef GN_PLAN_PROF
 // diagnostics build only: plan_kernel cycles (s_memtime) per section, summed over waves:
-// [0] parent setup [1] slot descriptors, lists and PSQT of segments [2] a refreshed parent's
-// rows [3] king-move jobs
+// [0] parent setup [1] slot descriptors, prefix sums, PSQT, the parent rows [2] delta puts, tile ends
+// [3] king-move jobs
 __device__ unsigned long long gn_pp[4];
 #define PP_T() __builtin_amdgcn_s_memtime()
 #define PP_ADD(k, v) atomicAdd(&gn_pp[k], (unsigned long long)(v))
@@ -279,15 +279,21 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
     }
 
     pp_a += PP_T() - pp_t;
-    for (int q0 = 0; q0 < total;) {
+    // ---- the parent's slots (lane = slot) in passes of up to 64 (one pass unless the parent has
+    // more than 63 children).  A pass fills the open tile (cut early where a third layer-stack
+    // bucket would enter it) and as many new 16-slot tiles as its slots need.  A tile's region
+    // of each list is [its delta entries: the parent's and the delta perspectives', slot order]
+    // then [its king-move refresh entries, slot order]: the king-move jobs run first, tile by
+    // tile (each tile's delta region is reserved when the cursor reaches it), then every lane
+    // puts its delta entries at once.
+    for (int q0 = 0; q0 < total; q0 += 64) {
       pp_t = PP_T();
-      if (t_fill == 0) p_first = p, t_first = u_fill;
-      const int cand = 16 - t_fill < total - q0 ? 16 - t_fill : total - q0;
-      const int q = q0 + lane, t = t_fill + lane;
+      const int n_in = total - q0 < 64 ? total - q0 : 64;
+      const int q = q0 + lane;
       // ---- descriptor of this lane's slot
       int vld = 0, cst = 0, cnt = 1, kinds = 0, n0 = 0, n1 = 0, s0 = 0, s1 = 0;
       uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
-      if (lane < cand && live) {
+      if (lane < n_in && live) {
         if (q == 0) {
           vld = need_parent ? need_parent[p] : 1;
           cst = stm, cnt = P, kinds = 3 | 3 << 2;
@@ -303,27 +309,30 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
           else kinds |= 1 << 2, s1 = (meta >> 4) & 3, n1 = s1 + ((meta >> 6) & 3);
         }
       }
+      const bool in = lane < n_in;
       const int bk = (cnt - 1) / 4;
-      // ---- the segment: the slots that keep the tile at <= 2 buckets among evaluated slots
-      int seg = cand;
-      {
-        uint32_t bits = lane < cand && live && vld ? 1u << bk : 0u;
+      // ---- tiles of the pass: the open tile takes c1 slots, then tiles of 16
+      const uint32_t mybit = in && live && vld ? 1u << bk : 0u;
+      uint32_t bits = mybit;
 #pragma unroll
-        for (int dd = 1; dd < 64; dd <<= 1) {
-          const uint32_t o = __shfl_up(bits, dd);
-          if (lane >= dd) bits |= o;
-        }
-        const uint64_t ok = __ballot(lane >= cand || __builtin_popcount(tile_bm | bits) <= 2);
-        const int lead = ok == ~0ull ? 64 : __builtin_ctzll(~ok);
-        if (lead < cand) seg = lead; // tiles cut early keep <= 2 buckets (the stream's fc_0 buffers)
-        if (seg == 0) { // the tile is full of other buckets: close it and take the slots again
-          flush();
-          continue;
-        }
-        const uint32_t segbits = (uint32_t)__builtin_amdgcn_readlane((int)bits, seg - 1);
-        tile_bm |= segbits;
+      for (int dd = 1; dd < 64; dd <<= 1) {
+        const uint32_t o = __shfl_up(bits, dd);
+        if (lane >= dd) bits |= o;
       }
-      const bool in = lane < seg;
+      const uint64_t ok = __ballot(!in || __builtin_popcount(tile_bm | bits) <= 2);
+      int lead = ok == ~0ull ? 64 : __builtin_ctzll(~ok);
+      if (lead == 0) { // the open tile holds two other buckets: close it; a fresh tile takes every
+        flush();       // slot of a parent (its slots hold <= 2 buckets: P and P - 1 pieces)
+        if (__ballot(in && __builtin_popcount(bits) > 2)) bad |= 1u; // cannot happen; reported
+        lead = 64;
+      }
+      if (t_fill == 0) p_first = p, t_first = u_fill;
+      const int tf0 = t_fill, room = 16 - tf0;
+      const int c1 = room < lead ? (room < n_in ? room : n_in) : (lead < n_in ? lead : n_in);
+      const int tix = lane < c1 ? 0 : 1 + (lane - c1) / 16;        // this slot's tile, from tk0
+      const int t = lane < c1 ? tf0 + lane : (lane - c1) % 16;     // its slot in that tile
+      const int ntp = n_in <= c1 ? 1 : 1 + (n_in - c1 + 15) / 16; // tiles the pass touches
+      const uint32_t tk0 = tile_k;
       if (!in) vld = 0, kinds = 0, n0 = n1 = s0 = s1 = 0, w0 = w1 = w2 = w3 = 0;
       // ---- sibling cache: a delta child whose from-row equals the previous delta child's (in
       // the same list) starts from the cached (parent - from-row) and drops that entry
@@ -336,7 +345,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
       const bool hit1 = key1 >= 0 && key1 == ((km1 & lt) ? pk1 : ckey1);
       if (km0) ckey0 = __builtin_amdgcn_readlane(key0, 63 - __builtin_clzll(km0));
       if (km1) ckey1 = __builtin_amdgcn_readlane(key1, 63 - __builtin_clzll(km1));
-      // ---- entries of the parent and of delta perspectives (prefix sums over the lanes)
+      // ---- delta entries per lane (the parent's and the delta perspectives'), prefix sums
       if (live && q0 == 0) { // the parent loads the carry / cache rows: after their stores
         if (pnd[0] >= 0) pad_to(0, safe0);
         if (pnd[1] >= 0) pad_to(1, safe1);
@@ -359,45 +368,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
         if (lane >= dd) inc += o;
       }
       const uint32_t exc = inc - c, tot = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
-      const uint32_t t0w = tmpl(t, cst != 0), t1w = tmpl(t, cst != 1);
       const bool nx = q == nxpos;
+      // ---- PSQT of the slot by side (a king-move perspective is written by its job below),
+      // slot metadata
       if (in && live) {
-        auto delta = [&](int g, uint32_t at, uint32_t lo2, uint32_t hi2, int s, int n, bool hit, uint32_t tw,
-                         uint32_t L) {
-          const uint32_t i0 = lo2 & 0xFFFF, i1 = lo2 >> 16, i2 = hi2 & 0xFFFF, i3 = hi2 >> 16;
-          auto cl = [](uint32_t r) { return r < (uint32_t)FT_INPUTS ? r : (uint32_t)FT_BIAS_ROW; };
-          const uint32_t r1 = cl(s >= 2 ? i1 : i2), r2 = cl(s >= 2 ? i2 : i3), r3 = cl(i3);
-          const uint32_t f1 = s >= 2 ? SUB : 0u;
-          if (!hit) {
-            put(g, at, cl(i0) | tw | SUB | I_PACC | (n == 1 ? L : 0u));
-            if (n > 1) put(g, at + 1, r1 | tw | f1 | (n == 2 ? L : 0u));
-            if (n > 2) put(g, at + 2, r2 | tw | (n == 3 ? L : 0u));
-            if (n > 3) put(g, at + 3, r3 | tw | L);
-          } else { // the from-row is in the cached base
-            put(g, at, r1 | tw | f1 | I_BASE | (n == 2 ? L : 0u));
-            if (n > 2) put(g, at + 1, r2 | tw | (n == 3 ? L : 0u));
-            if (n > 3) put(g, at + 2, r3 | tw | L);
-          }
-        };
-        if ((kinds & 3) == 1) delta(0, len0 + (exc & 0xFFFF), w0, w1, s0, n0, hit0, t0w, LAST | (nx ? PAR_E : 0u));
-        if ((kinds >> 2) == 1) delta(1, len1 + (exc >> 16), w2, w3, s1, n1, hit1, t1w, LAST | (nx ? PAR_E : 0u));
-        if (kinds == 15) {
-          if (have) { // the parent is its predecessor's last child: pacc, one entry per list
-            put(0, len0 + (exc & 0xFFFF), (uint32_t)ZERO_ROW | t0w | I_PACC | SUB | PAR_E | LAST);
-            put(1, len1 + (exc >> 16), (uint32_t)ZERO_ROW | t1w | I_PACC | SUB | PAR_E | LAST);
-          } else { // bias entry or the cache row; the rest follows (below, lane = square / row)
-            put(0, len0 + (exc & 0xFFFF),
-                (pnd[0] >= 0 ? SCR | (uint32_t)(2 + pkq[0]) : (uint32_t)FT_BIAS_ROW) | t0w | I_ZERO | PAR_E);
-            put(1, len1 + (exc >> 16),
-                (pnd[1] >= 0 ? SCR | (uint32_t)(2 + 64 + pkq[1]) : (uint32_t)FT_BIAS_ROW) | t1w | I_ZERO | PAR_E);
-          }
-        }
-        // PSQT of the slot by side (a king-move perspective is written by its job below)
-        int32_t v[2] = {0, 0};
 #pragma unroll
         for (int hh = 0; hh < 2; ++hh) {
           const int kd = hh ? kinds >> 2 : kinds & 3;
-          if (kd == 3) v[hh] = pp[hh][0];
+          int32_t v = 0;
+          if (kd == 3) v = pp[hh][0];
           if (kd == 1) {
             const uint32_t lo2 = hh ? w2 : w0, hi2 = hh ? w3 : w1;
             const int s = hh ? s1 : s0, n = hh ? n1 : n0;
@@ -405,21 +384,32 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
             const uint32_t r1 = s >= 2 ? i1 : i2, r2 = s >= 2 ? i2 : i3;
             const int32_t a0 = psqt(ft_row(i0), bk), a1 = psqt(ft_row(r1), bk);
             const int32_t a2 = n > 2 ? psqt(ft_row(r2), bk) : 0, a3 = n > 3 ? psqt(ft_row(i3), bk) : 0;
-            v[hh] = wadd(pp[hh][bk == bp ? 0 : 1], wadd(wadd(-a0, s >= 2 ? -a1 : a1), wadd(a2, a3)));
+            v = wadd(pp[hh][bk == bp ? 0 : 1], wadd(wadd(-a0, s >= 2 ? -a1 : a1), wadd(a2, a3)));
           }
-          if (kd != 2) T[tile_k].psq[t][hh != cst] = v[hh];
+          if (kd != 2) T[tk0 + tix].psq[t][hh != cst] = v;
         }
       }
-      if (in) T[tile_k].meta[t] = (uint8_t)((live && vld ? 1 : 0) | bk << 1 | (q == 0 ? 16 : 0) | cst << 5);
-      if (in) T[tile_k].adj[t] = (int16_t)(q == 0 ? 0 : child_of(q) - (q - 1));
-      pp_b += PP_T() - pp_t, pp_t = PP_T();
-      // the parent's rows (lane = row) after its bias entry (the parent is lane 0 of its segment)
+      if (in) T[tk0 + tix].meta[t] = (uint8_t)((live && vld ? 1 : 0) | bk << 1 | (q == 0 ? 16 : 0) | cst << 5);
+      if (in) T[tk0 + tix].adj[t] = (int16_t)(q == 0 ? 0 : child_of(q) - (q - 1));
+      // the parent's entries (the parent is lane 0: tile 0 of the pass, its delta region starts
+      // at the cursor), before the jobs: a cache-row load is put while the lists' last scratch
+      // stores are still the ones before it (put() checks the distance)
+      if (live && q0 == 0 && lane == 0) {
+        const uint32_t t0w = tmpl(tf0, stm != 0), t1w = tmpl(tf0, stm != 1);
+        if (have) { // the parent is its predecessor's last child: pacc, one entry per list
+          put(0, len0, (uint32_t)ZERO_ROW | t0w | I_PACC | SUB | PAR_E | LAST);
+          put(1, len1, (uint32_t)ZERO_ROW | t1w | I_PACC | SUB | PAR_E | LAST);
+        } else { // bias entry or the cache row; the rest follows (lane = square / row)
+          put(0, len0, (pnd[0] >= 0 ? SCR | (uint32_t)(2 + pkq[0]) : (uint32_t)FT_BIAS_ROW) | t0w | I_ZERO | PAR_E);
+          put(1, len1, (pnd[1] >= 0 ? SCR | (uint32_t)(2 + 64 + pkq[1]) : (uint32_t)FT_BIAS_ROW) | t1w | I_ZERO | PAR_E);
+        }
+      }
       if (live && q0 == 0 && !have) {
         const uint64_t lt2 = (1ull << lane) - 1;
         const int ppc = kc ? lane_piece(pb, lane) : 0;
 #pragma unroll 1
         for (int hh = 0; hh < 2; ++hh) {
-          const uint32_t tp = tmpl(t_fill, stm != hh), b0 = (hh ? len1 : len0) + 1;
+          const uint32_t tp = tmpl(tf0, stm != hh), b0 = (hh ? len1 : len0) + 1;
           const uint32_t krow = SCR | (uint32_t)(2 + 64 * hh + pkq[hh]);
           if (pnd[hh] >= 0) { // the cache row's differences: removed pieces, then added ones
             int spc;
@@ -449,16 +439,39 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
         }
         ps::wave_sync();
       }
-      len0 += tot & 0xFFFF, len1 += tot >> 16;
       rows += (tot & 0xFFFF) + (tot >> 16);
-      // ---- king-move refreshes, one job per slot in slot order, lane = square
-      pp_c += PP_T() - pp_t, pp_t = PP_T();
+      pp_b += PP_T() - pp_t, pp_t = PP_T();
+      // ---- tile by tile: reserve the tile's delta region, append its king-move jobs, close it
+      // (the last tile of the pass stays open unless full).  ts0 / ts1: lane j = where tile j's
+      // delta region starts in list 0 / 1.
+      uint32_t ts0 = 0, ts1 = 0;
+      auto excat = [&](int ln) -> uint32_t { // exclusive delta prefix at lane ln (n_in: the total)
+        return ln >= n_in ? tot : (uint32_t)__builtin_amdgcn_readlane((int)exc, ln);
+      };
+      auto tile_lane0 = [&](int j) { return j == 0 ? 0 : c1 + 16 * (j - 1); };
+      auto open_tile = [&](int j) {
+        ts0 = lane == j ? len0 : ts0, ts1 = lane == j ? len1 : ts1;
+        const uint32_t d = excat(j + 1 < ntp ? tile_lane0(j + 1) : n_in) - excat(tile_lane0(j));
+        len0 += d & 0xFFFF, len1 += d >> 16;
+      };
+      auto close_tile = [&](int j) { // a tile the pass filled (or cut), not the pass's last
+        TileDesc *dt = T + tk0 + j;
+        const int fill = j == 0 ? tf0 + c1 : 16;
+        if (lane >= fill && lane < 16) dt->meta[lane] = 0;
+        const uint32_t pf = j == 0 ? p_first : p, tf = j == 0 ? t_first : u_fill + (uint32_t)tile_lane0(j);
+        if (lane == 0) dt->e_end[0] = len0, dt->e_end[1] = len1, dt->p_first = pf, dt->first = tf;
+      };
+      int jc = 0;
+      open_tile(0);
       uint64_t jm = __ballot(in && live && vld && (ref0 || ref1));
       while (jm) {
         const int l = __builtin_ctzll(jm);
         jm &= jm - 1;
+        const int jt = __builtin_amdgcn_readlane(tix, l);
+        while (jc < jt) close_tile(jc), ++jc, open_tile(jc);
         const int hh = __builtin_amdgcn_readlane((int)ref1, l), st = __builtin_amdgcn_readlane(cst, l);
-        const int cn = __builtin_amdgcn_readlane(cnt, l), tl = t_fill + l;
+        const int cn = __builtin_amdgcn_readlane(cnt, l), tl = __builtin_amdgcn_readlane(t, l);
+        TileDesc *TD = T + tk0 + jt;
         const bool nxl = q0 + l == nxpos;
         const uint32_t sq01 = (uint32_t)__builtin_amdgcn_readlane((int)(hh ? w2 : w0), l),
                        sq23 = (uint32_t)__builtin_amdgcn_readlane((int)(hh ? w3 : w1), l);
@@ -467,7 +480,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
         const int row = king_move_row(pb, hh, sq01 & 0xFFFF, kt, sq23 & 0xFFFF, sq23 >> 16, lane, pos, &cpc);
         const int cb = (cn - 1) / 4;
         const int32_t ps_sum = wave_sum(row >= 0 ? psqt((uint32_t)row, cb) : 0);
-        if (lane == 0) T[tile_k].psq[tl][hh != st] = ps_sum;
+        if (lane == 0) TD->psq[tl][hh != st] = ps_sum;
         const uint32_t tw = tmpl(tl, hh != st);
         bool kuse = kc && (sq23 & 0xFFFF) == 64; // not castling
         const int kci = 64 * hh + kt;
@@ -526,8 +539,47 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
         if (g) len1 += (uint32_t)ne;
         else len0 += (uint32_t)ne;
       }
-      pp_d += PP_T() - pp_t;
-      t_fill += seg, q0 += seg, u_fill += (uint32_t)seg;
+      while (jc < ntp - 1) close_tile(jc), ++jc, open_tile(jc);
+      pp_d += PP_T() - pp_t, pp_t = PP_T();
+      // ---- the delta entries of every lane, in its tile's reserved region
+      {
+        const uint32_t rel = exc - (uint32_t)__shfl((int)exc, tile_lane0(tix)); // (no borrow: prefix sums)
+        const uint32_t at0 = (uint32_t)__shfl((int)ts0, tix) + (rel & 0xFFFF);
+        const uint32_t at1 = (uint32_t)__shfl((int)ts1, tix) + (rel >> 16);
+        const uint32_t t0w = tmpl(t, cst != 0), t1w = tmpl(t, cst != 1);
+        if (in && live) {
+          auto delta = [&](int g, uint32_t at, uint32_t lo2, uint32_t hi2, int s, int n, bool hit, uint32_t tw,
+                           uint32_t L) {
+            const uint32_t i0 = lo2 & 0xFFFF, i1 = lo2 >> 16, i2 = hi2 & 0xFFFF, i3 = hi2 >> 16;
+            auto cl = [](uint32_t r) { return r < (uint32_t)FT_INPUTS ? r : (uint32_t)FT_BIAS_ROW; };
+            const uint32_t r1 = cl(s >= 2 ? i1 : i2), r2 = cl(s >= 2 ? i2 : i3), r3 = cl(i3);
+            const uint32_t f1 = s >= 2 ? SUB : 0u;
+            if (!hit) {
+              put(g, at, cl(i0) | tw | SUB | I_PACC | (n == 1 ? L : 0u));
+              if (n > 1) put(g, at + 1, r1 | tw | f1 | (n == 2 ? L : 0u));
+              if (n > 2) put(g, at + 2, r2 | tw | (n == 3 ? L : 0u));
+              if (n > 3) put(g, at + 3, r3 | tw | L);
+            } else { // the from-row is in the cached base
+              put(g, at, r1 | tw | f1 | I_BASE | (n == 2 ? L : 0u));
+              if (n > 2) put(g, at + 1, r2 | tw | (n == 3 ? L : 0u));
+              if (n > 3) put(g, at + 2, r3 | tw | L);
+            }
+          };
+          if ((kinds & 3) == 1) delta(0, at0, w0, w1, s0, n0, hit0, t0w, LAST | (nx ? PAR_E : 0u));
+          if ((kinds >> 2) == 1) delta(1, at1, w2, w3, s1, n1, hit1, t1w, LAST | (nx ? PAR_E : 0u));
+        }
+      }
+      // ---- the pass's last tile stays open
+      uint32_t lbm = 0;
+#pragma unroll
+      for (int b = 0; b < 8; ++b)
+        if (__ballot(tix == ntp - 1 && ((mybit >> b) & 1))) lbm |= 1u << b;
+      if (ntp > 1) p_first = p, t_first = u_fill + (uint32_t)tile_lane0(ntp - 1);
+      tile_k = tk0 + (uint32_t)(ntp - 1);
+      t_fill = ntp == 1 ? tf0 + n_in : n_in - tile_lane0(ntp - 1);
+      tile_bm = ntp == 1 ? tile_bm | lbm : lbm;
+      u_fill += (uint32_t)n_in;
+      pp_c += PP_T() - pp_t;
       if (t_fill == 16) flush();
     }
   }
@@ -973,7 +1025,7 @@ hipError_t launch_plan_stream(const NetDevice &net, const gn_board *parents, siz
     unsigned long long c[4];
     (void)hipStreamSynchronize(s);
     (void)hipMemcpyFromSymbol(c, HIP_SYMBOL(gn_pp), sizeof(c));
-    fprintf(stderr, "plan prof: wave-cycles setup %llu segments %llu parent rows %llu king jobs %llu\n", c[0], c[1],
+    fprintf(stderr, "plan prof: wave-cycles setup %llu slots %llu delta puts %llu king jobs %llu\n", c[0], c[1],
             c[2], c[3]);
     memset(c, 0, sizeof(c));
     (void)hipMemcpyToSymbol(HIP_SYMBOL(gn_pp), c, sizeof(c));
