@@ -246,6 +246,19 @@ __device__ __forceinline__ int king_move_row(const gn_board &pb, int h, int kf, 
   return pc ? feature_index(h, lane, pc, kt) : -1;
 }
 
+// king_move_row from the parent's piece on this lane's square (lane_piece, computed once per
+// parent by the caller) instead of the packed board.
+__device__ __forceinline__ int king_move_row_pc(int pc, int h, int kf, int kt, int rf, int rt, int lane, int &pos,
+                                                int &piece) {
+  if (lane == kf || lane == rf) pc = 0;
+  if (lane == rt) pc = make_piece(h, ROOK);
+  if (lane == kt) pc = make_piece(h, KING);
+  const uint64_t cocc = __ballot(pc != 0);
+  pos = popcnt(cocc & ((1ull << lane) - 1));
+  piece = pc;
+  return pc ? feature_index(h, lane, pc, kt) : -1;
+}
+
 __device__ __forceinline__ int32_t wave_sum(int32_t v) {
 #pragma unroll
   for (int off = 32; off; off >>= 1) v = wadd(v, __shfl_xor(v, off));

@@ -53,7 +53,7 @@
 #include "kernels.h"
 
 #ifndef GN_PLAN_WPE
-#define GN_PLAN_WPE 4 // 128 VGPRs, no spills: 4 latency-bound plan waves per SIMD instead of 3
+#define GN_PLAN_WPE 3 // 168 VGPRs, (almost) no spills: measured 3 % faster than 4 waves per SIMD at 128 VGPRs with spills
 #endif
 #ifndef GN_EXPAND_WPE
 #define GN_EXPAND_WPE (GN_RING == 4 ? 5 : 4)
@@ -259,8 +259,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
       spc = (int)((__shfl(wv, lane >> 3) >> (4 * (lane & 7))) & 15);
       bs = __ballot(spc != pc && spc != 0), ba = __ballot(spc != pc && pc != 0);
     };
+    const int ppc = live ? lane_piece(pb, lane) : 0; // the parent's piece on this lane's square
     if (live && !have && kc) {
-      const int ppc = lane_piece(pb, lane);
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh) {
         const uint64_t kb = __ballot(ppc == make_piece(hh, KING));
@@ -406,7 +406,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
       }
       if (live && q0 == 0 && !have) {
         const uint64_t lt2 = (1ull << lane) - 1;
-        const int ppc = kc ? lane_piece(pb, lane) : 0;
 #pragma unroll 1
         for (int hh = 0; hh < 2; ++hh) {
           const uint32_t tp = tmpl(tf0, stm != hh), b0 = (hh ? len1 : len0) + 1;
@@ -477,10 +476,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
                        sq23 = (uint32_t)__builtin_amdgcn_readlane((int)(hh ? w3 : w1), l);
         const int kt = (int)(sq01 >> 16);
         int pos, cpc;
-        const int row = king_move_row(pb, hh, sq01 & 0xFFFF, kt, sq23 & 0xFFFF, sq23 >> 16, lane, pos, &cpc);
+        const int row = king_move_row_pc(ppc, hh, sq01 & 0xFFFF, kt, sq23 & 0xFFFF, sq23 >> 16, lane, pos, cpc);
         const int cb = (cn - 1) / 4;
-        const int32_t ps_sum = wave_sum(row >= 0 ? psqt((uint32_t)row, cb) : 0);
-        if (lane == 0) TD->psq[tl][hh != st] = ps_sum;
+        const int32_t prw = row >= 0 ? psqt((uint32_t)row, cb) : 0; // summed at the job's end (latency)
         const uint32_t tw = tmpl(tl, hh != st);
         bool kuse = kc && (sq23 & 0xFFFF) == 64; // not castling
         const int kci = 64 * hh + kt;
@@ -538,6 +536,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
         }
         if (g) len1 += (uint32_t)ne;
         else len0 += (uint32_t)ne;
+        const int32_t ps_sum = wave_sum(prw);
+        if (lane == 0) TD->psq[tl][hh != st] = ps_sum;
       }
       while (jc < ntp - 1) close_tile(jc), ++jc, open_tile(jc);
       pp_d += PP_T() - pp_t, pp_t = PP_T();
