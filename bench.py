@@ -48,11 +48,12 @@ sys.path.insert(0, ROOT)
 
 METRIC = "NNUE evals/sec (node) at 1/2/4/8 MI355X + FT gather HBM GB/s as % of peak"
 # /opt/skills/guides/MI355X_MICROARCH.md: HBM3E 8 TB/s peak; L2 34.5 TB/s aggregate (§L2);
-# gathered rows served by the Infinity Cache 8.6 TB/s (§Indexed rows, 38 MB table: the
-# guide's fastest past-L2 gather figure)
+# gathered rows past L2 (§Indexed rows: gather into LDS): 7.4-7.9 TB/s for uniformly random
+# rows of a 151 MB table, the row of that table that matches the 141 MB big-net FT table
+# (its top, 7.9, is the ceiling used; rounds 1-2 used the 38 MB table's 8.6)
 HBM_PEAK_GBS = 8000.0
 L2_PEAK_GBS = 34500.0
-IC_GATHER_GBS = 8600.0
+IC_GATHER_GBS = 7900.0
 SEED = 0x5EED0000
 PLIES = 80
 WORKLOADS = {
@@ -131,7 +132,8 @@ def roofline(alg_bytes, kern_ms, kernel, pmc):
     t_l2 = alg_bytes / (L2_PEAK_GBS * 1e9)
     r = {"bound": "hbm", "kernel": kernel, "achieved": round(achieved, 1), "unit": "GB/s",
          "traffic": None, "alg_bytes_per_launch": int(alg_bytes), "kernel_ms_per_launch": round(kern_ms, 4),
-         "peak_model": "alg_bytes / max(alg_bytes / 34.5 TB/s (L2), traffic / 8.6 TB/s (Infinity-Cache gather)); "
+         "peak_model": "alg_bytes / max(alg_bytes / 34.5 TB/s (L2), traffic / 7.9 TB/s (gathered rows past L2, "
+                       "151 MB table row of MI355X_MICROARCH.md)); "
                        "achieved = kernel-counted FT rows x (2*L1 + 4) B (row + its 4-B list entry) / kernel time"}
     if pmc:
         traffic = float(pmc["hbm_side_bytes_per_launch"])

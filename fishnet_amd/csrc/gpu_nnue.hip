@@ -250,11 +250,6 @@ struct Dev {
   // computes; the lichess replay's inputs and outputs (replay_games_kernel)
   hipStream_t copy = nullptr;
   hipEvent_t cev[2] = {nullptr, nullptr};
-  // the pipelined planned expansion (GN_PLAN_PIPE): the plan stream (lowest priority), its
-  // events, the small plan kernel's king-cache snapshots (1024 words per block)
-  hipStream_t pstream = nullptr;
-  hipEvent_t pev[GN_PIPE_MAX] = {};
-  DevBuf<uint32_t> ksg;
   DevBuf<gn_eval> po2[2], co2[2];
   DevBuf<uint16_t> mv2[2];
   DevBuf<gn_board> roots, rboards, par;
@@ -409,10 +404,7 @@ static void destroy(gn_ctx *ctx) {
     d.kkeys.release(), d.kkeys2.release(), d.kidx.release(), d.kperm.release();
     d.nslot.release(), d.tickets.release(), d.ksnap.release();
     d.ebound.release(), d.eoff.release(), d.ent.release(), d.pool.release(), d.perr.release(), d.tiles.release(), d.btiles.release();
-    d.pstat.release(), d.ksg.release();
-    for (auto &e : d.pev)
-      if (e) (void)hipEventDestroy(e);
-    if (d.pstream) (void)hipStreamSynchronize(d.pstream), (void)hipStreamDestroy(d.pstream);
+    d.pstat.release();
     d.bkeys.release(), d.bkeys2.release(), d.bidx.release(), d.border.release();
     d.lv[0].release(), d.lv[1].release();
     for (int i = 0; i < 2; ++i) {
@@ -464,13 +456,6 @@ static int create(const uint8_t *big, size_t big_len, const uint8_t *small, size
     HIP_TRY(hipEventCreateWithFlags(&d.done, hipEventDisableTiming));
     HIP_TRY(hipStreamCreateWithFlags(&d.copy, hipStreamNonBlocking));
     for (int i = 0; i < 2; ++i) HIP_TRY(hipEventCreateWithFlags(&d.cev[i], hipEventDisableTiming));
-    {
-      int least = 0, greatest = 0;
-      HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
-      static const int hi = getenv("GN_PLAN_PIPE_PRIO") ? atoi(getenv("GN_PLAN_PIPE_PRIO")) : 0; // A/B: 1 = normal
-      HIP_TRY(hipStreamCreateWithPriority(&d.pstream, hipStreamNonBlocking, hi ? 0 : least));
-      for (auto &e : d.pev) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    }
 #ifdef GN_AB_AUX_STREAMS // A/B only: two extra streams, as the removed range pipeline had
     {
       hipStream_t x[2];
@@ -766,18 +751,8 @@ static int expand_evaluate(gn_ctx *ctx, Dev &d, const gn_board *parents, size_t 
       HIP_TRY(d.ent.ensure(d.etot + 16 * (nblk + 1)));
       HIP_TRY(d.tiles.ensure((n + total) / 16 + (K + 2) * nblk + 2));
       HIP_TRY(d.btiles.ensure(nblk + 1));
-      // 8 XCDs x 8 words of scratch-slot bits, then the block claim counter of each range
-      HIP_TRY(d.pool.ensure(64 + GN_PIPE_MAX));
-      HIP_TRY(hipMemsetAsync(d.pool.p, 0, (64 + GN_PIPE_MAX) * sizeof(uint32_t), s));
-      // the pipelined form (A/B: GN_PLAN_PIPE = ranges, GN_PLAN_PIPE_FIRST = blocks of range 0)
-      static const int pipe_r = getenv("GN_PLAN_PIPE") ? atoi(getenv("GN_PLAN_PIPE")) : 1;
-      static const int pipe_first = getenv("GN_PLAN_PIPE_FIRST") ? atoi(getenv("GN_PLAN_PIPE_FIRST")) : 0;
-      PlanPipe pipe{};
-      if (pipe_r > 1 && d.chain_k > 1) { // (blocks of one parent: nothing worth overlapping)
-        HIP_TRY(d.ksg.ensure(nblk * 1024));
-        pipe.ranges = pipe_r, pipe.first = (uint32_t)std::max(0, pipe_first), pipe.ps = d.pstream, pipe.ksg = d.ksg.p;
-        for (int k = 0; k < GN_PIPE_MAX; ++k) pipe.ev[k] = d.pev[k];
-      }
+      HIP_TRY(d.pool.ensure(65)); // 8 XCDs x 8 words of scratch-slot bits, then the block claim counter
+      HIP_TRY(hipMemsetAsync(d.pool.p, 0, 65 * sizeof(uint32_t), s));
       // XCD-local block order
       static const bool bsort = !getenv("GN_BLOCK_SORT") || atoi(getenv("GN_BLOCK_SORT"));
       const uint32_t *order = nullptr;
@@ -793,8 +768,7 @@ static int expand_evaluate(gn_ctx *ctx, Dev &d, const gn_board *parents, size_t 
       HIP_TRY(launch_plan_stream(d.net[BIG], parents, n, off, dl, f ? d.p_nbg.p : nullptr, f ? d.nbg.p : nullptr,
                                  d.p_obg.p, d.obg.p, (ctx->swizzle >> 2) & 1, d.chain_k > 1 ? d.nslot.p : nullptr, d.chain_k,
                                  ctx->king_cache ? 1 : 0, d.eoff.p, d.ent.p, d.tiles.p, d.btiles.p, d.pool.p, d.perr.p,
-                                 rows_out, d.pstat.p, 0, nblk, order, ev ? ev[4] : nullptr, s,
-                                 pipe.ranges > 1 ? &pipe : nullptr));
+                                 rows_out, d.pstat.p, 0, nblk, order, ev ? ev[4] : nullptr, s));
     } else {
       HIP_TRY(launch_expand_net(d.net[BIG], parents, n, off, children, dl, f ? d.p_nbg.p : nullptr,
                                 f ? d.nbg.p : nullptr, d.p_obg.p, d.obg.p, ctx->swizzle & 1,

@@ -85,30 +85,19 @@ static_assert(sizeof(TileDesc) == 192, "TileDesc is 192 bytes");
 // of them), entries at ent + eoff[pbeg] + 16 * block (list 0 upward, list 1 downward from
 // the region's end, eoff = exclusive scan of write_children's per-parent entry bounds).
 // One call plans and evaluates blocks [b0, b1) of the n parents (every index absolute, so
-// block ranges can run as a pipeline on different streams).  pool: 64 + GN_PIPE_MAX words
-// (scratch-slot bits, then one block claim counter per range), zeroed by the caller before
-// each call; err: bit 0 entry overflow, bit 1 no scratch slot, bit 2 a
+// block ranges can run as a pipeline on different streams).  pool: 65 words (scratch-slot
+// bits, then the stream's block claim counter), zeroed by the caller before each call; err: bit 0 entry overflow, bit 1 no scratch slot, bit 2 a
 // king-cache load closer than GN_SCR_GAP entries to its list's last store to scratch.
 // rows_out: += FT rows the stream gathers (bias, carry and king-cache rows included);
 // pads_out (optional): += no-op entries the plan inserted to keep GN_SCR_GAP.
 // order: block order of the stream (block_order) or NULL; mid: recorded between the kernels.
-// pipe (optional, ranges > 1): the pipelined form: range 0 of the blocks is planned alone, then
-// the small plan kernel plans range k + 1 on pipe->ps while range k streams on s.
-#define GN_PIPE_MAX 8
-struct PlanPipe {
-  int ranges;            // > 1: pipelined (at most GN_PIPE_MAX)
-  uint32_t first;        // blocks of range 0 (0: an equal share)
-  hipStream_t ps;        // the plan stream
-  hipEvent_t ev[GN_PIPE_MAX];
-  uint32_t *ksg;         // the small plan's king-cache snapshots: 1024 words per block
-};
 hipError_t launch_plan_stream(const NetDevice &net, const gn_board *parents, size_t n, const uint64_t *offsets,
                               const ChildDelta *deltas, const uint8_t *need_parent, const uint8_t *need_child,
                               int2 *out_parent, int2 *out_child, int swz, const uint8_t *next_slot, int chain_k,
                               int kc, const uint64_t *eoff, uint64_t *ent, TileDesc *tiles, uint32_t *btiles,
                               uint32_t *pool, uint32_t *err, unsigned long long *rows_out,
                               unsigned long long *pads_out, size_t b0, size_t b1, const uint32_t *order,
-                              hipEvent_t mid, hipStream_t s, const PlanPipe *pipe = nullptr);
+                              hipEvent_t mid, hipStream_t s);
 // GN_MODE_FULL preparation: need_small = valid && |simple_eval| > threshold,
 // need_big = valid && !need_small.
 hipError_t launch_classify(const gn_board *boards, size_t n, const gn_eval_params &P, uint8_t *need_small,

@@ -131,35 +131,21 @@ __device__ __forceinline__ void wave_sync() {
 } // namespace ps
 
 // ------------------------------------------------------------------- plan --
-// SMALL: the plan of the pipelined expansion (launch_plan_stream, ranges > 1), which runs
-// beside the stream kernel of the range before: one wave per workgroup, <= 128 VGPRs and
-// 256 B of LDS (the king-cache snapshots in HBM, ksg: 4 KiB per block), so that it fits in
-// what three stream workgroups leave of a CU (LDS 3 x 53 KB of 160, 96 VGPRs x 18 waves).
-template <int L1, bool SMALL>
-__global__ void __launch_bounds__(SMALL ? 64 : 256) __attribute__((amdgpu_waves_per_eu(SMALL ? 4 : GN_PLAN_WPE)))
+template <int L1>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLAN_WPE)))
     plan_kernel(NetDevice net, const gn_board *__restrict__ parents, const uint64_t *__restrict__ offsets,
                 const ChildDelta *__restrict__ deltas, const uint8_t *__restrict__ need_parent,
                 const uint8_t *__restrict__ need_child, const uint8_t *__restrict__ next_slot, uint32_t np, uint32_t K,
                 uint32_t b0, uint32_t b1, int kc, const uint64_t *__restrict__ eoff, uint64_t *__restrict__ ent, TileDesc *__restrict__ tiles,
                 uint32_t *__restrict__ btiles, unsigned long long *__restrict__ rows_out,
-                unsigned long long *__restrict__ pads_out, uint32_t *__restrict__ err,
-                const uint32_t *__restrict__ order, uint32_t *__restrict__ ksg) {
+                unsigned long long *__restrict__ pads_out, uint32_t *__restrict__ err) {
   using namespace ps;
-  constexpr int NWG = SMALL ? 1 : 4; // waves per workgroup, one block each
-  __shared__ uint32_t ksnap_l[SMALL ? 1 : NWG][128][8]; // per wave: placement (64 nibbles) of each king-cache row
-  __shared__ uint8_t kstate[NWG][128];    // bit 0: row holds an accumulator, bit 1: the list that stored it
-  __shared__ uint16_t prow_s[NWG][2][32];
-  const int lane = threadIdx.x & 63, w = SMALL ? 0 : threadIdx.x >> 6;
-  const uint32_t bi = b0 + blockIdx.x * NWG + (uint32_t)w; // this launch plans blocks [b0, b1) (of the order)
-  if (bi >= b1) return; // the whole wave (no workgroup barriers in this kernel)
-  const uint32_t blk = order ? order[bi] : bi;
-  uint32_t *ksb = SMALL ? ksg + (size_t)blk * 1024 : nullptr;
-  // snapshot word j of king-cache row kci (written by this wave only: its own stores, in order)
-  auto snap_ld = [&](int kci, int j) -> uint32_t { return SMALL ? ksb[kci * 8 + j] : ksnap_l[w][kci][j]; };
-  auto snap_st = [&](int kci, int j, uint32_t x) {
-    if (SMALL) ksb[kci * 8 + j] = x;
-    else ksnap_l[w][kci][j] = x;
-  };
+  __shared__ uint32_t ksnap[4][128][8]; // per wave: placement (64 nibbles) of each king-cache row
+  __shared__ uint8_t kstate[4][128];    // bit 0: row holds an accumulator, bit 1: the list that stored it
+  __shared__ uint16_t prow_s[4][2][32];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint32_t blk = b0 + blockIdx.x * 4 + (uint32_t)w; // this launch plans blocks [b0, b1)
+  if (blk >= b1) return; // the whole wave (no workgroup barriers in this kernel)
   const __amdgpu_buffer_rsrc_t pst = __builtin_amdgcn_make_buffer_rsrc(
       (void *)net.psqt, 0, (int)((size_t)PSQT_BUCKETS * FT_ROWS * 4), 0x00020000);
   auto psqt = [&](uint32_t row, int bucket) -> int32_t { // bucket-major copy (L2-resident)
@@ -269,7 +255,7 @@ __global__ void __launch_bounds__(SMALL ? 64 : 256) __attribute__((amdgpu_waves_
     int pkq[2] = {0, 0};          // the perspective's king square
     // the cached placement's piece on this lane's square and the differences to ppc
     auto cache_diff = [&](int kci, int pc, int &spc, uint64_t &bs, uint64_t &ba) {
-      const uint32_t wv = lane < 8 ? snap_ld(kci, lane) : 0u;
+      const uint32_t wv = lane < 8 ? ksnap[w][kci][lane] : 0u;
       spc = (int)((__shfl(wv, lane >> 3) >> (4 * (lane & 7))) & 15);
       bs = __ballot(spc != pc && spc != 0), ba = __ballot(spc != pc && pc != 0);
     };
@@ -444,7 +430,7 @@ __global__ void __launch_bounds__(SMALL ? 64 : 256) __attribute__((amdgpu_waves_
             x |= __shfl_xor(x, 2);
             x |= __shfl_xor(x, 4);
             const int kci = 64 * hh + pkq[hh];
-            if ((lane & 7) == 0) snap_st(kci, lane >> 3, x);
+            if ((lane & 7) == 0) ksnap[w][kci][lane >> 3] = x;
             if (lane == 0) kstate[w][kci] = (uint8_t)(1 | hh << 1);
             uint32_t &sf = hh ? safe1 : safe0;
             sf = b0 + (uint32_t)(pnd[hh] >= 0 ? pnd[hh] : P) + GN_SCR_GAP; // the store's index + the gap
@@ -506,7 +492,7 @@ __global__ void __launch_bounds__(SMALL ? 64 : 256) __attribute__((amdgpu_waves_
         uint64_t bs = 0, ba = 0;
         int spc = 0;
         if (kst & 1) {
-          const uint32_t wv = lane < 8 ? snap_ld(kci, lane) : 0u;
+          const uint32_t wv = lane < 8 ? ksnap[w][kci][lane] : 0u;
           spc = (int)((__shfl(wv, lane >> 3) >> (4 * (lane & 7))) & 15);
           bs = __ballot(spc != cpc && spc != 0);
           ba = __ballot(spc != cpc && cpc != 0);
@@ -540,7 +526,7 @@ __global__ void __launch_bounds__(SMALL ? 64 : 256) __attribute__((amdgpu_waves_
           x |= __shfl_xor(x, 1);
           x |= __shfl_xor(x, 2);
           x |= __shfl_xor(x, 4);
-          if ((lane & 7) == 0) snap_st(kci, lane >> 3, x);
+          if ((lane & 7) == 0) ksnap[w][kci][lane >> 3] = x;
           if (lane == 0) kstate[w][kci] = (uint8_t)(1 | g << 1);
           ps::wave_sync();
         }
@@ -666,7 +652,7 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
     blk = (v & 7) * b8 + (v >> 3);
     if (blk >= nblk) return;
   }
-  blk = order ? order[blk] : blk + b0; // order: a permutation of [b0, b1) (block_order)
+  blk = order ? order[b0 + blk] : blk + b0; // order: a permutation of the blocks (block_order)
   const uint32_t pbeg = blk * K, pend = pbeg + K < np ? pbeg + K : np;
   const uint64_t us_b = pbeg + offsets[pbeg];
   const uint32_t ntiles = btiles[blk];
@@ -1006,73 +992,33 @@ hipError_t launch_plan_stream(const NetDevice &net, const gn_board *parents, siz
                               int kc, const uint64_t *eoff, uint64_t *ent, TileDesc *tiles, uint32_t *btiles,
                               uint32_t *pool, uint32_t *err, unsigned long long *rows_out,
                               unsigned long long *pads_out, size_t b0, size_t b1, const uint32_t *order,
-                              hipEvent_t mid, hipStream_t s, const PlanPipe *pipe) {
+                              hipEvent_t mid, hipStream_t s) {
   if (!n || b1 <= b0) return hipSuccess;
   if (n >= 0x80000000ull) return hipErrorInvalidValue; // 32-bit parent indices in the kernels
   const uint32_t K = chain_k > 1 && next_slot ? (uint32_t)chain_k : 1u;
   const int scr = K > 1 && kc; // the king cache's rows (the chained walk itself needs no scratch)
   if (b1 > (n + K - 1) / K) return hipErrorInvalidValue;
   const uint32_t nb = (uint32_t)(b1 - b0), B0 = (uint32_t)b0, B1 = (uint32_t)b1;
+  const unsigned pg = (nb + 3) / 4, g = swz ? 8 * ((nb + 7) / 8) : nb + nb / 16 + 8; // (stream_eval_kernel: claims)
   static const int ablate = getenv("GN_ABLATE") ? atoi(getenv("GN_ABLATE")) : 0; // timing diagnostics only
   // timing diagnostics only: extra dynamic LDS per workgroup (fewer workgroups per CU)
   static const size_t lds_pad = getenv("GN_STREAM_LDS_PAD") ? (size_t)atoi(getenv("GN_STREAM_LDS_PAD")) : 0;
-  if (net.L1 != 3072 && net.L1 != 1024) return hipErrorInvalidValue;
-  const uint8_t *nsl = K > 1 ? next_slot : nullptr;
-  const int kcu = K > 1 ? kc : 0;
-  auto plan = [&](bool small, uint32_t r0, uint32_t r1, hipStream_t st) {
-    const uint32_t m = r1 - r0;
-    if (net.L1 == 3072 && small)
-      hipLaunchKernelGGL((plan_kernel<3072, true>), dim3(m), dim3(64), 0, st, net, parents, offsets, deltas, need_parent,
-                         need_child, nsl, (uint32_t)n, K, r0, r1, kcu, eoff, ent,
-                         tiles, btiles, rows_out, pads_out, err, order, pipe->ksg);
-    else if (net.L1 == 3072)
-      hipLaunchKernelGGL((plan_kernel<3072, false>), dim3((m + 3) / 4), dim3(256), 0, st, net, parents, offsets, deltas,
-                         need_parent, need_child, nsl, (uint32_t)n, K, r0, r1, kcu,
-                         eoff, ent, tiles, btiles, rows_out, pads_out, err, order, nullptr);
-    else
-      hipLaunchKernelGGL((plan_kernel<1024, false>), dim3((m + 3) / 4), dim3(256), 0, st, net, parents, offsets, deltas,
-                         need_parent, need_child, nsl, (uint32_t)n, K, r0, r1, kcu,
-                         eoff, ent, tiles, btiles, rows_out, pads_out, err, order, nullptr);
-  };
-  auto stream = [&](uint32_t r0, uint32_t r1, uint32_t *claim, hipStream_t st) {
-    const uint32_t m = r1 - r0;
-    const unsigned g = swz ? 8 * ((m + 7) / 8) : m + m / 16 + 8; // (stream_eval_kernel: claims)
-    if (net.L1 == 3072)
-      hipLaunchKernelGGL((stream_eval_kernel<3072>), dim3(g), dim3(384), lds_pad, st, net, offsets, (uint32_t)n, K, r0,
-                         r1, swz, eoff, ent, tiles, btiles, order, out_parent, out_child, pool, scr, err, ablate, claim);
-    else
-      hipLaunchKernelGGL((stream_eval_kernel<1024>), dim3(g), dim3(128), 0, st, net, offsets, (uint32_t)n, K, r0, r1,
-                         swz, eoff, ent, tiles, btiles, order, out_parent, out_child, pool, scr, err, ablate, claim);
-  };
-  // ranges > 1 (the pipelined expansion): the blocks (in their order) are cut into R ranges;
-  // range 0 is planned alone, then range k + 1 is planned on pipe->ps by the small plan
-  // kernel while range k streams on s (events order each stream range after its plan)
-  const int R = pipe && pipe->ranges > 1 && net.L1 == 3072 && nb >= (uint32_t)(256 * pipe->ranges)
-                    ? (pipe->ranges < GN_PIPE_MAX ? pipe->ranges : GN_PIPE_MAX) : 1;
-  if (R == 1) {
-    plan(false, B0, B1, s);
+  if (net.L1 == 3072) {
+    hipLaunchKernelGGL((plan_kernel<3072>), dim3(pg), dim3(256), 0, s, net, parents, offsets, deltas, need_parent,
+                       need_child, K > 1 ? next_slot : nullptr, (uint32_t)n, K, B0, B1, K > 1 ? kc : 0, eoff, ent,
+                       tiles, btiles, rows_out, pads_out, err);
     if (mid) (void)hipEventRecord(mid, s);
-    stream(B0, B1, pool + 64, s);
+    hipLaunchKernelGGL((stream_eval_kernel<3072>), dim3(g), dim3(384), lds_pad, s, net, offsets, (uint32_t)n, K, B0, B1,
+                       swz, eoff, ent, tiles, btiles, order, out_parent, out_child, pool, scr, err, ablate, pool + 64);
+  } else if (net.L1 == 1024) {
+    hipLaunchKernelGGL((plan_kernel<1024>), dim3(pg), dim3(256), 0, s, net, parents, offsets, deltas, need_parent,
+                       need_child, K > 1 ? next_slot : nullptr, (uint32_t)n, K, B0, B1, K > 1 ? kc : 0, eoff, ent,
+                       tiles, btiles, rows_out, pads_out, err);
+    if (mid) (void)hipEventRecord(mid, s);
+    hipLaunchKernelGGL((stream_eval_kernel<1024>), dim3(g), dim3(128), 0, s, net, offsets, (uint32_t)n, K, B0, B1,
+                       swz, eoff, ent, tiles, btiles, order, out_parent, out_child, pool, scr, err, ablate, pool + 64);
   } else {
-    uint32_t rb[GN_PIPE_MAX + 1];
-    for (int k = 0; k <= R; ++k) rb[k] = B0 + (uint32_t)((uint64_t)nb * (uint64_t)k / (uint64_t)R);
-    if (pipe->first > 0 && pipe->first < rb[1] - B0) { // a shorter first range: less plan before the first stream
-      const uint32_t f = B0 + pipe->first;
-      for (int k = 1; k < R; ++k) rb[k] = f + (uint32_t)((uint64_t)(B1 - f) * (uint64_t)(k - 1) / (uint64_t)(R - 1));
-    }
-    plan(false, rb[0], rb[1], s);
-    hipError_t e = hipEventRecord(pipe->ev[0], s);
-    if (e != hipSuccess) return e;
-    if (mid) (void)hipEventRecord(mid, s);
-    if ((e = hipStreamWaitEvent(pipe->ps, pipe->ev[0], 0)) != hipSuccess) return e;
-    for (int k = 1; k < R; ++k) {
-      plan(true, rb[k], rb[k + 1], pipe->ps);
-      if ((e = hipEventRecord(pipe->ev[k], pipe->ps)) != hipSuccess) return e;
-    }
-    for (int k = 0; k < R; ++k) {
-      if (k && (e = hipStreamWaitEvent(s, pipe->ev[k], 0)) != hipSuccess) return e;
-      stream(rb[k], rb[k + 1], pool + 64 + k, s);
-    }
+    return hipErrorInvalidValue;
   }
 #ifdef GN_PLAN_PROF
   {
