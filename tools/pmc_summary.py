@@ -70,7 +70,7 @@ def main(tag):
         bl = json.load(open(bench_p)) if os.path.exists(bench_p) else None
         fetch = avg["FETCH_SIZE"] * 1024 * 2
         write = avg.get("WRITE_SIZE", 0.0) * 1024
-        s = {"kernel": kname, "launches": len(vals["FETCH_SIZE"]), "abi": 2,
+        s = {"kernel": kname, "launches": len(vals["FETCH_SIZE"]), "abi": 3,
              "FETCH_SIZE_kB": avg["FETCH_SIZE"], "WRITE_SIZE_kB": avg.get("WRITE_SIZE"),
              "hbm_side_bytes_per_launch": fetch + write,
              "correction": "bytes = FETCH_SIZE kB x 1024 x 2 (gfx950 wide reads) + WRITE_SIZE kB x 1024; "
@@ -78,6 +78,9 @@ def main(tag):
              "source": f"profiles/{tag}/pmc_fetch_{wl}.csv + pmc_write_{wl}.csv (rocprofv3 --pmc, one pass each)"}
         if "TCC_HIT_sum" in avg and "TCC_MISS_sum" in avg:
             s["l2_hit_rate"] = avg["TCC_HIT_sum"] / max(1.0, avg["TCC_HIT_sum"] + avg["TCC_MISS_sum"])
+            s["TCC_HIT_plus_MISS"] = avg["TCC_HIT_sum"] + avg["TCC_MISS_sum"]
+        if "TCC_REQ_sum" in avg:
+            s["TCC_REQ"] = avg["TCC_REQ_sum"]
         if "SQ_VALU_MFMA_BUSY_CYCLES" in avg and "GRBM_GUI_ACTIVE" in avg:
             s["SQ_VALU_MFMA_BUSY_CYCLES"] = avg["SQ_VALU_MFMA_BUSY_CYCLES"]
             s["GRBM_GUI_ACTIVE"] = avg["GRBM_GUI_ACTIVE"]
@@ -89,6 +92,9 @@ def main(tag):
             alg = bl["roofline"]["alg_bytes_per_launch"]
             s["alg_bytes_per_launch"] = alg
             s["traffic_over_alg"] = s["hbm_side_bytes_per_launch"] / alg
+            # L2-side requests (128 B lines) against the algorithmic row bytes
+            if "TCC_HIT_plus_MISS" in s:
+                s["l2_request_bytes_over_alg"] = s["TCC_HIT_plus_MISS"] * 128 / alg
             s["kernel_ms_per_launch_bench"] = bl["roofline"]["kernel_ms_per_launch"]
         json.dump(s, open(os.path.join(dst, f"pmc_{wl}.json"), "w"), indent=1)
         latest[wl] = s
