@@ -600,7 +600,7 @@ def load_pmc(workload, n):
     if not os.path.exists(p):
         return None
     e = json.load(open(p)).get(workload)
-    return e if e and e.get("positions") == n and e.get("abi", 1) >= 2 else None
+    return e if e and e.get("positions") == n and e.get("abi", 1) >= 3 else None
 
 
 def main():
