@@ -169,14 +169,15 @@ __device__ __forceinline__ void layer_stack_wave(const NetDevice &net, const uin
   const int32_t b1l = net.b1[b * 32 + row], b1h = net.b1[b * 32 + 16 + row];
   const int32_t w2l = net.w2[b * 32 + row], w2h = net.w2[b * 32 + 16 + row];
   const int32_t b2v = net.b2[b];
-  const int8_t *wb = net.w0f + ((size_t)b * KS * 64 + lane) * 16; // (nnue.h: 1 KiB per k-step)
+  constexpr bool FRAG = L1 > 128; // as layer_stack_tile: w0f for the big nets, row-major w0 for 128
+  const int8_t *wb = FRAG ? net.w0f + ((size_t)b * KS * 64 + lane) * 16 : net.w0 + ((size_t)b * 16 + row) * L1 + kg * 16;
   const uint8_t *xa = xt + row * XS + kg * 16;
   int4v acc = zero;
 #pragma unroll 1
   for (int k0 = 0; k0 < KS; k0 += BATCH) {
     int4v w[BATCH], a[BATCH];
 #pragma unroll
-    for (int j = 0; j < BATCH; ++j) w[j] = *reinterpret_cast<const int4v *>(wb + 1024 * (k0 + j));
+    for (int j = 0; j < BATCH; ++j) w[j] = *reinterpret_cast<const int4v *>(wb + (FRAG ? 1024 : 64) * (k0 + j));
 #pragma unroll
     for (int j = 0; j < BATCH; ++j) a[j] = *reinterpret_cast<const int4v *>(xa + 64 * (k0 + j));
 #pragma unroll

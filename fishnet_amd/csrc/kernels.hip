@@ -83,14 +83,17 @@ __device__ __forceinline__ void layer_stack_tile(const NetDevice &net, const uin
     {
       int4v acc = {0, 0, 0, 0};
       const uint8_t *xa = xt + row * XS + kg * 16;
-      const int8_t *wb = net.w0f + ((size_t)b * KS * 64 + lane) * 16; // (nnue.h: 1 KiB per k-step)
+      // big nets: w0f (nnue.h: 1 KiB per k-step, 176 -> 166 ms on configs[2]); the small net's two
+      // k-steps keep the row-major w0 (its 16 rows are one 2 KiB block; w0f measured 6 % slower)
+      constexpr bool FRAG = L1 > 128;
+      const int8_t *wb = FRAG ? net.w0f + ((size_t)b * KS * 64 + lane) * 16 : net.w0 + ((size_t)b * 16 + row) * L1 + kg * 16;
       bool any = false;
 #pragma unroll
       for (int t = 0; t < (KS + NW - 1) / NW; ++t) {
         const int ks = wave + t * NW;
         if (KS % NW == 0 || ks < KS) { // static when the k-steps split evenly: all loads issue together
           const int4v a = *reinterpret_cast<const int4v *>(xa + 64 * ks);
-          const int4v w = *reinterpret_cast<const int4v *>(wb + 1024 * ks);
+          const int4v w = *reinterpret_cast<const int4v *>(wb + (FRAG ? 1024 : 64) * ks);
           acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, w, acc, 0, 0, 0);
           any = true;
         }
