@@ -1860,9 +1860,13 @@ __global__ void gather_boards_kernel(const gn_board *__restrict__ src, const uin
 // the start position's piece still stands there.  A tile of 16 positions then shares
 // its kings and unmoved pieces (eval_net's common-row base); invalid last.
 // Key = uint16_t: kings only (wk << 6 | bk), for small-net-only batches.
+// bkt: the layer-stack bucket ((pieces - 1) / 4) enters the key, so that a tile's 16
+// positions mostly share one bucket and the layer stack runs once per tile instead of
+// once per bucket present: small net above the kings (its table is L2-resident, the king
+// order buys little there), big net between the kings and the home-square bits.
 template <class Key>
 __global__ void king_keys_kernel(const gn_board *__restrict__ boards, size_t n, Key *__restrict__ keys,
-                                 uint32_t *__restrict__ idx) {
+                                 uint32_t *__restrict__ idx, int bkt) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const gn_board p = boards[i];
@@ -1882,8 +1886,9 @@ __global__ void king_keys_kernel(const gn_board *__restrict__ boards, size_t n, 
                    : r == 6 ? make_piece(BLACK, PAWN) : r == 7 ? make_piece(BLACK, BACK[f]) : -1;
     if (pc == want) home |= 1ull << s;
   }
+  const uint32_t b = c ? (uint32_t)(c - 1) / 4 : 0;
   if constexpr (sizeof(Key) == 2) {
-    keys[i] = (Key)(wk < 64 && bk < 64 ? (wk << 6 | bk) : 0xFFFF);
+    keys[i] = (Key)(wk < 64 && bk < 64 ? ((bkt ? b << 12 : 0u) | (uint32_t)(wk << 6 | bk)) : 0xFFFF);
     idx[i] = (uint32_t)i;
     return;
   }
@@ -1895,7 +1900,8 @@ __global__ void king_keys_kernel(const gn_board *__restrict__ boards, size_t n, 
                          | ((hi16 & 0xFFF) | ((hi16 >> 1) & ~0xFFFull)) << 15; // 15 bits: 48-59, 61-63
     uint64_t r = 0, t = h30; // square order, lowest square most significant
     for (int k = 0; k < 30; ++k, t >>= 1) r = r << 1 | (t & 1);
-    key = (uint64_t)wk << 58 | (uint64_t)bk << 52 | r << 22;
+    key = bkt ? (uint64_t)wk << 58 | (uint64_t)bk << 52 | (uint64_t)b << 49 | r << 19
+              : (uint64_t)wk << 58 | (uint64_t)bk << 52 | r << 22;
   }
   keys[i] = (Key)key;
   idx[i] = (uint32_t)i;
@@ -1999,7 +2005,8 @@ hipError_t launch_offsets_u32(const uint64_t *in, size_t n, uint32_t *out, hipSt
 template <class Key>
 static hipError_t king_sort_t(const gn_board *boards, size_t n, Key *keys, uint32_t *idx, Key *keys_out,
                               uint32_t *perm, void *&temp, size_t &temp_bytes, hipStream_t s) {
-  hipLaunchKernelGGL(king_keys_kernel<Key>, dim3(blocks_for(n, 256)), dim3(256), 0, s, boards, n, keys, idx);
+  static const int bkt = !getenv("GN_SORT_BUCKET") || atoi(getenv("GN_SORT_BUCKET")); // A/B: 0 = kings (+ home bits) only
+  hipLaunchKernelGGL(king_keys_kernel<Key>, dim3(blocks_for(n, 256)), dim3(256), 0, s, boards, n, keys, idx, bkt);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   constexpr int BITS = 8 * sizeof(Key);

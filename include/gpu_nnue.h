@@ -71,11 +71,13 @@ extern "C" {
                                          atomic counter) */
 #define GN_OPT_KING_SORT 3            /* 1 (default): evaluate a batch in (white king, black
                                          king) square order for L2 / Infinity-Cache
-                                         locality, then (big net) by 30 home-square bits
-                                         (ranks 1, 2, 7, 8 without e1/e8: the start
-                                         position's piece still stands there) so that
-                                         16-position tiles share rows gathered once per
-                                         tile; results in input order; 0: input order     */
+                                         locality, then (big net) by layer-stack bucket and
+                                         30 home-square bits (ranks 1, 2, 7, 8 without
+                                         e1/e8: the start position's piece still stands
+                                         there) so that 16-position tiles share rows
+                                         gathered once per tile and one layer stack; small
+                                         net: by bucket, then kings; results in input
+                                         order; 0: input order                            */
 #define GN_OPT_KING_CACHE 5           /* 1 (default): with the chained walk, a king-move
                                          child's refresh starts from the accumulator the
                                          workgroup last computed for that (perspective,
