@@ -157,7 +157,9 @@ def test_evaluate_games_vs_oracle(gpu_ctx, oracle_nets, oracle_lib, mode):
 def test_evaluate_games_with_children_vs_oracle(gpu_ctx, oracle_nets, oracle_lib):
     big, small = oracle_nets
     rng = random.Random(5)
-    games = [(START, OPERA, [1, 2]), (C960, _random_game(oracle_lib, rng, C960, 30), [30])]
+    many = "R6R/3Q4/1Q4Q1/4Q3/2Q4Q/Q4Q2/pp1Q4/kBNN1KB1 w - - 0 1"  # 218 legal moves: multi-pass plan
+    games = [(START, OPERA, [1, 2]), (C960, _random_game(oracle_lib, rng, C960, 30), [30]),
+             (many, _random_game(oracle_lib, rng, many, 12), [])]
     out = gpu_ctx.evaluate_games(games, 0, children=True)
     for (root, moves, skip), o in zip(games, out):
         assert o["status"] == 0
