@@ -176,8 +176,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
     }
     // a scratch-row load must sit GN_SCR_GAP entries after the list's last scratch store
     if ((v & (SCR | KST)) == SCR && i < (g ? safe1 : safe0)) bad |= 4u;
+#ifdef GN_ENT_NT // A/B: the entries stored non-temporal (they are read once, by the stream)
+    if (g) __builtin_nontemporal_store(enc64<L1>(v), &E1[-(int64_t)i]);
+    else __builtin_nontemporal_store(enc64<L1>(v), &E0[i]);
+#else
     if (g) E1[-(int64_t)i] = enc64<L1>(v);
     else E0[i] = enc64<L1>(v);
+#endif
   };
   for (int i = lane; i < 128; i += 64) kstate[w][i] = 0;
   uint16_t(*prow)[32] = prow_s[w];
@@ -783,8 +788,11 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
       if (h & H_KST) { // the accumulator to its king-cache row
         asm volatile("");
         const uint32_t so = (scr + (h & 0xFFFFu)) * RS;
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(int4v, lo), ftr, j16, so, 0);
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(int4v, hi), ftr, j16 + L1, so, 0);
+#ifndef GN_KC_POLICY
+#define GN_KC_POLICY 0 // A/B: the cache-policy bits of the king-cache stores (2: non-temporal)
+#endif
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(int4v, lo), ftr, j16, so, GN_KC_POLICY);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(int4v, hi), ftr, j16 + L1, so, GN_KC_POLICY);
         // no drain: the ring's vmcnt(6) still covers an entry's own loads with these two stores
         // outstanding (loads complete in order, so >= 2 of the >= 4 completions it waits for are
         // that entry's loads), and a later load of the row is issued after the store in program
