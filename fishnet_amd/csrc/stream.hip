@@ -745,8 +745,11 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
     // the ring's loads are invisible to the compiler's wait insertion (which, merging the
     // paths of the entry kinds at the loop head, waits for far more of the ring than an entry
     // needs); consume() waits for exactly its own row: see ring_wait
-    asm volatile("buffer_load_dwordx4 %0, %2, %3, %4 offen\n\t"
-                 "buffer_load_dwordx4 %1, %2, %3, %4 offen offset:%5"
+#ifndef GN_ROW_POLICY
+#define GN_ROW_POLICY "" // A/B: cache-policy modifiers of the row loads (e.g. " nt")
+#endif
+    asm volatile("buffer_load_dwordx4 %0, %2, %3, %4 offen" GN_ROW_POLICY "\n\t"
+                 "buffer_load_dwordx4 %1, %2, %3, %4 offen offset:%5" GN_ROW_POLICY
                  : "=&v"(rlo[r]), "=&v"(rhi[r])
                  : "v"(j16), "s"(rsq), "s"(offset(lo, h)), "n"(L1));
   };
@@ -789,7 +792,7 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
         asm volatile("");
         const uint32_t so = (scr + (h & 0xFFFFu)) * RS;
 #ifndef GN_KC_POLICY
-#define GN_KC_POLICY 0 // A/B: the cache-policy bits of the king-cache stores (2: non-temporal)
+#define GN_KC_POLICY 2 // the king-cache stores non-temporal (nt): stream 205.5 -> 205.0 ms, two A/B pairs
 #endif
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(int4v, lo), ftr, j16, so, GN_KC_POLICY);
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(int4v, hi), ftr, j16 + L1, so, GN_KC_POLICY);
