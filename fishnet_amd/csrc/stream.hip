@@ -792,7 +792,7 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
         asm volatile("");
         const uint32_t so = (scr + (h & 0xFFFFu)) * RS;
 #ifndef GN_KC_POLICY
-#define GN_KC_POLICY 0 // A/B: 2 = the king-cache stores non-temporal (nt): stream 205.5 -> 205.0 ms in two A/B pairs
+#define GN_KC_POLICY 2 // king-cache stores non-temporal (nt): stream 205.5 -> 205.0 ms in two A/B pairs; 0 = default policy
 #endif
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(int4v, lo), ftr, j16, so, GN_KC_POLICY);
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(int4v, hi), ftr, j16 + L1, so, GN_KC_POLICY);
