@@ -1447,55 +1447,58 @@ __global__ void finalize_kernel(const gn_board *__restrict__ boards, size_t n, i
                                 const Board *__restrict__ unpacked, int score, const uint64_t *__restrict__ counts) {
   __shared__ Tables T;
   load_tables(T, tables);
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  Board B;
-  gn_eval e = {0, 0, 0, 0, 0, 0, 0};
-  if (unpacked) {
-    B = do_move(unpacked[owner[i]], moves[i], nullptr); // a legal child of a valid parent
-  } else if (!unpack(boards[i], B)) {
-    e.flags = GN_FLAG_BAD_FEN | GN_FLAG_NO_SCORE;
+  // a bounded grid striding over the positions: the 4 KiB table load and its barrier once
+  // per workgroup and many positions, not once per 256 (480 k workgroups per expansion)
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    Board B;
+    gn_eval e = {0, 0, 0, 0, 0, 0, 0};
+    if (unpacked) {
+      B = do_move(unpacked[owner[i]], moves[i], nullptr); // a legal child of a valid parent
+    } else if (!unpack(boards[i], B)) {
+      e.flags = GN_FLAG_BAD_FEN | GN_FLAG_NO_SCORE;
+      out[i] = e;
+      continue;
+    }
+    const Material m = material(B, P);
+    bool small;
+    int2 o;
+    uint32_t flags = 0;
+    if (mode == GN_MODE_SMALL) {
+      small = true, o = out_small[i];
+    } else if (mode == GN_MODE_BIG) {
+      small = false, o = out_big[i];
+    } else if (need_small[i] && !need_big[i]) {
+      small = true, o = out_small[i];
+    } else {
+      small = false, o = out_big[i];
+      if (need_small[i]) flags |= GN_FLAG_REEVAL;
+    }
+    int32_t nnue = wadd(wmul(P.psqt_weight, o.x), wmul(P.positional_weight, o.y)) / 128;
+    const int32_t complexity = abs(wadd(o.x, -o.y));
+    nnue = wadd(nnue, -(wmul(nnue, complexity) / (small ? P.complexity_div_small : P.complexity_div_big)));
+    const int32_t mat = (small ? P.material_pawn_small : P.material_pawn_big) * (m.pawns[0] + m.pawns[1]) +
+                        m.npm[0] + m.npm[1];
+    int32_t v = wmul(nnue, P.material_base + mat) / P.material_base;
+    v = wadd(v, -(wmul(v, (int32_t)B.rule50) / P.rule50_div));
+    v = clampi(v, -P.value_clamp, P.value_clamp);
+    if (small) flags |= GN_FLAG_SMALLNET;
+    const bool check = in_check(B, T);
+    if (check) flags |= GN_FLAG_IN_CHECK;
+    e.psqt = o.x, e.positional = o.y, e.final_v = v;
+    e.final_cp = wdl_to_cp(v, wdl_material(B, P), P);
+    // the score rule's static part (include/gpu_nnue.h); in-check positions with legal moves
+    // keep final_cp until score_reduce_kernel replaces it
+    if (!score) {
+      flags |= GN_FLAG_NO_SCORE; // a child record
+    } else if (counts ? counts[i] == 0 : !any_legal(B, T)) {
+      flags |= GN_FLAG_NO_MOVES | (check ? GN_FLAG_MATE : 0u); // mate 0 / cp 0
+    } else {
+      e.score = e.final_cp;
+    }
+    e.flags = (uint16_t)flags;
     out[i] = e;
-    return;
   }
-  const Material m = material(B, P);
-  bool small;
-  int2 o;
-  uint32_t flags = 0;
-  if (mode == GN_MODE_SMALL) {
-    small = true, o = out_small[i];
-  } else if (mode == GN_MODE_BIG) {
-    small = false, o = out_big[i];
-  } else if (need_small[i] && !need_big[i]) {
-    small = true, o = out_small[i];
-  } else {
-    small = false, o = out_big[i];
-    if (need_small[i]) flags |= GN_FLAG_REEVAL;
-  }
-  int32_t nnue = wadd(wmul(P.psqt_weight, o.x), wmul(P.positional_weight, o.y)) / 128;
-  const int32_t complexity = abs(wadd(o.x, -o.y));
-  nnue = wadd(nnue, -(wmul(nnue, complexity) / (small ? P.complexity_div_small : P.complexity_div_big)));
-  const int32_t mat = (small ? P.material_pawn_small : P.material_pawn_big) * (m.pawns[0] + m.pawns[1]) +
-                      m.npm[0] + m.npm[1];
-  int32_t v = wmul(nnue, P.material_base + mat) / P.material_base;
-  v = wadd(v, -(wmul(v, (int32_t)B.rule50) / P.rule50_div));
-  v = clampi(v, -P.value_clamp, P.value_clamp);
-  if (small) flags |= GN_FLAG_SMALLNET;
-  const bool check = in_check(B, T);
-  if (check) flags |= GN_FLAG_IN_CHECK;
-  e.psqt = o.x, e.positional = o.y, e.final_v = v;
-  e.final_cp = wdl_to_cp(v, wdl_material(B, P), P);
-  // the score rule's static part (include/gpu_nnue.h); in-check positions with legal moves
-  // keep final_cp until score_reduce_kernel replaces it
-  if (!score) {
-    flags |= GN_FLAG_NO_SCORE; // a child record
-  } else if (counts ? counts[i] == 0 : !any_legal(B, T)) {
-    flags |= GN_FLAG_NO_MOVES | (check ? GN_FLAG_MATE : 0u); // mate 0 / cp 0
-  } else {
-    e.score = e.final_cp;
-  }
-  e.flags = (uint16_t)flags;
-  out[i] = e;
 }
 
 // ---- the score rule's in-check positions (gpu_nnue.hip resolve_scores) ------------------
@@ -1612,8 +1615,14 @@ hipError_t launch_finalize(const gn_board *boards, size_t n, int mode, const int
                            const Tables *tables, gn_eval *out, hipStream_t s, int score, const uint64_t *counts,
                            const uint32_t *owner, const uint16_t *moves, const Board *unpacked) {
   if (!n) return hipSuccess;
-  hipLaunchKernelGGL(finalize_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, boards, n, mode, out_small, out_big,
-                     need_small, need_big, P, tables, out, owner, moves, unpacked, score, counts);
+  static const size_t max_blocks = [] {
+    const char *e = getenv("GN_FIN_BLOCKS"); // A/B: finalize workgroups (0 = one per 256 positions)
+    return e ? (size_t)strtoull(e, nullptr, 10) : (size_t)8192;
+  }();
+  size_t blocks = blocks_for(n, 256);
+  if (max_blocks) blocks = std::min(blocks, max_blocks);
+  hipLaunchKernelGGL(finalize_kernel, dim3(blocks), dim3(256), 0, s, boards, n, mode, out_small, out_big, need_small,
+                     need_big, P, tables, out, owner, moves, unpacked, score, counts);
   return hipGetLastError();
 }
 
