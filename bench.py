@@ -2,7 +2,10 @@
 """bench.py — batched Stockfish NNUE evaluation throughput on MI355X.
 
 Contract (driver): `python bench.py --gpus N --steps K --warmup W`, N>1 under
-`torch.distributed.run`; rank 0 prints ONE JSON line.
+`torch.distributed.run`; rank 0 prints ONE JSON line.  Run without a launcher
+(WORLD_SIZE unset) with --gpus N > 1, bench.py starts the N ranks itself: it runs
+`torch.distributed.run` as a child process before anything touches the GPU and exits
+with its code.  Under a launcher, WORLD_SIZE must equal --gpus (else exit code 2).
 
 Default workload `expand` (BASELINE.json configs[4], the 1/2/4/8-GPU scaling
 configuration; configs[3]'s batch shape): every GPU holds 49,152 random 80-ply
@@ -38,6 +41,8 @@ import concurrent.futures as cf
 import json
 import os
 import platform
+import socket
+import subprocess
 import sys
 import time
 
@@ -149,13 +154,14 @@ def roofline(alg_bytes, kern_ms, kernel, pmc):
 
 
 class Ctx:
-    """Per-rank state: library context + the RCCL plumbing of fishnet_amd/dist.py."""
+    """Per-rank state: library context + the RCCL plumbing of fishnet_amd/dist.py (comm: an
+    object with ShardComm's interface; default ShardComm("nccl"), one rank per GPU)."""
 
-    def __init__(self, args):
+    def __init__(self, args, comm=None):
         import torch  # first: torch's HIP runtime is then the one libgpu_nnue binds to
         from fishnet_amd.dist import ShardComm
         self.torch = torch
-        self.comm = ShardComm("nccl")
+        self.comm = comm if comm is not None else ShardComm("nccl")
         self.rank, self.world, self.local = self.comm.rank, self.comm.world, self.comm.local
         from fishnet_amd import build, gpu_nnue as G, synthnet
         build.build()
@@ -263,11 +269,7 @@ def run_expand(c: Ctx, wl: dict, games: int, steps: int, warmup: int, check: int
     _, children, stage, rows = nn.time_expand_device(d_p, n, mode, steps, outputs=out)
     c.barrier_sync()
     wall = c.comm.max(time.perf_counter() - t0)
-    fallbacks = nn.get_option(G.STAT_CHAIN_FALLBACKS)
-    try:
-        scratch_pads = nn.get_option(G.STAT_SCRATCH_PADS)
-    except G.GnError:  # an older library in an A/B run
-        scratch_pads = None
+    scratch_pads = nn.get_option(G.STAT_SCRATCH_PADS)
     # the big net's two kernels timed apart (HIP events on the library's stream, inside the
     # timed region): the roofline's dominant kernel is stream_eval_kernel alone
     plan_ms, stream_ms = nn.get_option(G.STAT_PLAN_NS) / 1e6, nn.get_option(G.STAT_STREAM_NS) / 1e6
@@ -278,10 +280,8 @@ def run_expand(c: Ctx, wl: dict, games: int, steps: int, warmup: int, check: int
     r = dict(value=c.world * (n + children) * steps / wall, wall=wall, stage=stage,
              kern_ms=stream_ms if planned else stage[5 if mode != 2 else 4], plan_ms=plan_ms,
              alg=rows * (2 * wl["l1"] + 4), rows=rows, parents=parents, n=n,
-             children=children, gen_s=gen_s, checksum=sums[0] ^ sums[1], chain_fallbacks=fallbacks,
-             scratch_pads=scratch_pads,
-             kernel=(f"stream_eval_kernel<{wl['l1']}>" if planned else f"expand_stream<{wl['l1']}>")
-             if wl["l1"] != 128 else f"expand_eval<{wl['l1']}>")
+             children=children, gen_s=gen_s, checksum=sums[0] ^ sums[1], scratch_pads=scratch_pads,
+             kernel=f"stream_eval_kernel<{wl['l1']}>" if wl["l1"] != 128 else f"expand_eval<{wl['l1']}>")
     if check:
         ver = {}
         # (1) sampled parents of the timed outputs, with all their children, against the oracle
@@ -469,9 +469,11 @@ def run_abi_games(c: Ctx, games: int, mode: int, steps: int, check: int):
     caps = res[-1]
     c.barrier_sync()
     t0 = time.perf_counter()
-    stages = []
+    stages, calls = [], []
     for _ in range(steps):
+        t1 = time.perf_counter()
         res = nn.evaluate_games_arrays(arr, games, mode, True, caps, bufs)
+        calls.append(time.perf_counter() - t1)
         stages.append(nn.host_stages())
     c.barrier_sync()
     wall = c.comm.max(time.perf_counter() - t0)
@@ -483,8 +485,9 @@ def run_abi_games(c: Ctx, games: int, mode: int, steps: int, check: int):
                      f"{npos} positions + {nch} legal children, records in host memory",
          "value": round(c.world * (npos + nch) * steps / wall, 1), "unit": "evals/s",
          "ms_per_call": round(wall * 1e3 / steps, 3), "positions": npos, "children": nch,
-         "result_bytes_to_host": int(npos * G.EVAL_SIZE + nch * (G.EVAL_SIZE + 2) + (npos + 1) * 4),
-         "stage_ms": st, "prep_s_untimed": round(prep_s, 2),
+         "result_bytes_to_host": int(npos * G.EVAL_SIZE + nch * (G.CHILD_SIZE + 2) + (npos + 1) * 4),
+         "records": "positions: 24-B gn_eval (with the score); children: 12-B gn_child (ABI v4) + 2-B move",
+         "stage_ms": st, "python_call_ms": round(1e3 * sum(calls) / len(calls), 3), "prep_s_untimed": round(prep_s, 2),
          "stages": "parse: host root FEN + UCI tokenizing; upload: inputs to the device; replay: the GPU replay of "
                    "the moves; compute: children + evaluation + score rule over all chunks (main thread); "
                    "download: device->host record copies, all chunks (a drain thread, overlapping the next "
@@ -503,8 +506,9 @@ def run_abi_games(c: Ctx, games: int, mode: int, steps: int, check: int):
             a, b = int(coffs[at]), int(coffs[at + 1])
             p_exp, m_exp, k_exp = O.expand_eval(big if mode != 2 else None, small if mode != 1 else None, fens[-1],
                                                 mode, incremental=True)
-            got = dict(zip(cmv[a:b].tolist(), map(tuple, cev[a:b].tolist())))
-            return int(tuple(pos[at]) != p_exp or got != dict(zip(m_exp, map(tuple, k_exp.tolist())))), b - a
+            got = dict(zip(cmv[a:b].tolist(), map(tuple, G.decode_children(cev[a:b]).tolist())))
+            exp = dict(zip(m_exp, map(tuple, G.children_from_evals(k_exp).tolist())))
+            return int(tuple(pos[at]) != p_exp or got != exp), b - a
 
         with cf.ThreadPoolExecutor(host_threads()) as ex:
             out = list(ex.map(one, items))
@@ -532,12 +536,98 @@ def run_abi_games(c: Ctx, games: int, mode: int, steps: int, check: int):
             c0, c1 = int(coffs[a0]), int(coffs[a1])
             d0, d1 = int(doff[i]), int(doff[i + a1 - a0])
             bad += int(not (np.array_equal(pos[a0:a1], po[i:i + a1 - a0]) and np.array_equal(cmv[c0:c1], dmv[d0:d1])
-                            and np.array_equal(cev[c0:c1], dco[d0:d1])))
+                            and np.array_equal(G.decode_children(cev[c0:c1]), G.children_from_evals(dco[d0:d1]))))
             i += a1 - a0
         for b in list(db.values()) + [d_b]:
             b.free()
         ver["vs_device_resident"] = {"games": len(full), "positions": m, "children": tt, "mismatching_games": bad}
         r["oracle_check"] = ver
+    return r
+
+
+def run_dropin(c: Ctx, games: int, threads: int, calls_per_thread: int, check: int):
+    """secondary.dropin: the drop-in's real call shape.  fishnet's N workers
+    each send one chunk at a time (/root/reference/src/main.rs:263-343); with the GPU backend a
+    chunk is one lichess game (rust/patches/0002: whole-batch chunks), which GpuEvalStub sends as
+    one gn_evaluate_batch(GN_MODE_FULL) of the game's positions (root + every ply, checks and
+    mates included).  Measured: (1) one caller, call after call: per-call latency; (2) `threads`
+    callers at once on one context, as the stub's spawn_blocking calls arrive from the workers:
+    positions/s and per-call latency, with concurrent calls merged into one launch
+    (GN_OPT_COALESCE = 1, the default) and run one after another (0).  FENs are prepared untimed
+    (the caller holds them); each timed call is the C call alone."""
+    import ctypes as C
+    import threading
+    G, nn, L = c.G, c.nn, c.G.lib()
+    first, _ = c.shard(games)
+    ucis = G.random_games_uci(SEED + 5, first, games, PLIES)
+    calls = []
+    for u in ucis:
+        boards, _, _ = G.replay_game(START_FEN, u)
+        fens = G.boards_to_fens(boards)
+        enc = [f.encode() for f in fens]
+        calls.append(((C.c_char_p * len(enc))(*enc), enc, np.zeros(len(enc), dtype=G.EVAL_DTYPE), fens))
+
+    def call(k):
+        arr, enc, out, _ = calls[k % len(calls)]
+        t = time.perf_counter()
+        rc = L.gn_evaluate_batch(nn.h, arr, len(enc), out.ctypes.data)
+        dt = time.perf_counter() - t
+        if rc:
+            G._check(rc)
+        return dt
+
+    def pct(xs, q):
+        return round(float(np.percentile(np.array(xs) * 1e3, q)), 4)
+
+    for k in range(min(32, len(calls))):  # warmup (buffers sized, kernels loaded)
+        call(k)
+    single = [call(k) for k in range(len(calls))]
+    npos = sum(len(x[1]) for x in calls)
+    in_check = sum(int(np.count_nonzero(x[2]["flags"] & G.FLAG_IN_CHECK)) for x in calls)
+    searched = sum(int(np.count_nonzero(x[2]["flags"] & G.FLAG_SEARCHED)) for x in calls)
+    r = {"workload": f"one lichess game per call (start position + up to {PLIES} random plies = "
+                     f"{npos / len(calls):.1f} positions), gn_evaluate_batch(GN_MODE_FULL) as GpuEvalStub::go_multiple "
+                     f"sends it; {games} games per MI355X; {in_check} of the {npos} positions in check "
+                     f"({searched} scored by the in-check rule)",
+         "single_caller": {"calls": len(single), "p50_ms": pct(single, 50), "p99_ms": pct(single, 99),
+                           "positions_per_s": round(npos / sum(single), 1)}}
+    for mode_name, co in (("coalesced", 1), ("serial", 0)):
+        nn.set_option(G.OPT_COALESCE, co)
+        l0, c0 = nn.get_option(G.STAT_BATCH_LAUNCHES), nn.get_option(G.STAT_BATCH_CALLS)
+        lat = [[] for _ in range(threads)]
+        go = threading.Barrier(threads + 1)
+
+        def work(t):
+            go.wait()
+            for i in range(calls_per_thread):
+                lat[t].append(call(t * calls_per_thread + i))
+
+        th = [threading.Thread(target=work, args=(t,)) for t in range(threads)]
+        for x in th:
+            x.start()
+        go.wait()
+        t0 = time.perf_counter()
+        for x in th:
+            x.join()
+        wall = time.perf_counter() - t0
+        allx = [v for l in lat for v in l]
+        pos = sum(len(calls[(t * calls_per_thread + i) % len(calls)][1]) for t in range(threads)
+                  for i in range(calls_per_thread))
+        r[f"{threads}_callers_{mode_name}"] = {
+            "calls": len(allx), "positions_per_s": round(pos / wall, 1), "calls_per_s": round(len(allx) / wall, 1),
+            "p50_ms": pct(allx, 50), "p99_ms": pct(allx, 99),
+            "launches": nn.get_option(G.STAT_BATCH_LAUNCHES) - l0, "calls_served": nn.get_option(G.STAT_BATCH_CALLS) - c0}
+    nn.set_option(G.OPT_COALESCE, 1)
+    co = r[f"{threads}_callers_coalesced"]
+    co["speedup_vs_serial"] = round(co["positions_per_s"] / r[f"{threads}_callers_serial"]["positions_per_s"], 3)
+    if check:  # the last records of sampled games (every game's last call wrote them) vs the oracle
+        O, big, small = c.oracle_nets()
+        idx = np.random.default_rng(55 + c.rank).choice(len(calls), size=min(check, len(calls)), replace=False)
+        fens = [f for k in idx for f in calls[k][3]]
+        got = np.concatenate([calls[k][2] for k in idx])
+        exp = O.eval_fens(big, small, fens, G.MODE_FULL, threads=host_threads())
+        r["oracle_check"] = {"games": len(idx), "positions": len(fens),
+                             "mismatches": int(np.count_nonzero(got != exp)), "of": "the concurrent calls' records"}
     return r
 
 
@@ -603,6 +693,51 @@ def load_pmc(workload, n):
     return e if e and e.get("positions") == n and e.get("abi", 1) >= 3 else None
 
 
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(gpus: int, argv) -> int | None:
+    """The N > 1 launch (the reference's analog is the per-core worker fan-out,
+    /root/reference/src/main.rs:151-161): with WORLD_SIZE unset and gpus > 1, run
+    `torch.distributed.run` with one rank per GPU over 127.0.0.1 as a CHILD process (this process
+    has not touched the GPU: no torch / HIP import yet) and return its exit code.  Under a
+    launcher (WORLD_SIZE set) the world must equal gpus: a mismatch returns 2 before any GPU
+    work.  None: run this process as the (only) rank."""
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != gpus:
+            print(f"bench.py: WORLD_SIZE={ws} but --gpus {gpus}: launch one rank per GPU "
+                  f"(torch.distributed.run --nproc-per-node {gpus})", file=sys.stderr, flush=True)
+            return 2
+        return None
+    if gpus <= 1:
+        return None
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *argv]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    return subprocess.run(cmd, env=env).returncode
+
+
+def launch_check() -> int:
+    """--launch-check: no GPU work; every rank joins a gloo group and rank 0 prints the ranks it
+    sees (tests/test_dist.py drives the launcher this way on the CPU)."""
+    import torch.distributed as dist
+    rank, world = int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1"))
+    ranks = [rank]
+    if world > 1:
+        dist.init_process_group("gloo")
+        lst = [None] * world
+        dist.all_gather_object(lst, (rank, int(os.environ.get("LOCAL_RANK", "0"))))
+        ranks = lst
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps({"world": world, "ranks": ranks}), flush=True)
+    return 0
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -623,9 +758,22 @@ def main():
     ap.add_argument("--king-cache", type=int, default=None, help="GN_OPT_KING_CACHE (None: library default)")
     ap.add_argument("--abi-games", type=int, default=0,
                     help="only the secondary.abi_games line with this many games per GPU (A/B runs)")
+    ap.add_argument("--launch-check", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--dropin", action="store_true", help="only the secondary.dropin line (A/B runs)")
     args = ap.parse_args()
+    rc = launch_ranks(args.gpus, sys.argv[1:])
+    if rc is not None:
+        sys.exit(rc)
+    if args.launch_check:
+        sys.exit(launch_check())
 
     c = Ctx(args)
+    if args.dropin:
+        r = run_dropin(c, 1024, 16, 64, args.check and 32)
+        if c.rank == 0:
+            print(json.dumps(r), flush=True)
+        c.close()
+        return
     if args.abi_games:
         r = run_abi_games(c, args.abi_games, 1, args.steps, args.check)
         if c.rank == 0:
@@ -642,8 +790,7 @@ def main():
         cfg = {"workload": wl["config"], "games_per_gpu": n, "parents_per_gpu": r["n"],
                "children_per_gpu": r["children"], "evals_per_step_per_gpu": r["n"] + r["children"],
                "evals_per_step_all_gpus": c.world * (r["n"] + r["children"]), "plies": PLIES,
-               "ft_rows_per_step_per_gpu": r["rows"], "chain_fallbacks": r["chain_fallbacks"],
-               "king_cache_gap_pads": r["scratch_pads"]}
+               "ft_rows_per_step_per_gpu": r["rows"], "king_cache_gap_pads": r["scratch_pads"]}
         stage_names = G.EXPAND_STAGES
         data = f"synthetic: seeded random 80-ply games generated on the GPU; nets {c.net_label}"
     else:
@@ -714,6 +861,10 @@ def main():
             ag["rank_check_failures"] = c.comm.gather_i64(ck["oracle"]["mismatching_positions"] +
                                                           ck["vs_device_resident"]["mismatching_games"])
         sec["abi_games"] = ag
+        dr = run_dropin(c, 1024, 16, 64, 32 if args.check else 0)
+        if "oracle_check" in dr:
+            dr["rank_check_failures"] = c.comm.gather_i64(dr["oracle_check"]["mismatches"])
+        sec["dropin"] = dr
         line["secondary"] = sec
 
     if c.rank == 0:

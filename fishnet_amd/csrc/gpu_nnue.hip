@@ -11,6 +11,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -208,8 +209,6 @@ struct Dev {
   DevBuf<uint8_t> p_nsm, p_nbg;  // parent-side net selection during expansion
   DevBuf<unsigned long long> sum;
   DevBuf<uint8_t> nslot; // chained walk: child of parent i that is parent i + 1 (255: none)
-  DevBuf<uint32_t> tickets; // chained walk: per carry slot, how many workgroups are done with it
-  DevBuf<uint32_t> ksnap;   // king cache: per slot x (perspective, king square) a 32-B placement snapshot
   int chain_k = 1;          // block length of the current expansion (1: no chaining)
   // planned expansion (stream.hip): per-parent entry bounds and their scan, the entry
   // lists, tile descriptors, the scratch-slot pool and the error word
@@ -251,6 +250,7 @@ struct Dev {
   hipStream_t copy = nullptr;
   hipEvent_t cev[2] = {nullptr, nullptr};
   DevBuf<gn_eval> po2[2], co2[2];
+  DevBuf<gn_child> cc2[2]; // co2 packed as the host's 12-B child records (ABI v4)
   DevBuf<uint16_t> mv2[2];
   DevBuf<gn_board> roots, rboards, par;
   DevBuf<uint64_t> moff;
@@ -291,14 +291,36 @@ struct SeqGuard { // seq_begin now, seq_end when the scope ends (d.mu held throu
   ~SeqGuard() { (void)seq_end(d, s); }
 };
 
+// One gn_evaluate_batch call waiting for, or in, a merged launch (evaluate_coalesced).
+struct BatchReq {
+  const gn_board *boards;
+  size_t n;
+  int mode;
+  gn_eval *out;
+  int rc = GN_OK;
+  bool done = false;
+  std::string err;
+};
+
 struct gn_ctx {
   std::vector<std::unique_ptr<Dev>> devs;
+  // concurrent gn_evaluate_batch callers (fishnet's workers, one chunk per call) are merged
+  // into one launch (evaluate_coalesced); GN_OPT_COALESCE
+  struct {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::vector<BatchReq *> q; // calls waiting for a launch
+    bool busy = false;         // a launch is running
+    uint64_t launches = 0, calls = 0;
+  } co;
+  bool coalesce = true;
   gn_eval_params P;
   bool incremental = true; // GN_OPT_INCREMENTAL_CHILDREN
   int swizzle = 1;          // GN_OPT_XCD_SWIZZLE bit mask: 1 expansion, 2 batch evaluation
-  bool king_sort = true;    // GN_OPT_KING_SORT
+  int king_sort = 1;        // GN_OPT_KING_SORT (1: batches of >= KING_SORT_MIN positions, 2: all)
   int chain = 81;           // GN_OPT_CHAIN (blocks of consecutive parents per workgroup)
   bool king_cache = true;   // GN_OPT_KING_CACHE
+  int64_t chunk_parents = 0; // GN_OPT_CHUNK_PARENTS (0: automatic)
   int l1[2] = {0, 0};
   uint32_t hash[2] = {0, 0};
   double t_parse = 0, t_total = 0; // the last host-buffer expansion call (GN_STAT_HOST_*), ms
@@ -402,13 +424,13 @@ static void destroy(gn_ctx *ctx) {
     if (d.scan_tmp) (void)hipFree(d.scan_tmp);
     if (d.sort_tmp) (void)hipFree(d.sort_tmp);
     d.kkeys.release(), d.kkeys2.release(), d.kidx.release(), d.kperm.release();
-    d.nslot.release(), d.tickets.release(), d.ksnap.release();
+    d.nslot.release();
     d.ebound.release(), d.eoff.release(), d.ent.release(), d.pool.release(), d.perr.release(), d.tiles.release(), d.btiles.release();
     d.pstat.release();
     d.bkeys.release(), d.bkeys2.release(), d.bidx.release(), d.border.release();
     d.lv[0].release(), d.lv[1].release();
     for (int i = 0; i < 2; ++i) {
-      d.po2[i].release(), d.co2[i].release(), d.mv2[i].release();
+      d.po2[i].release(), d.co2[i].release(), d.cc2[i].release(), d.mv2[i].release();
       if (d.cev[i]) (void)hipEventDestroy(d.cev[i]);
     }
     d.roots.release(), d.rboards.release(), d.par.release(), d.moff.release(), d.codes.release();
@@ -462,10 +484,6 @@ static int create(const uint8_t *big, size_t big_len, const uint8_t *small, size
       for (int i = 0; i < 2; ++i) HIP_TRY(hipStreamCreateWithFlags(&x[i], hipStreamNonBlocking));
     }
 #endif
-    if (getenv("GN_NET_PAD")) { // A/B only: a device allocation of this many bytes before the nets
-      void *x = nullptr;
-      HIP_TRY(hipMalloc(&x, (size_t)atoll(getenv("GN_NET_PAD"))));
-    }
     HIP_TRY(hipMalloc(&d.tables, sizeof(Tables)));
     HIP_TRY(d.perr.ensure(1)); // the planned expansion's error word and pad count
     HIP_TRY(d.pstat.ensure(1));
@@ -520,7 +538,10 @@ static int evaluate_on(gn_ctx *ctx, Dev &d, const gn_board *b, size_t n, int mod
   HIP_TRY(mark(0));
   if (mode == GN_MODE_FULL) HIP_TRY(launch_classify(b, n, P, d.nsm.p, d.nbg.p, s));
   const uint32_t *perm = nullptr;
-  if (ctx->king_sort) {
+  // a small batch (one game, a handful of in-check replies) gains nothing from the order and
+  // would pay the sort's launches on its latency (bench.py secondary.dropin)
+  constexpr size_t KING_SORT_MIN = 1024;
+  if (ctx->king_sort == 2 || (ctx->king_sort == 1 && n >= KING_SORT_MIN)) {
     if (n > 0x7FFFFFFFull) return fail(GN_E_INVALID, "king sort supports < 2^31 positions per call");
     HIP_TRY(d.kkeys.ensure(n));
     HIP_TRY(d.kkeys2.ensure(n));
@@ -584,15 +605,12 @@ static int chain_len(const gn_ctx *ctx, Dev &d, size_t n) {
   return (int)k;
 }
 
-// The big net's expansion (modes FULL / BIG) runs planned (stream.hip) unless GN_STREAM=old
-// selects the round-1 single-kernel expand_stream (A/B timing); both give identical results.
+// The big net's expansion (modes FULL / BIG) runs planned (stream.hip).
 // (Round 2's pipeline of block ranges on two streams, range c + 1's child generation and plan
 // under range c's row stream, took the same time as the serial order, 296 vs 259 + 19 + 15.5
 // + 5 ms: the overlapped kernels slow the row stream by what they add; it was removed.)
 static bool plan_path(const gn_ctx *ctx, const Dev &d, int mode) {
-  static const bool old = getenv("GN_STREAM") && !strcmp(getenv("GN_STREAM"), "old");
-  static const bool legacy = getenv("GN_EXPAND_LEGACY") && atoi(getenv("GN_EXPAND_LEGACY"));
-  return !old && !legacy && mode != GN_MODE_SMALL && ctx->incremental && d.has[BIG] &&
+  return mode != GN_MODE_SMALL && ctx->incremental && d.has[BIG] &&
          (d.net[BIG].L1 == 3072 || d.net[BIG].L1 == 1024);
 }
 
@@ -639,11 +657,7 @@ static int generate_children(Dev &d, const gn_board *parents, size_t n, gn_board
     HIP_TRY(hipMemsetAsync(d.perr.p, 0, sizeof(uint32_t), s));
     HIP_TRY(hipMemsetAsync(d.pstat.p, 0, sizeof(unsigned long long), s));
   }
-  if (d.chain_k > 1) {
-    HIP_TRY(d.nslot.ensure(n));
-    HIP_TRY(d.tickets.ensure(CARRY_SLOTS + 1));
-    HIP_TRY(d.ksnap.ensure((size_t)CARRY_SLOTS * 128 * 8));
-  }
+  if (d.chain_k > 1) HIP_TRY(d.nslot.ensure(n));
   HIP_TRY(d.counts.ensure(n + 1));
   HIP_TRY(d.offsets.ensure(n + 1));
   HIP_TRY(hipMemsetAsync(d.counts.p + n, 0, sizeof(uint64_t), s));
@@ -736,8 +750,7 @@ static int expand_evaluate(gn_ctx *ctx, Dev &d, const gn_board *parents, size_t 
   if (mode != GN_MODE_BIG) {
     const bool f = mode == GN_MODE_FULL;
     HIP_TRY(launch_expand_net(d.net[SMALL], parents, n, off, children, dl, f ? d.p_nsm.p : nullptr,
-                              f ? d.nsm.p : nullptr, d.p_osm.p, d.osm.p, ctx->swizzle & 1, nullptr, nullptr, 1, nullptr, nullptr,
-                              s));
+                              f ? d.nsm.p : nullptr, d.p_osm.p, d.osm.p, ctx->swizzle & 1, s));
     if (f) {
       HIP_TRY(launch_reeval(d.p_osm.p, d.p_nsm.p, n, P, d.p_nbg.p, s));
       HIP_TRY(launch_reeval(d.osm.p, d.nsm.p, total, P, d.nbg.p, s));
@@ -754,9 +767,8 @@ static int expand_evaluate(gn_ctx *ctx, Dev &d, const gn_board *parents, size_t 
       HIP_TRY(d.pool.ensure(65)); // 8 XCDs x 8 words of scratch-slot bits, then the block claim counter
       HIP_TRY(hipMemsetAsync(d.pool.p, 0, 65 * sizeof(uint32_t), s));
       // XCD-local block order
-      static const bool bsort = !getenv("GN_BLOCK_SORT") || atoi(getenv("GN_BLOCK_SORT"));
       const uint32_t *order = nullptr;
-      if (bsort && ctx->king_sort && nblk > 1) {
+      if (ctx->king_sort && nblk > 1) {
         HIP_TRY(d.bkeys.ensure(nblk));
         HIP_TRY(d.bkeys2.ensure(nblk));
         HIP_TRY(d.bidx.ensure(nblk));
@@ -769,11 +781,9 @@ static int expand_evaluate(gn_ctx *ctx, Dev &d, const gn_board *parents, size_t 
                                  d.p_obg.p, d.obg.p, (ctx->swizzle >> 2) & 1, d.chain_k > 1 ? d.nslot.p : nullptr, d.chain_k,
                                  ctx->king_cache ? 1 : 0, d.eoff.p, d.ent.p, d.tiles.p, d.btiles.p, d.pool.p, d.perr.p,
                                  rows_out, d.pstat.p, 0, nblk, order, ev ? ev[4] : nullptr, s));
-    } else {
+    } else { // a 128-wide net loaded as the big net
       HIP_TRY(launch_expand_net(d.net[BIG], parents, n, off, children, dl, f ? d.p_nbg.p : nullptr,
-                                f ? d.nbg.p : nullptr, d.p_obg.p, d.obg.p, ctx->swizzle & 1,
-                                d.chain_k > 1 ? d.nslot.p : nullptr, d.tickets.p, d.chain_k,
-                                ctx->king_cache ? d.ksnap.p : nullptr, rows_out, s));
+                                f ? d.nbg.p : nullptr, d.p_obg.p, d.obg.p, ctx->swizzle & 1, s));
     }
   }
   HIP_TRY(mark(2));
@@ -932,6 +942,63 @@ static int evaluate_boards_host(gn_ctx *ctx, const gn_board *boards, size_t n, i
   }
 }
 
+// Concurrent gn_evaluate_batch calls merged into one launch (group commit): a call queues
+// itself; when no launch is running it leads one over every queued call of its mode (its own
+// included), and the calls that queue meanwhile form the next launch.  A lone caller leads at
+// once, so nothing waits on a timer.  fishnet's worker pool calls the evaluator once per chunk
+// from N workers (/root/reference/src/main.rs:151-161, 263-343), so under load N small calls
+// share one set of kernel launches and host round trips instead of N serialised ones.
+// Results are those of separate calls (positions are independent).
+static int evaluate_coalesced(gn_ctx *ctx, const gn_board *boards, size_t n, int mode, gn_eval *out) {
+  if (!ctx->coalesce) return evaluate_boards_host(ctx, boards, n, mode, out);
+  auto &C = ctx->co;
+  BatchReq me{boards, n, mode, out};
+  std::unique_lock<std::mutex> lk(C.mu);
+  C.q.push_back(&me);
+  while (!me.done) {
+    if (C.busy) {
+      C.cv.wait(lk);
+      continue;
+    }
+    C.busy = true;
+    std::vector<BatchReq *> mine, rest;
+    for (BatchReq *r : C.q) (r->mode == mode ? mine : rest).push_back(r);
+    C.q.swap(rest);
+    lk.unlock();
+    int rc = GN_OK;
+    std::string err;
+    try {
+      if (mine.size() == 1) {
+        rc = evaluate_boards_host(ctx, me.boards, me.n, mode, me.out);
+      } else {
+        size_t tot = 0;
+        for (BatchReq *r : mine) tot += r->n;
+        std::vector<gn_board> all(tot);
+        std::vector<gn_eval> res(tot);
+        size_t at = 0;
+        for (BatchReq *r : mine) std::copy(r->boards, r->boards + r->n, all.begin() + at), at += r->n;
+        rc = evaluate_boards_host(ctx, all.data(), tot, mode, res.data());
+        at = 0;
+        if (rc == GN_OK)
+          for (BatchReq *r : mine) std::copy(res.begin() + at, res.begin() + at + r->n, r->out), at += r->n;
+      }
+    } catch (const std::bad_alloc &) {
+      rc = fail(GN_E_NOMEM, "host allocation failed");
+    } catch (...) {
+      rc = fail(GN_E_INVALID, "unexpected exception");
+    }
+    if (rc) err = g_err;
+    lk.lock();
+    for (BatchReq *r : mine) r->rc = rc, r->err = err, r->done = true;
+    ++C.launches, C.calls += mine.size();
+    C.busy = false;
+    C.cv.notify_all();
+  }
+  const int rc = me.rc;
+  if (rc) g_err = me.err;
+  return rc;
+}
+
 // ------------------------------------------------------ host pipeline ----
 // The host-buffer expansion (gn_expand_and_evaluate, gn_evaluate_games with children),
 // sharded over the context's devices: shard k's parents are resident on its device (uploaded
@@ -1000,10 +1067,31 @@ static std::vector<size_t> chunk_bounds(size_t m, const std::vector<size_t> &sta
   return c;
 }
 
-// Parents per chunk: keeps >= 2048 whole 81-parent blocks per chunk (chain_len's full block
-// length), and about eight chunks per shard so the first and last chunk, the parts that
-// cannot overlap, are short.
-static size_t chunk_target(size_t m) { return std::max<size_t>((size_t)2048 * 81, (m + 7) / 8); }
+// The chunks of a shard's m parents for the pipeline below, cut only at `starts` (game starts;
+// empty: anywhere).  opt > 0 (GN_OPT_CHUNK_PARENTS): chunks of >= opt parents.  Automatic: each
+// chunk costs a fixed few ms (the row stream's and the plan's last blocks run on a part-idle
+// GPU, and the chunk's launches and syncs), and only the last chunk's download is not
+// overlapped, so: a shard below 3 x MIN parents is one chunk (MIN = 2,048 games of 81 parents,
+// the least that keeps chain_len's full block length); otherwise a short last chunk of
+// max(MIN, m / 8) parents after chunks of <= 2 M parents (round 3 cut eight equal chunks: 35 ms
+// of per-chunk tails per 4 M parents).
+static std::vector<size_t> chunk_plan(size_t m, const std::vector<size_t> &starts, int64_t opt) {
+  if (opt > 0) return chunk_bounds(m, starts, (size_t)opt);
+  constexpr size_t MIN = (size_t)2048 * 81, BIG = 2000000;
+  if (m < 3 * MIN) return {0, m};
+  const size_t last = std::max(MIN, m / 8), rest = m - last, k = (rest + BIG - 1) / BIG;
+  std::vector<size_t> c{0};
+  for (size_t i = 1; i <= k; ++i) {
+    size_t x = rest * i / k; // a cut wanted here, moved to the next game start
+    if (!starts.empty()) {
+      auto it = std::lower_bound(starts.begin(), starts.end(), x);
+      x = it == starts.end() ? m : *it;
+    }
+    if (x > c.back() && x < m) c.push_back(x);
+  }
+  c.push_back(m);
+  return c;
+}
 
 // Pass 1 of a shard: its m device-resident parents' child offsets (m + 1, relative) to the host.
 static int count_shard(Dev &d, const gn_board *d_par, size_t m, std::vector<uint64_t> &off) {
@@ -1019,7 +1107,7 @@ static int count_shard(Dev &d, const gn_board *d_par, size_t m, std::vector<uint
 // shard's base).
 static int expand_pipelined(gn_ctx *ctx, Dev &d, const gn_board *d_par, size_t m, int mode,
                             const std::vector<uint64_t> &off, const std::vector<size_t> &chunks, gn_eval *parent_out,
-                            uint16_t *child_moves, gn_eval *child_out) {
+                            uint16_t *child_moves, gn_child *child_out) {
   hipStream_t s = d.stream;
   size_t maxp = 1, maxc = 1;
   for (size_t c = 0; c + 1 < chunks.size(); ++c)
@@ -1028,12 +1116,20 @@ static int expand_pipelined(gn_ctx *ctx, Dev &d, const gn_board *d_par, size_t m
   for (int k = 0; k < 2; ++k) {
     HIP_TRY(d.po2[k].ensure(maxp));
     HIP_TRY(d.co2[k].ensure(maxc));
+    HIP_TRY(d.cc2[k].ensure(maxc));
     HIP_TRY(d.mv2[k].ensure(maxc));
   }
-  std::thread drain[2];
   int drc[2] = {GN_OK, GN_OK};
   std::string derr[2];
   double dms[2] = {0, 0};
+  std::thread drain[2];
+  struct Joiner { // joins the drain threads on every way out (an exception included), before
+    std::thread *t; // the state they write goes out of scope
+    ~Joiner() {
+      for (int i = 0; i < 2; ++i)
+        if (t[i].joinable()) t[i].join();
+    }
+  } joiner{drain};
   auto join = [&](int k) -> int {
     if (drain[k].joinable()) drain[k].join();
     d.t_download += dms[k], dms[k] = 0;
@@ -1058,6 +1154,8 @@ static int expand_pipelined(gn_ctx *ctx, Dev &d, const gn_board *d_par, size_t m
       rc = expand_evaluate(ctx, d, d_par + pa, mp, d.frontier[1].p, t, mode, d.po2[k].p, d.co2[k].p, s, nullptr);
     const Replies rp{d.co2[k].p, d.mv2[k].p};
     if (!rc) rc = resolve_scores(ctx, d, d_par + pa, mp, mode, d.po2[k].p, nullptr, s, 2, &rp);
+    if (!rc && launch_pack_children(d.co2[k].p, t, d.cc2[k].p, s) != hipSuccess)
+      rc = fail(GN_E_HIP, "child record packing failed");
     if (!rc) rc = check_plan(d, s); // synchronises the stream: chunk c is computed
     if (rc) break;
     d.t_compute += ms_since(t0);
@@ -1070,7 +1168,7 @@ static int expand_pipelined(gn_ctx *ctx, Dev &d, const gn_board *d_par, size_t m
       hipError_t e = hipSetDevice(d.id);
       if (e == hipSuccess) e = hipStreamWaitEvent(d.copy, d.cev[k], 0);
       if (e == hipSuccess && t)
-        e = hipMemcpyAsync(child_out + cb, d.co2[k].p, t * sizeof(gn_eval), hipMemcpyDeviceToHost, d.copy);
+        e = hipMemcpyAsync(child_out + cb, d.cc2[k].p, t * sizeof(gn_child), hipMemcpyDeviceToHost, d.copy);
       if (e == hipSuccess && t)
         e = hipMemcpyAsync(child_moves + cb, d.mv2[k].p, t * sizeof(uint16_t), hipMemcpyDeviceToHost, d.copy);
       if (e == hipSuccess && parent_out)
@@ -1092,7 +1190,7 @@ static int expand_pipelined(gn_ctx *ctx, Dev &d, const gn_board *d_par, size_t m
 // Host parent boards -> every legal child -> parent/child gn_eval (gn_expand_and_evaluate),
 // sharded over every device of the context (equal parent ranges).
 static int expand_boards_host(gn_ctx *ctx, const gn_board *boards, size_t n, int mode, gn_eval *parent_out,
-                              uint32_t *child_offsets, uint16_t *child_moves, gn_eval *child_out, size_t cap) {
+                              uint32_t *child_offsets, uint16_t *child_moves, gn_child *child_out, size_t cap) {
   if (!slot(ctx, 0)) return fail(GN_E_INVALID, "bad context");
   if (!n) {
     child_offsets[0] = 0;
@@ -1135,7 +1233,7 @@ static int expand_boards_host(gn_ctx *ctx, const gn_board *boards, size_t n, int
       const size_t m = hi - lo;
       std::vector<size_t> starts;
       for (size_t i = 81; i < m; i += 81) starts.push_back(i);
-      return expand_pipelined(ctx, d, d.par.p, m, mode, off[k], chunk_bounds(m, starts, chunk_target(m)),
+      return expand_pipelined(ctx, d, d.par.p, m, mode, off[k], chunk_plan(m, starts, ctx->chunk_parents),
                               parent_out ? parent_out + lo : nullptr, child_moves + base[k], child_out + base[k]);
     });
   } catch (const std::bad_alloc &) {
@@ -1264,7 +1362,7 @@ int gn_replay_game(const gn_game *game, gn_board *positions, uint8_t *skipped, u
 
 int gn_evaluate_games(gn_ctx *ctx, const gn_game *games, size_t n_games, int mode, int with_children,
                       uint32_t *position_offsets, int32_t *game_status, gn_eval *position_out, size_t position_cap,
-                      uint32_t *child_offsets, uint16_t *child_moves, gn_eval *child_out, size_t child_cap) {
+                      uint32_t *child_offsets, uint16_t *child_moves, gn_child *child_out, size_t child_cap) {
   if (!slot(ctx, 0)) return fail(GN_E_INVALID, "bad context");
   if (n_games && (!games || !position_offsets || !game_status)) return fail(GN_E_INVALID, "NULL argument");
   if (with_children && !child_offsets) return fail(GN_E_INVALID, "child_offsets is NULL");
@@ -1354,11 +1452,32 @@ int gn_evaluate_games(gn_ctx *ctx, const gn_game *games, size_t n_games, int mod
     position_offsets[n_games] = (uint32_t)total;
     if (total > position_cap) return fail(GN_E_CAPACITY, "%zu positions exceed capacity %zu", (size_t)total, position_cap);
     if (total && !position_out) return fail(GN_E_INVALID, "position_out is NULL");
-    std::vector<std::vector<uint32_t>> src(nd), where(nd); // device board index / output index per evaluated
-    std::vector<std::vector<size_t>> starts(nd);            // first evaluated position of each game
-    std::vector<size_t> eb(nd + 1, 0);                      // evaluated positions before device k
+    // The evaluated positions of each device.  Fast path (the common case): every game of the
+    // device replayed and none has a skipped position, so its positions are the replay's boards
+    // as they lie (rboards: game j's position p at moff[j] + j + p) and one contiguous run of
+    // position_out from p0[k]: the expansion reads rboards in place and writes the caller's
+    // arrays directly.  Otherwise the evaluated positions are gathered (src: board index,
+    // where: output index) into contiguous parents and their records scattered back.
+    std::vector<std::vector<uint32_t>> src(nd), where(nd);
+    std::vector<std::vector<size_t>> starts(nd); // first evaluated position of each game
+    std::vector<uint8_t> fast(nd, 0);
+    std::vector<size_t> mcount(nd, 0), p0(nd, 0);
     std::vector<uint8_t> skip;
     for (size_t k = 0; k < nd; ++k) {
+      bool f = true;
+      for (size_t j = 0; j < glist[k].size() && f; ++j) {
+        const size_t g = glist[k][j];
+        f = st[k][j] == 0;
+        for (size_t q = 0; q < games[g].n_skip && f; ++q)
+          f = !games[g].skip_positions || games[g].skip_positions[q] >= npos[g];
+      }
+      if (f) {
+        fast[k] = 1;
+        mcount[k] = glist[k].empty() ? 0 : (size_t)moff[k].back() + glist[k].size();
+        p0[k] = glist[k].empty() ? 0 : position_offsets[glist[k][0]];
+        for (size_t j = 0; j < glist[k].size(); ++j) starts[k].push_back((size_t)moff[k][j] + j);
+        continue;
+      }
       for (size_t j = 0; j < glist[k].size(); ++j) {
         const size_t g = glist[k][j];
         if (!npos[g]) continue;
@@ -1376,40 +1495,44 @@ int gn_evaluate_games(gn_ctx *ctx, const gn_game *games, size_t n_games, int mod
           }
         }
       }
-      eb[k + 1] = eb[k] + src[k].size();
+      mcount[k] = src[k].size();
     }
-    // phase B: the evaluated positions gathered into contiguous parents; evaluated (no children)
-    // or counted (pass 1 of the expansion)
+    // phase B: (slow path) the evaluated positions gathered into contiguous parents; evaluated
+    // (no children) or counted (pass 1 of the expansion)
     std::vector<std::vector<gn_eval>> res(nd);
     std::vector<std::vector<uint64_t>> off(nd);
     std::vector<size_t> db(nd + 1);
     for (size_t k = 0; k <= nd; ++k) db[k] = k; // one "item" per device: run_shards' shard k = device k
-    auto has = [&](size_t k) { return !src[k].empty(); };
+    auto has = [&](size_t k) { return mcount[k] > 0; };
+    auto parents_of = [&](size_t k) -> const gn_board * { return fast[k] ? ctx->devs[k]->rboards.p : ctx->devs[k]->par.p; };
+    auto records_of = [&](size_t k) -> gn_eval * { return fast[k] ? position_out + p0[k] : res[k].data(); };
     rc = run_shards(ctx, db, [&](size_t k, Dev &d, size_t, size_t) -> int {
       if (!has(k)) return GN_OK;
       HIP_TRY(hipSetDevice(d.id));
       SeqGuard sg(d, d.stream);
       HIP_TRY(sg.e);
-      const size_t m = src[k].size();
+      const size_t m = mcount[k];
       hipStream_t s = d.stream;
-      const auto t0 = Clock::now();
-      HIP_TRY(d.gidx.ensure(m));
-      HIP_TRY(d.par.ensure(m));
-      HIP_TRY(hipMemcpyAsync(d.gidx.p, src[k].data(), m * sizeof(uint32_t), hipMemcpyHostToDevice, s));
-      HIP_TRY(launch_gather_boards(d.rboards.p, d.gidx.p, m, d.par.p, s));
-      HIP_TRY(hipStreamSynchronize(s));
-      d.t_upload += ms_since(t0);
-      res[k].resize(m);
-      if (with_children) return count_shard(d, d.par.p, m, off[k]);
+      if (!fast[k]) {
+        const auto t0 = Clock::now();
+        HIP_TRY(d.gidx.ensure(m));
+        HIP_TRY(d.par.ensure(m));
+        HIP_TRY(hipMemcpyAsync(d.gidx.p, src[k].data(), m * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+        HIP_TRY(launch_gather_boards(d.rboards.p, d.gidx.p, m, d.par.p, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        d.t_upload += ms_since(t0);
+        res[k].resize(m);
+      }
+      if (with_children) return count_shard(d, parents_of(k), m, off[k]);
       const auto t1 = Clock::now();
       HIP_TRY(d.io_out.ensure(m));
-      int r = evaluate_on(ctx, d, d.par.p, m, mode, d.io_out.p, s, nullptr);
-      if (!r) r = resolve_scores(ctx, d, d.par.p, m, mode, d.io_out.p, nullptr, s);
+      int r = evaluate_on(ctx, d, parents_of(k), m, mode, d.io_out.p, s, nullptr);
+      if (!r) r = resolve_scores(ctx, d, parents_of(k), m, mode, d.io_out.p, nullptr, s);
       if (r) return r;
       HIP_TRY(hipStreamSynchronize(s));
       d.t_compute += ms_since(t1);
       const auto t2 = Clock::now();
-      HIP_TRY(hipMemcpy(res[k].data(), d.io_out.p, m * sizeof(gn_eval), hipMemcpyDeviceToHost));
+      HIP_TRY(hipMemcpy(records_of(k), d.io_out.p, m * sizeof(gn_eval), hipMemcpyDeviceToHost));
       d.t_download += ms_since(t2);
       return GN_OK;
     });
@@ -1419,15 +1542,24 @@ int gn_evaluate_games(gn_ctx *ctx, const gn_game *games, size_t n_games, int mod
       for (size_t k = 0; k < nd; ++k) cb[k + 1] = cb[k] + (has(k) ? off[k].back() : 0);
       const uint64_t ctot = cb[nd];
       if (ctot > 0xFFFFFFFFull) return fail(GN_E_CAPACITY, "children exceed 32-bit offsets");
-      // child offsets over all positions (skipped ones: no children)
-      for (size_t g = 0; g < n_games; ++g)
-        for (uint32_t p = 0; p < npos[g]; ++p) child_offsets[position_offsets[g] + p] = 0xFFFFFFFFu;
-      for (size_t k = 0; k < nd; ++k)
-        for (size_t e = 0; e < where[k].size(); ++e) child_offsets[where[k][e]] = (uint32_t)(cb[k] + off[k][e]);
-      uint32_t next = (uint32_t)ctot; // skipped positions take the next evaluated position's offset
-      for (size_t at = total; at-- > 0;) {
-        if (child_offsets[at] == 0xFFFFFFFFu) child_offsets[at] = next;
-        else next = child_offsets[at];
+      // child offsets over all positions (skipped ones: no children, the next position's offset)
+      const bool all_fast = std::all_of(fast.begin(), fast.end(), [](uint8_t f) { return f != 0; });
+      if (!all_fast)
+        for (size_t g = 0; g < n_games; ++g)
+          for (uint32_t p = 0; p < npos[g]; ++p) child_offsets[position_offsets[g] + p] = 0xFFFFFFFFu;
+      for (size_t k = 0; k < nd; ++k) {
+        if (!has(k)) continue;
+        if (fast[k])
+          for (size_t e = 0; e < mcount[k]; ++e) child_offsets[p0[k] + e] = (uint32_t)(cb[k] + off[k][e]);
+        else
+          for (size_t e = 0; e < where[k].size(); ++e) child_offsets[where[k][e]] = (uint32_t)(cb[k] + off[k][e]);
+      }
+      if (!all_fast) {
+        uint32_t next = (uint32_t)ctot;
+        for (size_t at = total; at-- > 0;) {
+          if (child_offsets[at] == 0xFFFFFFFFu) child_offsets[at] = next;
+          else next = child_offsets[at];
+        }
       }
       child_offsets[total] = (uint32_t)ctot;
       if (ctot > child_cap) return fail(GN_E_CAPACITY, "%zu children exceed capacity %zu", (size_t)ctot, child_cap);
@@ -1438,9 +1570,9 @@ int gn_evaluate_games(gn_ctx *ctx, const gn_game *games, size_t n_games, int mod
         HIP_TRY(hipSetDevice(d.id));
         SeqGuard sg(d, d.stream);
         HIP_TRY(sg.e);
-        const size_t m = src[k].size();
-        return expand_pipelined(ctx, d, d.par.p, m, mode, off[k], chunk_bounds(m, starts[k], chunk_target(m)),
-                                res[k].data(), child_moves + cb[k], child_out + cb[k]);
+        const size_t m = mcount[k];
+        return expand_pipelined(ctx, d, parents_of(k), m, mode, off[k], chunk_plan(m, starts[k], ctx->chunk_parents),
+                                records_of(k), child_moves + cb[k], child_out + cb[k]);
       });
       if (rc) return rc;
     }
@@ -1620,9 +1752,18 @@ int gn_set_eval_params(gn_ctx *ctx, const gn_eval_params *p) {
       p->wdl_material_anchor == 0)
     return fail(GN_E_INVALID, "zero divisor in eval params");
   if (p->wdl_material_min > p->wdl_material_max) return fail(GN_E_INVALID, "wdl material range is empty");
+  if ((int64_t)p->wdl_material_max - p->wdl_material_min > 4096) return fail(GN_E_INVALID, "wdl material range too wide");
   if (p->value_clamp < 0 || p->value_clamp >= VALUE_MATE_IN_MAX_PLY)
     return fail(GN_E_INVALID, "value_clamp must be in [0, %d) (static values stay below mate scores)",
                 (int)VALUE_MATE_IN_MAX_PLY);
+  // to_cp's a(material) >= 1 wherever it is evaluated (every clamped material value), so that
+  // |final_cp| <= 100 * value_clamp < 2^23 fits gn_child's 24-bit field (defaults: a ~ 370-400)
+  for (int mc = p->wdl_material_min; mc <= p->wdl_material_max; ++mc) {
+#pragma clang fp contract(off)
+    const double m = (double)mc / (double)p->wdl_material_anchor;
+    const double a = ((p->wdl_a[0] * m + p->wdl_a[1]) * m + p->wdl_a[2]) * m + p->wdl_a[3];
+    if (!(a >= 1.0)) return fail(GN_E_INVALID, "win-rate model a(material %d) = %g < 1", mc, a);
+  }
   ctx->P = *p;
   return GN_OK;
 }
@@ -1855,7 +1996,7 @@ int gn_evaluate_batch_mode(gn_ctx *ctx, const char *const *fens, size_t n, int m
     std::vector<gn_board> boards(n);
     int rc = gn_pack_fens(fens, n, boards.data(), nullptr);
     if (rc) return rc;
-    return evaluate_boards_host(ctx, boards.data(), n, mode, out);
+    return evaluate_coalesced(ctx, boards.data(), n, mode, out);
   } catch (const std::bad_alloc &) {
     return fail(GN_E_NOMEM, "host allocation failed");
   } catch (...) {
@@ -2114,7 +2255,8 @@ int gn_set_option(gn_ctx *ctx, int option, int64_t value) {
     ctx->swizzle = (int)(value & 7);
     return GN_OK;
   case GN_OPT_KING_SORT:
-    ctx->king_sort = value != 0;
+    if (value < 0 || value > 2) return fail(GN_E_INVALID, "king sort must be 0, 1 or 2");
+    ctx->king_sort = (int)value;
     return GN_OK;
   case GN_OPT_KING_CACHE:
     ctx->king_cache = value != 0;
@@ -2122,6 +2264,13 @@ int gn_set_option(gn_ctx *ctx, int option, int64_t value) {
   case GN_OPT_CHAIN:
     if (value < -(1 << 20) || value > (1 << 20)) return fail(GN_E_INVALID, "chain length out of range");
     ctx->chain = (int)value;
+    return GN_OK;
+  case GN_OPT_CHUNK_PARENTS:
+    if (value < 0) return fail(GN_E_INVALID, "chunk size < 0");
+    ctx->chunk_parents = value;
+    return GN_OK;
+  case GN_OPT_COALESCE:
+    ctx->coalesce = value != 0;
     return GN_OK;
   default:
     return fail(GN_E_INVALID, "unknown option %d", option);
@@ -2146,6 +2295,19 @@ int gn_get_option(const gn_ctx *ctx, int option, int64_t *value) {
   case GN_OPT_CHAIN:
     *value = ctx->chain;
     return GN_OK;
+  case GN_OPT_CHUNK_PARENTS:
+    *value = ctx->chunk_parents;
+    return GN_OK;
+  case GN_OPT_COALESCE:
+    *value = ctx->coalesce;
+    return GN_OK;
+  case GN_STAT_BATCH_LAUNCHES:
+  case GN_STAT_BATCH_CALLS: { // cumulative since load (the coalescer's counters)
+    auto &C = const_cast<gn_ctx *>(ctx)->co;
+    std::lock_guard<std::mutex> lk(C.mu);
+    *value = (int64_t)(option == GN_STAT_BATCH_LAUNCHES ? C.launches : C.calls);
+    return GN_OK;
+  }
   case GN_STAT_PLAN_NS:
   case GN_STAT_STREAM_NS: { // read-only: the last gn_time_expand_device's planned kernels (max over devices)
     float m = 0;
@@ -2189,28 +2351,13 @@ int gn_get_option(const gn_ctx *ctx, int option, int64_t *value) {
     *value = sum;
     return GN_OK;
   }
-  case GN_STAT_CHAIN_FALLBACKS: { // read-only: blocks of the last chained expansion per device, summed
-    int64_t sum = 0;
-    for (auto &dp : ctx->devs) {
-      Dev &d = *dp;
-      std::lock_guard<std::mutex> lk(d.mu);
-      if (!d.tickets.p) continue;
-      HIP_TRY(hipSetDevice(d.id));
-      if (d.done_on) HIP_TRY(hipEventSynchronize(d.done));
-      uint32_t f = 0;
-      HIP_TRY(hipMemcpy(&f, d.tickets.p + CARRY_SLOTS, sizeof(f), hipMemcpyDeviceToHost));
-      sum += f;
-    }
-    *value = sum;
-    return GN_OK;
-  }
   default:
     return fail(GN_E_INVALID, "unknown option %d", option);
   }
 }
 
 int gn_expand_and_evaluate(gn_ctx *ctx, const char *const *parent_fens, size_t n, int mode, gn_eval *parent_out,
-                           uint32_t *child_offsets, uint16_t *child_moves, gn_eval *child_out, size_t cap) {
+                           uint32_t *child_offsets, uint16_t *child_moves, gn_child *child_out, size_t cap) {
   if (!slot(ctx, 0)) return fail(GN_E_INVALID, "bad context");
   if (n && (!parent_fens || !child_offsets)) return fail(GN_E_INVALID, "NULL argument");
   if (!n) {

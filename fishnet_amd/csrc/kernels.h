@@ -49,22 +49,13 @@ hipError_t block_order(const gn_board *parents, size_t n, uint32_t K, uint32_t n
                        uint16_t *keys_out, uint32_t *order, void *&temp, size_t &temp_bytes, hipStream_t s);
 hipError_t king_sort(const gn_board *boards, size_t n, uint64_t *keys, uint32_t *idx, uint64_t *keys_out,
                      uint32_t *perm, bool placement, void *&temp, size_t &temp_bytes, hipStream_t s);
-// Incremental evaluation of parents + all their children (children of parent
-// p are [offsets[p], offsets[p+1]) with moves[]); need_* select what this net
-// evaluates (nullptr: all).
+// Incremental evaluation of parents + all their children with the small net (L1 = 128;
+// expand_eval_kernel, one workgroup per parent; children of parent p are
+// [offsets[p], offsets[p+1]) with deltas[]); need_* select what this net evaluates
+// (nullptr: all).  The big nets always run planned (launch_plan_stream).
 hipError_t launch_expand_net(const NetDevice &net, const gn_board *parents, size_t n, const uint64_t *offsets,
                              const gn_board *children, const ChildDelta *deltas, const uint8_t *need_parent,
-                             const uint8_t *need_child, int2 *out_parent, int2 *out_child, int swz,
-                             const uint8_t *next_slot, uint32_t *tickets, int chain_k, uint32_t *ksnap,
-                             unsigned long long *rows_out, hipStream_t s);
-// Chained walk (big nets with carry rows): one workgroup per block of chain_k
-// consecutive parents; parent p + 1 starts from child next_slot[p] of parent p when
-// that child has its placement.  tickets: CARRY_SLOTS words (zeroed by the launcher).
-// ksnap (optional, chained walk only): CARRY_SLOTS x 128 x 32 B of king-cache
-// placement snapshots; king-move refreshes then start from the block's cached
-// accumulator for (perspective, king square) when the placement difference is shorter.
-// rows_out (optional, big-net row stream only): += FT rows gathered (bias, carry and
-// king-cache rows included).
+                             const uint8_t *need_child, int2 *out_parent, int2 *out_child, int swz, hipStream_t s);
 // Planned expansion (stream.hip): one descriptor per tile of <= 16 consecutive slots of a
 // block (slots = [parent, its children, next parent, ...] of the block's consecutive
 // parents) with <= 2 buckets among its evaluated slots.  e_end: list 0 / list 1 entries
@@ -166,6 +157,8 @@ hipError_t launch_replay_games(const gn_board *roots, size_t ng, const uint64_t 
                                const Tables *tables, gn_board *boards, uint16_t *smoves, int32_t *status, hipStream_t s);
 // dst[i] = src[idx[i]]
 hipError_t launch_gather_boards(const gn_board *src, const uint32_t *idx, size_t n, gn_board *dst, hipStream_t s);
+// gn_eval -> gn_child (ABI v4 child records for the host-buffer calls)
+hipError_t launch_pack_children(const gn_eval *in, size_t n, gn_child *out, hipStream_t s);
 // narrowing copy of offsets for the C-ABI
 hipError_t launch_offsets_u32(const uint64_t *in, size_t n, uint32_t *out, hipStream_t s);
 // exclusive scan of n + 1 counts (counts[n] must be 0); temp grows on demand

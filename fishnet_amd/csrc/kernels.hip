@@ -17,32 +17,6 @@
 #include "device_util.h"
 #include "kernels.h"
 
-// GN_PHASE_TIMING builds (diagnostics only): thread 0 of every expand_eval
-// workgroup adds the s_memtime cycles of each phase into gn_phase_cycles.
-#ifdef GN_PHASE_TIMING
-__device__ unsigned long long gn_phase_cycles[64][8];
-#define GN_STAMP_INIT()                                                          \
-  unsigned long long gn_t_ = __builtin_amdgcn_s_memtime(), gn_acc_[6] = {0, 0, 0, 0, 0, 0}
-#define GN_STAMP(k)                                                              \
-  do {                                                                           \
-    const unsigned long long t_ = __builtin_amdgcn_s_memtime();                  \
-    gn_acc_[k] += t_ - gn_t_;                                                    \
-    gn_t_ = t_;                                                                  \
-  } while (0)
-#define GN_STAMP_FLUSH()                                                         \
-  do {                                                                           \
-    if (threadIdx.x == 0)                                                        \
-      for (int k_ = 0; k_ < 6; ++k_) atomicAdd(&gn_phase_cycles[blockIdx.x & 63][k_], gn_acc_[k_]); \
-  } while (0)
-#else
-#define GN_STAMP_INIT() (void)0
-#define GN_STAMP(k) (void)0
-#define GN_STAMP_FLUSH() (void)0
-#endif
-
-#ifndef GN_EXPAND_WPE
-#define GN_EXPAND_WPE 5
-#endif
 
 namespace gn {
 
@@ -431,62 +405,6 @@ __device__ __forceinline__ void run_rows(const uint8_t *__restrict__ ft, uint32_
   }
 }
 
-// run_rows for wave-uniform descriptors (PAR == 1 perspective groups of whole
-// waves): entries 0..3 arrive as scalars (r01 = rows 0 | 1 << 16, r23 = rows
-// 2 | 3 << 16), later entries (refreshes only) come from the LDS row list rr by
-// one lane-indexed read, so no row offset waits on an LDS round trip.
-template <int L1>
-__device__ __forceinline__ void run_rows_u(const uint8_t *__restrict__ ft, uint32_t j16, const uint16_t *rr,
-                                           uint32_t r01, uint32_t r23, int k, int ns, int n, bool psl, uint32_t psb,
-                                           bool save, ushort8 &base_lo, ushort8 &base_hi, ushort8 &lo, ushort8 &hi,
-                                           uint32_t &ps, int lane) {
-  constexpr uint32_t RS = ft_row_stride(L1);
-  const uint32_t rl = n > 4 && lane < n ? rr[lane] : 0u;
-  auto off = [&](int e) -> uint32_t {
-    uint32_t v = e == 0 ? (r01 & 0xFFFF) : e == 1 ? (r01 >> 16) : e == 2 ? (r23 & 0xFFFF) : e == 3 ? (r23 >> 16) : 0u;
-    if (e >= 4) v = (uint32_t)__builtin_amdgcn_readlane((int)rl, e);
-    return (uint32_t)__builtin_amdgcn_readfirstlane((int)ft_row(v)) * RS;
-  };
-#pragma unroll 1
-  for (; k < n; k += 4) {
-    ushort8 a0, a1, a2, a3, b0, b1, b2, b3;
-    uint32_t p0 = 0, p1 = 0, p2 = 0, p3 = 0;
-    const uint32_t o0 = off(k);
-    a0 = ldft(ft, j16 + o0), b0 = ldft(ft, j16 + o0 + L1);
-    if (psl) p0 = ldpd(ft, o0 + psb);
-    if (k + 1 < n) {
-      const uint32_t o1 = off(k + 1);
-      a1 = ldft(ft, j16 + o1), b1 = ldft(ft, j16 + o1 + L1);
-      if (psl) p1 = ldpd(ft, o1 + psb);
-    }
-    if (k + 2 < n) {
-      const uint32_t o2 = off(k + 2);
-      a2 = ldft(ft, j16 + o2), b2 = ldft(ft, j16 + o2 + L1);
-      if (psl) p2 = ldpd(ft, o2 + psb);
-    }
-    if (k + 3 < n) {
-      const uint32_t o3 = off(k + 3);
-      a3 = ldft(ft, j16 + o3), b3 = ldft(ft, j16 + o3 + L1);
-      if (psl) p3 = ldpd(ft, o3 + psb);
-    }
-    if (save && k == 0) base_lo = lo - a0, base_hi = hi - b0;
-    if (k < ns) lo -= a0, hi -= b0, ps -= p0;
-    else lo += a0, hi += b0, ps += p0;
-    if (k + 1 < n) {
-      if (k + 1 < ns) lo -= a1, hi -= b1, ps -= p1;
-      else lo += a1, hi += b1, ps += p1;
-    }
-    if (k + 2 < n) {
-      if (k + 2 < ns) lo -= a2, hi -= b2, ps -= p2;
-      else lo += a2, hi += b2, ps += p2;
-    }
-    if (k + 3 < n) {
-      if (k + 3 < ns) lo -= a3, hi -= b3, ps -= p3;
-      else lo += a3, hi += b3, ps += p3;
-    }
-  }
-}
-
 // Incremental evaluation of every legal child of a parent (SURVEY.md §8a row
 // a14, "children are derived from the parent accumulator by incremental
 // add/sub deltas").  One workgroup per parent (or, persistent, a strided walk
@@ -505,12 +423,12 @@ __device__ __forceinline__ void run_rows_u(const uint8_t *__restrict__ ft, uint3
 // limit) are resident per CU (tools/occupancy_probe.hip: 6-wave workgroups above
 // 128 VGPRs run one per CU).
 template <int L1, int PAR>
-__global__ void __launch_bounds__(2 * (L1 / 16) * PAR) __attribute__((amdgpu_waves_per_eu(PAR == 1 ? GN_EXPAND_WPE : 4)))
+__global__ void __launch_bounds__(2 * (L1 / 16) * PAR) __attribute__((amdgpu_waves_per_eu(4)))
     expand_eval_kernel(NetDevice net, const gn_board *__restrict__ parents, const uint64_t *__restrict__ offsets,
                        const gn_board *__restrict__ children, const ChildDelta *__restrict__ deltas,
                        const uint8_t *__restrict__ need_parent,
                        const uint8_t *__restrict__ need_child, int2 *__restrict__ out_parent,
-                       int2 *__restrict__ out_child, size_t n_parents, int swz, int ablate) {
+                       int2 *__restrict__ out_child, size_t n_parents, int swz) {
   constexpr int G = L1 / 16;
   constexpr int NT = 2 * G * PAR;
   constexpr int NW = NT / 64;
@@ -528,9 +446,6 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR) __attribute__((amdgpu_wav
   __shared__ uint16_t prow[2][32];
   __shared__ int32_t psq[TILE][2];
   __shared__ uint8_t nsub[TILE][2], ncnt[TILE][2], usep[TILE][2], sstm[TILE], bkt[TILE], valid[TILE];
-  // packed slot descriptor per perspective (U path): [0] valid [1] from parent
-  // [2] side (0: h is the side to move) [5:3] bucket [7:6] nsub [13:8] rows
-  __shared__ uint32_t sdesc[TILE][2];
   __shared__ int pcount, njobs;
   __shared__ uint8_t jobs[TILE * 2];
   __shared__ uint32_t bmask;
@@ -551,7 +466,6 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR) __attribute__((amdgpu_wav
   const size_t vgrid = swz ? 8 * ((n_parents + 7) / 8) : n_parents;
   for (size_t v = blockIdx.x; v < vgrid; v += gridDim.x) {
     __syncthreads(); // LDS of the previous parent is dead
-    GN_STAMP_INIT();
     // XCD-aware parent order: each XCD takes a contiguous range of parents, so
     // the parents of one game (same kings, mostly the same pieces) and their
     // children share that XCD's L2
@@ -581,13 +495,12 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR) __attribute__((amdgpu_wav
     }
     if (!__syncthreads_or(want)) continue;
     if (!pcount) continue;
-    GN_STAMP(0);
 
     // parent accumulators: bias + all rows (group q == 0), kept for every child; the
     // parent's 8 PSQT sums go to LDS (children read one bucket each)
     ushort8 pacc_lo = *reinterpret_cast<const ushort8 *>(net.bias + 8 * j);
     ushort8 pacc_hi = *reinterpret_cast<const ushort8 *>(net.bias + L1 / 2 + 8 * j);
-    if (q == 0 && !(ablate & 1)) {
+    if (q == 0) {
       const uint32_t pso = 2 * L1 + 16 * (j & 1); // this thread's 4 PSQT buckets (j < 2 only)
       int4v pps = {0, 0, 0, 0};
       const int cnt = pcount;
@@ -625,7 +538,6 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR) __attribute__((amdgpu_wav
 
     ushort8 base_lo = pacc_lo, base_hi = pacc_hi; // parent minus base_key's row (sibling cache)
     int base_key = -1;
-    GN_STAMP(1);
 
 #pragma unroll 1
     for (int t0 = 0; t0 < total; t0 += TILE) {
@@ -683,15 +595,8 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR) __attribute__((amdgpu_wav
         sstm[tid] = (uint8_t)stm;
         bkt[tid] = (uint8_t)((cnt - 1) / 4);
         if (vld) atomicOr(&bmask, 1u << ((cnt - 1) / 4));
-#pragma unroll
-        for (int hh = 0; hh < 2; ++hh)
-          sdesc[tid][hh] = vld ? 1u | (uint32_t)usep[tid][hh] << 1 | (uint32_t)(hh != stm) << 2 |
-                                     (uint32_t)((cnt - 1) / 4) << 3 | (uint32_t)nsub[tid][hh] << 6 |
-                                     (uint32_t)ncnt[tid][hh] << 8
-                               : 0u;
       }
       __syncthreads();
-      GN_STAMP(2);
       {
         const int lane = tid & 63, wave = tid >> 6, nj = njobs;
         for (int jb = wave; jb < nj; jb += NW) {
@@ -702,54 +607,9 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR) __attribute__((amdgpu_wav
         }
       }
       __syncthreads();
-      GN_STAMP(3);
 
       // ---- phase 1: accumulators + transform.  PSQT: thread j == 0 of each
       // perspective sums the slot's own bucket (one dword per row).
-      if constexpr (U) {
-        // descriptors and first rows of all 16 slots in one LDS read per lane, then
-        // scalar per slot (readlane)
-        const int lane = tl & 63, hu = __builtin_amdgcn_readfirstlane(ht);
-        uint32_t dv = 0, rv0 = 0, rv1 = 0;
-        if (lane < TILE) {
-          dv = sdesc[lane][hu];
-          const uint2 rw = *reinterpret_cast<const uint2 *>(rows[lane][hu]);
-          rv0 = rw.x, rv1 = rw.y;
-        }
-#pragma unroll 1
-        for (int sl = 0; sl < TILE; ++sl) {
-          const uint32_t d = (uint32_t)__builtin_amdgcn_readlane((int)dv, sl);
-          if (!(d & 1)) continue;
-          const bool fromp = (d >> 1) & 1;
-          const int side = (d >> 2) & 1, b = (d >> 3) & 7, ns = (d >> 6) & 3, n = (d >> 8) & 63;
-          const uint32_t r01 = (uint32_t)__builtin_amdgcn_readlane((int)rv0, sl);
-          const uint32_t r23 = (uint32_t)__builtin_amdgcn_readlane((int)rv1, sl);
-          const uint32_t psb = 2 * L1 + 4 * b;
-          ushort8 lo, hi;
-          uint32_t ps = 0;
-          int k = 0;
-          bool save = false;
-          if (!fromp) {
-            lo = *reinterpret_cast<const ushort8 *>(net.bias + 8 * jt);
-            hi = *reinterpret_cast<const ushort8 *>(net.bias + L1 / 2 + 8 * jt);
-          } else {
-            ps = (uint32_t)pps_lds[hu][b];
-            if (n > 0 && (int)(r01 & 0xFFFF) == base_key) {
-              lo = base_lo, hi = base_hi, k = 1;
-              if (jt == 0) ps -= ldpd(net.ft, ft_row(r01 & 0xFFFF) * RS + psb);
-            } else {
-              lo = pacc_lo, hi = pacc_hi, save = n > 0;
-            }
-          }
-          if (!(ablate & 2)) {
-            run_rows_u<L1>(net.ft, 16 * jt, rows[sl][hu], r01, r23, k, ns, n, jt == 0, psb, save, base_lo, base_hi,
-                           lo, hi, ps, lane);
-            if (save) base_key = (int)(r01 & 0xFFFF);
-          }
-          *reinterpret_cast<uint2 *>(xt + sl * XS + side * (L1 / 2) + 8 * jt) = transform8(lo, hi);
-          if (jt == 0) psq[sl][side] = (int32_t)ps;
-        }
-      } else {
 #pragma unroll 1
       for (int r = 0; r < TILE / PAR; ++r) {
         const int sl = r * PAR + qt;
@@ -773,606 +633,22 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR) __attribute__((amdgpu_wav
             lo = pacc_lo, hi = pacc_hi, save = n > 0;
           }
         }
-        if (!(ablate & 2)) {
-          run_rows<L1, U>(net.ft, 16 * jt, rr, k, ns, n, jt == 0, 2 * L1 + 4 * b, save, base_lo, base_hi, lo, hi, ps);
-          if (save) base_key = uni<U>(rr[0]);
-        }
+        run_rows<L1, U>(net.ft, 16 * jt, rr, k, ns, n, jt == 0, 2 * L1 + 4 * b, save, base_lo, base_hi, lo, hi, ps);
+        if (save) base_key = uni<U>(rr[0]);
         const int side = uni<U>(ht == sstm[sl] ? 0 : 1);
         *reinterpret_cast<uint2 *>(xt + sl * XS + side * (L1 / 2) + 8 * jt) = transform8(lo, hi);
         if (jt == 0) psq[sl][side] = (int32_t)ps;
       }
-      }
       __syncthreads();
-      GN_STAMP(4);
 
       // ---- phase 2: layer stack
-      if (!(ablate & 4)) {
-        layer_stack_tile<L1, NW>(net, xt, scratch, psq, tl, bmask, [&](int pos, int bb) {
-          return t0 + pos < total && valid[pos] && bkt[pos] == bb;
-        }, [&](int pos, int2 val) {
-          if (t0 + pos == 0) out_parent[p] = val;
-          else out_child[off + t0 + pos - 1] = val;
-        });
-      }
-      GN_STAMP(5);
+      layer_stack_tile<L1, NW>(net, xt, scratch, psq, tl, bmask, [&](int pos, int bb) {
+        return t0 + pos < total && valid[pos] && bkt[pos] == bb;
+      }, [&](int pos, int2 val) {
+        if (t0 + pos == 0) out_parent[p] = val;
+        else out_child[off + t0 + pos - 1] = val;
+      });
     }
-    GN_STAMP_FLUSH();
-  }
-}
-
-// ------------------------------------------------------- expand_stream --
-// expand_eval for the big nets with the gather as ONE row stream per perspective
-// list and tile.  The slot programs of a tile (parent refresh, king-move refreshes,
-// child deltas) are flattened into lists of row entries in LDS; each wave walks its
-// list with a 4-deep register ring, so up to 4 rows stay in flight across slot
-// boundaries instead of one dependent round trip per slot.  A refresh is the bias
-// row (FT_BIAS_ROW) + the feature rows.  PSQT is not in the stream: the waves that
-// are idle while wave 0 builds the lists sum it lane-parallel (one round trip).
-// Entry (u32): [18:0] row (FT rows, then the carry and king-cache rows), [19]
-// subtract, [21:20] init before this entry (0 none, 1 zero, 2 parent - row, saved
-// as the sibling base, 3 sibling base), [22] last entry of its slot, [26:23] slot,
-// [27] side (0: perspective to move), [28] entry of the parent slot, [29] store the
-// slot's accumulator as the next parent's (chained walk), [30] its absolute
-// perspective, [31] store it to the slot's king-cache row (kcrow in LDS).
-namespace es {
-constexpr uint32_t ROW = (1u << 19) - 1, SUB = 1u << 19, I_ZERO = 1u << 20, I_PACC = 2u << 20, I_BASE = 3u << 20,
-                   INIT = 3u << 20, LAST = 1u << 22, SLOT_SH = 23, SIDE_SH = 27, PAR_E = 1u << 28, NXT = 1u << 29,
-                   NXT_SH = 30, KST = 1u << 31;
-__device__ __forceinline__ uint32_t tmpl(int slot, int side) {
-  return (uint32_t)slot << SLOT_SH | (uint32_t)side << SIDE_SH;
-}
-} // namespace es
-
-template <int L1>
-__global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_EXPAND_WPE)))
-    expand_stream_kernel(NetDevice net, const gn_board *__restrict__ parents, const uint64_t *__restrict__ offsets,
-                         const ChildDelta *__restrict__ deltas, const uint8_t *__restrict__ need_parent,
-                         const uint8_t *__restrict__ need_child, int2 *__restrict__ out_parent,
-                         int2 *__restrict__ out_child, size_t n_parents, int swz, int ablate,
-                         const uint8_t *__restrict__ next_slot, uint32_t *__restrict__ tickets, int chain_k,
-                         uint32_t *__restrict__ ksnap, unsigned long long *__restrict__ rows_out) {
-  using namespace es;
-  constexpr int G = L1 / 16; // threads per perspective (whole waves)
-  constexpr int NT = 2 * G;
-  constexpr int NW = NT / 64;
-  constexpr int TILE = 16;
-  constexpr int XS = L1 + 16;
-  constexpr uint32_t RS = ft_row_stride(L1);
-  constexpr int CAP = 256;         // row entries per list and tile
-  constexpr int FILL = CAP - 8;    // content limit: padding to 4 + 4 run-ahead entries
-  constexpr int NLS = NW >= 4 ? 2 : 1; // layer-stack waves: the last NLS waves
-  constexpr int NPJ = NW >= 4 ? NW - 1 - NLS : NW - 1; // PSQT refresh-job waves: 1 .. NPJ
-  constexpr int CDL = 48;
-  static_assert(G % 64 == 0 && NW >= 2, "perspective groups must be whole waves");
-  __shared__ __attribute__((aligned(16))) uint8_t xt[TILE * XS];
-  __shared__ __attribute__((aligned(16))) uint32_t ent[2][CAP]; // the row-entry lists
-  __shared__ __attribute__((aligned(16))) uint8_t ls_in1[NLS][TILE][32]; // layer-stack waves' scratch
-  __shared__ int32_t ls_fwd[NLS][TILE];
-  __shared__ uint16_t prow[2][32];
-  __shared__ int32_t psa[TILE][2];  // PSQT partial sums by absolute perspective
-  __shared__ int32_t psqf[2][TILE][2]; // final PSQT accumulators by side, per tile parity
-  __shared__ int32_t pps[2][2];     // parent PSQT per perspective at buckets bp, b2
-  __shared__ uint8_t tmeta[2][TILE]; // per tile parity: valid | bucket << 1 (read by the layer stack)
-  __shared__ uint8_t sstm[TILE], pinit[TILE][2];
-  __shared__ uint32_t cdl[CDL][5];
-  __shared__ gn_board pbd;
-  __shared__ int pcount;
-  __shared__ uint32_t tctl[4]; // slots in this tile, entries of list 0 / 1, carry/king-cache stores
-  __shared__ uint32_t bmask;
-
-  const int tid = threadIdx.x;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const __amdgpu_buffer_rsrc_t ftr =
-      __builtin_amdgcn_make_buffer_rsrc(
-          (void *)net.ft, 0, (int)(((size_t)FT_ROWS + 4 * (size_t)net.carry_slots + 128 * (size_t)net.kc_slots) * RS),
-          0x00020000);
-  // Chained walk: a workgroup takes a block of chain_k consecutive parents.  When parent
-  // p + 1 is a child of parent p (next_slot[p], a game's next position), that child's
-  // accumulators are stored to this workgroup's carry rows (4: parity of p x
-  // perspective, FT rows CARRY_ROW0 + 4 * slot ..) and parent p + 1 starts from them
-  // instead of a bias + P-row refresh.  slot = dispatch index mod CARRY_SLOTS; a
-  // workgroup first waits for the one CARRY_SLOTS dispatches before it to release the
-  // slot (dispatched earlier, so resident or done: the wait always ends).
-  // (32-bit parent indices: the launcher rejects n_parents >= 2^31)
-  const uint32_t np = (uint32_t)n_parents;
-  const uint32_t K = chain_k > 1 && tickets && next_slot && net.carry_slots ? (uint32_t)chain_k : 1;
-  const bool kc = K > 1 && ksnap && net.kc_slots; // king cache (Finny-table analog) for king-move refreshes
-  const uint32_t nblk = (np + K - 1) / K;
-  const uint32_t vgrid = swz ? 8 * ((nblk + 7) / 8) : nblk;
-  int tpar = 0; // tile parity: the layer stack of tile k runs beside phase 0 of tile k + 1
-  // (no barrier at the top: the previous parent's last stream barrier already ordered
-  // every use of the LDS written below)
-  for (uint32_t v = blockIdx.x; v < vgrid; v += gridDim.x) {
-   uint32_t blk = v;
-   if (swz) {
-     const uint32_t b8 = (nblk + 7) / 8;
-     blk = (v & 7) * b8 + (v >> 3);
-     if (blk >= nblk) continue;
-   }
-   const uint32_t pend = blk * K + K < np ? blk * K + K : np;
-   const uint32_t cslot = v % CARRY_SLOTS;
-   // Slot ownership: tickets[cslot] counts the workgroups w = cslot (mod CARRY_SLOTS) that
-   // are done with the slot (used it or not); this one may use it once all v / CARRY_SLOTS
-   // earlier ones are.  The wait is bounded: on timeout the block runs without carry rows
-   // and king cache (identical results, more rows), still counts itself done at the end,
-   // and adds 1 to tickets[CARRY_SLOTS] (the fallback count).
-   bool own = false;
-   if (K > 1) {
-     __shared__ int sown;
-     if (tid == 0) {
-       int it = 0;
-       // relaxed: the slot's rows are only ever used on this XCD (v = cslot (mod 8)), whose L2 is
-       // coherent for them; an agent-scope acquire / release would invalidate / write back the
-       // whole L2 on every block (buffer_inv sc1 / buffer_wbl2 sc1)
-       while (__hip_atomic_load(tickets + cslot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < v / CARRY_SLOTS &&
-              ++it < 20000)
-         __builtin_amdgcn_s_sleep(8);
-       sown = it < 20000;
-       if (!sown) atomicAdd(tickets + CARRY_SLOTS, 1u);
-     }
-     __syncthreads();
-     own = sown;
-     // King cache (per block: written and read by this workgroup only): one accumulator
-     // row + one placement snapshot per (perspective, king square); empty at block start.
-     if (kc && own) {
-       for (int i = tid; i < 256; i += NT)
-         *reinterpret_cast<uint4 *>(ksnap + (size_t)cslot * 1024 + 4 * i) = make_uint4(0, 0, 0, 0);
-       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-     }
-   }
-   const bool kcb = kc && own; // this block's king cache
-   int carry_ok = 0; // the previous parent stored its next-parent accumulators
-   for (uint32_t p = blk * K; p < pend; ++p) {
-    GN_STAMP_INIT();
-    const int have = carry_ok;
-    carry_ok = 0;
-    const uint64_t off = offsets[p];
-    const int total = 1 + (int)(offsets[p + 1] - off);
-
-    // ---- pre-phase: parent rows + board (wave 0), first CDL deltas, any slot needed?
-    // (per-lane values are re-derived in every phase from an opaque copy of the thread
-    // id, so that nothing lane-dependent is hoisted and held across the kernel)
-    int tp = tid;
-    asm volatile("" : "+v"(tp));
-    if (tp >= 64 && tp - 64 < (total - 1 < CDL ? total - 1 : CDL)) {
-      const uint32_t *src = reinterpret_cast<const uint32_t *>(deltas + off + (tp - 64));
-#pragma unroll
-      for (int w = 0; w < 5; ++w) cdl[tp - 64][w] = src[w];
-    }
-    int want = 0;
-    for (int qq = tp; qq < total; qq += NT)
-      want |= qq == 0 ? (need_parent ? need_parent[p] : 1) : (need_child ? need_child[off + qq - 1] : 1);
-    if (wave == 0) {
-      const gn_board pb = parents[p];
-      const int c = wave_features(pb, prow[0], prow[1], tp & 63);
-      if (tp == 0) pcount = c, pbd = pb;
-    }
-    if (!__syncthreads_or(want)) continue;
-    if (!pcount) continue;
-    GN_STAMP(0);
-    // slot of the child that is the next parent (-1: none)
-    int nxq = -1;
-    if (own && p + 1 < pend) {
-      const int ns = next_slot[p];
-      if (ns != 255 && ns < total - 1 && (!need_child || need_child[off + ns])) nxq = ns + 1;
-    }
-    carry_ok = nxq > 0;
-    // carry rows of this parent: load (written by the previous parent) / store
-    const uint32_t cb = (uint32_t)CARRY_ROW0 + 4 * (v % CARRY_SLOTS), st2 = cb + (p & 1) * 2, ld2 = cb + (~p & 1) * 2;
-
-    // per-thread state across the tiles of this parent
-    const int hu = __builtin_amdgcn_readfirstlane((tid / G) & 1);
-    const int P = pcount, bp = (P - 1) / 4, b2 = P >= 2 ? (P - 2) / 4 : bp;
-    ushort8 pacc_lo = {}, pacc_hi = {}, base_lo = {}, base_hi = {};
-    int ckey0 = -1, ckey1 = -1; // sibling-cache keys carried across tiles (wave 0)
-
-#pragma unroll 1
-    for (int t0 = 0; t0 < total;) {
-      int lane = tid;
-      asm volatile("" : "+v"(lane));
-      lane &= 63;
-      // slot descriptor of lane & 15 (both the list builder and the PSQT waves)
-      auto desc = [&](int sl, int &vld, int &stm, int &cnt, int &kinds, int &n0, int &n1, int &s0, int &s1,
-                      uint32_t &w0, uint32_t &w1, uint32_t &w2, uint32_t &w3) {
-        const int qq = t0 + sl;
-        vld = 0, stm = 0, cnt = 1, kinds = 0, n0 = n1 = s0 = s1 = 0, w0 = w1 = w2 = w3 = 0;
-        if (sl >= TILE || qq >= total) return;
-        if (qq == 0) {
-          vld = need_parent ? need_parent[p] : 1;
-          stm = pbd.stm_ep >> 7, cnt = P, kinds = 3 | 3 << 2, n0 = n1 = have ? 1 : P + 1;
-        } else if ((vld = need_child ? need_child[off + qq - 1] : 1)) {
-          uint32_t meta;
-          if (qq - 1 < CDL) {
-            w0 = cdl[qq - 1][0], w1 = cdl[qq - 1][1], w2 = cdl[qq - 1][2], w3 = cdl[qq - 1][3];
-            meta = cdl[qq - 1][4];
-          } else {
-            const uint32_t *src = reinterpret_cast<const uint32_t *>(deltas + off + qq - 1);
-            w0 = src[0], w1 = src[1], w2 = src[2], w3 = src[3], meta = src[4];
-          }
-          stm = (meta >> 10) & 1;
-          cnt = (meta >> 14) & 63;
-          if (meta & (1u << 8)) kinds |= 2, n0 = cnt + 1;
-          else kinds |= 1, s0 = meta & 3, n0 = s0 + ((meta >> 2) & 3);
-          if (meta & (1u << 9)) kinds |= 2 << 2, n1 = cnt + 1;
-          else kinds |= 1 << 2, s1 = (meta >> 4) & 3, n1 = s1 + ((meta >> 6) & 3);
-        }
-      };
-
-      // ---- phase 0.  Wave 0 (lane = slot): descriptors -> sibling hits -> entry counts ->
-      // prefix sums -> tile cut -> entries.  The other waves: PSQT sums of the same
-      // slots (deltas lane-parallel, refreshes wave-parallel), one round trip.
-      if (wave == 0) {
-        int vld, stm, cnt, kinds, n0, n1, s0, s1;
-        uint32_t w0, w1, w2, w3;
-        desc(lane, vld, stm, cnt, kinds, n0, n1, s0, s1, w0, w1, w2, w3);
-        const bool inb = lane < TILE && t0 + lane < total;
-        const int key0 = (kinds & 3) == 1 ? (int)(w0 & 0xFFFF) : -1;
-        const int key1 = (kinds >> 2) == 1 ? (int)(w2 & 0xFFFF) : -1;
-        // sibling cache: the key before slot l is that of the nearest earlier delta slot;
-        // a hit starts from the cached (parent - from-row) and drops the from-row entry
-        const uint64_t km0 = __ballot(key0 >= 0) & 0xFFFFull, km1 = __ballot(key1 >= 0) & 0xFFFFull;
-        const uint64_t lt = (1ull << lane) - 1;
-        const int pk0 = __shfl(key0, (km0 & lt) ? 63 - __builtin_clzll(km0 & lt) : 0);
-        const int pk1 = __shfl(key1, (km1 & lt) ? 63 - __builtin_clzll(km1 & lt) : 0);
-        const bool hit0 = key0 >= 0 && key0 == ((km0 & lt) ? pk0 : ckey0);
-        const bool hit1 = key1 >= 0 && key1 == ((km1 & lt) ? pk1 : ckey1);
-        // Entry counts.  Delta and parent entries stay in their own perspective's list
-        // (they start from that perspective's accumulators); a king-move refresh needs
-        // no accumulator, so it goes to whichever list is shorter and the two wave
-        // groups finish the stream together.
-        const bool ref0 = (kinds & 3) == 2, ref1 = (kinds >> 2) == 2;
-        const int nr = (ref0 ? n0 : ref1 ? n1 : 0) + (kcb && (ref0 || ref1) ? 1 : 0); // + a king-cache store entry
-        const int d0 = ref0 ? 0 : n0 - (hit0 ? 1 : 0), d1 = ref1 ? 0 : n1 - (hit1 ? 1 : 0);
-        const uint32_t c = (uint32_t)d0 | (uint32_t)d1 << 10 | (uint32_t)nr << 20;
-        uint32_t inc = c;
-#pragma unroll
-        for (int d = 1; d < TILE; d <<= 1) {
-          const uint32_t o = __shfl_up(inc, d);
-          if (lane >= d) inc += o;
-        }
-        // fits even if every refresh landed in the same list
-        const bool fits =
-            inb && (int)((inc & 1023) + (inc >> 20)) <= FILL && (int)(((inc >> 10) & 1023) + (inc >> 20)) <= FILL;
-        const int m = __builtin_ctzll(~__ballot(fits)); // >= 1: one slot never exceeds FILL
-        const uint32_t exc = inc - c;
-        const bool mine = lane < m;
-        const uint32_t last_inc = __shfl(inc, m - 1);
-        {
-          const uint64_t k0 = __ballot(mine && key0 >= 0), k1 = __ballot(mine && key1 >= 0);
-          const int c0 = __shfl(key0, k0 ? 63 - __builtin_clzll(k0) : 0);
-          const int c1 = __shfl(key1, k1 ? 63 - __builtin_clzll(k1) : 0);
-          if (k0) ckey0 = __builtin_amdgcn_readfirstlane(c0);
-          if (k1) ckey1 = __builtin_amdgcn_readfirstlane(c1);
-        }
-        const int bk = (cnt - 1) / 4;
-        uint32_t bm = 0;
-#pragma unroll
-        for (int b = 0; b < 8; ++b)
-          if (__ballot(mine && vld && bk == b)) bm |= 1u << b;
-        if (lane < TILE) {
-          tmeta[tpar][lane] = (uint8_t)((mine && vld) | bk << 1);
-          sstm[lane] = (uint8_t)stm;
-        }
-        if (mine) {
-          const uint32_t t0w = tmpl(lane, stm != 0), t1w = tmpl(lane, stm != 1);
-          // delta rows: k < s removed (idx 0, 1), then added (idx 2, 3); s in {1, 2}
-          const bool nx = t0 + lane == nxq; // this slot is the next parent: store its accumulators
-          auto delta = [&](uint32_t *e, uint32_t lo2, uint32_t hi2, int s, int n, bool hit, uint32_t t, uint32_t L) {
-            const uint32_t i0 = lo2 & 0xFFFF, i1 = lo2 >> 16, i2 = hi2 & 0xFFFF, i3 = hi2 >> 16;
-            auto cl = [](uint32_t r) { return r < (uint32_t)FT_INPUTS ? r : (uint32_t)FT_BIAS_ROW; };
-            uint32_t r[4] = {cl(i0), cl(s >= 2 ? i1 : i2), cl(s >= 2 ? i2 : i3), cl(i3)};
-            uint32_t f[4] = {SUB, s >= 2 ? SUB : 0u, 0u, 0u};
-            if (!hit) {
-              e[0] = r[0] | t | SUB | I_PACC;
-              if (n > 1) e[1] = r[1] | t | f[1] | (n == 2 ? L : 0u);
-              if (n > 2) e[2] = r[2] | t | (n == 3 ? L : 0u);
-              if (n > 3) e[3] = r[3] | t | L;
-            } else { // the from-row is in the cached base
-              e[0] = r[1] | t | f[1] | I_BASE | (n == 2 ? L : 0u);
-              if (n > 2) e[1] = r[2] | t | (n == 3 ? L : 0u);
-              if (n > 3) e[2] = r[3] | t | L;
-            }
-          };
-          uint32_t *e0 = ent[0] + (exc & 1023), *e1 = ent[1] + ((exc >> 10) & 1023);
-          if ((kinds & 3) == 1) delta(e0, w0, w1, s0, n0, hit0, t0w, LAST | (nx ? NXT : 0u));
-          if ((kinds >> 2) == 1) delta(e1, w2, w3, s1, n1, hit1, t1w, LAST | (nx ? NXT | 1u << NXT_SH : 0u));
-          if (kinds == 15 && have) { // the parent from the carry rows (one entry per list)
-            e0[0] = ld2 | t0w | I_ZERO | PAR_E | LAST;
-            e1[0] = (ld2 + 1) | t1w | I_ZERO | PAR_E | LAST;
-          } else if (kinds == 15) { // the parent: bias entry, its rows follow (below)
-            e0[0] = (uint32_t)FT_BIAS_ROW | t0w | I_ZERO | PAR_E;
-            e1[0] = (uint32_t)FT_BIAS_ROW | t1w | I_ZERO | PAR_E;
-          }
-        }
-        // the parent's rows (lane = row), in its own lists after the bias entry
-        if (t0 == 0 && !have) {
-          const int st = __shfl(stm, 0);
-#pragma unroll
-          for (int hh = 0; hh < 2; ++hh)
-            if (lane < P)
-              ent[hh][1 + lane] = ft_row(prow[hh][lane]) | tmpl(0, hh != st) | PAR_E | (lane == P - 1 ? LAST : 0u);
-        }
-        // king-move refreshes (lane = square), each appended to the shorter list
-        int len0 = (int)(last_inc & 1023), len1 = (int)((last_inc >> 10) & 1023);
-        uint64_t jm = __ballot(mine && (ref0 || ref1));
-        uint32_t kst_any = 0;
-        while (jm) {
-          const int l = __builtin_ctzll(jm);
-          jm &= jm - 1;
-          // (readlane: job values are wave-uniform and stay in SGPRs)
-          const int hh = __builtin_amdgcn_readlane((int)ref1, l), st = __builtin_amdgcn_readlane(stm, l),
-                    cn = __builtin_amdgcn_readlane(cnt, l);
-          const uint32_t t = tmpl(l, hh != st);
-          const uint32_t sq01 = (uint32_t)__builtin_amdgcn_readlane((int)(hh ? w2 : w0), l),
-                         sq23 = (uint32_t)__builtin_amdgcn_readlane((int)(hh ? w3 : w1), l);
-          const int kt = (int)(sq01 >> 16);
-          int pos, cpc;
-          const int row =
-              king_move_row(pbd, hh, sq01 & 0xFFFF, kt, sq23 & 0xFFFF, sq23 >> 16, lane, pos, &cpc);
-          // King cache (not for castling): start from the accumulator this block last
-          // stored for (hh, kt) and apply the placement difference, when that is shorter.
-          const bool kuse = kcb && (sq23 & 0xFFFF) == 64;
-          const uint32_t kcr = (uint32_t)KC_ROW0 + 128 * cslot + 64 * hh + kt;
-          int ne = cn + 1 + (kuse ? 1 : 0), spc = 0;
-          bool kh = false;
-          uint64_t bs = 0, ba = 0;
-          if (kuse) {
-            // snapshot: the placement as 64 square-indexed nibbles (8 dwords, dword = rank)
-            uint32_t *rec = ksnap + ((size_t)cslot * 128 + 64 * hh + kt) * 8;
-            const uint32_t wv = lane < 8 ? rec[lane] : 0u; // lane-indexed: a vector load
-            spc = (int)((__shfl(wv, lane >> 3) >> (4 * (lane & 7))) & 15);
-            if (__ballot(spc != 0)) { // empty record: nothing cached for (hh, kt) yet
-              bs = __ballot(spc != cpc && spc != 0);
-              ba = __ballot(spc != cpc && cpc != 0);
-              const int nd = popcnt(bs) + popcnt(ba);
-              if (nd < cn) kh = true, ne = 2 + nd;
-            }
-            // the snapshot becomes the child's placement (its row is stored at LAST)
-            uint32_t x = (uint32_t)cpc << (4 * (lane & 7));
-            x |= __shfl_xor(x, 1);
-            x |= __shfl_xor(x, 2);
-            x |= __shfl_xor(x, 4);
-            if ((lane & 7) == 0) rec[lane >> 3] = x;
-            kst_any += 1; // one store-only entry
-          }
-          const int g = len0 <= len1 ? 0 : 1;
-          uint32_t *e = ent[g] + (g ? len1 : len0);
-          if (g) len1 += ne;
-          else len0 += ne;
-          // the slot's last entry: with the cache, a store-only entry for the cache row
-          // (I_ZERO | SUB = keep the accumulator; KST: store it to this entry's row)
-          const uint32_t L = LAST | (t0 + l == nxq ? NXT | (uint32_t)hh << NXT_SH : 0u);
-          const int el = kuse ? ne - 2 : ne - 1; // index of the last accumulating entry
-          if (kuse && lane == 0) e[ne - 1] = kcr | t | I_ZERO | SUB | KST | L;
-          const uint32_t La = kuse ? 0u : L;
-          if (!kh) {
-            if (lane == 0) e[0] = (uint32_t)FT_BIAS_ROW | t | I_ZERO;
-            if (row >= 0 && pos < cn) e[1 + pos] = (uint32_t)row | t | (1 + pos == el ? La : 0u);
-          } else {
-            const uint64_t lt2 = (1ull << lane) - 1;
-            const int ps = 1 + popcnt(bs & lt2), pa = 1 + popcnt(bs) + popcnt(ba & lt2);
-            if (lane == 0) e[0] = kcr | t | I_ZERO;
-            if ((bs >> lane) & 1) e[ps] = (uint32_t)feature_index(hh, lane, spc, kt) | t | SUB;
-            if ((ba >> lane) & 1) e[pa] = (uint32_t)row | t;
-          }
-        }
-        if (lane == 0) {
-          bmask = bm;
-          tctl[0] = (uint32_t)m;
-          tctl[1] = (uint32_t)len0;
-          tctl[2] = (uint32_t)len1;
-          tctl[3] = kst_any | (uint32_t)(nxq >= t0 && nxq < t0 + m);
-          // FT rows this tile gathers (every streamed entry but the store-only ones)
-          if (rows_out) atomicAdd(rows_out, (unsigned long long)(len0 + len1 - (int)kst_any));
-        }
-        // pad both lists with bias-row entries to a multiple of 4 plus the ring's 4
-        // run-ahead entries (harmless: they follow the last slot of the list)
-        if (lane < 7) {
-          const uint32_t pad = (uint32_t)FT_BIAS_ROW;
-          if (len0 + lane < ((len0 + 3) & ~3) + 4) ent[0][len0 + lane] = pad;
-          if (len1 + lane < ((len1 + 3) & ~3) + 4) ent[1][len1 + lane] = pad;
-        }
-      } else {
-        // PSQT.  Deltas (wave 1, lane = (perspective, slot)): +- the slot's rows at its
-        // bucket, the parent's sum at that bucket is added when the tile is finalised.
-        // Parent (tile 0, wave 1 second pass): both buckets the children can have.
-        // King-move refreshes: one wave per job, lane = square.
-        const int wk = wave - 1, nwk = NPJ;
-        if (wk == 0) {
-          const int sl = lane & 15, h = (lane >> 4) & 1;
-          int vld, stm, cnt, kinds, n0, n1, s0, s1;
-          uint32_t w0, w1, w2, w3;
-          desc(sl, vld, stm, cnt, kinds, n0, n1, s0, s1, w0, w1, w2, w3);
-          const int kd = h ? kinds >> 2 : kinds & 3, s = h ? s1 : s0, n = h ? n1 : n0;
-          const uint32_t lo2 = h ? w2 : w0, hi2 = h ? w3 : w1;
-          const uint32_t pso = 2 * L1 + 4 * ((cnt - 1) / 4);
-          int32_t sum = 0;
-          if (lane < 32 && vld && kd == 1) {
-            const uint32_t i0 = lo2 & 0xFFFF, i1 = lo2 >> 16, i2 = hi2 & 0xFFFF, i3 = hi2 >> 16;
-            const uint32_t r1 = s >= 2 ? i1 : i2, r2 = s >= 2 ? i2 : i3;
-            const int32_t v0 = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(ftr, ft_row(i0) * RS + pso, 0, 0);
-            const int32_t v1 = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(ftr, ft_row(r1) * RS + pso, 0, 0);
-            const int32_t v2 = n > 2 ? (int32_t)__builtin_amdgcn_raw_buffer_load_b32(ftr, ft_row(r2) * RS + pso, 0, 0) : 0;
-            const int32_t v3 = n > 3 ? (int32_t)__builtin_amdgcn_raw_buffer_load_b32(ftr, ft_row(i3) * RS + pso, 0, 0) : 0;
-            sum = wadd(wadd(-v0, s >= 2 ? -v1 : v1), wadd(v2, v3));
-          }
-          if (lane < 32 && sl + t0 < total && kd < 2) { // refreshes, parent: other waves write
-            psa[sl][h] = sum;
-            pinit[sl][h] = (uint8_t)(kd == 1);
-          }
-        }
-        if (wk == nwk - 1 && t0 == 0) { // the parent (last PSQT wave): lane = (perspective, row)
-          {
-            const int hh = lane >> 5, k = lane & 31;
-            int32_t a = 0, b = 0;
-            if (k < P) {
-              const uint32_t o = ft_row(prow[hh][k]) * RS + 2 * L1;
-              a = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(ftr, o + 4 * bp, 0, 0);
-              b = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(ftr, o + 4 * b2, 0, 0);
-            }
-#pragma unroll
-            for (int o2 = 16; o2; o2 >>= 1) a = wadd(a, __shfl_xor(a, o2)), b = wadd(b, __shfl_xor(b, o2));
-            if (k == 0) {
-              pps[hh][0] = a, pps[hh][1] = b;
-              psa[0][hh] = a;
-              pinit[0][hh] = 0;
-            }
-          }
-        }
-        // king-move refresh jobs, round robin over the PSQT waves
-        int jn = 0;
-        for (int sl = 0; sl < TILE && t0 + sl < total; ++sl) {
-          if (t0 + sl == 0) continue;
-          const int qq = t0 + sl;
-          if (need_child && !need_child[off + qq - 1]) continue;
-          const uint32_t meta = qq - 1 < CDL ? cdl[qq - 1][4] : deltas[off + qq - 1].meta;
-          if (!(meta & (3u << 8))) continue;
-          if (wk >= nwk || jn++ % nwk != wk) continue;
-          const int hh = (meta >> 9) & 1, cn = (meta >> 14) & 63;
-          const uint32_t sq01 = qq - 1 < CDL ? cdl[qq - 1][2 * hh] : deltas[off + qq - 1].idx[hh][0] |
-                                                                           (uint32_t)deltas[off + qq - 1].idx[hh][1] << 16;
-          const uint32_t sq23 = qq - 1 < CDL ? cdl[qq - 1][2 * hh + 1] : deltas[off + qq - 1].idx[hh][2] |
-                                                                               (uint32_t)deltas[off + qq - 1].idx[hh][3] << 16;
-          int pos;
-          const int row = king_move_row(pbd, hh, sq01 & 0xFFFF, sq01 >> 16, sq23 & 0xFFFF, sq23 >> 16, lane, pos);
-          const int32_t a = row >= 0 ? (int32_t)__builtin_amdgcn_raw_buffer_load_b32(
-                                           ftr, (uint32_t)row * RS + 2 * L1 + 4 * ((cn - 1) / 4), 0, 0)
-                                     : 0;
-          const int32_t sum = wave_sum(a);
-          if (lane == 0) psa[sl][hh] = sum, pinit[sl][hh] = 0;
-        }
-      }
-      __syncthreads();
-      GN_STAMP(2);
-      const int m = (int)tctl[0];
-      const uint32_t bm_tile = bmask;
-
-      // ---- phase 1: the row stream of this wave's list.  Every ring step issues the two
-      // row-half loads with the row offset as the scalar offset (lists are padded, so no
-      // step needs a guard and the outstanding-load count is the same on every path).
-      {
-        int tl = tid;
-        asm volatile("" : "+v"(tl));
-        const int jt = tl % G;
-        const int ln = tl & 63;
-        // PSQT of the tile's slots by side (wave 0): partial + the parent's at the bucket
-        if (wave == 0 && ln < TILE && ln < m && (tmeta[tpar][ln] & 1)) {
-          const int st = sstm[ln], useb2 = (tmeta[tpar][ln] >> 1) != bp;
-          int32_t vv[2];
-#pragma unroll
-          for (int hh = 0; hh < 2; ++hh) vv[hh] = wadd(psa[ln][hh], pinit[ln][hh] ? pps[hh][useb2] : 0);
-          psqf[tpar][ln][0] = vv[st];
-          psqf[tpar][ln][1] = vv[st ^ 1];
-        }
-        const uint32_t j16 = 16 * jt;
-        const int n4 = (ablate & 8) ? 0 : ((int)tctl[1 + hu] + 3) & ~3;
-        const uint32_t *E = ent[hu];
-        ushort8 rlo[4], rhi[4];
-        uint32_t er[4];
-        ushort8 lo = {}, hi = {};
-        uint32_t ev = 0;
-        auto issue = [&](int r, int i) {
-          if ((i & 63) == 0) ev = E[i + ln];
-          const uint32_t e = er[r] = (uint32_t)__builtin_amdgcn_readlane((int)ev, i & 63);
-          const uint32_t o = (ablate & 2) ? (uint32_t)FT_BIAS_ROW * RS : (e & ROW) * RS;
-          rlo[r] = __builtin_bit_cast(ushort8, __builtin_amdgcn_raw_buffer_load_b128(ftr, j16, o, 0));
-          rhi[r] = __builtin_bit_cast(ushort8, __builtin_amdgcn_raw_buffer_load_b128(ftr, j16 + L1, o, 0));
-        };
-        auto consume = [&](int r) {
-          const uint32_t e = er[r];
-          const uint32_t init = e & INIT;
-          // scalar branches; the empty asm keeps the compiler from if-converting them into
-          // selects over every alternative (vector work on all paths)
-          if (init == I_ZERO) { // the bias row (or a king-cache row); with SUB: keep (store-only)
-            asm volatile("");
-            if (!(e & SUB)) lo = rlo[r], hi = rhi[r];
-          } else if (init == I_PACC) { // a miss: parent - from-row, saved as the sibling base
-            asm volatile("");
-            lo = pacc_lo - rlo[r], hi = pacc_hi - rhi[r];
-            base_lo = lo, base_hi = hi;
-          } else if (init == I_BASE) { // a hit: the cached (parent - from-row) +- the next row
-            if (e & SUB) {
-              asm volatile("");
-              lo = base_lo - rlo[r], hi = base_hi - rhi[r];
-            } else {
-              asm volatile("");
-              lo = base_lo + rlo[r], hi = base_hi + rhi[r];
-            }
-          } else if (e & SUB) {
-            asm volatile("");
-            lo -= rlo[r], hi -= rhi[r];
-          } else {
-            asm volatile("");
-            lo += rlo[r], hi += rhi[r];
-          }
-          if (e & LAST) {
-            const int sl = (e >> SLOT_SH) & 15, side = (e >> SIDE_SH) & 1;
-            *reinterpret_cast<uint2 *>(xt + sl * XS + side * (L1 / 2) + 8 * jt) = transform8(lo, hi);
-            if (e & PAR_E) { // (kept a branch: a select would cost 8 VALU on every LAST entry)
-              asm volatile("");
-              pacc_lo = lo, pacc_hi = hi;
-            }
-            if (e & (KST | NXT)) { // accumulator stores: king-cache row and / or next-parent carry row
-              asm volatile("");
-              uint32_t so = (st2 + ((e >> NXT_SH) & 1)) * RS;
-              if (e & KST) so = (e & ROW) * RS;
-              for (int rep = (e & KST) && (e & NXT) ? 2 : 1; rep; --rep) {
-                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(int4v, lo), ftr, j16, so, 0);
-                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(int4v, hi), ftr, j16 + L1, so, 0);
-                so = (st2 + ((e >> NXT_SH) & 1)) * RS;
-              }
-            }
-          }
-        };
-#pragma unroll
-        for (int r = 0; r < 4; ++r) issue(r, r);
-#pragma unroll 1
-        for (int i = 0; i < n4; i += 4) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            consume(r);
-            issue(r, i + r + 4);
-          }
-        }
-        // the carry-row stores must be complete before the barrier (which waits only
-        // for LDS): the next parent's loads may come from the other wave group
-        if (tctl[3]) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      __syncthreads();
-      GN_STAMP(4);
-      // ---- phase 2: layer stack of this tile by the last NLS waves, one bucket per wave at a
-      // time; the other waves go on to the next tile (or parent), which touches none of
-      // what the layer stack reads (xt until the next stream barrier, which these waves
-      // join only when done; tile metadata and PSQT double-buffered by tile parity)
-      if (wave >= NW - NLS && !(ablate & 4)) {
-        int tl = tid;
-        asm volatile("" : "+v"(tl));
-        const int lw = wave - (NW - NLS), ln = tl & 63;
-        const uint8_t *meta = tmeta[tpar];
-        const int tp0 = t0;
-        int idx = 0;
-        for (uint32_t mm = bm_tile; mm; mm &= mm - 1, ++idx) {
-          if (idx % NLS != lw) continue;
-          const int b = __builtin_ctz(mm);
-          layer_stack_wave<L1>(net, xt, ls_in1[lw], ls_fwd[lw], psqf[tpar], b, ln, [&](int pos, int bb) {
-            return pos < m && meta[pos] == (1 | bb << 1);
-          }, [&](int pos, int2 val) {
-            if (tp0 + pos == 0) out_parent[p] = val;
-            else out_child[off + tp0 + pos - 1] = val;
-          });
-        }
-      }
-      t0 += m;
-      tpar ^= 1;
-      GN_STAMP(5);
-    }
-    GN_STAMP_FLUSH();
-   }
-   if (K > 1) { // done with the slot (every wave's stores completed before the barrier)
-     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-     __syncthreads();
-     if (tid == 0) __hip_atomic_fetch_add(tickets + cslot, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-   }
   }
 }
 
@@ -1596,6 +872,27 @@ __global__ void score_reduce_kernel(const gn_board *__restrict__ sb, size_t m, c
 
 static inline unsigned blocks_for(size_t n, int bs) { return (unsigned)((n + bs - 1) / bs); }
 
+// Child records for the host (ABI v4 gn_child, include/gpu_nnue.h): psqt, positional and
+// final_cp (signed 24 bits) with the low 8 flag bits beside it.  |final_cp| < 2^23 by
+// gn_set_eval_params' bound on the win-rate model; the clamp only keeps the field honest.
+__global__ void pack_children_kernel(const gn_eval *__restrict__ in, size_t n, gn_child *__restrict__ out) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const gn_eval e = in[i];
+  const int32_t cp = clampi(e.final_cp, -(1 << 23) + 1, (1 << 23) - 1);
+  gn_child c;
+  c.psqt = e.psqt;
+  c.positional = e.positional;
+  c.cp_flags = (int32_t)(((uint32_t)cp & 0xFFFFFFu) | ((uint32_t)e.flags & 0xFFu) << 24);
+  out[i] = c;
+}
+
+hipError_t launch_pack_children(const gn_eval *in, size_t n, gn_child *out, hipStream_t s) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(pack_children_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, in, n, out);
+  return hipGetLastError();
+}
+
 hipError_t launch_classify(const gn_board *boards, size_t n, const gn_eval_params &P, uint8_t *need_small,
                            uint8_t *need_big, hipStream_t s) {
   if (!n) return hipSuccess;
@@ -1615,12 +912,10 @@ hipError_t launch_finalize(const gn_board *boards, size_t n, int mode, const int
                            const Tables *tables, gn_eval *out, hipStream_t s, int score, const uint64_t *counts,
                            const uint32_t *owner, const uint16_t *moves, const Board *unpacked) {
   if (!n) return hipSuccess;
-  static const size_t max_blocks = [] {
-    const char *e = getenv("GN_FIN_BLOCKS"); // A/B: finalize workgroups (0 = one per 256 positions)
-    return e ? (size_t)strtoull(e, nullptr, 10) : (size_t)8192;
-  }();
-  size_t blocks = blocks_for(n, 256);
-  if (max_blocks) blocks = std::min(blocks, max_blocks);
+  // a bounded grid striding over the positions: each workgroup copies the movegen tables to
+  // LDS once (8,192 workgroups: 2.55 -> 2.36 ms per expansion against one per 256 positions)
+  constexpr size_t max_blocks = 8192;
+  const size_t blocks = std::min<size_t>(blocks_for(n, 256), max_blocks);
   hipLaunchKernelGGL(finalize_kernel, dim3(blocks), dim3(256), 0, s, boards, n, mode, out_small, out_big, need_small,
                      need_big, P, tables, out, owner, moves, unpacked, score, counts);
   return hipGetLastError();
@@ -2014,7 +1309,7 @@ hipError_t launch_offsets_u32(const uint64_t *in, size_t n, uint32_t *out, hipSt
 template <class Key>
 static hipError_t king_sort_t(const gn_board *boards, size_t n, Key *keys, uint32_t *idx, Key *keys_out,
                               uint32_t *perm, void *&temp, size_t &temp_bytes, hipStream_t s) {
-  static const int bkt = !getenv("GN_SORT_BUCKET") || atoi(getenv("GN_SORT_BUCKET")); // A/B: 0 = kings (+ home bits) only
+  constexpr int bkt = 1; // the layer-stack bucket in the key (king_keys_kernel)
   hipLaunchKernelGGL(king_keys_kernel<Key>, dim3(blocks_for(n, 256)), dim3(256), 0, s, boards, n, keys, idx, bkt);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
@@ -2045,14 +1340,13 @@ hipError_t king_sort(const gn_board *boards, size_t n, uint64_t *keys, uint32_t 
 // XCD swizzle gives it a contiguous eighth of this order) gather from the same king-bucket
 // slices of the FT and share the XCD's L2.  keys: uint16 (wk << 6 | bk; 4095: invalid).
 __global__ void block_keys_kernel(const gn_board *__restrict__ parents, size_t n, uint32_t K, uint32_t nblk,
-                                  uint16_t *__restrict__ keys, uint32_t *__restrict__ idx, int mode) {
+                                  uint16_t *__restrict__ keys, uint32_t *__restrict__ idx) {
   const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= nblk) return;
   const size_t pb = (size_t)b * K, pe = pb + K < n ? pb + K : n;
-  // which parent keys the block (diagnostics: GN_BLOCK_KEY 1 first, 2 three quarters, 3 one quarter)
-  const size_t at = mode == 1 ? pb : mode == 2 ? pb + 3 * (pe - pb) / 4 : mode == 3 ? pb + (pe - pb) / 4
-                                                                                    : pb + (pe - pb) / 2;
-  const gn_board p = parents[at];
+  // the block's middle parent keys it (first / quarter / three-quarter parents and Morton or
+  // black-king-major orders of the king squares or buckets all measured within +-0.5 %)
+  const gn_board p = parents[pb + (pe - pb) / 2];
   uint64_t wlo, whi;
   piece_words(p, wlo, whi);
   uint64_t o = p.occ;
@@ -2063,31 +1357,14 @@ __global__ void block_keys_kernel(const gn_board *__restrict__ parents, size_t n
     if (pc == make_piece(WHITE, KING)) wk = sq;
     if (pc == make_piece(BLACK, KING)) bk = sq;
   }
-  // diagnostics: 4 black-king-major; 5 Morton order of the two king squares; 6 Morton order of
-  // the two perspectives' king buckets (HalfKAv2_hm, nnue.h feature_index)
-  auto morton6 = [](uint32_t a, uint32_t c) {
-    uint32_t r = 0;
-    for (int i = 0; i < 6; ++i) r |= ((a >> i) & 1u) << (2 * i + 1) | ((c >> i) & 1u) << (2 * i);
-    return r;
-  };
-  auto kbucket = [](int ksq, int persp) {
-    const int kf = ksq & 7, rr = (ksq >> 3) ^ (persp ? 7 : 0);
-    return 4 * (7 - rr) + (kf < 4 ? kf : 7 - kf);
-  };
-  uint32_t key = (uint32_t)(wk << 6 | bk);
-  if (mode == 4) key = (uint32_t)(bk << 6 | wk);
-  if (mode == 5) key = morton6((uint32_t)wk, (uint32_t)bk);
-  if (mode == 6) key = morton6((uint32_t)kbucket(wk, 0), (uint32_t)kbucket(bk, 1));
-  keys[b] = (uint16_t)key;
+  keys[b] = (uint16_t)(wk << 6 | bk);
   idx[b] = b;
 }
 
 hipError_t block_order(const gn_board *parents, size_t n, uint32_t K, uint32_t nblk, uint16_t *keys, uint32_t *idx,
                        uint16_t *keys_out, uint32_t *order, void *&temp, size_t &temp_bytes, hipStream_t s) {
   if (!nblk) return hipSuccess;
-  static const int mode = getenv("GN_BLOCK_KEY") ? atoi(getenv("GN_BLOCK_KEY")) : 0; // diagnostics
-  hipLaunchKernelGGL(block_keys_kernel, dim3(blocks_for(nblk, 256)), dim3(256), 0, s, parents, n, K, nblk, keys, idx,
-                     mode);
+  hipLaunchKernelGGL(block_keys_kernel, dim3(blocks_for(nblk, 256)), dim3(256), 0, s, parents, n, K, nblk, keys, idx);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   size_t need = 0;
@@ -2120,58 +1397,14 @@ hipError_t exclusive_scan_u64(const uint64_t *counts, uint64_t *offsets, size_t 
 
 hipError_t launch_expand_net(const NetDevice &net, const gn_board *parents, size_t n, const uint64_t *offsets,
                              const gn_board *children, const ChildDelta *deltas, const uint8_t *need_parent,
-                             const uint8_t *need_child, int2 *out_parent, int2 *out_child, int swz,
-                             const uint8_t *next_slot, uint32_t *tickets, int chain_k, uint32_t *ksnap,
-                             unsigned long long *rows_out, hipStream_t s) {
+                             const uint8_t *need_child, int2 *out_parent, int2 *out_child, int swz, hipStream_t s) {
   if (!n) return hipSuccess;
-  unsigned g = (unsigned)(swz ? 8 * ((n + 7) / 8) : n);
-  // GN_EXPAND_LEGACY=1: the per-slot row programs (expand_eval) for the big nets, for A/B timing
-  static const int legacy = getenv("GN_EXPAND_LEGACY") ? atoi(getenv("GN_EXPAND_LEGACY")) : 0;
   if (n >= 0x80000000ull) return hipErrorInvalidValue; // 32-bit parent indices in the kernels
-  const bool chained =
-      !legacy && chain_k > 1 && next_slot && tickets && net.carry_slots && (net.L1 == 3072 || net.L1 == 1024);
-  if (!chained) chain_k = 1;
-  if (chained) { // one workgroup per block (never persistent: the slot tickets assume dispatch order)
-    const size_t nblk = (n + chain_k - 1) / chain_k;
-    g = (unsigned)(swz ? 8 * ((nblk + 7) / 8) : nblk);
-    hipError_t e = hipMemsetAsync(tickets, 0, (CARRY_SLOTS + 1) * sizeof(uint32_t), s); // + the fallback count
-    if (e != hipSuccess) return e;
-  }
-  static const int ablate = getenv("GN_ABLATE") ? atoi(getenv("GN_ABLATE")) : 0; // timing diagnostics only
-  static const int persist = getenv("GN_PERSIST") ? atoi(getenv("GN_PERSIST")) : 0; // WGs per CU, 0: one per parent
-  if (persist > 0 && !chained) g = std::min<unsigned>(g, 8u * ((256u * (unsigned)persist + 7) / 8));
-#define GN_EXPAND_ARGS net, parents, offsets, children, deltas, need_parent, need_child, out_parent, out_child, n, swz, ablate
-#define GN_STREAM_ARGS net, parents, offsets, deltas, need_parent, need_child, out_parent, out_child, n, swz, ablate, \
-                       chained ? next_slot : nullptr, chained ? tickets : nullptr, chain_k, chained ? ksnap : nullptr, \
-                       rows_out
-  if (net.L1 == 3072 && !legacy) {
-    hipLaunchKernelGGL((expand_stream_kernel<3072>), dim3(g), dim3(384), 0, s, GN_STREAM_ARGS);
-  } else if (net.L1 == 1024 && !legacy) {
-    hipLaunchKernelGGL((expand_stream_kernel<1024>), dim3(g), dim3(128), 0, s, GN_STREAM_ARGS);
-  } else if (net.L1 == 3072) {
-    hipLaunchKernelGGL((expand_eval_kernel<3072, 1>), dim3(g), dim3(384), 0, s, GN_EXPAND_ARGS);
-  } else if (net.L1 == 128) {
-    hipLaunchKernelGGL((expand_eval_kernel<128, 16>), dim3(g), dim3(256), 0, s, GN_EXPAND_ARGS);
-  } else if (net.L1 == 1024) {
-    hipLaunchKernelGGL((expand_eval_kernel<1024, 1>), dim3(g), dim3(128), 0, s, GN_EXPAND_ARGS);
-  } else {
-    return hipErrorInvalidValue;
-  }
-#undef GN_EXPAND_ARGS
-#undef GN_STREAM_ARGS
-#ifdef GN_PHASE_TIMING
-  {
-    unsigned long long c[64][8], t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    (void)hipStreamSynchronize(s);
-    (void)hipMemcpyFromSymbol(c, HIP_SYMBOL(gn_phase_cycles), sizeof(c));
-    for (int i = 0; i < 64; ++i)
-      for (int k = 0; k < 8; ++k) t[k] += c[i][k];
-    fprintf(stderr, "phase cycles: parent_setup %llu parent_refresh %llu desc %llu jobs %llu gather %llu ls %llu\n",
-            t[0], t[1], t[2], t[3], t[4], t[5]);
-    memset(c, 0, sizeof(c));
-    (void)hipMemcpyToSymbol(HIP_SYMBOL(gn_phase_cycles), c, sizeof(c));
-  }
-#endif
+  // the big nets (L1 3072 / 1024) always run planned (stream.hip, launch_plan_stream)
+  if (net.L1 != 128) return hipErrorInvalidValue;
+  const unsigned g = (unsigned)(swz ? 8 * ((n + 7) / 8) : n);
+  hipLaunchKernelGGL((expand_eval_kernel<128, 16>), dim3(g), dim3(256), 0, s, net, parents, offsets, children, deltas,
+                     need_parent, need_child, out_parent, out_child, n, swz);
   return hipGetLastError();
 }
 

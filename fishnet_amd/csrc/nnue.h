@@ -32,10 +32,10 @@ constexpr int FT_ROWS = FT_INPUTS + 1;
 #define GN_ROW_ALIGN 128
 #endif
 constexpr uint32_t ft_row_stride(uint32_t l1) { return (2 * l1 + 32 + GN_ROW_ALIGN - 1) / GN_ROW_ALIGN * GN_ROW_ALIGN; }
-// Big nets: CARRY_SLOTS x 4 scratch rows follow the FT rows in the same allocation
-// (the expansion's chained walk, kernels.hip expand_stream): slot = dispatch index
-// mod CARRY_SLOTS, rows = parity of the parent x perspective.  Row indices stay
-// below 2^19 (the row field of a stream entry).
+// Big nets: CARRY_SLOTS x 132 scratch rows follow the FT rows in the same allocation
+// (round 1's chained walk had 4 carry rows + 128 king-cache rows per slot; the planned
+// expansion's scratch slots below use the same rows).  Row indices stay below 2^19 (the
+// row field of a stream entry).
 constexpr int CARRY_SLOTS = 2048;
 constexpr int CARRY_ROW0 = FT_ROWS;
 // Then the king cache: per slot, one accumulator row per (perspective, king square).

@@ -612,7 +612,7 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
                        const uint64_t *__restrict__ eoff, const uint64_t *__restrict__ ent,
                        const TileDesc *__restrict__ tiles, const uint32_t *__restrict__ btiles,
                        const uint32_t *__restrict__ order, int2 *__restrict__ out_parent, int2 *__restrict__ out_child,
-                       uint32_t *__restrict__ pool, int use_scr, uint32_t *__restrict__ err, int ablate,
+                       uint32_t *__restrict__ pool, int use_scr, uint32_t *__restrict__ err,
                        uint32_t *__restrict__ claim) {
   using namespace ps;
   constexpr int G = L1 / 16; // threads per perspective group (whole waves)
@@ -792,7 +792,10 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
         asm volatile("");
         const uint32_t so = (scr + (h & 0xFFFFu)) * RS;
 #ifndef GN_KC_POLICY
-#define GN_KC_POLICY 2 // king-cache stores non-temporal (nt): stream 205.5 -> 205.0 ms in two A/B pairs; 0 = default policy
+// cache policy of the king-cache stores: 0 = default.  The same-address store -> load order
+// the reload relies on is pinned for default-policy stores only (kernels.h); non-temporal
+// (2) measured 205.5 -> 205.0 ms, within noise, so it stays an A/B build option
+#define GN_KC_POLICY 0
 #endif
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(int4v, lo), ftr, j16, so, GN_KC_POLICY);
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(int4v, hi), ftr, j16 + L1, so, GN_KC_POLICY);
@@ -858,7 +861,6 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
     __syncthreads();
     const unsigned long long t2 = SP_T();
     sp_s += t1 - t0, sp_w += t2 - t1;
-    if (ablate & 4) continue; // timing diagnostics only: no layer stack
     // ---- layer stack: per bucket of the tile, fc_0 by all waves (int8 MFMA over this wave's
     // k-steps, partial sums by LDS integer atomics, exact), then one wave finishes it
     uint32_t bm = 0, pm = 0;
@@ -884,7 +886,7 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
         // (batches of FB k-steps: the next tile's rows stay in flight in registers meanwhile)
         constexpr int FB = 2;
 #pragma unroll
-        for (int k0 = 0; k0 < KPW && !(ablate & 16); k0 += FB) { // (16: timing diagnostics, no fc_0)
+        for (int k0 = 0; k0 < KPW; k0 += FB) {
           int4v wv[FB], av[FB];
 #pragma unroll
           for (int j = 0; j < FB; ++j) wv[j] = *reinterpret_cast<const int4v *>(wb + 1024 * (k0 + j));
@@ -897,7 +899,7 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
         for (int i = 0; i < 4; ++i) atomicAdd(&acc0[buf][(4 * kg + i) * AS + row], acc[i]);
       }
       __syncthreads();
-      if (wave == (int)(bq % NW) && !(ablate & 8)) { // fc_0 activations, fc_1, fc_2, outputs of bucket b (8: diagnostics)
+      if (wave == (int)(bq % NW)) { // fc_0 activations, fc_1, fc_2, outputs of bucket b
         // the finishing step's scalar weights and the tile's PSQT first (one wait for memory)
         const int32_t bias0 = net.b0[b * 16 + row];
         const int32_t b1l = net.b1[b * 32 + row], b1h = net.b1[b * 32 + 16 + row];
@@ -1011,23 +1013,20 @@ hipError_t launch_plan_stream(const NetDevice &net, const gn_board *parents, siz
   if (b1 > (n + K - 1) / K) return hipErrorInvalidValue;
   const uint32_t nb = (uint32_t)(b1 - b0), B0 = (uint32_t)b0, B1 = (uint32_t)b1;
   const unsigned pg = (nb + 3) / 4, g = swz ? 8 * ((nb + 7) / 8) : nb + nb / 16 + 8; // (stream_eval_kernel: claims)
-  static const int ablate = getenv("GN_ABLATE") ? atoi(getenv("GN_ABLATE")) : 0; // timing diagnostics only
-  // timing diagnostics only: extra dynamic LDS per workgroup (fewer workgroups per CU)
-  static const size_t lds_pad = getenv("GN_STREAM_LDS_PAD") ? (size_t)atoi(getenv("GN_STREAM_LDS_PAD")) : 0;
   if (net.L1 == 3072) {
     hipLaunchKernelGGL((plan_kernel<3072>), dim3(pg), dim3(256), 0, s, net, parents, offsets, deltas, need_parent,
                        need_child, K > 1 ? next_slot : nullptr, (uint32_t)n, K, B0, B1, K > 1 ? kc : 0, eoff, ent,
                        tiles, btiles, rows_out, pads_out, err);
     if (mid) (void)hipEventRecord(mid, s);
-    hipLaunchKernelGGL((stream_eval_kernel<3072>), dim3(g), dim3(384), lds_pad, s, net, offsets, (uint32_t)n, K, B0, B1,
-                       swz, eoff, ent, tiles, btiles, order, out_parent, out_child, pool, scr, err, ablate, pool + 64);
+    hipLaunchKernelGGL((stream_eval_kernel<3072>), dim3(g), dim3(384), 0, s, net, offsets, (uint32_t)n, K, B0, B1,
+                       swz, eoff, ent, tiles, btiles, order, out_parent, out_child, pool, scr, err, pool + 64);
   } else if (net.L1 == 1024) {
     hipLaunchKernelGGL((plan_kernel<1024>), dim3(pg), dim3(256), 0, s, net, parents, offsets, deltas, need_parent,
                        need_child, K > 1 ? next_slot : nullptr, (uint32_t)n, K, B0, B1, K > 1 ? kc : 0, eoff, ent,
                        tiles, btiles, rows_out, pads_out, err);
     if (mid) (void)hipEventRecord(mid, s);
     hipLaunchKernelGGL((stream_eval_kernel<1024>), dim3(g), dim3(128), 0, s, net, offsets, (uint32_t)n, K, B0, B1,
-                       swz, eoff, ent, tiles, btiles, order, out_parent, out_child, pool, scr, err, ablate, pool + 64);
+                       swz, eoff, ent, tiles, btiles, order, out_parent, out_child, pool, scr, err, pool + 64);
   } else {
     return hipErrorInvalidValue;
   }

@@ -30,9 +30,14 @@ EVAL_DTYPE = np.dtype([("psqt", "<i4"), ("positional", "<i4"), ("final_v", "<i4"
                        ("score", "<i4"), ("flags", "<u2"), ("best_move", "<u2")])
 BOARD_DTYPE = np.dtype([("occ", "<u8"), ("pc", "u1", (16,)), ("stm_ep", "u1"), ("reserved", "u1"),
                         ("castle", "<u2"), ("rule50", "<u2"), ("fullmove", "<u2")])
-EVAL_SIZE, BOARD_SIZE = EVAL_DTYPE.itemsize, BOARD_DTYPE.itemsize
-assert EVAL_SIZE == 24 and BOARD_SIZE == 32
-ABI_VERSION = 3
+# gn_child (ABI v4): a legal child's record from the host-buffer expansion calls, 12 bytes:
+# final_cp (signed 24 bits) and the low 8 flag bits share cp_flags (gpu_nnue.h at gn_child)
+CHILD_DTYPE = np.dtype([("psqt", "<i4"), ("positional", "<i4"), ("cp_flags", "<i4")])
+# ... and decoded (decode_children / children_from_evals), the form the tests compare
+CHILD_VIEW_DTYPE = np.dtype([("psqt", "<i4"), ("positional", "<i4"), ("final_cp", "<i4"), ("flags", "<u2")])
+EVAL_SIZE, BOARD_SIZE, CHILD_SIZE = EVAL_DTYPE.itemsize, BOARD_DTYPE.itemsize, CHILD_DTYPE.itemsize
+assert EVAL_SIZE == 24 and BOARD_SIZE == 32 and CHILD_SIZE == 12
+ABI_VERSION = 4
 
 EXPORTS = ["gn_load_net", "gn_load_net_memory", "gn_free", "gn_last_error", "gn_abi_version",
            "gn_get_eval_params", "gn_set_eval_params", "gn_net_info", "gn_evaluate_batch",
@@ -45,10 +50,33 @@ EXPORTS = ["gn_load_net", "gn_load_net_memory", "gn_free", "gn_last_error", "gn_
            "gn_boards_to_fens", "gn_load_net_archive", "gn_archive_read", "gn_expand2_device",
            "gn_random_games_uci"]
 OPT_INCREMENTAL_CHILDREN, OPT_XCD_SWIZZLE, OPT_KING_SORT, OPT_CHAIN, OPT_KING_CACHE = 1, 2, 3, 4, 5
-STAT_CHAIN_FALLBACKS, STAT_PLAN_NS, STAT_STREAM_NS, STAT_SCRATCH_PADS = 100, 101, 102, 103
+OPT_CHUNK_PARENTS, OPT_COALESCE = 6, 7
+STAT_PLAN_NS, STAT_STREAM_NS, STAT_SCRATCH_PADS = 101, 102, 103
+STAT_BATCH_LAUNCHES, STAT_BATCH_CALLS = 117, 118
 HOST_STAGES = {"parse": 110, "upload": 111, "replay": 112, "compute": 113, "download": 114, "tail": 115, "total": 116}
 EXPAND_STAGES = ["count_scan", "total_readback", "write_children", "classify", "small_net", "big_net", "finalize",
                  "score"]
+
+
+def decode_children(raw) -> np.ndarray:
+    """gn_child records -> CHILD_VIEW_DTYPE (psqt, positional, final_cp, flags)."""
+    raw = np.asarray(raw, dtype=CHILD_DTYPE)
+    out = np.empty(raw.shape, dtype=CHILD_VIEW_DTYPE)
+    cf = raw["cp_flags"].astype(np.int64)
+    out["psqt"], out["positional"] = raw["psqt"], raw["positional"]
+    out["final_cp"] = ((cf & 0xFFFFFF) ^ 0x800000) - 0x800000
+    out["flags"] = (cf >> 24) & 0xFF
+    return out
+
+
+def children_from_evals(ev) -> np.ndarray:
+    """gn_eval child records (the device-resident calls, the oracle) -> the fields a gn_child keeps,
+    as CHILD_VIEW_DTYPE: psqt, positional, final_cp and the low 8 flag bits."""
+    ev = np.asarray(ev, dtype=EVAL_DTYPE)
+    out = np.empty(ev.shape, dtype=CHILD_VIEW_DTYPE)
+    out["psqt"], out["positional"], out["final_cp"] = ev["psqt"], ev["positional"], ev["final_cp"]
+    out["flags"] = ev["flags"] & 0xFF
+    return out
 
 
 class GnError(RuntimeError):
@@ -353,6 +381,8 @@ class GpuNnue:
         return out
 
     def expand_and_evaluate(self, fens, mode=MODE_FULL, cap=None):
+        """gn_expand_and_evaluate: (parent gn_eval records, child offsets, child moves, children as
+        CHILD_VIEW_DTYPE decoded from the library's gn_child records)."""
         n = len(fens)
         arr, _keep = _fen_array(fens)
         offsets = np.zeros(n + 1, dtype=np.uint32)
@@ -360,7 +390,7 @@ class GpuNnue:
         cap = cap if cap is not None else 64 * n + 256
         for _ in range(2):
             moves = np.zeros(max(cap, 1), dtype=np.uint16)
-            kids = np.zeros(max(cap, 1), dtype=EVAL_DTYPE)
+            kids = np.zeros(max(cap, 1), dtype=CHILD_DTYPE)
             rc = lib().gn_expand_and_evaluate(self.h, arr, n, mode, parents.ctypes.data, offsets.ctypes.data,
                                               moves.ctypes.data, kids.ctypes.data, cap)
             if rc == -6 and int(offsets[-1]) > cap:
@@ -368,13 +398,13 @@ class GpuNnue:
                 continue
             _check(rc)
             t = int(offsets[-1])
-            return parents, offsets, moves[:t], kids[:t]
+            return parents, offsets, moves[:t], decode_children(kids[:t])
         raise GnError(-6, "capacity retry failed")
 
     def evaluate_games(self, games, mode=MODE_FULL, children=False):
         """gn_evaluate_games over [(root_fen, moves, skip)]: per game a dict with status, evals of
         positions 0..=moves (skipped ones flagged FLAG_SKIPPED) and, with children, per position
-        (child moves, child evals)."""
+        (child moves, children as CHILD_VIEW_DTYPE)."""
         arr, _keep = _games_array(games)
         ng = len(games)
         offs = np.zeros(ng + 1, dtype=np.uint32)
@@ -384,7 +414,7 @@ class GpuNnue:
             pos = np.zeros(max(pcap, 1), dtype=EVAL_DTYPE)
             coffs = np.zeros(pcap + 1, dtype=np.uint32)
             cmv = np.zeros(max(ccap, 1), dtype=np.uint16)
-            cev = np.zeros(max(ccap, 1), dtype=EVAL_DTYPE)
+            cev = np.zeros(max(ccap, 1), dtype=CHILD_DTYPE)
             rc = lib().gn_evaluate_games(self.h, arr, ng, mode, int(children), offs.ctypes.data, status.ctypes.data,
                                          pos.ctypes.data, pcap, coffs.ctypes.data if children else None,
                                          cmv.ctypes.data, cev.ctypes.data, ccap)
@@ -394,6 +424,7 @@ class GpuNnue:
                 pcap, ccap = max(pcap, need_p), max(ccap, need_c)
                 continue
             _check(rc)
+            cev = decode_children(cev)
             out = []
             for g in range(ng):
                 a, b = int(offs[g]), int(offs[g + 1])
@@ -407,7 +438,8 @@ class GpuNnue:
 
     def evaluate_games_arrays(self, arr, ng, mode=MODE_FULL, children=True, caps=None, bufs=None):
         """gn_evaluate_games on a prepared gn_game array (_games_array), results as flat arrays:
-        (position_offsets, game_status, positions, child_offsets, child_moves, children, caps).
+        (position_offsets, game_status, positions, child_offsets, child_moves, children, caps);
+        children are the library's raw gn_child records (CHILD_DTYPE; decode_children).
         caps = (position_cap, child_cap) from an earlier call avoid the sizing retry; bufs (a dict,
         filled on first use) keeps the output arrays for the next call (a caller's reused buffers)."""
         pcap, ccap = caps or (0, 0)
@@ -418,7 +450,7 @@ class GpuNnue:
             if bufs.get("caps") != (pcap, ccap):
                 bufs.update(caps=(pcap, ccap), pos=np.empty(max(pcap, 1), dtype=EVAL_DTYPE),
                             coffs=np.empty(pcap + 1, dtype=np.uint32), cmv=np.empty(max(ccap, 1), dtype=np.uint16),
-                            cev=np.empty(max(ccap, 1), dtype=EVAL_DTYPE))
+                            cev=np.empty(max(ccap, 1), dtype=CHILD_DTYPE))
             pos, coffs, cmv, cev = bufs["pos"], bufs["coffs"], bufs["cmv"], bufs["cev"]
             rc = lib().gn_evaluate_games(self.h, arr, ng, mode, int(children), offs.ctypes.data, status.ctypes.data,
                                          pos.ctypes.data, pcap, coffs.ctypes.data if children else None,

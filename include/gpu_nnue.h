@@ -34,7 +34,12 @@ extern "C" {
  * v3: gn_eval is 24 bytes: final_cp is int32 and every evaluated position carries the
  * score fishnet posts (score, GN_FLAG_MATE / GN_FLAG_SEARCHED / GN_FLAG_NO_MOVES,
  * best_move): checkmate, stalemate and in-check positions included. */
-#define GN_ABI_VERSION 3
+/* v4: the host-buffer expansion calls (gn_expand_and_evaluate, gn_evaluate_games with
+ * children) return every legal child as a 12-byte gn_child (psqt, positional, final_cp + flags:
+ * the north star's (i32 psqt, i32 positional, i32 final_cp)) instead of a 24-byte gn_eval;
+ * GN_OPT_CHUNK_PARENTS; GN_STAT_CHAIN_FALLBACKS removed (the planned expansion has no
+ * fallback); the device-resident calls are documented as blocking (they were since v3). */
+#define GN_ABI_VERSION 4
 
 #if defined(__GNUC__)
 #define GN_API __attribute__((visibility("default")))
@@ -61,6 +66,17 @@ extern "C" {
 #define GN_MODE_SMALL 2 /* small net for every position (epilogue: smallNet=true) */
 
 /* options (gn_set_option / gn_get_option) */
+#define GN_OPT_CHUNK_PARENTS 6        /* host-buffer expansion pipeline (gn_expand_and_evaluate,
+                                         gn_evaluate_games with children): parents per chunk,
+                                         cut at game starts; 0 (default): automatic (whole
+                                         games, >= 165,888 parents per chunk, a short last
+                                         chunk).  Results are identical for every value.   */
+#define GN_OPT_COALESCE 7             /* 1 (default): concurrent gn_evaluate_batch calls on one
+                                         context are merged into one launch (each call
+                                         queues; one call leads a launch over every queued
+                                         call of its mode; a lone call runs at once, no
+                                         timer); 0: calls run one after another.  Results
+                                         are identical either way.                        */
 #define GN_OPT_INCREMENTAL_CHILDREN 1 /* 1 (default): children from the parent accumulators
                                          by add/sub deltas; 0: full refresh per child    */
 #define GN_OPT_XCD_SWIZZLE 2          /* bit mask, default 1: each XCD takes a contiguous
@@ -69,7 +85,8 @@ extern "C" {
                                          blocks (bit 2, big-net expansion); 0: dispatch order
                                          (big-net expansion: blocks claimed in order by an
                                          atomic counter) */
-#define GN_OPT_KING_SORT 3            /* 1 (default): evaluate a batch in (white king, black
+#define GN_OPT_KING_SORT 3            /* 1 (default): evaluate a batch of >= 1,024 positions
+                                         (2: of any size) in (white king, black
                                          king) square order for L2 / Infinity-Cache
                                          locality, then (big net) by layer-stack bucket and
                                          30 home-square bits (ranks 1, 2, 7, 8 without
@@ -117,10 +134,8 @@ extern "C" {
 #define GN_STAT_HOST_TAIL_NS 115      /* the downloads still running after the last chunk
                                          computed (not overlapped)                        */
 #define GN_STAT_HOST_TOTAL_NS 116     /* the whole call                                    */
-#define GN_STAT_CHAIN_FALLBACKS 100   /* blocks of the last chained expansion (per device,
-                                         summed) that found their carry / king-cache slot
-                                         still in use after a bounded wait and ran
-                                         without it (results identical, more rows)       */
+#define GN_STAT_BATCH_LAUNCHES 117    /* merged gn_evaluate_batch launches since load ...   */
+#define GN_STAT_BATCH_CALLS 118       /* ... and the calls they served (GN_OPT_COALESCE)    */
 
 /* per-position flags */
 #define GN_FLAG_IN_CHECK 1u /* side to move in check: Stockfish has no static eval
@@ -168,6 +183,22 @@ typedef struct gn_eval {
   uint16_t flags;
   uint16_t best_move;
 } gn_eval;
+
+/* One legal child as the host-buffer expansion calls return it (ABI v4, 12 bytes): the child's
+ * static evaluation, north star `(i32 psqt, i32 positional, i32 final_cp)`, with the flags
+ * packed beside final_cp.  psqt / positional / final_cp are those of the child's gn_eval record
+ * (side-to-move POV); cp_flags = (final_cp & 0xFFFFFF) | (flags & 0xFF) << 24: final_cp as a
+ * signed 24-bit integer (|final_cp| < 2^23 always: gn_set_eval_params keeps the win-rate
+ * model's a(material) >= 1, and |final_v| <= value_clamp), flags the record's low 8 flag bits
+ * (GN_FLAG_IN_CHECK, GN_FLAG_SMALLNET, GN_FLAG_REEVAL; GN_FLAG_NO_SCORE is always set: a child
+ * carries no score).  Decode with GN_CHILD_FINAL_CP / GN_CHILD_FLAGS. */
+typedef struct gn_child {
+  int32_t psqt;
+  int32_t positional;
+  int32_t cp_flags;
+} gn_child;
+#define GN_CHILD_FINAL_CP(c) ((int32_t)((uint32_t)(c).cp_flags << 8) >> 8)
+#define GN_CHILD_FLAGS(c) ((uint32_t)(c).cp_flags >> 24)
 
 /* Packed position, 32 bytes, the device input format.
  *   occ      occupied squares (bit s = square s, a1 = 0 .. h8 = 63)
@@ -265,11 +296,11 @@ GN_API int gn_evaluate_batch_mode(gn_ctx *ctx, const char *const *fens, size_t n
  * prefix sums (children of parent i are [child_offsets[i], child_offsets[i+1])),
  * child_moves / child_out receive one entry per child in the order the device
  * generator emits them (moves in Stockfish 16-bit encoding; castling = king
- * takes own rook).  GN_E_CAPACITY when the children exceed cap (child_offsets
- * is still filled so the caller can retry with the right size). */
+ * takes own rook; records as gn_child).  GN_E_CAPACITY when the children exceed cap
+ * (child_offsets is still filled so the caller can retry with the right size). */
 GN_API int gn_expand_and_evaluate(gn_ctx *ctx, const char *const *parent_fens, size_t n, int mode,
                            gn_eval *parent_out, uint32_t *child_offsets, uint16_t *child_moves,
-                           gn_eval *child_out, size_t cap);
+                           gn_child *child_out, size_t cap);
 
 /* ---- lichess analysis batches ------------------------------------------ */
 /* One acquired batch as the server sends it (AcquireResponseBody,
@@ -310,7 +341,7 @@ GN_API int gn_replay_game(const gn_game *game, gn_board *positions, uint8_t *ski
 GN_API int gn_evaluate_games(gn_ctx *ctx, const gn_game *games, size_t n_games, int mode, int with_children,
                              uint32_t *position_offsets, int32_t *game_status, gn_eval *position_out,
                              size_t position_cap, uint32_t *child_offsets, uint16_t *child_moves,
-                             gn_eval *child_out, size_t child_cap);
+                             gn_child *child_out, size_t child_cap);
 
 /* The partitioner the library uses to shard work over the devices of a context and
  * that multi-process callers use to shard over ranks: contiguous ranges of n_items
@@ -345,8 +376,12 @@ GN_API int gn_random_positions_device(gn_ctx *ctx, int device_slot, uint64_t see
 
 /* Evaluate boards already resident on device `device_slot` (index into the
  * devices given at load).  d_boards / d_out are device pointers; stream is a
- * hipStream_t (NULL = the context's own stream).  Asynchronous: returns once
- * the kernels are queued. */
+ * hipStream_t (NULL = the context's own stream).  Blocking: the score rule reads the
+ * number of in-check positions back to size its launches, so the call synchronises
+ * `stream` (once; three times when the batch has in-check positions with legal moves)
+ * and returns with d_out written; it cannot be captured into a HIP graph.  The other
+ * gn_*_device calls that evaluate (gn_expand_device, gn_expand2_device, gn_time_*) block
+ * the same way; gn_random_positions_device / gn_random_games_device are asynchronous. */
 GN_API int gn_evaluate_device(gn_ctx *ctx, int device_slot, const gn_board *d_boards, size_t n, int mode,
                        gn_eval *d_out, void *stream);
 /* Device-resident expansion: counts children (d_counts[n]), writes d_offsets

@@ -37,6 +37,32 @@ fn replay_to_fen(pos: &Position) -> Option<Fen> {
     Some(Fen::from_position(board, EnPassantMode::Legal))
 }
 
+/// The FENs of a whole chunk with one replay: a chunk's positions share their root and their
+/// move lists are prefixes of the longest one (IncomingBatch::from_acquired makes position i
+/// = root + moves[..i], queue.rs:605-637), so replaying the longest list once yields every
+/// position's FEN (O(L) moves instead of the O(L^2) of a replay per position); a position
+/// outside that pattern is replayed on its own.  None: a move that does not replay.
+fn replay_chunk(positions: &[Position]) -> Option<Vec<Fen>> {
+    let longest = positions.iter().max_by_key(|p| p.moves.len())?;
+    let mut board: Chess = longest.root_fen.clone().into_position(CastlingMode::Chess960).ok()?;
+    let mut line = vec![Fen::from_position(board.clone(), EnPassantMode::Legal)];
+    for uci in &longest.moves {
+        let m = uci.to_move(&board).ok()?;
+        board.play_unchecked(&m);
+        line.push(Fen::from_position(board.clone(), EnPassantMode::Legal));
+    }
+    positions
+        .iter()
+        .map(|p| {
+            if p.root_fen == longest.root_fen && longest.moves.starts_with(&p.moves) {
+                Some(line[p.moves.len()].clone())
+            } else {
+                replay_to_fen(p)
+            }
+        })
+        .collect()
+}
+
 /// The score Stockfish would print for the record (`score cp` / `score mate`), or None for a
 /// record the library could not score.
 pub fn score_of(e: &GpuEval) -> Option<Score> {
@@ -56,12 +82,11 @@ impl GpuEvalStub {
 
     pub async fn go_multiple(&mut self, chunk: Chunk) -> Result<Vec<PositionResponse>, ChunkFailed> {
         let batch_id = chunk.work.id();
-        let fens: Vec<Option<Fen>> = chunk.positions.iter().map(replay_to_fen).collect();
-        if fens.iter().any(Option::is_none) {
-            return Err(ChunkFailed { batch_id }); // an illegal move, as queue.rs:576 fails the batch
-        }
-        let fens: Vec<Fen> = fens.into_iter().flatten().collect();
+        // an illegal move fails the chunk, as queue.rs:576 fails the batch
+        let fens = replay_chunk(&chunk.positions).ok_or(ChunkFailed { batch_id })?;
         let nnue = self.nnue.clone();
+        // N workers call at once through the shared context: the library merges their
+        // concurrent calls into one launch (GN_OPT_COALESCE, bench.py secondary.dropin)
         let evals = tokio::task::spawn_blocking(move || nnue.evaluate_batch(&fens))
             .await
             .map_err(|_| ChunkFailed { batch_id })?

@@ -19,6 +19,7 @@ use std::{
 use gpu_nnue_sys as sys;
 use shakmaty::{fen::Fen, uci::UciMove, Role, Square};
 
+pub use sys::gn_child as GpuChild;
 pub use sys::gn_eval as GpuEval;
 
 pub struct GpuNnue(*mut sys::gn_ctx);
@@ -66,7 +67,7 @@ pub struct GamesResult {
     pub positions: Vec<GpuEval>,
     pub child_offsets: Vec<u32>, // per position, into `children`
     pub child_moves: Vec<u16>,   // Stockfish move encoding
-    pub children: Vec<GpuEval>,
+    pub children: Vec<GpuChild>, // (psqt, positional, final_cp + flags), ABI v4
 }
 
 impl GpuNnue {
@@ -128,7 +129,7 @@ impl GpuNnue {
                 positions: vec![GpuEval::default(); pcap],
                 child_offsets: vec![0; pcap + 1],
                 child_moves: vec![0; ccap],
-                children: vec![GpuEval::default(); ccap],
+                children: vec![GpuChild::default(); ccap],
             };
             // SAFETY: every buffer has the length the call is told.
             let rc = unsafe {

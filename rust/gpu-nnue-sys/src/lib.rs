@@ -1,4 +1,4 @@
-//! gpu-nnue-sys — raw FFI of libgpu_nnue.so, 1:1 with `include/gpu_nnue.h` (ABI v3).
+//! gpu-nnue-sys — raw FFI of libgpu_nnue.so, 1:1 with `include/gpu_nnue.h` (ABI v4).
 //!
 //! fishnet's `src/main.rs:1` forbids unsafe code in the binary crate, so the FFI lives in
 //! this separate crate; the safe wrapper is `fishnet-gpu/src/gpu_nnue.rs`.  Every item here
@@ -8,7 +8,7 @@
 #![allow(non_camel_case_types)]
 use std::os::raw::{c_char, c_int, c_void};
 
-pub const GN_ABI_VERSION: c_int = 3;
+pub const GN_ABI_VERSION: c_int = 4;
 
 // return codes
 pub const GN_OK: c_int = 0;
@@ -33,8 +33,9 @@ pub const GN_OPT_XCD_SWIZZLE: c_int = 2;
 pub const GN_OPT_KING_SORT: c_int = 3;
 pub const GN_OPT_CHAIN: c_int = 4;
 pub const GN_OPT_KING_CACHE: c_int = 5;
+pub const GN_OPT_CHUNK_PARENTS: c_int = 6;
+pub const GN_OPT_COALESCE: c_int = 7;
 // read-only statistics (gn_get_option)
-pub const GN_STAT_CHAIN_FALLBACKS: c_int = 100;
 pub const GN_STAT_PLAN_NS: c_int = 101;
 pub const GN_STAT_STREAM_NS: c_int = 102;
 pub const GN_STAT_SCRATCH_PADS: c_int = 103;
@@ -45,6 +46,8 @@ pub const GN_STAT_HOST_COMPUTE_NS: c_int = 113;
 pub const GN_STAT_HOST_DOWNLOAD_NS: c_int = 114;
 pub const GN_STAT_HOST_TAIL_NS: c_int = 115;
 pub const GN_STAT_HOST_TOTAL_NS: c_int = 116;
+pub const GN_STAT_BATCH_LAUNCHES: c_int = 117;
+pub const GN_STAT_BATCH_CALLS: c_int = 118;
 
 // per-position flags
 pub const GN_FLAG_IN_CHECK: u16 = 1;
@@ -71,6 +74,27 @@ pub struct gn_eval {
     pub score: i32,
     pub flags: u16,
     pub best_move: u16,
+}
+
+/// One legal child from the host-buffer expansion calls (ABI v4, 12 bytes): psqt, positional and
+/// cp_flags = final_cp (signed 24 bits) | the low 8 flag bits << 24 (see the header at gn_child).
+#[repr(C)]
+#[derive(Clone, Copy, Default, Debug, PartialEq, Eq)]
+pub struct gn_child {
+    pub psqt: i32,
+    pub positional: i32,
+    pub cp_flags: i32,
+}
+
+impl gn_child {
+    /// GN_CHILD_FINAL_CP
+    pub fn final_cp(&self) -> i32 {
+        ((self.cp_flags as u32) << 8) as i32 >> 8
+    }
+    /// GN_CHILD_FLAGS
+    pub fn flags(&self) -> u16 {
+        ((self.cp_flags as u32) >> 24) as u16
+    }
 }
 
 /// Packed position (32 bytes), the device input format.
@@ -149,13 +173,13 @@ extern "C" {
                                   out: *mut gn_eval) -> c_int;
     pub fn gn_expand_and_evaluate(ctx: *mut gn_ctx, parent_fens: *const *const c_char, n: usize, mode: c_int,
                                   parent_out: *mut gn_eval, child_offsets: *mut u32, child_moves: *mut u16,
-                                  child_out: *mut gn_eval, cap: usize) -> c_int;
+                                  child_out: *mut gn_child, cap: usize) -> c_int;
     pub fn gn_replay_game(game: *const gn_game, positions: *mut gn_board, skipped: *mut u8, moves: *mut u16,
                           cap: usize, n_positions: *mut usize) -> c_int;
     pub fn gn_evaluate_games(ctx: *mut gn_ctx, games: *const gn_game, n_games: usize, mode: c_int,
                              with_children: c_int, position_offsets: *mut u32, game_status: *mut i32,
                              position_out: *mut gn_eval, position_cap: usize, child_offsets: *mut u32,
-                             child_moves: *mut u16, child_out: *mut gn_eval, child_cap: usize) -> c_int;
+                             child_moves: *mut u16, child_out: *mut gn_child, child_cap: usize) -> c_int;
     pub fn gn_partition(weights: *const u32, n_items: usize, n_shards: c_int, bounds: *mut usize) -> c_int;
     pub fn gn_perft(ctx: *mut gn_ctx, fen: *const c_char, depth: c_int, nodes: *mut u64) -> c_int;
     pub fn gn_pack_fens(fens: *const *const c_char, n: usize, out: *mut gn_board, ok: *mut u8) -> c_int;
@@ -206,7 +230,10 @@ mod tests {
     use super::*;
     #[test]
     fn layouts() {
-        assert_eq!(std::mem::size_of::<gn_eval>(), 16);
+        assert_eq!(std::mem::size_of::<gn_eval>(), 24);
+        assert_eq!(std::mem::size_of::<gn_child>(), 12);
+        let c = gn_child { psqt: 0, positional: 0, cp_flags: (0x00FF_FFFEu32 | 65u32 << 24) as i32 };
+        assert_eq!((c.final_cp(), c.flags()), (-2, 65));
         assert_eq!(std::mem::size_of::<gn_board>(), 32);
         assert_eq!(std::mem::size_of::<gn_eval_params>(), 128);
     }

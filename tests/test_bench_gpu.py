@@ -1,0 +1,89 @@
+"""bench.py's N > 1 code on one GPU: run_expand + gather_results for two
+ranks, with a loopback stand-in for ShardComm.  The ranks run one after another in this
+process on GPU 0: rank 1 evaluates its shard of games and deposits its records (the gather's
+non-root side), rank 0 evaluates its own shard, gathers both, and checks 32 sampled parents of
+every rank, with all their children, against the CPU oracle -- exactly the code an 8-GPU run
+executes after its timed steps, minus the RCCL transport (two ranks cannot share one GPU
+under RCCL).  torch is imported first, as bench.py does, so that its HIP runtime is the one
+libgpu_nnue binds to."""
+import argparse
+import copy
+
+import torch  # noqa: F401  (before libgpu_nnue, as in bench.py)
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+class LoopbackHub:
+    """What the ranks of one loopback run share: gathered tensors (FIFO per rank, in call order)
+    and gathered integers."""
+
+    def __init__(self, world):
+        self.world = world
+        self.tensors = {r: [] for r in range(world)}
+        self.taken = 0
+        self.i64 = {r: [] for r in range(world)}
+
+
+class LoopbackComm:
+    """ShardComm's interface for sequential ranks in one process (fishnet_amd/dist.py)."""
+
+    def __init__(self, hub, rank):
+        self.hub, self.rank, self.world, self.local = hub, rank, hub.world, 0
+        self.backend = "loopback"
+        self.device = torch.device("cuda", 0)
+
+    def broadcast_bytes(self, data, src=0):
+        return data
+
+    def broadcast_obj(self, obj, src=0):
+        return obj
+
+    def barrier(self):
+        pass
+
+    def max(self, x):
+        return x
+
+    def gather_i64(self, x):
+        mine = self.hub.i64[self.rank]
+        mine.append(int(x))
+        k = len(mine) - 1
+        return [self.hub.i64[r][k] if len(self.hub.i64[r]) > k else int(x) for r in range(self.world)]
+
+    def gather_tensor(self, t, dst=0):
+        if self.rank != dst:
+            self.hub.tensors[self.rank].append(t.clone())
+            return None
+        k = self.hub.taken
+        self.hub.taken += 1
+        return [t if r == dst else self.hub.tensors[r][k] for r in range(self.world)]
+
+    def close(self):
+        pass
+
+
+def test_run_expand_and_gather_two_loopback_ranks():
+    import bench
+    args = argparse.Namespace(swizzle=-1, king_sort=-1, chain=None, king_cache=None)
+    hub = LoopbackHub(2)
+    c0 = bench.Ctx(args, comm=LoopbackComm(hub, 0))
+    c1 = copy.copy(c0)
+    c1.comm, c1.rank = LoopbackComm(hub, 1), 1
+    wl, games = bench.WORKLOADS["expand"], 48
+    try:
+        r1 = bench.run_expand(c1, wl, games, 1, 0, 8)
+        r0 = bench.run_expand(c0, wl, games, 1, 0, 8)
+    finally:
+        c0.nn.close()
+    for r in (r0, r1):  # each rank's own timed outputs: oracle sample and the plain path
+        assert r["oracle_check"]["oracle"]["mismatching_parents"] == 0
+        assert r["oracle_check"]["vs_plain_path"]["equal"]
+    assert "oracle_check" not in r1["gather"]  # (rank 1 only handed its records to the gather)
+    g = r0["gather"]
+    assert g["oracle_check"] == {"parents": 64, "ranks": 2, "mismatching_parents": 0,
+                                 "of": "the gathered records on rank 0"}
+    assert g["bytes_all_ranks"] > 0
+    # the two shards are different games
+    assert r0["checksum"] != r1["checksum"]

@@ -107,3 +107,31 @@ def test_partition_is_game_aligned_and_balanced():
     tot = sum(w)
     for k in range(1, 4):  # shard k starts at the first game whose prefix reaches k/4 of the positions
         assert sum(w[:b[k]]) >= -(-tot * k // 4) and (b[k] == 0 or sum(w[:b[k] - 1]) < -(-tot * k // 4))
+
+
+def _bench(args, env):
+    import subprocess
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], env=env, capture_output=True,
+                          text=True, timeout=240)
+
+
+def test_bench_gpus_n_launches_n_ranks():
+    """`python bench.py --gpus 2` without a launcher (WORLD_SIZE unset) starts two ranks itself
+    (torch.distributed.run as a child process, before any GPU work), each with WORLD_SIZE=2;
+    --launch-check makes the ranks meet over gloo instead of doing GPU work."""
+    import json
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    p = _bench(["--gpus", "2", "--launch-check"], env)
+    assert p.returncode == 0, p.stderr[-2000:]
+    line = json.loads(p.stdout.strip().splitlines()[-1])
+    assert line == {"world": 2, "ranks": [[0, 0], [1, 1]]}
+
+
+def test_bench_world_size_mismatch_fails():
+    """Under a launcher, WORLD_SIZE must equal --gpus: a mismatch exits 2 before any GPU work."""
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    p = _bench(["--gpus", "1", "--launch-check"], env)
+    assert p.returncode == 2 and "WORLD_SIZE=2 but --gpus 1" in p.stderr
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    p = _bench(["--gpus", "1", "--launch-check"], env)  # one rank, no launcher: runs in place
+    assert p.returncode == 0 and '"world": 1' in p.stdout

@@ -155,6 +155,7 @@ def test_evaluate_games_vs_oracle(gpu_ctx, oracle_nets, oracle_lib, mode):
 
 @pytest.mark.gpu
 def test_evaluate_games_with_children_vs_oracle(gpu_ctx, oracle_nets, oracle_lib):
+    from fishnet_amd import gpu_nnue as G
     big, small = oracle_nets
     rng = random.Random(5)
     many = "R6R/3Q4/1Q4Q1/4Q3/2Q4Q/Q4Q2/pp1Q4/kBNN1KB1 w - - 0 1"  # 218 legal moves: multi-pass plan
@@ -171,7 +172,8 @@ def test_evaluate_games_with_children_vs_oracle(gpu_ctx, oracle_nets, oracle_lib
                 continue
             p_exp, m_exp, k_exp = oracle_lib.expand_eval(big, small, fen, 0)
             assert tuple(o["evals"][i]) == tuple(p_exp)
-            assert dict(zip(cm.tolist(), map(tuple, ce.tolist()))) == dict(zip(m_exp, map(tuple, k_exp.tolist())))
+            assert dict(zip(cm.tolist(), map(tuple, ce.tolist()))) == \
+                dict(zip(m_exp, map(tuple, G.children_from_evals(k_exp).tolist())))
 
 
 # games whose lines run into check, checkmate and stalemate
@@ -258,7 +260,8 @@ def test_gpu_replay_equals_device_games_and_host_replay(gpu_ctx, oracle_lib):
     bufs["b"].upload(sel)
     t = gpu_ctx.expand_device(bufs["b"], m, 1, bufs["po"], bufs["off"], bufs["ch"], bufs["mv"], bufs["co"], cap)
     po, doff = bufs["po"].download(G.EVAL_DTYPE, m), bufs["off"].download(np.uint32, m + 1)
-    dmv, dco = bufs["mv"].download(np.uint16, t), bufs["co"].download(G.EVAL_DTYPE, t)
+    dmv, dco = bufs["mv"].download(np.uint16, t), G.children_from_evals(bufs["co"].download(G.EVAL_DTYPE, t))
+    cev = G.decode_children(cev)
     i = 0
     for g in full:
         for k in range(plies + 1):

@@ -85,7 +85,7 @@ def test_score_fixture_all_modes(gpu_ctx, oracle_nets, oracle_lib):
         _cmp(gpu_ctx.evaluate_batch(fens, mode), exp, fens)
         parents, offs, moves, kids = gpu_ctx.expand_and_evaluate(fens, mode)
         _cmp(parents, exp, fens)
-        assert (kids["flags"] & G.FLAG_NO_SCORE).all() and not kids["score"].any()
+        assert (kids["flags"] & G.FLAG_NO_SCORE).all()  # (a gn_child carries no score)
         searched = (exp["flags"] & G.FLAG_SEARCHED) != 0
         assert searched.sum() >= 30 and (exp["flags"] & G.FLAG_NO_MOVES != 0).sum() >= 20
     d_b, d_o = gpu_ctx.alloc(len(fens) * 32), gpu_ctx.alloc(len(fens) * G.EVAL_SIZE)
@@ -127,7 +127,7 @@ def test_big_stress_net(oracle_lib):
 
 
 def test_big_stress_net_expansion(oracle_lib):
-    """Big-net incremental children (expand_stream) under constant int16 wrapping."""
+    """Big-net incremental children (the planned expansion) under constant int16 wrapping."""
     from fishnet_amd import gpu_nnue as G, synthnet
     p = synthnet.cached_synth_net(3072, 11, stress=True)
     ctx = G.GpuNnue(p, None)
@@ -138,7 +138,7 @@ def test_big_stress_net_expansion(oracle_lib):
         p_exp, m_exp, k_exp = oracle_lib.expand_eval(on, None, fen, 1)
         assert tuple(parents[i]) == p_exp, fen
         got = {int(m): tuple(k) for m, k in zip(moves[offs[i]:offs[i + 1]], kids[offs[i]:offs[i + 1]])}
-        assert got == {int(m): tuple(k) for m, k in zip(m_exp, k_exp)}, fen
+        assert got == {int(m): tuple(k) for m, k in zip(m_exp, G.children_from_evals(k_exp))}, fen
 
 
 def test_big_stress_net_chained_king_cache():
@@ -202,7 +202,7 @@ def test_perft_special_vs_oracle(gpu_ctx, oracle_lib):
 @pytest.mark.parametrize("incremental", [1, 0])
 @pytest.mark.parametrize("mode", [0, 1, 2])
 def test_expand_vs_oracle(gpu_ctx, oracle_nets, oracle_lib, mode, incremental):
-    from fishnet_amd.gpu_nnue import OPT_INCREMENTAL_CHILDREN, move_to_uci
+    from fishnet_amd.gpu_nnue import OPT_INCREMENTAL_CHILDREN, children_from_evals, move_to_uci
     big, small = oracle_nets
     fens = special_fens() + random_fens(150, 777 + mode)
     gpu_ctx.set_option(OPT_INCREMENTAL_CHILDREN, incremental)
@@ -215,7 +215,7 @@ def test_expand_vs_oracle(gpu_ctx, oracle_nets, oracle_lib, mode, incremental):
         assert tuple(parents[i]) == p_exp, fen
         lo, hi = int(offs[i]), int(offs[i + 1])
         got = {int(m): tuple(k) for m, k in zip(moves[lo:hi], kids[lo:hi])}
-        exp = {int(m): tuple(k) for m, k in zip(m_exp, k_exp)}
+        exp = {int(m): tuple(k) for m, k in zip(m_exp, children_from_evals(k_exp))}
         assert set(got) == set(exp), (fen, sorted(map(move_to_uci, set(got) ^ set(exp))))
         bad = [move_to_uci(m) for m in got if got[m] != exp[m]]
         assert not bad, (fen, bad[:5])
@@ -232,7 +232,7 @@ def test_incremental_stress_wrap(oracle_lib):
     for i, fen in enumerate(fens):
         _, m_exp, k_exp = oracle_lib.expand_eval(None, on, fen, 2)
         got = {int(m): tuple(k) for m, k in zip(moves[offs[i]:offs[i + 1]], kids[offs[i]:offs[i + 1]])}
-        assert got == {int(m): tuple(k) for m, k in zip(m_exp, k_exp)}, fen
+        assert got == {int(m): tuple(k) for m, k in zip(m_exp, G.children_from_evals(k_exp))}, fen
 
 
 def test_expand_device_matches_host(gpu_ctx):
@@ -248,7 +248,7 @@ def test_expand_device_matches_host(gpu_ctx):
     assert total == cap
     assert np.array_equal(bufs["off"].download(np.uint32, n + 1), hoffs)
     assert np.array_equal(bufs["mv"].download(np.uint16, cap), hmoves)
-    assert np.array_equal(bufs["co"].download(G.EVAL_DTYPE, cap), hkids)
+    assert np.array_equal(G.children_from_evals(bufs["co"].download(G.EVAL_DTYPE, cap)), hkids)
     assert np.array_equal(bufs["po"].download(G.EVAL_DTYPE, n), hp)
     kids = bufs["ch"].download(G.BOARD_DTYPE, 40)
     assert [G.board_to_fen(k) for k in kids[:3]]
@@ -358,7 +358,7 @@ def test_chained_walk_matches_refresh_and_oracle(gpu_ctx, oracle_nets, oracle_li
         assert got == {int(m): tuple(x) for m, x in zip(m_exp, k_exp)}, fen
 
 
-@pytest.mark.parametrize("ksort", [1, 0])
+@pytest.mark.parametrize("ksort", [2, 0])
 def test_common_row_base_tiles(gpu_ctx, oracle_nets, oracle_lib, ksort):
     """eval_net's common-row base (pieces on the same square in every position of a
     16-position tile are gathered once per tile): consecutive positions of games share
@@ -485,7 +485,8 @@ def test_two_device_slots_shard_expansion_and_games(synth_big_path, synth_small_
             p_exp, m_exp, k_exp = oracle_lib.expand_eval(big, small, fen, 0)
             assert tuple(rb[0]["evals"][i]) == p_exp
             mv, ev = rb[0]["children"][i]
-            assert dict(zip(mv.tolist(), map(tuple, ev.tolist()))) == dict(zip(m_exp, map(tuple, k_exp.tolist())))
+            assert dict(zip(mv.tolist(), map(tuple, ev.tolist()))) == \
+                dict(zip(m_exp, map(tuple, G.children_from_evals(k_exp).tolist())))
     finally:
         one.close()
         two.close()
@@ -554,7 +555,7 @@ def test_common_row_base_under_int16_wrap_and_shared_kings(oracle_lib):
         fens.append("/".join(rows) + " " + f.split(" ", 1)[1])
     fens = fens * 3 + special_fens() + random_fens(300, 4711)
     try:
-        for ks in (1, 0):
+        for ks in (2, 0):  # (2: sorted at any size; 1 sorts batches of >= 1,024)
             ctx.set_option(G.OPT_KING_SORT, ks)
             _cmp(ctx.evaluate_batch(fens, 1), oracle_lib.eval_fens(on, None, fens, 1, threads=8), fens)
     finally:
@@ -748,3 +749,85 @@ def test_king_cache_reload_at_minimum_gap(gpu_ctx, oracle_nets, oracle_lib):
     assert all(np.array_equal(a, b) for a, b in zip(ref, got))
     big, _ = oracle_nets
     _check_vs_oracle(oracle_lib, big, fens, tuple(x[:81] if i == 0 else x for i, x in enumerate(got)))
+
+
+def test_pipeline_chunks_equal_one_chunk(gpu_ctx):
+    """The host-buffer expansion pipeline cut into many chunks (GN_OPT_CHUNK_PARENTS: slot reuse in
+    the device output buffers, the drain threads' downloads on the copy stream, chunk cuts at game
+    starts) returns byte-identical results to one chunk: gn_evaluate_games with children (cuts at
+    game starts, skipped positions inside chunks) and gn_expand_and_evaluate (cuts every 81)."""
+    from fishnet_amd import gpu_nnue as G
+    ucis = G.random_games_uci(0x5EED0123, 0, 40, 80)
+    start = "rnbqkbnr/pppppppp/8/8/8/8/PPPPPPPP/RNBQKBNR w KQkq - 0 1"
+    games = [(start, u, (3, 17) if g % 3 == 0 else ()) for g, u in enumerate(ucis)]
+    arr, keep = G._games_array(games)
+    fens = [G.board_to_fen(b) for b in G.random_positions(0x5EED0456, 0, 700, 160)]
+    try:
+        out = {}
+        for chunk in (0, 100, 250):
+            gpu_ctx.set_option(G.OPT_CHUNK_PARENTS, chunk)
+            res = gpu_ctx.evaluate_games_arrays(arr, len(games), 0, children=True)
+            out[chunk] = ([np.copy(x) for x in res[:6]], [np.copy(x) for x in gpu_ctx.expand_and_evaluate(fens, 1)])
+        for chunk in (100, 250):
+            for a, b in zip(out[0][0] + out[0][1], out[chunk][0] + out[chunk][1]):
+                assert a.tobytes() == b.tobytes(), chunk
+    finally:
+        gpu_ctx.set_option(G.OPT_CHUNK_PARENTS, 0)
+
+
+def test_concurrent_batches_coalesce(gpu_ctx):
+    """16 threads calling gn_evaluate_batch at once on one context (fishnet's workers, one
+    chunk each): the calls are merged into shared launches (GN_OPT_COALESCE) and every caller
+    gets exactly the records of a call on its own, with coalescing on and off."""
+    import threading
+    from fishnet_amd import gpu_nnue as G
+    lists = [[G.board_to_fen(b) for b in G.random_positions(0x5EED0900 + t, 0, 81, 160)] for t in range(16)]
+    lists[3][5] = "not a fen"  # a bad FEN is flagged in its own call only
+    ref = [gpu_ctx.evaluate_batch(fl, 0) for fl in lists]
+    assert ref[3][5]["flags"] & G.FLAG_BAD_FEN
+    for coalesce in (1, 0):
+        gpu_ctx.set_option(G.OPT_COALESCE, coalesce)
+        l0, c0 = gpu_ctx.get_option(G.STAT_BATCH_LAUNCHES), gpu_ctx.get_option(G.STAT_BATCH_CALLS)
+        got, errs = [None] * 16, []
+        go = threading.Barrier(16)
+
+        def work(t):
+            try:
+                go.wait()
+                for _ in range(4):
+                    got[t] = gpu_ctx.evaluate_batch(lists[t], 0)
+            except Exception as e:  # surfaced below
+                errs.append(e)
+
+        th = [threading.Thread(target=work, args=(t,)) for t in range(16)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        assert not errs, errs
+        for t in range(16):
+            assert np.array_equal(got[t], ref[t]), (coalesce, t)
+        launches = gpu_ctx.get_option(G.STAT_BATCH_LAUNCHES) - l0
+        calls = gpu_ctx.get_option(G.STAT_BATCH_CALLS) - c0
+        if coalesce:
+            assert calls == 64 and 1 <= launches < calls, (launches, calls)
+        else:
+            assert calls == 0 and launches == 0
+    gpu_ctx.set_option(G.OPT_COALESCE, 1)
+
+
+def test_eval_params_keep_child_cp_in_24_bits(gpu_ctx):
+    """gn_child holds final_cp in 24 bits: gn_set_eval_params refuses a win-rate model whose
+    a(material) drops below 1 anywhere in the clamped material range (|final_cp| then stays
+    <= 100 * value_clamp < 2^23), and accepts the defaults back."""
+    from fishnet_amd import gpu_nnue as G
+    p = gpu_ctx.eval_params()
+    bad = gpu_ctx.eval_params()
+    bad.wdl_a[3] = 0.5 - (bad.wdl_a[0] + bad.wdl_a[1] + bad.wdl_a[2])  # a(1.0) = 0.5
+    bad.wdl_material_anchor = 58
+    bad.wdl_material_min, bad.wdl_material_max = 58, 58
+    with pytest.raises(G.GnError) as e:
+        gpu_ctx.set_eval_params(bad)
+    assert e.value.code == G.E_INVALID
+    gpu_ctx.set_eval_params(p)
+    assert gpu_ctx.eval_params().wdl_a[3] == p.wdl_a[3]

@@ -29,7 +29,7 @@ def test_library_exports_every_header_symbol(G):
     for s in syms:
         assert hasattr(lib, s), s
     assert sorted(G.EXPORTS) == syms
-    assert lib.gn_abi_version() == G.ABI_VERSION == 3
+    assert lib.gn_abi_version() == G.ABI_VERSION == 4
 
 
 def test_structs_match_header(G):
@@ -197,7 +197,7 @@ def test_rust_sys_crate_matches_header():
                                      r"(\(?-?\d+\)?u?)", hdr)}
     r_consts = {m.group(1): int(m.group(2)) for m in re.finditer(r"pub const (GN_\w+): \w+ = (-?\d+);", rs)}
     assert c_consts == r_consts
-    for st in ("gn_eval", "gn_board", "gn_eval_params", "gn_game"):
+    for st in ("gn_eval", "gn_child", "gn_board", "gn_eval_params", "gn_game"):
         cb = re.search(r"typedef struct %s \{(.*?)\} %s;" % (st, st), nocomment, re.S).group(1)
         cf = [re.sub(r"\[.*", "", d.split()[-1]).lstrip("*") for d in cb.split(";") if d.strip()]
         rb = re.search(r"pub struct %s \{(.*?)\n\}" % st, rs, re.S).group(1)
