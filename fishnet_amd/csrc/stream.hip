@@ -884,9 +884,14 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
         const int8_t *wb = net.w0f + (((size_t)b * KS + KPW * wave) * 64 + ln) * 16;
         int4v acc = {0, 0, 0, 0};
         // (batches of FB k-steps: the next tile's rows stay in flight in registers meanwhile)
+        // (`stop`, always 0, is opaque to the compiler: without a runtime exit test it schedules the
+        // fully unrolled loop's loads so that the kernel spills 20 VGPRs, a 3 % slower stream;
+        // tests/test_host.py::test_stream_kernel_does_not_spill)
         constexpr int FB = 2;
+        int stop = 0;
+        asm volatile("" : "+s"(stop));
 #pragma unroll
-        for (int k0 = 0; k0 < KPW; k0 += FB) {
+        for (int k0 = 0; k0 < KPW && !stop; k0 += FB) {
           int4v wv[FB], av[FB];
 #pragma unroll
           for (int j = 0; j < FB; ++j) wv[j] = *reinterpret_cast<const int4v *>(wb + 1024 * (k0 + j));

@@ -8,3 +8,5 @@ cat gpurun_out/r04c/dropin.json
 timeout -k 10 300 python -u bench.py --abi-games 49152 --steps 3 > gpurun_out/r04c/abi.json 2> gpurun_out/r04c/abi.err || { tail -30 gpurun_out/r04c/abi.err; exit 1; }
 cat gpurun_out/r04c/abi.json
 timeout -k 10 600 python tools/ab.py --variants libgpu_nnue.so libgpu_nnue_kc2.so libgpu_nnue.so libgpu_nnue_kc2.so -- --steps 8 --check 0 || exit 1
+GPU_NNUE_LIB=$GRAFT_REPO_ROOT/fishnet_amd/lib/libgpu_nnue_pp.so timeout -k 10 300 python -u bench.py --steps 1 --warmup 0 --no-secondary --no-cpu-baseline --check 0 > gpurun_out/r04c/pp.json 2> gpurun_out/r04c/pp.err || { tail -30 gpurun_out/r04c/pp.err; exit 1; }
+grep "plan prof" gpurun_out/r04c/pp.err | tail -3
