@@ -316,7 +316,8 @@ struct gn_ctx {
   bool coalesce = true;
   gn_eval_params P;
   bool incremental = true; // GN_OPT_INCREMENTAL_CHILDREN
-  int swizzle = 1;          // GN_OPT_XCD_SWIZZLE bit mask: 1 expansion, 2 batch evaluation
+  int swizzle = 9;          // GN_OPT_XCD_SWIZZLE bit mask: 1 small-net expansion, 2 batch evaluation,
+                            // 4 / 8 big-net expansion (static eighths / XCD-local claiming)
   int king_sort = 1;        // GN_OPT_KING_SORT (1: batches of >= KING_SORT_MIN positions, 2: all)
   int chain = 81;           // GN_OPT_CHAIN (blocks of consecutive parents per workgroup)
   bool king_cache = true;   // GN_OPT_KING_CACHE
@@ -764,8 +765,8 @@ static int expand_evaluate(gn_ctx *ctx, Dev &d, const gn_board *parents, size_t 
       HIP_TRY(d.ent.ensure(d.etot + 16 * (nblk + 1)));
       HIP_TRY(d.tiles.ensure((n + total) / 16 + (K + 2) * nblk + 2));
       HIP_TRY(d.btiles.ensure(nblk + 1));
-      HIP_TRY(d.pool.ensure(65)); // 8 XCDs x 8 words of scratch-slot bits, then the block claim counter
-      HIP_TRY(hipMemsetAsync(d.pool.p, 0, 65 * sizeof(uint32_t), s));
+      HIP_TRY(d.pool.ensure(72)); // 8 XCDs x 8 words of scratch-slot bits, then 8 block claim counters
+      HIP_TRY(hipMemsetAsync(d.pool.p, 0, 72 * sizeof(uint32_t), s));
       // XCD-local block order
       const uint32_t *order = nullptr;
       if (ctx->king_sort && nblk > 1) {
@@ -778,7 +779,8 @@ static int expand_evaluate(gn_ctx *ctx, Dev &d, const gn_board *parents, size_t 
         order = d.border.p;
       }
       HIP_TRY(launch_plan_stream(d.net[BIG], parents, n, off, dl, f ? d.p_nbg.p : nullptr, f ? d.nbg.p : nullptr,
-                                 d.p_obg.p, d.obg.p, (ctx->swizzle >> 2) & 1, d.chain_k > 1 ? d.nslot.p : nullptr, d.chain_k,
+                                 d.p_obg.p, d.obg.p, (ctx->swizzle >> 2) & 1 ? 1 : (ctx->swizzle >> 3) & 1 ? 2 : 0,
+                                 d.chain_k > 1 ? d.nslot.p : nullptr, d.chain_k,
                                  ctx->king_cache ? 1 : 0, d.eoff.p, d.ent.p, d.tiles.p, d.btiles.p, d.pool.p, d.perr.p,
                                  rows_out, d.pstat.p, 0, nblk, order, ev ? ev[4] : nullptr, s));
     } else { // a 128-wide net loaded as the big net
@@ -2252,7 +2254,7 @@ int gn_set_option(gn_ctx *ctx, int option, int64_t value) {
     ctx->incremental = value != 0;
     return GN_OK;
   case GN_OPT_XCD_SWIZZLE:
-    ctx->swizzle = (int)(value & 7);
+    ctx->swizzle = (int)(value & 15);
     return GN_OK;
   case GN_OPT_KING_SORT:
     if (value < 0 || value > 2) return fail(GN_E_INVALID, "king sort must be 0, 1 or 2");

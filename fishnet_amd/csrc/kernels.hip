@@ -278,9 +278,12 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR) __attribute__((amdgpu_wav
     const uint32_t j16 = 16 * j; // byte offset of this thread's columns in a row
     const int nc = ccnt;
     const uint16_t *cr = crow[h];
-    // rows rr[0..cnt) added to lo/hi and, on lane j == 0 when wps, their PSQT dword
-    // (16-B half at pso, element pse) to ps; 4 rows in flight, tail as one batch
-    auto gather = [&](const uint16_t *rr, int cnt, ushort8 &lo, ushort8 &hi, uint32_t &ps, uint32_t pso, int pse,
+    // rows rr[0..cnt) added to lo/hi and, on lane j == 0 when wps, their PSQT at the position's
+    // bucket to ps, read from the bucket-major copy pt = net.psqt + bucket * FT_ROWS (90 KB per
+    // bucket, its lines shared by all the rows of a king bucket) rather than the row's own PSQT
+    // part, a line of its own per row (a third line per row for the small net, whose weights are
+    // two); 4 rows in flight, tail as one batch
+    auto gather = [&](const uint16_t *rr, int cnt, ushort8 &lo, ushort8 &hi, uint32_t &ps, const int32_t *pt,
                       bool wps) {
       int k = 0;
       for (; k + 4 <= cnt; k += 4) {
@@ -293,13 +296,9 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR) __attribute__((amdgpu_wav
         const ushort8 b1 = ldft(net.ft, j16 + o1 + L1);
         const ushort8 b2 = ldft(net.ft, j16 + o2 + L1);
         const ushort8 b3 = ldft(net.ft, j16 + o3 + L1);
-        if (wps && j == 0) {
-          const int4v v0 = ldps(net.ft, o0 + pso);
-          const int4v v1 = ldps(net.ft, o1 + pso);
-          const int4v v2 = ldps(net.ft, o2 + pso);
-          const int4v v3 = ldps(net.ft, o3 + pso);
-          ps += (uint32_t)v0[pse] + (uint32_t)v1[pse] + (uint32_t)v2[pse] + (uint32_t)v3[pse];
-        }
+        if (wps && j == 0)
+          ps += (uint32_t)pt[ft_row(rr[k])] + (uint32_t)pt[ft_row(rr[k + 1])] + (uint32_t)pt[ft_row(rr[k + 2])] +
+                (uint32_t)pt[ft_row(rr[k + 3])];
         lo += (a0 + a1) + (a2 + a3);
         hi += (b0 + b1) + (b2 + b3);
       }
@@ -312,9 +311,9 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR) __attribute__((amdgpu_wav
         const ushort8 b2 = ldft(net.ft, j16 + o2 + L1);
         uint32_t q0 = 0, q1 = 0, q2 = 0;
         if (wps && j == 0) {
-          q0 = (uint32_t)(ldps(net.ft, o0 + pso))[pse];
-          q1 = (uint32_t)(ldps(net.ft, o1 + pso))[pse];
-          q2 = (uint32_t)(ldps(net.ft, o2 + pso))[pse];
+          q0 = (uint32_t)pt[ft_row(rr[k])];
+          q1 = (uint32_t)pt[ft_row(rr[k1])];
+          q2 = (uint32_t)pt[ft_row(rr[k2])];
         }
         lo += a0, hi += b0, ps += q0;
         if (k + 1 < cnt) lo += a1, hi += b1, ps += q1;
@@ -326,7 +325,7 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR) __attribute__((amdgpu_wav
     ushort8 base_hi = *reinterpret_cast<const ushort8 *>(net.bias + L1 / 2 + 8 * j);
     {
       uint32_t unused = 0;
-      gather(cr, nc, base_lo, base_hi, unused, 0, 0, false);
+      gather(cr, nc, base_lo, base_hi, unused, nullptr, false);
     }
 #pragma unroll 1
     for (int r = 0; r < TILE / PAR; ++r) {
@@ -335,12 +334,11 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR) __attribute__((amdgpu_wav
       if (!cnt) continue;
       ushort8 lo = base_lo, hi = base_hi;
       uint32_t ps = 0;
-      const uint32_t pso = 2 * L1 + ((bkt[p] >> 2) << 4);
-      const int pse = bkt[p] & 3;
+      const int32_t *pt = net.psqt + (size_t)bkt[p] * FT_ROWS;
       if (j == 0) { // PSQT of the common rows at this position's bucket (one lane)
-        for (int k = 0; k < nc; ++k) ps += (uint32_t)(ldps(net.ft, ft_row(cr[k]) * RS + pso))[pse];
+        for (int k = 0; k < nc; ++k) ps += (uint32_t)pt[ft_row(cr[k])];
       }
-      gather(rows[p][h], cnt - nc, lo, hi, ps, pso, pse, true);
+      gather(rows[p][h], cnt - nc, lo, hi, ps, pt, true);
       // transform: clamp to [0, 254] in the doubled domain, product / 512
       const int rel = CB ? h ^ sstm[p] : h; // 0: side to move
       *reinterpret_cast<uint2 *>(xt + p * XS + rel * (L1 / 2) + 8 * j) = transform8(lo, hi);

@@ -642,17 +642,37 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
   // The grid has nblk + nblk / 16 + 8 workgroups then: the hardware hands every XCD the same
   // number of them, so a faster XCD needs spare workgroups to take more blocks, and the ones
   // left over once every block is claimed end here.
+  // swz 2: each XCD claims the blocks of its own contiguous eighth of the order (claim[x]), so
+  // that the blocks resident on one XCD (sharing its L2) are neighbours in the king order, and
+  // one that has run out takes the next unclaimed block of another XCD's eighth.
   const uint32_t nblk = b1 - b0;
-  const uint32_t vgrid = swz ? 8 * ((nblk + 7) / 8) : nblk;
+  const uint32_t vgrid = swz == 1 ? 8 * ((nblk + 7) / 8) : nblk;
   uint32_t v = blockIdx.x;
-  if (!swz) {
+  if (swz == 0) {
     if (tid == 0) sblk = atomicAdd(claim, 1u);
     __syncthreads();
     v = sblk;
+  } else if (swz == 2) {
+    if (tid == 0) {
+      uint32_t x;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+      x &= 7;
+      const uint32_t per = (nblk + 7) / 8;
+      uint32_t got = ~0u;
+      for (uint32_t t = 0; t < 8 && got == ~0u; ++t) {
+        const uint32_t y = (x + t) & 7, lo = y * per, hi = lo + per < nblk ? lo + per : nblk;
+        if (lo >= hi || __hip_atomic_load(claim + y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= hi - lo) continue;
+        const uint32_t i = atomicAdd(claim + y, 1u);
+        if (i < hi - lo) got = lo + i;
+      }
+      sblk = got;
+    }
+    __syncthreads();
+    v = sblk; // ~0u: every block is claimed (v >= vgrid below)
   }
   if (v >= vgrid) return;
   uint32_t blk = v;
-  if (swz) {
+  if (swz == 1) {
     const uint32_t b8 = (nblk + 7) / 8;
     blk = (v & 7) * b8 + (v >> 3);
     if (blk >= nblk) return;
@@ -1017,7 +1037,7 @@ hipError_t launch_plan_stream(const NetDevice &net, const gn_board *parents, siz
   const int scr = K > 1 && kc; // the king cache's rows (the chained walk itself needs no scratch)
   if (b1 > (n + K - 1) / K) return hipErrorInvalidValue;
   const uint32_t nb = (uint32_t)(b1 - b0), B0 = (uint32_t)b0, B1 = (uint32_t)b1;
-  const unsigned pg = (nb + 3) / 4, g = swz ? 8 * ((nb + 7) / 8) : nb + nb / 16 + 8; // (stream_eval_kernel: claims)
+  const unsigned pg = (nb + 3) / 4, g = swz == 1 ? 8 * ((nb + 7) / 8) : nb + nb / 16 + 8; // (stream_eval_kernel: claims)
   if (net.L1 == 3072) {
     hipLaunchKernelGGL((plan_kernel<3072>), dim3(pg), dim3(256), 0, s, net, parents, offsets, deltas, need_parent,
                        need_child, K > 1 ? next_slot : nullptr, (uint32_t)n, K, B0, B1, K > 1 ? kc : 0, eoff, ent,

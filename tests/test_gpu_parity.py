@@ -308,8 +308,11 @@ def test_locality_options_do_not_change_results(gpu_ctx, swz, ksort):
         gpu_ctx.set_option(G.OPT_XCD_SWIZZLE, 7 - swz)
         _, offs2, moves2, kids2 = gpu_ctx.expand_and_evaluate(fens, 1)
         assert np.array_equal(kids, kids2) and np.array_equal(moves, moves2)
+        gpu_ctx.set_option(G.OPT_XCD_SWIZZLE, 8)  # XCD-local block claiming
+        _, offs3, moves3, kids3 = gpu_ctx.expand_and_evaluate(fens, 1)
+        assert np.array_equal(kids, kids3) and np.array_equal(moves, moves3)
     finally:
-        gpu_ctx.set_option(G.OPT_XCD_SWIZZLE, 1)
+        gpu_ctx.set_option(G.OPT_XCD_SWIZZLE, 9)
         gpu_ctx.set_option(G.OPT_KING_SORT, 1)
 
 
