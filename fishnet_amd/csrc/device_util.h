@@ -145,6 +145,88 @@ __device__ __forceinline__ uint2 transform8(ushort8 lo, ushort8 hi) {
   return make_uint2(__builtin_amdgcn_perm(o[1], o[0], 0x06040200u), __builtin_amdgcn_perm(o[3], o[2], 0x06040200u));
 }
 
+// Layer stack of one bucket by ONE wave (eval_net's small net): fc_0 accumulates all L1/64
+// k-steps in registers (no partial sums through LDS, no workgroup barrier), so a tile's
+// buckets run on separate waves at once and the workgroup's other waves are done.  The fc_0
+// result is in the lane layout of the MFMA accumulator, which is exactly what the
+// epilogue of layer_stack_tile reads back from LDS, so the math below is the same.
+// in1: this wave's 16 x 32 B, fwd: its 16 ints (LDS, private to the wave).
+template <int L1, class Valid, class Emit>
+__device__ __forceinline__ void layer_stack_wave(const NetDevice &net, const uint8_t *xt, uint8_t (*in1)[32],
+                                                 int32_t *fwd, const int32_t (*psq)[2], int b, int lane,
+                                                 Valid &&valid, Emit &&emit) {
+  constexpr int XS = L1 + 16, KS = L1 / 64, BATCH = KS % 6 == 0 ? 6 : KS % 4 == 0 ? 4 : KS;
+  static_assert(KS % BATCH == 0, "k-steps per batch");
+  const int row = lane & 15, kg = lane >> 4;
+  // fc_1 / fc_2 parameters first: their latency hides behind fc_0
+  const int4v zero = {0, 0, 0, 0};
+  int4v wl = zero, wh = zero;
+  if (kg < 2) {
+    wl = *reinterpret_cast<const int4v *>(net.w1 + ((size_t)b * 32 + row) * 32 + kg * 16);
+    wh = *reinterpret_cast<const int4v *>(net.w1 + ((size_t)b * 32 + 16 + row) * 32 + kg * 16);
+  }
+  const int32_t bias0 = net.b0[b * 16 + row];
+  const int32_t b1l = net.b1[b * 32 + row], b1h = net.b1[b * 32 + 16 + row];
+  const int32_t w2l = net.w2[b * 32 + row], w2h = net.w2[b * 32 + 16 + row];
+  const int32_t b2v = net.b2[b];
+  constexpr bool FRAG = L1 > 128; // as layer_stack_tile: w0f for the big nets, row-major w0 for 128
+  const int8_t *wb = FRAG ? net.w0f + ((size_t)b * KS * 64 + lane) * 16 : net.w0 + ((size_t)b * 16 + row) * L1 + kg * 16;
+  const uint8_t *xa = xt + row * XS + kg * 16;
+  int4v acc = zero;
+#pragma unroll 1
+  for (int k0 = 0; k0 < KS; k0 += BATCH) {
+    int4v w[BATCH], a[BATCH];
+#pragma unroll
+    for (int j = 0; j < BATCH; ++j) w[j] = *reinterpret_cast<const int4v *>(wb + (FRAG ? 1024 : 64) * (k0 + j));
+#pragma unroll
+    for (int j = 0; j < BATCH; ++j) a[j] = *reinterpret_cast<const int4v *>(xa + 64 * (k0 + j));
+#pragma unroll
+    for (int j = 0; j < BATCH; ++j) acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[j], w[j], acc, 0, 0, 0);
+  }
+  // SqrClippedReLU / ClippedReLU of fc_0 outputs 0..14, skip term from output 15
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int pos = 4 * kg + i;
+    const int32_t v = wadd(acc[i], bias0);
+    if (row < 15) {
+      const long long s2 = ((long long)v * v) >> 19;
+      in1[pos][row] = (uint8_t)(s2 < 127 ? s2 : 127);
+      in1[pos][15 + row] = (uint8_t)clampi(v >> 6, 0, 127);
+    } else {
+      fwd[pos] = wmul(v, 600 * 16) / (127 * 64);
+      in1[pos][30] = 0;
+      in1[pos][31] = 0;
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const int4v a1 = kg < 2 ? *reinterpret_cast<const int4v *>(&in1[row][kg * 16]) : zero;
+  const int4v cl = __builtin_amdgcn_mfma_i32_16x16x64_i8(a1, wl, zero, 0, 0, 0);
+  const int4v ch = __builtin_amdgcn_mfma_i32_16x16x64_i8(a1, wh, zero, 0, 0, 0);
+  int32_t part[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int32_t l = clampi(wadd(cl[i], b1l) >> 6, 0, 127), hh = clampi(wadd(ch[i], b1h) >> 6, 0, 127);
+    part[i] = w2l * l + w2h * hh;
+  }
+#pragma unroll
+  for (int off = 8; off; off >>= 1)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) part[i] = wadd(part[i], __shfl_xor(part[i], off, 16));
+  if (row == 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int pos = 4 * kg + i;
+      if (valid(pos, b)) {
+        const int32_t positional = wadd(wadd(b2v, part[i]), fwd[pos]);
+        const int32_t psqt = (int32_t)((uint32_t)psq[pos][0] - (uint32_t)psq[pos][1]) / 2;
+        emit(pos, make_int2(psqt / 16, positional / 16));
+      }
+    }
+  }
+}
+
 // rows of perspective h of a child whose h-king moved kf -> kt (castling: rook rf -> rt,
 // 64 = none), from the parent board, lane = square: the row of this lane's piece in
 // the child (or -1) and its rank among the child's pieces.  All 64 lanes.

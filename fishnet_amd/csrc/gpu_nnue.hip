@@ -287,8 +287,17 @@ struct SeqGuard { // seq_begin now, seq_end when the scope ends (d.mu held throu
   Dev &d;
   hipStream_t s;
   hipError_t e;
+  bool ended = false;
   SeqGuard(Dev &d_, hipStream_t s_) : d(d_), s(s_) { e = seq_begin(d, s); }
-  ~SeqGuard() { (void)seq_end(d, s); }
+  // the sequence's end marker now, then wait for the stream: the call returns with its stream idle
+  hipError_t finish() {
+    ended = true;
+    hipError_t r = seq_end(d, s);
+    return r == hipSuccess ? hipStreamSynchronize(s) : r;
+  }
+  ~SeqGuard() {
+    if (!ended) (void)seq_end(d, s);
+  }
 };
 
 // One gn_evaluate_batch call waiting for, or in, a merged launch (evaluate_coalesced).
@@ -1846,7 +1855,10 @@ int gn_evaluate_device(gn_ctx *ctx, int device_slot, const gn_board *d_boards, s
   SeqGuard sg(*d, s);
   HIP_TRY(sg.e);
   int rc = evaluate_on(ctx, *d, d_boards, n, mode, d_out, s, nullptr);
-  return rc ? rc : resolve_scores(ctx, *d, d_boards, n, mode, d_out, nullptr, s);
+  if (!rc) rc = resolve_scores(ctx, *d, d_boards, n, mode, d_out, nullptr, s);
+  if (rc) return rc;
+  HIP_TRY(sg.finish()); // blocking (gpu_nnue.h): d_out is written when the call returns
+  return GN_OK;
 }
 
 int gn_time_evaluate_device(gn_ctx *ctx, int device_slot, const gn_board *d_boards, size_t n, int mode,

@@ -170,6 +170,8 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR) __attribute__((amdgpu_wav
   __shared__ uint32_t cmask[2];     // squares holding the same piece in every valid position
   __shared__ uint16_t crow[2][32];  // the tile's common rows by ABSOLUTE perspective
   __shared__ int ccnt;
+  __shared__ gn_board tb[TILE];     // the tile's boards (a dead slot: zeroed, occ 0)
+  __shared__ uint32_t tix[TILE];    // their batch indices
   uint16_t(*rows)[2][32] = reinterpret_cast<uint16_t(*)[2][32]>(scratch);
 
   const int tid = threadIdx.x;
@@ -183,11 +185,19 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR) __attribute__((amdgpu_wav
     if (tile >= tiles) return;
   }
   const size_t base = (size_t)tile * TILE;
-  auto pos_index = [&](int sl) -> size_t {
-    const size_t q = base + sl;
-    return q < n ? (perm ? perm[q] : q) : 0;
-  };
-  auto pos_live = [&](int sl, size_t i) { return base + sl < n && (!need || need[i]); };
+  // the tile's 16 boards to LDS by 16 lanes in one round trip (perm, need, board), instead of a
+  // dependent board load per position in each phase-0 loop below
+  if (tid < TILE) {
+    const size_t q = base + tid;
+    const size_t i = q < n ? (perm ? perm[q] : q) : 0;
+    gn_board b = {};
+    if (q < n && (!need || need[i])) b = boards[i];
+    tb[tid] = b;
+    tix[tid] = (uint32_t)i;
+  }
+  __syncthreads();
+  auto pos_index = [&](int sl) -> size_t { return tix[sl]; };
+  auto pos_live = [&](int sl, size_t) { return tb[sl].occ != 0; }; // (a live board without pieces has no features either)
 
   // ---- phase 0: feature rows of both ABSOLUTE perspectives, one wave per position.
   // Common-row base: the rows of the pieces that stand on the same square in every
@@ -208,7 +218,7 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR) __attribute__((amdgpu_wav
         const size_t i = pos_index(0);
         int pc = 0xFF;
         if (pos_live(0, i)) {
-          const gn_board p = boards[i];
+          const gn_board p = tb[0];
           if (wave_features(p, nullptr, nullptr, lane)) pc = lane_piece(p, lane);
         }
         refpc[lane] = (uint8_t)pc;
@@ -218,7 +228,7 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR) __attribute__((amdgpu_wav
       for (int sl = wave; sl < TILE; sl += NW) { // B: AND of the per-position agreement masks
         const size_t i = pos_index(sl);
         if (!pos_live(sl, i)) continue;
-        const gn_board p = boards[i];
+        const gn_board p = tb[sl];
         const int pc = lane_piece(p, lane);
         const uint64_t eq = __ballot(pc == refpc[lane]);
         if (wave_features(p, nullptr, nullptr, lane) && lane == 0) {
@@ -246,7 +256,7 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR) __attribute__((amdgpu_wav
       const size_t i = pos_index(sl);
       int cnt = 0, stm = 0;
       if (pos_live(sl, i)) {
-        const gn_board p = boards[i];
+        const gn_board p = tb[sl];
         stm = p.stm_ep >> 7;
         // big net: rows by absolute perspective (the base is per colour); small net: by
         // relative perspective (h = 0: side to move), as the transform consumes them
@@ -347,10 +357,21 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR) __attribute__((amdgpu_wav
   }
   __syncthreads();
 
-  // ---- phase 2: layer stack (MFMA), one wave per distinct bucket in the tile
-  layer_stack_tile<L1, NW>(net, xt, scratch, psq, (int)threadIdx.x, bmask, [&](int pos, int b) {
-    return base + pos < n && nfeat[pos] && bkt[pos] == b;
-  }, [&](int pos, int2 v) { out[gidx[pos]] = v; });
+  // ---- phase 2: layer stack (MFMA).  Big net: every wave takes part in each bucket's fc_0
+  // (48 k-steps); small net (2 k-steps): one wave per bucket present runs the whole stack
+  // (layer_stack_wave: no LDS partial sums, no further barrier), the other waves are done
+  auto valid = [&](int pos, int b) { return base + pos < n && nfeat[pos] && bkt[pos] == b; };
+  auto emit = [&](int pos, int2 v) { out[gidx[pos]] = v; };
+  if constexpr (PAR == 1) {
+    layer_stack_tile<L1, NW>(net, xt, scratch, psq, (int)threadIdx.x, bmask, valid, emit);
+  } else {
+    __shared__ __attribute__((aligned(16))) uint8_t lin1[NW][16][32];
+    __shared__ int32_t lfwd[NW][16];
+    const int lane = tid & 63, wave = tid >> 6;
+    int idx = 0;
+    for (uint32_t m = bmask; m; m &= m - 1, ++idx)
+      if (idx % NW == wave) layer_stack_wave<L1>(net, xt, lin1[wave], lfwd[wave], psq, __builtin_ctz(m), lane, valid, emit);
+  }
 }
 
 // ---------------------------------------------------------- expand_eval --

@@ -380,11 +380,11 @@ GN_API int gn_random_positions_device(gn_ctx *ctx, int device_slot, uint64_t see
 /* Evaluate boards already resident on device `device_slot` (index into the
  * devices given at load).  d_boards / d_out are device pointers; stream is a
  * hipStream_t (NULL = the context's own stream).  Blocking: the score rule reads the
- * number of in-check positions back to size its launches, so the call synchronises
- * `stream` (once; three times when the batch has in-check positions with legal moves)
- * and returns with d_out written; it cannot be captured into a HIP graph.  The other
- * gn_*_device calls that evaluate (gn_expand_device, gn_expand2_device, gn_time_*) block
- * the same way; gn_random_positions_device / gn_random_games_device are asynchronous. */
+ * number of in-check positions back to size its launches (so the call synchronises
+ * `stream` while it runs and cannot be captured into a HIP graph), and the call returns
+ * with `stream` idle and d_out written.  The other gn_*_device calls that evaluate
+ * (gn_expand_device, gn_expand2_device, gn_time_*) block the same way;
+ * gn_random_positions_device / gn_random_games_device are asynchronous. */
 GN_API int gn_evaluate_device(gn_ctx *ctx, int device_slot, const gn_board *d_boards, size_t n, int mode,
                        gn_eval *d_out, void *stream);
 /* Device-resident expansion: counts children (d_counts[n]), writes d_offsets

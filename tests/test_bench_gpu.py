@@ -9,7 +9,8 @@ libgpu_nnue binds to."""
 import argparse
 import copy
 
-import torch  # noqa: F401  (before libgpu_nnue, as in bench.py)
+import numpy as np
+import torch  # (before libgpu_nnue, as in bench.py)
 import pytest
 
 pytestmark = pytest.mark.gpu
@@ -87,3 +88,18 @@ def test_run_expand_and_gather_two_loopback_ranks():
     assert g["bytes_all_ranks"] > 0
     # the two shards are different games
     assert r0["checksum"] != r1["checksum"]
+
+
+def test_evaluate_device_blocks_until_written(gpu_ctx):
+    """gn_evaluate_device is documented as blocking (gpu_nnue.h: the score rule reads
+    the in-check count back, so the call synchronises the stream it is given).  On a caller's
+    stream the call returns with nothing left queued on that stream and the records written."""
+    from fishnet_amd import gpu_nnue as G
+    boards = G.random_positions(0x5EED0777, 0, 4096, 160)
+    d_b, d_o = gpu_ctx.alloc(boards.nbytes), gpu_ctx.alloc(len(boards) * G.EVAL_SIZE)
+    d_b.upload(boards)
+    ref = gpu_ctx.evaluate_batch([G.board_to_fen(b) for b in boards], G.MODE_FULL)
+    s = torch.cuda.Stream()
+    gpu_ctx.evaluate_device(d_b, len(boards), G.MODE_FULL, d_o, stream=s.cuda_stream)
+    assert s.query()
+    assert np.array_equal(d_o.download(G.EVAL_DTYPE, len(boards)), ref)
