@@ -22,22 +22,19 @@
 //                       all waves run fc_0 as int8 MFMAs; one wave per bucket finishes
 //                       fc_1 / fc_2 and writes the outputs while the others stream on.
 //
-// Entry (u32), as the plan kernel builds it:
-//   [18:0] row: an FT row, the zero row, or (SCR) a row of the workgroup's scratch slot
-//          (2 + 64 h + ksq: the king-cache row of (h, ksq))
-//   [19] SUB   [21:20] init before this entry: 0 none, 1 ZERO (lo = row; with SUB: keep,
-//          a store-only entry), 2 PACC (lo = parent - row, saved as the sibling base),
-//          3 BASE (lo = base +- row)   [22] LAST entry of its slot   [26:23] slot in tile
-//   [27] side (0: the perspective to move)   [28] PAR_E (the slot's accumulator becomes
-//   pacc: a parent, or the child that is the next parent)   [30] SCR   [31] KST (store
-//   the slot's accumulator to the row of this entry)
-// The plan kernel stores each entry as the stream kernel's pre-decoded u64 (enc64):
-// lo = the row's byte offset (scratch rows: from the first scratch row, the workgroup
-// adds its slot's offset), hi = [15:0] the 16-bit multiplier of the row (1 add, 0xFFFF
-// subtract, 0 no-op: ZERO | SUB entries; a store-only KST entry loads the zero row and
-// has its target scratch row here), [16] PRE (an init before the entry), [18:17] the init
-// kind, [19] LAST, [23:20] slot, [24] side, [25] PAR_E, [27] KST, [31] SCR; so the
-// stream's common entry is a multiply-add with hi as its scalar operand and two bit tests.
+// Entry (u64, built by the plan kernel in the form the stream consumes):
+//   lo = the row's byte offset: an FT row, the zero row, or (hi SCR) a row of the
+//        workgroup's scratch slot counted from its first row (2 + 64 h + ksq: the
+//        king-cache row of (h, ksq)); the workgroup adds its slot's offset
+//   hi = [15:0] the 16-bit multiplier of the row (1 add, 0xFFFF subtract, 0 no-op; a
+//        store-only KST entry loads the zero row and has its target scratch row here),
+//        [16] PRE (an init before the entry), [18:17] the init kind (1 ZERO: acc = row,
+//        2 PACC: acc = parent - row, saved as the sibling base, 3 BASE: acc = base +- row),
+//        [19] LAST entry of its slot, [23:20] slot in tile, [24] side (0: the perspective
+//        to move), [25] PAR_E (the slot's accumulator becomes pacc: a parent, or the child
+//        that is the next parent), [27] KST (store the slot's accumulator to the scratch row
+//        of this entry), [31] SCR
+// so the stream's common entry is a multiply-add with hi as its scalar operand and two bit tests.
 // The ring issues a row load 4 entries before it
 // consumes it, so an entry that loads a scratch row sits at least GN_SCR_GAP (= 4) entries
 // after the last store to scratch in its list (no-op entries are inserted when needed): the
@@ -95,33 +92,15 @@ __device__ unsigned long long gn_xp[32] = {0, 0, 0, 0, 0, 0, 0, 0, ~0ull, ~0ull,
 
 namespace gn {
 namespace ps {
-constexpr uint32_t ROW = (1u << 19) - 1, SUB = 1u << 19, I_ZERO = 1u << 20, I_PACC = 2u << 20, I_BASE = 3u << 20,
-                   LAST = 1u << 22, SLOT_SH = 23, SIDE_SH = 27, PAR_E = 1u << 28,
-                   SCR = 1u << 30, KST = 1u << 31;
-constexpr uint32_t PAD = (uint32_t)FT_BIAS_ROW | I_ZERO | SUB;
-// pre-decoded form (see the header)
 constexpr uint32_t H_PRE = 1u << 16, H_INIT_SH = 17, H_LAST = 1u << 19, H_SLOT_SH = 20, H_SIDE_SH = 24,
                    H_PAR_E = 1u << 25, H_KST = 1u << 27, H_SCR = 1u << 31;
-template <int L1>
-__device__ __forceinline__ uint64_t enc64(uint32_t e) {
-  constexpr uint32_t RS = ft_row_stride(L1);
-  const uint32_t row = e & ROW, init = (e >> 20) & 3, sub = e & SUB;
-  const bool keep = init == 1 && sub; // ZERO | SUB: no init, no row (padding, store-only entries)
-  // a store-only KST entry loads the zero row and carries its target (a scratch row) as its
-  // multiplier: the store's offset is then known without the entry's lo word
-  const bool kst = (e & KST) != 0;
-  const uint32_t lo = kst ? (uint32_t)ZERO_ROW * RS : ((e & SCR) ? (uint32_t)FT_ROWS + row : row) * RS;
-  uint32_t hi = kst ? row : keep ? 0u : sub ? 0xFFFFu : 1u;
-  if (!keep && init) hi |= H_PRE | init << H_INIT_SH;
-  hi |= (e & LAST) ? H_LAST : 0u;
-  hi |= ((e >> SLOT_SH) & 15) << H_SLOT_SH | ((e >> SIDE_SH) & 1) << H_SIDE_SH;
-  hi |= (e & PAR_E) ? H_PAR_E : 0u;
-  hi |= (e & KST) ? H_KST : 0u;
-  hi |= (e & SCR) && !kst ? H_SCR : 0u;
-  return (uint64_t)hi << 32 | lo;
-}
-__device__ __forceinline__ uint32_t tmpl(int slot, int side) {
-  return (uint32_t)slot << SLOT_SH | (uint32_t)side << SIDE_SH;
+// Each put site knows its entry's kind, so hi is a constant mask or'd with the slot / side
+// bits (round 3 built a u32 entry and decoded it per put: ~25 VALU per entry in an
+// issue-bound kernel).
+constexpr uint32_t M_ADD = 1u, M_SUB = 0xFFFFu;
+constexpr uint32_t HZ = H_PRE | 1u << H_INIT_SH, HP = H_PRE | 2u << H_INIT_SH, HB = H_PRE | 3u << H_INIT_SH;
+__device__ __forceinline__ uint32_t hs(int slot, int side) {
+  return (uint32_t)slot << H_SLOT_SH | (uint32_t)side << H_SIDE_SH;
 }
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -164,25 +143,20 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
   // <= 2 buckets, so a tile is cut at most once per parent), hence this base
   TileDesc *T = tiles + us_b / 16 + (uint64_t)(K + 2) * blk;
   uint32_t safe0 = 0, safe1 = 0; // first index of each list at which a scratch row may be loaded
-  auto put = [&](int g, uint32_t i, uint32_t v) {
-#ifdef GN_AB_PLAN_NOCHECK // A/B only
-    if (g) E1[-(int64_t)i] = enc64<L1>(v);
-    else E0[i] = enc64<L1>(v);
-    return;
-#endif
+  constexpr uint32_t RS = ft_row_stride(L1);
+  constexpr uint32_t LO_BIAS = (uint32_t)FT_BIAS_ROW * RS, LO_ZERO = (uint32_t)ZERO_ROW * RS;
+  auto lo_scr = [](uint32_t r) -> uint32_t { return ((uint32_t)FT_ROWS + r) * RS; }; // scratch row r
+  // entry i of list g: the row at byte offset lo, hi = multiplier + flags (see above)
+  auto put = [&](int g, uint32_t i, uint32_t lo, uint32_t hi) {
     if (i >= rtot) { // never past the block's region (the final check reports the overflow)
       bad |= 1u;
       return;
     }
     // a scratch-row load must sit GN_SCR_GAP entries after the list's last scratch store
-    if ((v & (SCR | KST)) == SCR && i < (g ? safe1 : safe0)) bad |= 4u;
-#ifdef GN_ENT_NT // A/B: the entries stored non-temporal (they are read once, by the stream)
-    if (g) __builtin_nontemporal_store(enc64<L1>(v), &E1[-(int64_t)i]);
-    else __builtin_nontemporal_store(enc64<L1>(v), &E0[i]);
-#else
-    if (g) E1[-(int64_t)i] = enc64<L1>(v);
-    else E0[i] = enc64<L1>(v);
-#endif
+    if ((hi & H_SCR) && i < (g ? safe1 : safe0)) bad |= 4u;
+    const uint64_t e = (uint64_t)hi << 32 | lo;
+    if (g) E1[-(int64_t)i] = e;
+    else E0[i] = e;
   };
   for (int i = lane; i < 128; i += 64) kstate[w][i] = 0;
   uint16_t(*prow)[32] = prow_s[w];
@@ -194,7 +168,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
     uint32_t &len = g ? len1 : len0;
     if (len < target) {
       pads += target - len;
-      if ((uint32_t)lane < target - len) put(g, len + lane, PAD);
+      if ((uint32_t)lane < target - len) put(g, len + lane, LO_BIAS, 0u); // (no-op: multiplier 0)
       len = target;
     }
   };
@@ -400,34 +374,36 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
       // at the cursor), before the jobs: a cache-row load is put while the lists' last scratch
       // stores are still the ones before it (put() checks the distance)
       if (live && q0 == 0 && lane == 0) {
-        const uint32_t t0w = tmpl(tf0, stm != 0), t1w = tmpl(tf0, stm != 1);
+        const uint32_t t0w = hs(tf0, stm != 0), t1w = hs(tf0, stm != 1);
         if (have) { // the parent is its predecessor's last child: pacc, one entry per list
-          put(0, len0, (uint32_t)ZERO_ROW | t0w | I_PACC | SUB | PAR_E | LAST);
-          put(1, len1, (uint32_t)ZERO_ROW | t1w | I_PACC | SUB | PAR_E | LAST);
+          put(0, len0, LO_ZERO, M_SUB | HP | t0w | H_PAR_E | H_LAST);
+          put(1, len1, LO_ZERO, M_SUB | HP | t1w | H_PAR_E | H_LAST);
         } else { // bias entry or the cache row; the rest follows (lane = square / row)
-          put(0, len0, (pnd[0] >= 0 ? SCR | (uint32_t)(2 + pkq[0]) : (uint32_t)FT_BIAS_ROW) | t0w | I_ZERO | PAR_E);
-          put(1, len1, (pnd[1] >= 0 ? SCR | (uint32_t)(2 + 64 + pkq[1]) : (uint32_t)FT_BIAS_ROW) | t1w | I_ZERO | PAR_E);
+          put(0, len0, pnd[0] >= 0 ? lo_scr(2 + pkq[0]) : LO_BIAS, M_ADD | HZ | t0w | H_PAR_E | (pnd[0] >= 0 ? H_SCR : 0u));
+          put(1, len1, pnd[1] >= 0 ? lo_scr(2 + 64 + pkq[1]) : LO_BIAS,
+              M_ADD | HZ | t1w | H_PAR_E | (pnd[1] >= 0 ? H_SCR : 0u));
         }
       }
       if (live && q0 == 0 && !have) {
         const uint64_t lt2 = (1ull << lane) - 1;
 #pragma unroll 1
         for (int hh = 0; hh < 2; ++hh) {
-          const uint32_t tp = tmpl(tf0, stm != hh), b0 = (hh ? len1 : len0) + 1;
-          const uint32_t krow = SCR | (uint32_t)(2 + 64 * hh + pkq[hh]);
+          const uint32_t tp = hs(tf0, stm != hh), b0 = (hh ? len1 : len0) + 1;
+          const uint32_t kr = (uint32_t)(2 + 64 * hh + pkq[hh]); // the cache row (scratch row index)
           if (pnd[hh] >= 0) { // the cache row's differences: removed pieces, then added ones
             int spc;
             uint64_t bs, ba;
             cache_diff(64 * hh + pkq[hh], ppc, spc, bs, ba);
             if ((bs >> lane) & 1)
-              put(hh, b0 + popcnt(bs & lt2), (uint32_t)feature_index(hh, lane, spc, pkq[hh]) | tp | SUB | PAR_E);
+              put(hh, b0 + popcnt(bs & lt2), (uint32_t)feature_index(hh, lane, spc, pkq[hh]) * RS, M_SUB | tp | H_PAR_E);
             if ((ba >> lane) & 1)
-              put(hh, b0 + popcnt(bs) + popcnt(ba & lt2), (uint32_t)feature_index(hh, lane, ppc, pkq[hh]) | tp | PAR_E);
-            if (lane == 0) put(hh, b0 + pnd[hh], krow | tp | I_ZERO | SUB | KST | LAST | PAR_E);
+              put(hh, b0 + popcnt(bs) + popcnt(ba & lt2), (uint32_t)feature_index(hh, lane, ppc, pkq[hh]) * RS,
+                  M_ADD | tp | H_PAR_E);
+            if (lane == 0) put(hh, b0 + pnd[hh], LO_ZERO, kr | tp | H_KST | H_LAST | H_PAR_E);
           } else {
             if (lane < P)
-              put(hh, b0 + lane, ft_row(prow[hh][lane]) | tp | PAR_E | (lane == P - 1 && !pst[hh] ? LAST : 0u));
-            if (pst[hh] && lane == 0) put(hh, b0 + P, krow | tp | I_ZERO | SUB | KST | LAST | PAR_E);
+              put(hh, b0 + lane, ft_row(prow[hh][lane]) * RS, M_ADD | tp | H_PAR_E | (lane == P - 1 && !pst[hh] ? H_LAST : 0u));
+            if (pst[hh] && lane == 0) put(hh, b0 + P, LO_ZERO, kr | tp | H_KST | H_LAST | H_PAR_E);
           }
           if (pnd[hh] >= 0 || pst[hh]) { // list hh stored the row: its snapshot and state
             uint32_t x = (uint32_t)ppc << (4 * (lane & 7));
@@ -484,7 +460,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
         const int row = king_move_row_pc(ppc, hh, sq01 & 0xFFFF, kt, sq23 & 0xFFFF, sq23 >> 16, lane, pos, cpc);
         const int cb = (cn - 1) / 4;
         const int32_t prw = row >= 0 ? psqt((uint32_t)row, cb) : 0; // summed at the job's end (latency)
-        const uint32_t tw = tmpl(tl, hh != st);
+        const uint32_t tw = hs(tl, hh != st);
         bool kuse = kc && (sq23 & 0xFFFF) == 64; // not castling
         const int kci = 64 * hh + kt;
         const int kst = kuse ? kstate[w][kci] : 0;
@@ -507,23 +483,23 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
         const int g = hit ? own : nxl ? hh : kuse && own >= 0 ? own : (len0 <= len1 ? 0 : 1);
         if (hit) pad_to(g, g ? safe1 : safe0); // the cache row load after the list's last scratch store
         const uint32_t base = g ? len1 : len0;
-        const uint32_t L = LAST | (nxl ? PAR_E : 0u);
-        const uint32_t krow = SCR | (uint32_t)(2 + kci);
+        const uint32_t L = H_LAST | (nxl ? H_PAR_E : 0u);
+        const uint32_t kr = (uint32_t)(2 + kci); // the cache row (scratch row index)
         int ne;
         if (hit) {
           const int nd = popcnt(bs) + popcnt(ba);
           ne = nd + 2;
           const int ps = 1 + popcnt(bs & lt), pa = 1 + popcnt(bs) + popcnt(ba & lt);
-          if (lane == 0) put(g, base, krow | tw | I_ZERO);
-          if ((bs >> lane) & 1) put(g, base + ps, (uint32_t)feature_index(hh, lane, spc, kt) | tw | SUB);
-          if ((ba >> lane) & 1) put(g, base + pa, (uint32_t)row | tw);
-          if (lane == 0) put(g, base + ne - 1, krow | tw | I_ZERO | SUB | KST | L);
+          if (lane == 0) put(g, base, lo_scr(kr), M_ADD | HZ | tw | H_SCR);
+          if ((bs >> lane) & 1) put(g, base + ps, (uint32_t)feature_index(hh, lane, spc, kt) * RS, M_SUB | tw);
+          if ((ba >> lane) & 1) put(g, base + pa, (uint32_t)row * RS, M_ADD | tw);
+          if (lane == 0) put(g, base + ne - 1, LO_ZERO, kr | tw | H_KST | L);
           rows += (unsigned long long)(nd + 1);
         } else {
           ne = cn + 1 + (kuse ? 1 : 0);
-          if (lane == 0) put(g, base, (uint32_t)FT_BIAS_ROW | tw | I_ZERO);
-          if (row >= 0 && pos < cn) put(g, base + 1 + pos, (uint32_t)row | tw | (!kuse && pos == cn - 1 ? L : 0u));
-          if (kuse && lane == 0) put(g, base + ne - 1, krow | tw | I_ZERO | SUB | KST | L);
+          if (lane == 0) put(g, base, LO_BIAS, M_ADD | HZ | tw);
+          if (row >= 0 && pos < cn) put(g, base + 1 + pos, (uint32_t)row * RS, M_ADD | tw | (!kuse && pos == cn - 1 ? L : 0u));
+          if (kuse && lane == 0) put(g, base + ne - 1, LO_ZERO, kr | tw | H_KST | L);
           rows += (unsigned long long)(cn + 1);
         }
         if (kuse) { // the cache row now holds this child's accumulator, stored by list g
@@ -551,27 +527,27 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
         const uint32_t rel = exc - (uint32_t)__shfl((int)exc, tile_lane0(tix)); // (no borrow: prefix sums)
         const uint32_t at0 = (uint32_t)__shfl((int)ts0, tix) + (rel & 0xFFFF);
         const uint32_t at1 = (uint32_t)__shfl((int)ts1, tix) + (rel >> 16);
-        const uint32_t t0w = tmpl(t, cst != 0), t1w = tmpl(t, cst != 1);
+        const uint32_t t0w = hs(t, cst != 0), t1w = hs(t, cst != 1);
         if (in && live) {
           auto delta = [&](int g, uint32_t at, uint32_t lo2, uint32_t hi2, int s, int n, bool hit, uint32_t tw,
                            uint32_t L) {
             const uint32_t i0 = lo2 & 0xFFFF, i1 = lo2 >> 16, i2 = hi2 & 0xFFFF, i3 = hi2 >> 16;
-            auto cl = [](uint32_t r) { return r < (uint32_t)FT_INPUTS ? r : (uint32_t)FT_BIAS_ROW; };
+            auto cl = [](uint32_t r) { return (r < (uint32_t)FT_INPUTS ? r : (uint32_t)FT_BIAS_ROW) * RS; };
             const uint32_t r1 = cl(s >= 2 ? i1 : i2), r2 = cl(s >= 2 ? i2 : i3), r3 = cl(i3);
-            const uint32_t f1 = s >= 2 ? SUB : 0u;
+            const uint32_t f1 = s >= 2 ? M_SUB : M_ADD;
             if (!hit) {
-              put(g, at, cl(i0) | tw | SUB | I_PACC | (n == 1 ? L : 0u));
-              if (n > 1) put(g, at + 1, r1 | tw | f1 | (n == 2 ? L : 0u));
-              if (n > 2) put(g, at + 2, r2 | tw | (n == 3 ? L : 0u));
-              if (n > 3) put(g, at + 3, r3 | tw | L);
+              put(g, at, cl(i0), M_SUB | HP | tw | (n == 1 ? L : 0u));
+              if (n > 1) put(g, at + 1, r1, f1 | tw | (n == 2 ? L : 0u));
+              if (n > 2) put(g, at + 2, r2, M_ADD | tw | (n == 3 ? L : 0u));
+              if (n > 3) put(g, at + 3, r3, M_ADD | tw | L);
             } else { // the from-row is in the cached base
-              put(g, at, r1 | tw | f1 | I_BASE | (n == 2 ? L : 0u));
-              if (n > 2) put(g, at + 1, r2 | tw | (n == 3 ? L : 0u));
-              if (n > 3) put(g, at + 2, r3 | tw | L);
+              put(g, at, r1, f1 | HB | tw | (n == 2 ? L : 0u));
+              if (n > 2) put(g, at + 1, r2, M_ADD | tw | (n == 3 ? L : 0u));
+              if (n > 3) put(g, at + 2, r3, M_ADD | tw | L);
             }
           };
-          if ((kinds & 3) == 1) delta(0, at0, w0, w1, s0, n0, hit0, t0w, LAST | (nx ? PAR_E : 0u));
-          if ((kinds >> 2) == 1) delta(1, at1, w2, w3, s1, n1, hit1, t1w, LAST | (nx ? PAR_E : 0u));
+          if ((kinds & 3) == 1) delta(0, at0, w0, w1, s0, n0, hit0, t0w, H_LAST | (nx ? H_PAR_E : 0u));
+          if ((kinds >> 2) == 1) delta(1, at1, w2, w3, s1, n1, hit1, t1w, H_LAST | (nx ? H_PAR_E : 0u));
         }
       }
       // ---- the pass's last tile stays open
