@@ -266,4 +266,37 @@ __device__ __forceinline__ int32_t wave_sum(int32_t v) {
   return v;
 }
 
+// Inclusive scans over the 64 lanes on DPP: six VALU steps with no LDS round trip (a
+// __shfl_up / __shfl_xor step is a ds_bpermute, ~100 cycles of latency each in a chain).
+// row_shr:1/2/4/8 scan each row of 16 (lanes shifted in from outside the row read 0), then
+// row_bcast:15 adds row 0's total to row 1 and row 2's to row 3, and row_bcast:31 adds
+// lane 31's (rows 0-1) to rows 2 and 3.
+template <class Op>
+__device__ __forceinline__ uint32_t dpp_scan(uint32_t x, Op op) {
+  x = op(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, true)); // row_shr:1
+  x = op(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, true)); // row_shr:2
+  x = op(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, true)); // row_shr:4
+  x = op(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, true)); // row_shr:8
+  x = op(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false)); // row_bcast:15
+  x = op(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false)); // row_bcast:31
+  return x;
+}
+__device__ __forceinline__ uint32_t scan_add(uint32_t x) {
+  return dpp_scan(x, [](uint32_t a, uint32_t b) { return a + b; });
+}
+__device__ __forceinline__ uint32_t scan_or(uint32_t x) {
+  return dpp_scan(x, [](uint32_t a, uint32_t b) { return a | b; });
+}
+// OR over each group of 8 lanes (quad_perm [1,0,3,2], [2,3,0,1], then row_half_mirror)
+__device__ __forceinline__ uint32_t or8(uint32_t x) {
+  x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xb1, 0xf, 0xf, false);
+  x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4e, 0xf, 0xf, false);
+  x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x141, 0xf, 0xf, false);
+  return x;
+}
+// the wave's (wrapping) sum, uniform
+__device__ __forceinline__ int32_t wave_sum_dpp(int32_t v) {
+  return __builtin_amdgcn_readlane((int)scan_add((uint32_t)v), 63);
+}
+
 } // namespace gn

@@ -17,6 +17,13 @@
 #include "device_util.h"
 #include "kernels.h"
 
+#ifndef GN_SMALL_DEPTH
+#define GN_SMALL_DEPTH 4 // eval_net<128>: FT rows in flight per thread (8 at 5 waves per SIMD: 0.72 ms, 6 at 6: 0.64, 4 at 8: 0.555)
+#endif
+#ifndef GN_SMALL_WPE
+#define GN_SMALL_WPE 8 // eval_net<128>: waves per SIMD (64 VGPRs)
+#endif
+
 
 namespace gn {
 
@@ -142,7 +149,7 @@ __device__ __forceinline__ void layer_stack_tile(const NetDevice &net, const uin
 // 16 positions of the tile one after another); small net: G = 8, PAR = 16
 // (256 threads, all 16 positions at once).
 template <int L1, int PAR>
-__global__ void __launch_bounds__(2 * (L1 / 16) * PAR) __attribute__((amdgpu_waves_per_eu(PAR == 1 ? 1 : 6)))
+__global__ void __launch_bounds__(2 * (L1 / 16) * PAR) __attribute__((amdgpu_waves_per_eu(PAR == 1 ? 1 : GN_SMALL_WPE)))
     eval_net_kernel(NetDevice net, const gn_board *__restrict__ boards, const uint8_t *__restrict__ need,
                     size_t n, int2 *__restrict__ out, const uint32_t *__restrict__ perm, unsigned tiles, int swz,
                     unsigned long long *__restrict__ rows_out) {
@@ -292,42 +299,40 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR) __attribute__((amdgpu_wav
     // bucket to ps, read from the bucket-major copy pt = net.psqt + bucket * FT_ROWS (90 KB per
     // bucket, its lines shared by all the rows of a king bucket) rather than the row's own PSQT
     // part, a line of its own per row (a third line per row for the small net, whose weights are
-    // two); 4 rows in flight, tail as one batch
+    // two); D rows in flight (big net 4: more cost a wave per SIMD; small net GN_SMALL_DEPTH), the
+    // tail as one batch (no serialized round trips)
+    constexpr int D = PAR == 1 ? 4 : GN_SMALL_DEPTH;
     auto gather = [&](const uint16_t *rr, int cnt, ushort8 &lo, ushort8 &hi, uint32_t &ps, const int32_t *pt,
                       bool wps) {
       int k = 0;
-      for (; k + 4 <= cnt; k += 4) {
-        const uint32_t o0 = ft_row(rr[k]) * RS, o1 = ft_row(rr[k + 1]) * RS, o2 = ft_row(rr[k + 2]) * RS, o3 = ft_row(rr[k + 3]) * RS;
-        const ushort8 a0 = ldft(net.ft, j16 + o0);
-        const ushort8 a1 = ldft(net.ft, j16 + o1);
-        const ushort8 a2 = ldft(net.ft, j16 + o2);
-        const ushort8 a3 = ldft(net.ft, j16 + o3);
-        const ushort8 b0 = ldft(net.ft, j16 + o0 + L1);
-        const ushort8 b1 = ldft(net.ft, j16 + o1 + L1);
-        const ushort8 b2 = ldft(net.ft, j16 + o2 + L1);
-        const ushort8 b3 = ldft(net.ft, j16 + o3 + L1);
-        if (wps && j == 0)
-          ps += (uint32_t)pt[ft_row(rr[k])] + (uint32_t)pt[ft_row(rr[k + 1])] + (uint32_t)pt[ft_row(rr[k + 2])] +
-                (uint32_t)pt[ft_row(rr[k + 3])];
-        lo += (a0 + a1) + (a2 + a3);
-        hi += (b0 + b1) + (b2 + b3);
-      }
-      if (k < cnt) { // tail of 1-3 rows as one batch (no serialized round trips)
-        const int k1 = k + 1 < cnt ? k + 1 : k, k2 = k + 2 < cnt ? k + 2 : k;
-        const uint32_t o0 = ft_row(rr[k]) * RS, o1 = ft_row(rr[k1]) * RS, o2 = ft_row(rr[k2]) * RS;
-        const ushort8 a0 = ldft(net.ft, j16 + o0), a1 = ldft(net.ft, j16 + o1);
-        const ushort8 a2 = ldft(net.ft, j16 + o2);
-        const ushort8 b0 = ldft(net.ft, j16 + o0 + L1), b1 = ldft(net.ft, j16 + o1 + L1);
-        const ushort8 b2 = ldft(net.ft, j16 + o2 + L1);
-        uint32_t q0 = 0, q1 = 0, q2 = 0;
+      for (; k + D <= cnt; k += D) {
+        ushort8 a[D], b[D];
+        uint32_t o[D];
+#pragma unroll
+        for (int i = 0; i < D; ++i) o[i] = ft_row(rr[k + i]) * RS;
+#pragma unroll
+        for (int i = 0; i < D; ++i) a[i] = ldft(net.ft, j16 + o[i]);
+#pragma unroll
+        for (int i = 0; i < D; ++i) b[i] = ldft(net.ft, j16 + o[i] + L1);
         if (wps && j == 0) {
-          q0 = (uint32_t)pt[ft_row(rr[k])];
-          q1 = (uint32_t)pt[ft_row(rr[k1])];
-          q2 = (uint32_t)pt[ft_row(rr[k2])];
+#pragma unroll
+          for (int i = 0; i < D; ++i) ps += (uint32_t)pt[ft_row(rr[k + i])];
         }
-        lo += a0, hi += b0, ps += q0;
-        if (k + 1 < cnt) lo += a1, hi += b1, ps += q1;
-        if (k + 2 < cnt) lo += a2, hi += b2, ps += q2;
+#pragma unroll
+        for (int i = 0; i < D; i += 2) lo += a[i] + a[i + 1], hi += b[i] + b[i + 1];
+      }
+      if (k < cnt) { // tail of 1 .. D - 1 rows (indices past the end repeat row k, not added)
+        ushort8 a[D - 1], b[D - 1];
+        uint32_t o[D - 1], q[D - 1];
+#pragma unroll
+        for (int i = 0; i < D - 1; ++i) o[i] = ft_row(rr[k + i < cnt ? k + i : k]) * RS;
+#pragma unroll
+        for (int i = 0; i < D - 1; ++i) a[i] = ldft(net.ft, j16 + o[i]), b[i] = ldft(net.ft, j16 + o[i] + L1);
+#pragma unroll
+        for (int i = 0; i < D - 1; ++i) q[i] = wps && j == 0 ? (uint32_t)pt[ft_row(rr[k + i < cnt ? k + i : k])] : 0u;
+#pragma unroll
+        for (int i = 0; i < D - 1; ++i)
+          if (k + i < cnt) lo += a[i], hi += b[i], ps += q[i];
       }
     };
     // the tile's starting accumulator: bias + common rows (PSQT per position below)

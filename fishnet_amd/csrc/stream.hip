@@ -122,7 +122,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
   __shared__ uint32_t ksnap[4][128][8]; // per wave: placement (64 nibbles) of each king-cache row
   __shared__ uint8_t kstate[4][128];    // bit 0: row holds an accumulator, bit 1: the list that stored it
   __shared__ uint16_t prow_s[4][2][32];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  // (w via readfirstlane: the compiler then knows that blk, p and every bound derived from them
+  // are wave-uniform, so they live in SGPRs and their branches are scalar)
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const uint32_t blk = b0 + blockIdx.x * 4 + (uint32_t)w; // this launch plans blocks [b0, b1)
   if (blk >= b1) return; // the whole wave (no workgroup barriers in this kernel)
   const __amdgpu_buffer_rsrc_t pst = __builtin_amdgcn_make_buffer_rsrc(
@@ -182,38 +184,79 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
     ++tile_k, t_fill = 0, tile_bm = 0;
   };
 
+  // ---- a parent's inputs are loaded while the previous parent is planned, so that a parent
+  // waits for memory about twice (its inputs; then all its PSQT rows at once) instead of once
+  // per dependent load: lanes 0..6 the board's first 28 bytes (bd), lane 1 + c child c's delta
+  // (a, b, c, d its rows, m its meta, nd the aligned word holding its need_child byte), lane 0
+  // m / nd the words holding next_slot[p] / need_parent[p].  Children beyond the 63rd are
+  // loaded in their own pass.  The values stay as loaded, with no branch around a load (any
+  // arithmetic on them, or a copy where two paths meet, would wait for them here); an absent
+  // array is read from the board instead and ignored.
+  struct In {
+    uint32_t bd, a, b, c, d, m, nd;
+  };
+  auto word = [](const uint8_t *b) { return *reinterpret_cast<const uint32_t *>((uintptr_t)b & ~(uintptr_t)3); };
+  auto byte_of = [](uint32_t wv, const uint8_t *b) { return (wv >> (8 * ((uintptr_t)b & 3))) & 0xFFu; };
+  auto fetch = [&](uint32_t p) -> In {
+    const uint64_t off = offsets[p];
+    const uint32_t nch = (uint32_t)(offsets[p + 1] - off);
+    const uint8_t *any = reinterpret_cast<const uint8_t *>(parents + p);
+    In x = {0, 0, 0, 0, 0, 0, 0};
+    if (lane < 7) x.bd = reinterpret_cast<const uint32_t *>(parents + p)[lane];
+    if (lane == 0) {
+      x.m = word(next_slot ? next_slot + p : any);
+      x.nd = word(need_parent ? need_parent + p : any);
+    } else if ((uint32_t)lane - 1 < nch) {
+      const uint32_t *src = reinterpret_cast<const uint32_t *>(deltas + off + lane - 1);
+      x.a = src[0], x.b = src[1], x.c = src[2], x.d = src[3], x.m = src[4];
+      x.nd = word(need_child ? need_child + off + lane - 1 : any);
+    }
+    return x;
+  };
+  In xd = {0, 0, 0, 0, 0, 0, 0};
+  if (pbeg < pend) xd = fetch(pbeg);
   for (uint32_t p = pbeg; p < pend; ++p) {
     unsigned long long pp_t = PP_T();
     const uint64_t off = offsets[p];
     const int nch = (int)(offsets[p + 1] - off), total = 1 + nch;
-    const gn_board pb = parents[p];
+    gn_board pb = {};
+    {
+      uint32_t pw[7];
+#pragma unroll
+      for (int i = 0; i < 7; ++i) pw[i] = (uint32_t)__builtin_amdgcn_readlane((int)xd.bd, i);
+      pb.occ = (uint64_t)pw[0] | (uint64_t)pw[1] << 32;
+      __builtin_memcpy(pb.pc, &pw[2], 16);
+      pb.stm_ep = (uint8_t)pw[6];
+    }
+    const uint32_t f0 =
+        (need_parent ? byte_of((uint32_t)__builtin_amdgcn_readlane((int)xd.nd, 0), need_parent + p) : 1u) |
+        (next_slot ? byte_of((uint32_t)__builtin_amdgcn_readlane((int)xd.m, 0), next_slot + p) : 255u) << 8;
+    const bool pre = total <= 64; // the parent's slots are one pass, its inputs prefetched
     const int P = wave_features(pb, prow[0], prow[1], lane);
     ps::wave_sync();
     int want = 0;
-    for (int q = lane; q < total; q += 64)
-      want |= q == 0 ? (need_parent ? need_parent[p] : 1) : (need_child ? need_child[off + q - 1] : 1);
+    if (pre) want = lane == 0 ? (int)(f0 & 0xFF) : lane < total ? (int)(need_child ? byte_of(xd.nd, need_child + off + lane - 1) : 1u) : 0;
+    else
+      for (int q = lane; q < total; q += 64)
+        want |= q == 0 ? (int)(f0 & 0xFF) : (need_child ? need_child[off + q - 1] : 1);
     const bool live = __ballot(want) != 0 && P != 0;
     const int have = live ? carried : 0;
     carried = 0;
     const int stm = pb.stm_ep >> 7;
     const int bp = P ? (P - 1) / 4 : 0, b2 = P >= 2 ? (P - 2) / 4 : bp;
-    // parent PSQT per perspective at the two buckets its children can have (lane = (h, row))
-    int32_t pp[2][2] = {{0, 0}, {0, 0}};
+    // parent PSQT per perspective at the two buckets its children can have (lane = (h, row)):
+    // loaded in pass 0 with the slots' rows, then summed
+    int32_t pp[2][2] = {{0, 0}, {0, 0}}, pa = 0, pb2 = 0;
     int nxq = -1; // slot (1 + child index) of the child that is the next parent
-    if (live) {
-      const int hh = lane >> 5, k = lane & 31;
-      int32_t a = 0, b = 0;
-      if (k < P) a = psqt(prow[hh][k], bp), b = psqt(prow[hh][k], b2);
-#pragma unroll
-      for (int o = 16; o; o >>= 1) a = wadd(a, __shfl_xor(a, o)), b = wadd(b, __shfl_xor(b, o));
-      pp[0][0] = __builtin_amdgcn_readlane(a, 0), pp[0][1] = __builtin_amdgcn_readlane(b, 0);
-      pp[1][0] = __builtin_amdgcn_readlane(a, 32), pp[1][1] = __builtin_amdgcn_readlane(b, 32);
-      if (K > 1 && p + 1 < pend) {
-        const int ns = next_slot[p];
-        if (ns != 255 && ns < nch && (!need_child || need_child[off + ns])) nxq = ns + 1;
+    if (live && K > 1 && p + 1 < pend) {
+      const int ns = (int)(f0 >> 8);
+      if (ns != 255 && ns < nch) {
+        const bool nd = ns + 1 < 64 ? (!need_child || byte_of((uint32_t)__builtin_amdgcn_readlane((int)xd.nd, ns + 1), need_child + off + ns) != 0)
+                                    : (!need_child || need_child[off + ns]);
+        if (nd) nxq = ns + 1;
       }
-      carried = nxq > 0;
     }
+    carried = nxq > 0;
     // the child that is the next parent is evaluated last among its siblings (its accumulators
     // then become the parent accumulators the next parent starts from): processing position q
     // (1..nch) takes child ci(q), the others keep their order
@@ -234,8 +277,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
     int pkq[2] = {0, 0};          // the perspective's king square
     // the cached placement's piece on this lane's square and the differences to ppc
     auto cache_diff = [&](int kci, int pc, int &spc, uint64_t &bs, uint64_t &ba) {
-      const uint32_t wv = lane < 8 ? ksnap[w][kci][lane] : 0u;
-      spc = (int)((__shfl(wv, lane >> 3) >> (4 * (lane & 7))) & 15);
+      spc = (int)((ksnap[w][kci][lane >> 3] >> (4 * (lane & 7))) & 15);
       bs = __ballot(spc != pc && spc != 0), ba = __ballot(spc != pc && pc != 0);
     };
     const int ppc = live ? lane_piece(pb, lane) : 0; // the parent's piece on this lane's square
@@ -272,14 +314,29 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
       // ---- descriptor of this lane's slot
       int vld = 0, cst = 0, cnt = 1, kinds = 0, n0 = 0, n1 = 0, s0 = 0, s1 = 0;
       uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
+      In y = {0, 0, 0, 0, 0, 0, 0};
+      if (pre) { // (pass 0) the prefetched inputs in processing order: slot q = child child_of(q)
+        const int sl = q >= 1 && q < total ? child_of(q) + 1 : 0;
+        y.a = (uint32_t)__shfl((int)xd.a, sl), y.b = (uint32_t)__shfl((int)xd.b, sl);
+        y.c = (uint32_t)__shfl((int)xd.c, sl), y.d = (uint32_t)__shfl((int)xd.d, sl);
+        y.m = (uint32_t)__shfl((int)xd.m, sl), y.nd = (uint32_t)__shfl((int)xd.nd, sl);
+      }
+      __builtin_amdgcn_sched_barrier(0); // (the shuffles' wait must not cover the loads below)
+      if (q0 == 0 && p + 1 < pend) xd = fetch(p + 1); // the next parent's inputs
+      if (q0 == 0 && live && (lane & 31) < P)
+        pa = psqt(prow[lane >> 5][lane & 31], bp), pb2 = psqt(prow[lane >> 5][lane & 31], b2);
       if (lane < n_in && live) {
         if (q == 0) {
-          vld = need_parent ? need_parent[p] : 1;
+          vld = (int)(f0 & 0xFF);
           cst = stm, cnt = P, kinds = 3 | 3 << 2;
-        } else if ((vld = need_child ? need_child[off + child_of(q)] : 1)) {
-          const uint32_t *src = reinterpret_cast<const uint32_t *>(deltas + off + child_of(q));
-          w0 = src[0], w1 = src[1], w2 = src[2], w3 = src[3];
-          const uint32_t meta = src[4];
+        } else if ((vld = pre ? (int)(need_child ? byte_of(y.nd, need_child + off + child_of(q)) : 1u) : need_child ? need_child[off + child_of(q)] : 1)) {
+          uint32_t meta;
+          if (pre) {
+            w0 = y.a, w1 = y.b, w2 = y.c, w3 = y.d, meta = y.m;
+          } else {
+            const uint32_t *src = reinterpret_cast<const uint32_t *>(deltas + off + child_of(q));
+            w0 = src[0], w1 = src[1], w2 = src[2], w3 = src[3], meta = src[4];
+          }
           cst = (meta >> 10) & 1;
           cnt = (meta >> 14) & 63;
           if (meta & (1u << 8)) kinds |= 2, n0 = cnt + 1;
@@ -292,12 +349,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
       const int bk = (cnt - 1) / 4;
       // ---- tiles of the pass: the open tile takes c1 slots, then tiles of 16
       const uint32_t mybit = in && live && vld ? 1u << bk : 0u;
-      uint32_t bits = mybit;
-#pragma unroll
-      for (int dd = 1; dd < 64; dd <<= 1) {
-        const uint32_t o = __shfl_up(bits, dd);
-        if (lane >= dd) bits |= o;
-      }
+      const uint32_t bits = scan_or(mybit);
       const uint64_t ok = __ballot(!in || __builtin_popcount(tile_bm | bits) <= 2);
       int lead = ok == ~0ull ? 64 : __builtin_ctzll(~ok);
       if (lead == 0) { // the open tile holds two other buckets: close it; a fresh tile takes every
@@ -330,6 +382,56 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
         if (pnd[1] >= 0) pad_to(1, safe1);
       }
       const bool ref0 = (kinds & 3) == 2, ref1 = (kinds >> 2) == 2;
+      // ---- every PSQT load of the pass before any of its waits (a wait for a load also waits
+      // for the stores issued before it, so loads go out first): the delta rows of each slot,
+      // and the first four king-move jobs' rows (lane = square); the rest of the jobs later
+      int32_t dq[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+      if (in && live) {
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+          if ((hh ? kinds >> 2 : kinds & 3) == 1) {
+            const uint32_t lo2 = hh ? w2 : w0, hi2 = hh ? w3 : w1;
+            const int s = hh ? s1 : s0, n = hh ? n1 : n0;
+            const uint32_t i0 = lo2 & 0xFFFF, i1 = lo2 >> 16, i2 = hi2 & 0xFFFF, i3 = hi2 >> 16;
+            const uint32_t r1 = s >= 2 ? i1 : i2, r2 = s >= 2 ? i2 : i3;
+            dq[hh][0] = psqt(ft_row(i0), bk), dq[hh][1] = psqt(ft_row(r1), bk);
+            if (n > 2) dq[hh][2] = psqt(ft_row(r2), bk);
+            if (n > 3) dq[hh][3] = psqt(ft_row(i3), bk);
+          }
+        }
+      }
+      uint64_t jm = __ballot(in && live && vld && (ref0 || ref1)), jrest = jm;
+      int32_t jv[4] = {0, 0, 0, 0};
+      auto job_row_psqt = [&](int l) -> int32_t { // job l's PSQT row on this lane's square
+        const int hh = __builtin_amdgcn_readlane((int)ref1, l), cn = __builtin_amdgcn_readlane(cnt, l);
+        const uint32_t sq01 = (uint32_t)__builtin_amdgcn_readlane((int)(hh ? w2 : w0), l),
+                       sq23 = (uint32_t)__builtin_amdgcn_readlane((int)(hh ? w3 : w1), l);
+        int pos, cpc;
+        const int row = king_move_row_pc(ppc, hh, sq01 & 0xFFFF, (int)(sq01 >> 16), sq23 & 0xFFFF, sq23 >> 16, lane, pos, cpc);
+        return row >= 0 ? psqt((uint32_t)row, (cn - 1) / 4) : 0;
+      };
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (jrest) {
+          const int l = __builtin_ctzll(jrest);
+          jrest &= jrest - 1;
+          jv[u] = job_row_psqt(l);
+        }
+      }
+      if (q0 == 0 && live) {
+        const int a = (int)scan_add((uint32_t)pa), b = (int)scan_add((uint32_t)pb2);
+        pp[0][0] = __builtin_amdgcn_readlane(a, 31), pp[0][1] = __builtin_amdgcn_readlane(b, 31);
+        pp[1][0] = wadd(__builtin_amdgcn_readlane(a, 63), -pp[0][0]);
+        pp[1][1] = wadd(__builtin_amdgcn_readlane(b, 63), -pp[0][1]);
+      }
+      // the king-move jobs' PSQT sums, lane i = the i-th job's: the first four now, the rest
+      // (rare: > 4 king-move children) four at a time before the jobs run
+      int32_t jps = 0;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int32_t s = wave_sum_dpp(jv[u]);
+        if (lane == u) jps = s;
+      }
       int d0 = 0, d1 = 0;
       if (kinds == 15) {
         d0 = have ? 1 : pnd[0] >= 0 ? pnd[0] + 2 : P + 1 + (pst[0] ? 1 : 0);
@@ -340,12 +442,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
         if ((kinds >> 2) == 1) d1 = n1 - (hit1 ? 1 : 0);
       }
       const uint32_t c = (uint32_t)d0 | (uint32_t)d1 << 16;
-      uint32_t inc = c;
-#pragma unroll
-      for (int dd = 1; dd < 64; dd <<= 1) {
-        const uint32_t o = __shfl_up(inc, dd);
-        if (lane >= dd) inc += o;
-      }
+      const uint32_t inc = scan_add(c); // (two 16-bit prefix sums; a pass's entries < 2^16)
       const uint32_t exc = inc - c, tot = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
       const bool nx = q == nxpos;
       // ---- PSQT of the slot by side (a king-move perspective is written by its job below),
@@ -356,14 +453,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
           const int kd = hh ? kinds >> 2 : kinds & 3;
           int32_t v = 0;
           if (kd == 3) v = pp[hh][0];
-          if (kd == 1) {
-            const uint32_t lo2 = hh ? w2 : w0, hi2 = hh ? w3 : w1;
-            const int s = hh ? s1 : s0, n = hh ? n1 : n0;
-            const uint32_t i0 = lo2 & 0xFFFF, i1 = lo2 >> 16, i2 = hi2 & 0xFFFF, i3 = hi2 >> 16;
-            const uint32_t r1 = s >= 2 ? i1 : i2, r2 = s >= 2 ? i2 : i3;
-            const int32_t a0 = psqt(ft_row(i0), bk), a1 = psqt(ft_row(r1), bk);
-            const int32_t a2 = n > 2 ? psqt(ft_row(r2), bk) : 0, a3 = n > 3 ? psqt(ft_row(i3), bk) : 0;
-            v = wadd(pp[hh][bk == bp ? 0 : 1], wadd(wadd(-a0, s >= 2 ? -a1 : a1), wadd(a2, a3)));
+          if (kd == 1) { // parent - from-row -+ the second row + the added rows
+            const int32_t d1 = (hh ? s1 : s0) >= 2 ? -dq[hh][1] : dq[hh][1];
+            v = wadd(pp[hh][bk == bp ? 0 : 1], wadd(wadd(-dq[hh][0], d1), wadd(dq[hh][2], dq[hh][3])));
           }
           if (kd != 2) T[tk0 + tix].psq[t][hh != cst] = v;
         }
@@ -407,9 +499,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
           }
           if (pnd[hh] >= 0 || pst[hh]) { // list hh stored the row: its snapshot and state
             uint32_t x = (uint32_t)ppc << (4 * (lane & 7));
-            x |= __shfl_xor(x, 1);
-            x |= __shfl_xor(x, 2);
-            x |= __shfl_xor(x, 4);
+            x = or8(x);
             const int kci = 64 * hh + pkq[hh];
             if ((lane & 7) == 0) ksnap[w][kci][lane >> 3] = x;
             if (lane == 0) kstate[w][kci] = (uint8_t)(1 | hh << 1);
@@ -443,7 +533,23 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
       };
       int jc = 0;
       open_tile(0);
-      uint64_t jm = __ballot(in && live && vld && (ref0 || ref1));
+      for (uint32_t i0 = 4; jrest; i0 += 4) {
+        int32_t v[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          if (jrest) {
+            const int l = __builtin_ctzll(jrest);
+            jrest &= jrest - 1;
+            v[u] = job_row_psqt(l);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int32_t s = wave_sum_dpp(v[u]);
+          if ((uint32_t)lane == i0 + u) jps = s;
+        }
+      }
+      int ji = 0;
       while (jm) {
         const int l = __builtin_ctzll(jm);
         jm &= jm - 1;
@@ -458,8 +564,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
         const int kt = (int)(sq01 >> 16);
         int pos, cpc;
         const int row = king_move_row_pc(ppc, hh, sq01 & 0xFFFF, kt, sq23 & 0xFFFF, sq23 >> 16, lane, pos, cpc);
-        const int cb = (cn - 1) / 4;
-        const int32_t prw = row >= 0 ? psqt((uint32_t)row, cb) : 0; // summed at the job's end (latency)
         const uint32_t tw = hs(tl, hh != st);
         bool kuse = kc && (sq23 & 0xFFFF) == 64; // not castling
         const int kci = 64 * hh + kt;
@@ -473,8 +577,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
         uint64_t bs = 0, ba = 0;
         int spc = 0;
         if (kst & 1) {
-          const uint32_t wv = lane < 8 ? ksnap[w][kci][lane] : 0u;
-          spc = (int)((__shfl(wv, lane >> 3) >> (4 * (lane & 7))) & 15);
+          spc = (int)((ksnap[w][kci][lane >> 3] >> (4 * (lane & 7))) & 15);
           bs = __ballot(spc != cpc && spc != 0);
           ba = __ballot(spc != cpc && cpc != 0);
           const int nd = popcnt(bs) + popcnt(ba);
@@ -504,9 +607,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
         }
         if (kuse) { // the cache row now holds this child's accumulator, stored by list g
           uint32_t x = (uint32_t)cpc << (4 * (lane & 7));
-          x |= __shfl_xor(x, 1);
-          x |= __shfl_xor(x, 2);
-          x |= __shfl_xor(x, 4);
+          x = or8(x);
           if ((lane & 7) == 0) ksnap[w][kci][lane >> 3] = x;
           if (lane == 0) kstate[w][kci] = (uint8_t)(1 | g << 1);
           ps::wave_sync();
@@ -517,7 +618,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
         }
         if (g) len1 += (uint32_t)ne;
         else len0 += (uint32_t)ne;
-        const int32_t ps_sum = wave_sum(prw);
+        const int32_t ps_sum = __builtin_amdgcn_readlane(jps, ji++);
         if (lane == 0) TD->psq[tl][hh != st] = ps_sum;
       }
       while (jc < ntp - 1) close_tile(jc), ++jc, open_tile(jc);
