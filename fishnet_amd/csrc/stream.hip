@@ -120,7 +120,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
                 unsigned long long *__restrict__ pads_out, uint32_t *__restrict__ err) {
   using namespace ps;
   __shared__ uint32_t ksnap[4][128][8]; // per wave: placement (64 nibbles) of each king-cache row
-  __shared__ uint8_t kstate[4][128];    // bit 0: row holds an accumulator, bit 1: the list that stored it
   __shared__ uint16_t prow_s[4][2][32];
   // (w via readfirstlane: the compiler then knows that blk, p and every bound derived from them
   // are wave-uniform, so they live in SGPRs and their branches are scalar)
@@ -138,7 +137,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
   const uint32_t pbeg = blk * K, pend = pbeg + K < np ? pbeg + K : np;
   const uint64_t us_b = pbeg + offsets[pbeg];
   const uint64_t rbeg = eoff[pbeg] + 16ull * blk, rend = eoff[pend] + 16ull * (blk + 1);
-  uint64_t *E0 = ent + rbeg, *E1 = ent + rend - 1;
+  uint2 *E = reinterpret_cast<uint2 *>(ent + rbeg); // list 0 from E[0] up, list 1 from E[rtot - 1] down
   const uint32_t rtot = (uint32_t)(rend - rbeg); // the block's entry region (both lists; < 2^32)
   uint32_t bad = 0;                  // this lane's error bits (reported once per wave)
   // a block's tiles: <= ceil(slots / 16) + one bucket cut per parent (a parent's own slots hold
@@ -149,23 +148,30 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
   constexpr uint32_t LO_BIAS = (uint32_t)FT_BIAS_ROW * RS, LO_ZERO = (uint32_t)ZERO_ROW * RS;
   auto lo_scr = [](uint32_t r) -> uint32_t { return ((uint32_t)FT_ROWS + r) * RS; }; // scratch row r
   // entry i of list g: the row at byte offset lo, hi = multiplier + flags (see above)
+  // (one SGPR base and an unsigned 32-bit element offset for both lists: the store's address
+  // is then the base + a VGPR offset, no 64-bit address arithmetic per entry)
   auto put = [&](int g, uint32_t i, uint32_t lo, uint32_t hi) {
-    if (i >= rtot) { // never past the block's region (the final check reports the overflow)
-      bad |= 1u;
-      return;
-    }
+    // never past the block's region: an overflow (reported by the final check, which fails the
+    // call) rewrites the region's last entry
+    bad |= i >= rtot ? 1u : 0u;
+    const uint32_t ic = i < rtot ? i : rtot - 1;
     // a scratch-row load must sit GN_SCR_GAP entries after the list's last scratch store
     if ((hi & H_SCR) && i < (g ? safe1 : safe0)) bad |= 4u;
-    const uint64_t e = (uint64_t)hi << 32 | lo;
-    if (g) E1[-(int64_t)i] = e;
-    else E0[i] = e;
+    E[g ? rtot - 1 - ic : ic] = make_uint2(lo, hi);
   };
-  for (int i = lane; i < 128; i += 64) kstate[w][i] = 0;
+  // king-cache row state, lane = king square, one register per perspective: bit 0 the row holds an
+  // accumulator, bit 1 the list that stored it (v_readlane / a select: no LDS round trip)
+  uint32_t ks0 = 0, ks1 = 0;
+  auto kstate_of = [&](int hh, int ksq) -> int { return __builtin_amdgcn_readlane((int)(hh ? ks1 : ks0), ksq); };
+  auto kstate_set = [&](int hh, int ksq, int v) {
+    if (hh) ks1 = lane == ksq ? (uint32_t)v : ks1;
+    else ks0 = lane == ksq ? (uint32_t)v : ks0;
+  };
   uint16_t(*prow)[32] = prow_s[w];
   uint32_t len0 = 0, len1 = 0, tile_k = 0, p_first = pbeg, u_fill = 0, t_first = 0, tile_bm = 0;
   unsigned long long pp_a = 0, pp_b = 0, pp_c = 0, pp_d = 0; // GN_PLAN_PROF: section cycles
   int t_fill = 0, carried = 0;
-  unsigned long long rows = 0, pads = 0, fpads = 0;
+  uint32_t rows = 0, pads = 0, fpads = 0; // (per block: < 2^32)
   auto pad_to = [&](int g, uint32_t target) { // no-op entries up to target (lane-parallel, < 64)
     uint32_t &len = g ? len1 : len0;
     if (len < target) {
@@ -287,7 +293,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
         const uint64_t kb = __ballot(ppc == make_piece(hh, KING));
         const int ksq = kb ? __builtin_ctzll(kb) : 0, kci = 64 * hh + ksq;
         pkq[hh] = ksq;
-        const int kst = kstate[w][kci];
+        const int kst = kstate_of(hh, ksq);
         pst[hh] = kb != 0 && (kst == 0 || ((kst >> 1) & 1) == hh); // the row is unused or list hh's
         if (pst[hh] && (kst & 1)) {
           int spc;
@@ -502,7 +508,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
             x = or8(x);
             const int kci = 64 * hh + pkq[hh];
             if ((lane & 7) == 0) ksnap[w][kci][lane >> 3] = x;
-            if (lane == 0) kstate[w][kci] = (uint8_t)(1 | hh << 1);
+            kstate_set(hh, pkq[hh], 1 | hh << 1);
             uint32_t &sf = hh ? safe1 : safe0;
             sf = b0 + (uint32_t)(pnd[hh] >= 0 ? pnd[hh] : P) + GN_SCR_GAP; // the store's index + the gap
           }
@@ -567,7 +573,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
         const uint32_t tw = hs(tl, hh != st);
         bool kuse = kc && (sq23 & 0xFFFF) == 64; // not castling
         const int kci = 64 * hh + kt;
-        const int kst = kuse ? kstate[w][kci] : 0;
+        const int kst = kuse ? kstate_of(hh, kt) : 0;
         // a cache row, once stored, stays with the list that stored it: the other list's
         // waves are not ordered with that list's stores inside a tile, so a second list
         // storing or loading the row could race with them
@@ -597,19 +603,19 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
           if ((bs >> lane) & 1) put(g, base + ps, (uint32_t)feature_index(hh, lane, spc, kt) * RS, M_SUB | tw);
           if ((ba >> lane) & 1) put(g, base + pa, (uint32_t)row * RS, M_ADD | tw);
           if (lane == 0) put(g, base + ne - 1, LO_ZERO, kr | tw | H_KST | L);
-          rows += (unsigned long long)(nd + 1);
+          rows += (uint32_t)(nd + 1);
         } else {
           ne = cn + 1 + (kuse ? 1 : 0);
           if (lane == 0) put(g, base, LO_BIAS, M_ADD | HZ | tw);
           if (row >= 0 && pos < cn) put(g, base + 1 + pos, (uint32_t)row * RS, M_ADD | tw | (!kuse && pos == cn - 1 ? L : 0u));
           if (kuse && lane == 0) put(g, base + ne - 1, LO_ZERO, kr | tw | H_KST | L);
-          rows += (unsigned long long)(cn + 1);
+          rows += (uint32_t)(cn + 1);
         }
         if (kuse) { // the cache row now holds this child's accumulator, stored by list g
           uint32_t x = (uint32_t)cpc << (4 * (lane & 7));
           x = or8(x);
           if ((lane & 7) == 0) ksnap[w][kci][lane >> 3] = x;
-          if (lane == 0) kstate[w][kci] = (uint8_t)(1 | g << 1);
+          kstate_set(hh, kt, 1 | g << 1);
           ps::wave_sync();
         }
         if (kuse) { // this slot's last entry stores to scratch
@@ -673,8 +679,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
   if (lane == 0) {
     if ((uint64_t)len0 + len1 > (uint64_t)rtot || werr) atomicOr(err, 1u);
     if (werr4) atomicOr(err, 4u);
-    if (rows_out) atomicAdd(rows_out, rows);
-    if (pads_out && pads) atomicAdd(pads_out, pads);
+    if (rows_out) atomicAdd(rows_out, (unsigned long long)rows);
+    if (pads_out && pads) atomicAdd(pads_out, (unsigned long long)pads);
     PP_ADD(0, pp_a), PP_ADD(1, pp_b), PP_ADD(2, pp_c), PP_ADD(3, pp_d);
     SP_ADD(6, pads), SP_ADD(7, fpads);
   }

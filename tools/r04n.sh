@@ -1,0 +1,9 @@
+set -o pipefail
+# plan_kernel after the latency work: section cycles (GN_PLAN_PROF build) and the instruction-mix PMC passes
+OUT=gpurun_out/r04n
+mkdir -p $OUT
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+GPU_NNUE_LIB=$GRAFT_REPO_ROOT/fishnet_amd/lib/libgpu_nnue_pprof.so timeout -k 10 300 python -u bench.py --steps 1 --warmup 0 --no-secondary --no-cpu-baseline --check 0 > $OUT/pprof.json 2> $OUT/pprof.err || { tail -20 $OUT/pprof.err; exit 1; }
+grep "plan prof" $OUT/pprof.err | tail -3
+timeout -k 10 400 bash tools/pmc_kernels.sh r04n/pk expand > $OUT/pmc.log 2>&1 || { tail -20 $OUT/pmc.log; exit 1; }
+tail -4 $OUT/pmc.log
