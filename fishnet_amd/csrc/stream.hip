@@ -148,16 +148,17 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
   constexpr uint32_t LO_BIAS = (uint32_t)FT_BIAS_ROW * RS, LO_ZERO = (uint32_t)ZERO_ROW * RS;
   auto lo_scr = [](uint32_t r) -> uint32_t { return ((uint32_t)FT_ROWS + r) * RS; }; // scratch row r
   // entry i of list g: the row at byte offset lo, hi = multiplier + flags (see above)
-  // (one SGPR base and an unsigned 32-bit element offset for both lists: the store's address
-  // is then the base + a VGPR offset, no 64-bit address arithmetic per entry)
+  // One SGPR base and an unsigned 32-bit byte offset for both lists: the store is the base + a
+  // VGPR offset, no 64-bit address arithmetic per entry.  Entries are only ever put below their
+  // list's final length, so the final check (len0 + len1 <= rtot) covers every put; the clamp
+  // keeps an overflow (which fails the call) inside the region.
+  const uint32_t rlast = rtot - 1;
   auto put = [&](int g, uint32_t i, uint32_t lo, uint32_t hi) {
-    // never past the block's region: an overflow (reported by the final check, which fails the
-    // call) rewrites the region's last entry
-    bad |= i >= rtot ? 1u : 0u;
-    const uint32_t ic = i < rtot ? i : rtot - 1;
     // a scratch-row load must sit GN_SCR_GAP entries after the list's last scratch store
     if ((hi & H_SCR) && i < (g ? safe1 : safe0)) bad |= 4u;
-    E[g ? rtot - 1 - ic : ic] = make_uint2(lo, hi);
+    const uint32_t ic = i < rlast ? i : rlast;
+    const uint32_t x = g ? rlast - ic : ic;
+    *reinterpret_cast<uint2 *>(reinterpret_cast<char *>(E) + (x << 3)) = make_uint2(lo, hi);
   };
   // king-cache row state, lane = king square, one register per perspective: bit 0 the row holds an
   // accumulator, bit 1 the list that stored it (v_readlane / a select: no LDS round trip)
@@ -408,12 +409,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
       }
       uint64_t jm = __ballot(in && live && vld && (ref0 || ref1)), jrest = jm;
       int32_t jv[4] = {0, 0, 0, 0};
-      auto job_row_psqt = [&](int l) -> int32_t { // job l's PSQT row on this lane's square
-        const int hh = __builtin_amdgcn_readlane((int)ref1, l), cn = __builtin_amdgcn_readlane(cnt, l);
+      int jl[4] = {-1, -1, -1, -1}; // their slot lanes
+      auto job_rows = [&](int l, int &row, int &pos, int &cpc) { // job l's row on this lane's square
+        const int hh = __builtin_amdgcn_readlane((int)ref1, l);
         const uint32_t sq01 = (uint32_t)__builtin_amdgcn_readlane((int)(hh ? w2 : w0), l),
                        sq23 = (uint32_t)__builtin_amdgcn_readlane((int)(hh ? w3 : w1), l);
-        int pos, cpc;
-        const int row = king_move_row_pc(ppc, hh, sq01 & 0xFFFF, (int)(sq01 >> 16), sq23 & 0xFFFF, sq23 >> 16, lane, pos, cpc);
+        row = king_move_row_pc(ppc, hh, sq01 & 0xFFFF, (int)(sq01 >> 16), sq23 & 0xFFFF, sq23 >> 16, lane, pos, cpc);
+      };
+      auto job_row_psqt = [&](int l, int row) -> int32_t { // its PSQT row
+        const int cn = __builtin_amdgcn_readlane(cnt, l);
         return row >= 0 ? psqt((uint32_t)row, (cn - 1) / 4) : 0;
       };
 #pragma unroll
@@ -421,7 +425,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
         if (jrest) {
           const int l = __builtin_ctzll(jrest);
           jrest &= jrest - 1;
-          jv[u] = job_row_psqt(l);
+          int row, pos, cpc;
+          job_rows(l, row, pos, cpc);
+          jv[u] = job_row_psqt(l, row), jl[u] = l;
         }
       }
       if (q0 == 0 && live) {
@@ -430,13 +436,32 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
         pp[1][0] = wadd(__builtin_amdgcn_readlane(a, 63), -pp[0][0]);
         pp[1][1] = wadd(__builtin_amdgcn_readlane(b, 63), -pp[0][1]);
       }
-      // the king-move jobs' PSQT sums, lane i = the i-th job's: the first four now, the rest
-      // (rare: > 4 king-move children) four at a time before the jobs run
-      int32_t jps = 0;
+      // the king-move jobs' PSQT sums, on their slot lanes: the first four now, the rest (rare:
+      // > 4 king-move children) four at a time
+      int32_t jsum = 0;
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int32_t s = wave_sum_dpp(jv[u]);
-        if (lane == u) jps = s;
+        if (lane == jl[u]) jsum = s;
+      }
+      while (jrest) {
+        int32_t v[4] = {0, 0, 0, 0};
+        int vl[4] = {-1, -1, -1, -1};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          if (jrest) {
+            const int l = __builtin_ctzll(jrest);
+            jrest &= jrest - 1;
+            int row, pos, cpc;
+            job_rows(l, row, pos, cpc);
+            v[u] = job_row_psqt(l, row), vl[u] = l;
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int32_t s = wave_sum_dpp(v[u]);
+          if (lane == vl[u]) jsum = s;
+        }
       }
       int d0 = 0, d1 = 0;
       if (kinds == 15) {
@@ -451,8 +476,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
       const uint32_t inc = scan_add(c); // (two 16-bit prefix sums; a pass's entries < 2^16)
       const uint32_t exc = inc - c, tot = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
       const bool nx = q == nxpos;
-      // ---- PSQT of the slot by side (a king-move perspective is written by its job below),
-      // slot metadata
+      // ---- PSQT of the slot by side (a king-move perspective: its job's sum), slot metadata
       if (in && live) {
 #pragma unroll
         for (int hh = 0; hh < 2; ++hh) {
@@ -463,7 +487,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
             const int32_t d1 = (hh ? s1 : s0) >= 2 ? -dq[hh][1] : dq[hh][1];
             v = wadd(pp[hh][bk == bp ? 0 : 1], wadd(wadd(-dq[hh][0], d1), wadd(dq[hh][2], dq[hh][3])));
           }
-          if (kd != 2) T[tk0 + tix].psq[t][hh != cst] = v;
+          T[tk0 + tix].psq[t][hh != cst] = kd == 2 ? jsum : v;
         }
       }
       if (in) T[tk0 + tix].meta[t] = (uint8_t)((live && vld ? 1 : 0) | bk << 1 | (q == 0 ? 16 : 0) | cst << 5);
@@ -539,31 +563,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
       };
       int jc = 0;
       open_tile(0);
-      for (uint32_t i0 = 4; jrest; i0 += 4) {
-        int32_t v[4] = {0, 0, 0, 0};
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          if (jrest) {
-            const int l = __builtin_ctzll(jrest);
-            jrest &= jrest - 1;
-            v[u] = job_row_psqt(l);
-          }
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int32_t s = wave_sum_dpp(v[u]);
-          if ((uint32_t)lane == i0 + u) jps = s;
-        }
-      }
-      int ji = 0;
+      // a job's slot descriptor in one register (one v_readlane per job): tile (< 8), side
+      // refreshed, side to move, slot in tile, piece count
+      const uint32_t jdesc = (uint32_t)tix | (uint32_t)ref1 << 3 | (uint32_t)cst << 4 | (uint32_t)t << 5 | (uint32_t)cnt << 9;
       while (jm) {
         const int l = __builtin_ctzll(jm);
         jm &= jm - 1;
-        const int jt = __builtin_amdgcn_readlane(tix, l);
+        const uint32_t jd = (uint32_t)__builtin_amdgcn_readlane((int)jdesc, l);
+        const int jt = (int)(jd & 7), hh = (int)((jd >> 3) & 1), st = (int)((jd >> 4) & 1);
+        const int tl = (int)((jd >> 5) & 15), cn = (int)(jd >> 9);
         while (jc < jt) close_tile(jc), ++jc, open_tile(jc);
-        const int hh = __builtin_amdgcn_readlane((int)ref1, l), st = __builtin_amdgcn_readlane(cst, l);
-        const int cn = __builtin_amdgcn_readlane(cnt, l), tl = __builtin_amdgcn_readlane(t, l);
-        TileDesc *TD = T + tk0 + jt;
         const bool nxl = q0 + l == nxpos;
         const uint32_t sq01 = (uint32_t)__builtin_amdgcn_readlane((int)(hh ? w2 : w0), l),
                        sq23 = (uint32_t)__builtin_amdgcn_readlane((int)(hh ? w3 : w1), l);
@@ -624,8 +633,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
         }
         if (g) len1 += (uint32_t)ne;
         else len0 += (uint32_t)ne;
-        const int32_t ps_sum = __builtin_amdgcn_readlane(jps, ji++);
-        if (lane == 0) TD->psq[tl][hh != st] = ps_sum;
       }
       while (jc < ntp - 1) close_tile(jc), ++jc, open_tile(jc);
       pp_d += PP_T() - pp_t, pp_t = PP_T();
