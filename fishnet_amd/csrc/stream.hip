@@ -182,12 +182,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
     }
   };
 
+  // a field of tile k of the block by a 32-bit byte offset from the block's first tile (the
+  // stores are then an SGPR base + a VGPR offset)
+  char *const Tb = reinterpret_cast<char *>(T);
+  auto tf = [&](uint32_t k, uint32_t field) -> char * { return Tb + (k * (uint32_t)sizeof(TileDesc) + field); };
   auto flush = [&]() {
     // (the lists need no padding at a tile's end: the stream enters and leaves its ring
     // revolutions at any entry)
-    TileDesc *d = T + tile_k;
-    if (lane >= t_fill && lane < 16) d->meta[lane] = 0;
-    if (lane == 0) d->e_end[0] = len0, d->e_end[1] = len1, d->p_first = p_first, d->first = t_first;
+    if (lane >= t_fill && lane < 16) *tf(tile_k, offsetof(TileDesc, meta) + lane) = 0;
+    if (lane == 0) *reinterpret_cast<uint4 *>(tf(tile_k, 0)) = make_uint4(len0, len1, p_first, t_first);
     ++tile_k, t_fill = 0, tile_bm = 0;
   };
 
@@ -354,40 +357,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
       }
       const bool in = lane < n_in;
       const int bk = (cnt - 1) / 4;
-      // ---- tiles of the pass: the open tile takes c1 slots, then tiles of 16
-      const uint32_t mybit = in && live && vld ? 1u << bk : 0u;
-      const uint32_t bits = scan_or(mybit);
-      const uint64_t ok = __ballot(!in || __builtin_popcount(tile_bm | bits) <= 2);
-      int lead = ok == ~0ull ? 64 : __builtin_ctzll(~ok);
-      if (lead == 0) { // the open tile holds two other buckets: close it; a fresh tile takes every
-        flush();       // slot of a parent (its slots hold <= 2 buckets: P and P - 1 pieces)
-        if (__ballot(in && __builtin_popcount(bits) > 2)) bad |= 1u; // cannot happen; reported
-        lead = 64;
-      }
-      if (t_fill == 0) p_first = p, t_first = u_fill;
-      const int tf0 = t_fill, room = 16 - tf0;
-      const int c1 = room < lead ? (room < n_in ? room : n_in) : (lead < n_in ? lead : n_in);
-      const int tix = lane < c1 ? 0 : 1 + (lane - c1) / 16;        // this slot's tile, from tk0
-      const int t = lane < c1 ? tf0 + lane : (lane - c1) % 16;     // its slot in that tile
-      const int ntp = n_in <= c1 ? 1 : 1 + (n_in - c1 + 15) / 16; // tiles the pass touches
-      const uint32_t tk0 = tile_k;
-      if (!in) vld = 0, kinds = 0, n0 = n1 = s0 = s1 = 0, w0 = w1 = w2 = w3 = 0;
-      // ---- sibling cache: a delta child whose from-row equals the previous delta child's (in
-      // the same list) starts from the cached (parent - from-row) and drops that entry
-      const int key0 = (kinds & 3) == 1 ? (int)(w0 & 0xFFFF) : -1;
-      const int key1 = (kinds >> 2) == 1 ? (int)(w2 & 0xFFFF) : -1;
-      const uint64_t km0 = __ballot(key0 >= 0), km1 = __ballot(key1 >= 0), lt = (1ull << lane) - 1;
-      const int pk0 = __shfl(key0, (km0 & lt) ? 63 - __builtin_clzll(km0 & lt) : 0);
-      const int pk1 = __shfl(key1, (km1 & lt) ? 63 - __builtin_clzll(km1 & lt) : 0);
-      const bool hit0 = key0 >= 0 && key0 == ((km0 & lt) ? pk0 : ckey0);
-      const bool hit1 = key1 >= 0 && key1 == ((km1 & lt) ? pk1 : ckey1);
-      if (km0) ckey0 = __builtin_amdgcn_readlane(key0, 63 - __builtin_clzll(km0));
-      if (km1) ckey1 = __builtin_amdgcn_readlane(key1, 63 - __builtin_clzll(km1));
-      // ---- delta entries per lane (the parent's and the delta perspectives'), prefix sums
-      if (live && q0 == 0) { // the parent loads the carry / cache rows: after their stores
-        if (pnd[0] >= 0) pad_to(0, safe0);
-        if (pnd[1] >= 0) pad_to(1, safe1);
-      }
       const bool ref0 = (kinds & 3) == 2, ref1 = (kinds >> 2) == 2;
       // ---- every PSQT load of the pass before any of its waits (a wait for a load also waits
       // for the stores issued before it, so loads go out first): the delta rows of each slot,
@@ -430,6 +399,36 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
           jv[u] = job_row_psqt(l, row), jl[u] = l;
         }
       }
+      // (the slot bookkeeping below runs while the PSQT loads are in flight)
+      // ---- tiles of the pass: the open tile takes c1 slots, then tiles of 16
+      const uint32_t mybit = in && live && vld ? 1u << bk : 0u;
+      const uint32_t bits = scan_or(mybit);
+      const uint64_t ok = __ballot(!in || __builtin_popcount(tile_bm | bits) <= 2);
+      int lead = ok == ~0ull ? 64 : __builtin_ctzll(~ok);
+      if (lead == 0) { // the open tile holds two other buckets: close it; a fresh tile takes every
+        flush();       // slot of a parent (its slots hold <= 2 buckets: P and P - 1 pieces)
+        if (__ballot(in && __builtin_popcount(bits) > 2)) bad |= 1u; // cannot happen; reported
+        lead = 64;
+      }
+      if (t_fill == 0) p_first = p, t_first = u_fill;
+      const int tf0 = t_fill, room = 16 - tf0;
+      const int c1 = room < lead ? (room < n_in ? room : n_in) : (lead < n_in ? lead : n_in);
+      const int tix = lane < c1 ? 0 : 1 + (lane - c1) / 16;        // this slot's tile, from tk0
+      const int t = lane < c1 ? tf0 + lane : (lane - c1) % 16;     // its slot in that tile
+      const int ntp = n_in <= c1 ? 1 : 1 + (n_in - c1 + 15) / 16; // tiles the pass touches
+      const uint32_t tk0 = tile_k;
+      if (!in) vld = 0, kinds = 0, n0 = n1 = s0 = s1 = 0, w0 = w1 = w2 = w3 = 0;
+      // ---- sibling cache: a delta child whose from-row equals the previous delta child's (in
+      // the same list) starts from the cached (parent - from-row) and drops that entry
+      const int key0 = (kinds & 3) == 1 ? (int)(w0 & 0xFFFF) : -1;
+      const int key1 = (kinds >> 2) == 1 ? (int)(w2 & 0xFFFF) : -1;
+      const uint64_t km0 = __ballot(key0 >= 0), km1 = __ballot(key1 >= 0), lt = (1ull << lane) - 1;
+      const int pk0 = __shfl(key0, (km0 & lt) ? 63 - __builtin_clzll(km0 & lt) : 0);
+      const int pk1 = __shfl(key1, (km1 & lt) ? 63 - __builtin_clzll(km1 & lt) : 0);
+      const bool hit0 = key0 >= 0 && key0 == ((km0 & lt) ? pk0 : ckey0);
+      const bool hit1 = key1 >= 0 && key1 == ((km1 & lt) ? pk1 : ckey1);
+      if (km0) ckey0 = __builtin_amdgcn_readlane(key0, 63 - __builtin_clzll(km0));
+      if (km1) ckey1 = __builtin_amdgcn_readlane(key1, 63 - __builtin_clzll(km1));
       if (q0 == 0 && live) {
         const int a = (int)scan_add((uint32_t)pa), b = (int)scan_add((uint32_t)pb2);
         pp[0][0] = __builtin_amdgcn_readlane(a, 31), pp[0][1] = __builtin_amdgcn_readlane(b, 31);
@@ -441,8 +440,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
       int32_t jsum = 0;
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const int32_t s = wave_sum_dpp(jv[u]);
-        if (lane == jl[u]) jsum = s;
+        if (jl[u] >= 0) { // (uniform)
+          const int32_t s = wave_sum_dpp(jv[u]);
+          if (lane == jl[u]) jsum = s;
+        }
       }
       while (jrest) {
         int32_t v[4] = {0, 0, 0, 0};
@@ -487,11 +488,19 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
             const int32_t d1 = (hh ? s1 : s0) >= 2 ? -dq[hh][1] : dq[hh][1];
             v = wadd(pp[hh][bk == bp ? 0 : 1], wadd(wadd(-dq[hh][0], d1), wadd(dq[hh][2], dq[hh][3])));
           }
-          T[tk0 + tix].psq[t][hh != cst] = kd == 2 ? jsum : v;
+          *reinterpret_cast<int32_t *>(tf(tk0 + tix, offsetof(TileDesc, psq) + 8 * t + 4 * (hh != cst))) =
+              kd == 2 ? jsum : v;
         }
       }
-      if (in) T[tk0 + tix].meta[t] = (uint8_t)((live && vld ? 1 : 0) | bk << 1 | (q == 0 ? 16 : 0) | cst << 5);
-      if (in) T[tk0 + tix].adj[t] = (int16_t)(q == 0 ? 0 : child_of(q) - (q - 1));
+      if (in) {
+        *tf(tk0 + tix, offsetof(TileDesc, meta) + t) = (char)((live && vld ? 1 : 0) | bk << 1 | (q == 0 ? 16 : 0) | cst << 5);
+        *reinterpret_cast<int16_t *>(tf(tk0 + tix, offsetof(TileDesc, adj) + 2 * t)) =
+            (int16_t)(q == 0 ? 0 : child_of(q) - (q - 1));
+      }
+      if (live && q0 == 0) { // the parent loads the carry / cache rows: after their stores
+        if (pnd[0] >= 0) pad_to(0, safe0);
+        if (pnd[1] >= 0) pad_to(1, safe1);
+      }
       // the parent's entries (the parent is lane 0: tile 0 of the pass, its delta region starts
       // at the cursor), before the jobs: a cache-row load is put while the lists' last scratch
       // stores are still the ones before it (put() checks the distance)
@@ -555,11 +564,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
         len0 += d & 0xFFFF, len1 += d >> 16;
       };
       auto close_tile = [&](int j) { // a tile the pass filled (or cut), not the pass's last
-        TileDesc *dt = T + tk0 + j;
         const int fill = j == 0 ? tf0 + c1 : 16;
-        if (lane >= fill && lane < 16) dt->meta[lane] = 0;
-        const uint32_t pf = j == 0 ? p_first : p, tf = j == 0 ? t_first : u_fill + (uint32_t)tile_lane0(j);
-        if (lane == 0) dt->e_end[0] = len0, dt->e_end[1] = len1, dt->p_first = pf, dt->first = tf;
+        if (lane >= fill && lane < 16) *tf(tk0 + j, offsetof(TileDesc, meta) + lane) = 0;
+        const uint32_t pf = j == 0 ? p_first : p, tfi = j == 0 ? t_first : u_fill + (uint32_t)tile_lane0(j);
+        if (lane == 0) *reinterpret_cast<uint4 *>(tf(tk0 + j, 0)) = make_uint4(len0, len1, pf, tfi);
       };
       int jc = 0;
       open_tile(0);
