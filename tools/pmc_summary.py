@@ -70,7 +70,7 @@ def main(tag):
         bl = json.load(open(bench_p)) if os.path.exists(bench_p) else None
         fetch = avg["FETCH_SIZE"] * 1024 * 2
         write = avg.get("WRITE_SIZE", 0.0) * 1024
-        s = {"kernel": kname, "launches": len(vals["FETCH_SIZE"]), "abi": 3,
+        s = {"kernel": kname, "launches": len(vals["FETCH_SIZE"]), "abi": 4,
              "FETCH_SIZE_kB": avg["FETCH_SIZE"], "WRITE_SIZE_kB": avg.get("WRITE_SIZE"),
              "hbm_side_bytes_per_launch": fetch + write,
              "correction": "bytes = FETCH_SIZE kB x 1024 x 2 (gfx950 wide reads) + WRITE_SIZE kB x 1024; "
