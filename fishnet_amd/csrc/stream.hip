@@ -121,6 +121,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
   using namespace ps;
   __shared__ uint32_t ksnap[4][128][8]; // per wave: placement (64 nibbles) of each king-cache row
   __shared__ uint16_t prow_s[4][2][32];
+  __shared__ uint32_t jrow_s[4][4][64]; // per wave: the first four jobs' (row + 1) | pos << 16 | cpc << 24, lane = square
   // (w via readfirstlane: the compiler then knows that blk, p and every bound derived from them
   // are wave-uniform, so they live in SGPRs and their branches are scalar)
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -397,6 +398,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
           int row, pos, cpc;
           job_rows(l, row, pos, cpc);
           jv[u] = job_row_psqt(l, row), jl[u] = l;
+          jrow_s[w][u][lane] = (uint32_t)(row + 1) | (uint32_t)pos << 16 | (uint32_t)cpc << 24; // (for the job loop)
         }
       }
       // (the slot bookkeeping below runs while the PSQT loads are in flight)
@@ -574,6 +576,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
       // a job's slot descriptor in one register (one v_readlane per job): tile (< 8), side
       // refreshed, side to move, slot in tile, piece count
       const uint32_t jdesc = (uint32_t)tix | (uint32_t)ref1 << 3 | (uint32_t)cst << 4 | (uint32_t)t << 5 | (uint32_t)cnt << 9;
+      int ji = 0; // the job's index in the pass
       while (jm) {
         const int l = __builtin_ctzll(jm);
         jm &= jm - 1;
@@ -585,8 +588,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
         const uint32_t sq01 = (uint32_t)__builtin_amdgcn_readlane((int)(hh ? w2 : w0), l),
                        sq23 = (uint32_t)__builtin_amdgcn_readlane((int)(hh ? w3 : w1), l);
         const int kt = (int)(sq01 >> 16);
-        int pos, cpc;
-        const int row = king_move_row_pc(ppc, hh, sq01 & 0xFFFF, kt, sq23 & 0xFFFF, sq23 >> 16, lane, pos, cpc);
+        int row, pos, cpc;
+        if (ji < 4) { // computed with the PSQT loads (LDS: no registers held across the pass)
+          const uint32_t r = jrow_s[w][ji][lane];
+          row = (int)(r & 0xFFFF) - 1, pos = (int)((r >> 16) & 0xFF), cpc = (int)(r >> 24);
+        } else {
+          row = king_move_row_pc(ppc, hh, sq01 & 0xFFFF, kt, sq23 & 0xFFFF, sq23 >> 16, lane, pos, cpc);
+        }
+        ++ji;
         const uint32_t tw = hs(tl, hh != st);
         bool kuse = kc && (sq23 & 0xFFFF) == 64; // not castling
         const int kci = 64 * hh + kt;
