@@ -158,13 +158,12 @@ __device__ __forceinline__ void layer_stack_wave(const NetDevice &net, const uin
   constexpr int XS = L1 + 16, KS = L1 / 64, BATCH = KS % 6 == 0 ? 6 : KS % 4 == 0 ? 4 : KS;
   static_assert(KS % BATCH == 0, "k-steps per batch");
   const int row = lane & 15, kg = lane >> 4;
-  // fc_1 / fc_2 parameters first: their latency hides behind fc_0
+  // fc_1 / fc_2 parameters first: their latency hides behind fc_0.  Loaded by every lane, with
+  // no branch around them (a branch made the compiler wait for them before fc_0's loads): the
+  // lanes kg >= 2 hold a copy whose products meet fc_1's zero A operand (a1 below)
   const int4v zero = {0, 0, 0, 0};
-  int4v wl = zero, wh = zero;
-  if (kg < 2) {
-    wl = *reinterpret_cast<const int4v *>(net.w1 + ((size_t)b * 32 + row) * 32 + kg * 16);
-    wh = *reinterpret_cast<const int4v *>(net.w1 + ((size_t)b * 32 + 16 + row) * 32 + kg * 16);
-  }
+  const int4v wl = *reinterpret_cast<const int4v *>(net.w1 + ((size_t)b * 32 + row) * 32 + (kg & 1) * 16);
+  const int4v wh = *reinterpret_cast<const int4v *>(net.w1 + ((size_t)b * 32 + 16 + row) * 32 + (kg & 1) * 16);
   const int32_t bias0 = net.b0[b * 16 + row];
   const int32_t b1l = net.b1[b * 32 + row], b1h = net.b1[b * 32 + 16 + row];
   const int32_t w2l = net.w2[b * 32 + row], w2h = net.w2[b * 32 + 16 + row];
