@@ -50,7 +50,7 @@
 #include "kernels.h"
 
 #ifndef GN_PLAN_WPE
-#define GN_PLAN_WPE 3 // 168 VGPRs, (almost) no spills: measured 3 % faster than 4 waves per SIMD at 128 VGPRs with spills
+#define GN_PLAN_WPE 4 // <= 128 VGPRs, no spills (round 3: 3 waves at 168 VGPRs beat 4 with spills; round 4 fits 4)
 #endif
 #ifndef GN_EXPAND_WPE
 #define GN_EXPAND_WPE (GN_RING == 4 ? 5 : 4)
@@ -574,30 +574,32 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
       int jc = 0;
       open_tile(0);
       // a job's slot descriptor in one register (one v_readlane per job): tile (< 8), side
-      // refreshed, side to move, slot in tile, piece count
-      const uint32_t jdesc = (uint32_t)tix | (uint32_t)ref1 << 3 | (uint32_t)cst << 4 | (uint32_t)t << 5 | (uint32_t)cnt << 9;
+      // refreshed, side to move, slot in tile, piece count, king destination, not castling
+      const uint32_t jsq01 = ref1 ? w2 : w0, jsq23 = ref1 ? w3 : w1;
+      const uint32_t jdesc = (uint32_t)tix | (uint32_t)ref1 << 3 | (uint32_t)cst << 4 | (uint32_t)t << 5 |
+                             (uint32_t)cnt << 9 | ((jsq01 >> 16) & 63) << 15 | ((jsq23 & 0xFFFF) == 64 ? 1u << 21 : 0u);
       int ji = 0; // the job's index in the pass
       while (jm) {
         const int l = __builtin_ctzll(jm);
         jm &= jm - 1;
         const uint32_t jd = (uint32_t)__builtin_amdgcn_readlane((int)jdesc, l);
         const int jt = (int)(jd & 7), hh = (int)((jd >> 3) & 1), st = (int)((jd >> 4) & 1);
-        const int tl = (int)((jd >> 5) & 15), cn = (int)(jd >> 9);
+        const int tl = (int)((jd >> 5) & 15), cn = (int)((jd >> 9) & 63);
         while (jc < jt) close_tile(jc), ++jc, open_tile(jc);
         const bool nxl = q0 + l == nxpos;
-        const uint32_t sq01 = (uint32_t)__builtin_amdgcn_readlane((int)(hh ? w2 : w0), l),
-                       sq23 = (uint32_t)__builtin_amdgcn_readlane((int)(hh ? w3 : w1), l);
-        const int kt = (int)(sq01 >> 16);
+        const int kt = (int)((jd >> 15) & 63);
         int row, pos, cpc;
         if (ji < 4) { // computed with the PSQT loads (LDS: no registers held across the pass)
           const uint32_t r = jrow_s[w][ji][lane];
           row = (int)(r & 0xFFFF) - 1, pos = (int)((r >> 16) & 0xFF), cpc = (int)(r >> 24);
         } else {
+          const uint32_t sq01 = (uint32_t)__builtin_amdgcn_readlane((int)(hh ? w2 : w0), l),
+                         sq23 = (uint32_t)__builtin_amdgcn_readlane((int)(hh ? w3 : w1), l);
           row = king_move_row_pc(ppc, hh, sq01 & 0xFFFF, kt, sq23 & 0xFFFF, sq23 >> 16, lane, pos, cpc);
         }
         ++ji;
         const uint32_t tw = hs(tl, hh != st);
-        bool kuse = kc && (sq23 & 0xFFFF) == 64; // not castling
+        bool kuse = kc && ((jd >> 21) & 1); // not castling
         const int kci = 64 * hh + kt;
         const int kst = kuse ? kstate_of(hh, kt) : 0;
         // a cache row, once stored, stays with the list that stored it: the other list's
@@ -790,6 +792,11 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
   const uint32_t ntiles = btiles[blk];
   const TileDesc *T = tiles + us_b / 16 + (uint64_t)(K + 2) * blk; // as plan_kernel
   const uint64_t rbeg = eoff[pbeg] + 16ull * blk, rend = eoff[pend] + 16ull * (blk + 1);
+  // a list never ends past the block's entry bound (the region less its 16 spare entries): a
+  // tile end beyond it can only come from a plan that overflowed, which the plan reports (err
+  // bit 0, the call fails); clamped, the entry loads (and their prefetch, 8 ahead) stay inside
+  // the region whatever the descriptors say
+  const uint32_t elim = (uint32_t)(rend - rbeg) - 16u;
 #ifdef GN_XCD_PROF
   const unsigned long long xp_t0 = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -955,7 +962,7 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
       sp_e0 = a0, sp_e1 = a1;
     }
 #endif
-    const uint32_t e_end = __builtin_amdgcn_readfirstlane(D->e_end[HU]);
+    const uint32_t e_end = min((uint32_t)__builtin_amdgcn_readfirstlane(D->e_end[HU]), elim);
     const uint32_t p_first = __builtin_amdgcn_readfirstlane(D->p_first);
     const uint32_t first = __builtin_amdgcn_readfirstlane(D->first);
     uint32_t mw[4];
