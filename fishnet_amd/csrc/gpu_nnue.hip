@@ -173,7 +173,9 @@ struct DevBuf {
     if (p) (void)hipFree(p);
     p = nullptr;
     cap = 0;
-    hipError_t e = hipMalloc(&p, std::max<size_t>(want, 1) * sizeof(T));
+    // (whole 16-B units: a kernel may read the aligned word holding a byte array's last byte,
+    // plan_kernel's need / next-slot loads)
+    hipError_t e = hipMalloc(&p, (std::max<size_t>(want, 1) * sizeof(T) + 15) & ~(size_t)15);
     if (e == hipSuccess) cap = want;
     return e;
   }

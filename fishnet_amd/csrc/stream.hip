@@ -202,7 +202,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
   // m / nd the words holding next_slot[p] / need_parent[p].  Children beyond the 63rd are
   // loaded in their own pass.  The values stay as loaded, with no branch around a load (any
   // arithmetic on them, or a copy where two paths meet, would wait for them here); an absent
-  // array is read from the board instead and ignored.
+  // array is read from the board instead and ignored.  (The library allocates its byte arrays in
+  // whole 16-B units, so the aligned word holding a last byte is inside the allocation.)
   struct In {
     uint32_t bd, a, b, c, d, m, nd;
   };
