@@ -1069,12 +1069,12 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
 #pragma unroll
         for (int i = 0; i < 4; ++i) acc0[buf][(4 * kg + i) * AS + row] = 0; // free for bucket bq + 2
         const int4v zero = {0, 0, 0, 0};
-        int4v wl = zero, wh = zero, a1 = zero;
-        if (kg < 2) {
-          wl = *reinterpret_cast<const int4v *>(net.w1 + ((size_t)b * 32 + row) * 32 + kg * 16);
-          wh = *reinterpret_cast<const int4v *>(net.w1 + ((size_t)b * 32 + 16 + row) * 32 + kg * 16);
-          a1 = *reinterpret_cast<const int4v *>(&in1[buf][row][kg * 16]);
-        }
+        // (fc_1's weights by every lane, no branch around the loads: lanes kg >= 2 hold a copy whose
+        // products meet the zero A operand)
+        const int4v wl = *reinterpret_cast<const int4v *>(net.w1 + ((size_t)b * 32 + row) * 32 + (kg & 1) * 16);
+        const int4v wh = *reinterpret_cast<const int4v *>(net.w1 + ((size_t)b * 32 + 16 + row) * 32 + (kg & 1) * 16);
+        int4v a1 = zero;
+        if (kg < 2) a1 = *reinterpret_cast<const int4v *>(&in1[buf][row][kg * 16]);
         const int4v cl = __builtin_amdgcn_mfma_i32_16x16x64_i8(a1, wl, zero, 0, 0, 0);
         const int4v ch = __builtin_amdgcn_mfma_i32_16x16x64_i8(a1, wh, zero, 0, 0, 0);
         int32_t part[4];
