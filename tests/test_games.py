@@ -275,3 +275,32 @@ def test_gpu_replay_equals_device_games_and_host_replay(gpu_ctx, oracle_lib):
         boards, _, _ = G.replay_game(START, ucis[g])
         got = gpu_ctx.evaluate_batch([G.board_to_fen(b) for b in boards], 1)
         assert np.array_equal(got, pos[int(offs[g]):int(offs[g + 1])]), g
+
+
+@pytest.mark.gpu
+def test_king_walk_games_vs_oracle(gpu_ctx, oracle_nets, oracle_lib):
+    """Games in which most children are king moves: kings alone (every child refreshes the
+    mover's perspective from the king cache), and kings with both rooks and castling rights.
+    A parent then has more than four king-move jobs, so the plan takes its second job path
+    (PSQT rows loaded four jobs at a time, the job rows recomputed in the job loop), and
+    castling children skip the cache; every position and child vs the oracle."""
+    from fishnet_amd import gpu_nnue as G
+    big, small = oracle_nets
+    rng = random.Random(11)
+    roots = ["8/8/3k4/8/8/4K3/8/8 w - - 0 1", "r3k2r/8/8/8/8/8/8/R3K2R w KQkq - 0 1",
+             "8/2k5/8/8/8/8/5K2/8 b - - 0 1"]
+    games = [(r, _random_game(oracle_lib, rng, r, 40), []) for r in roots]
+    out = gpu_ctx.evaluate_games(games, 0, children=True)
+    most = 0  # most children of a kings-only parent (every child there a king move)
+    for g, ((root, moves, _), o) in enumerate(zip(games, out)):
+        assert o["status"] == 0
+        fens, _ = oracle_lib.replay_game(root, moves)
+        for i, fen in enumerate(fens):
+            cm, ce = o["children"][i]
+            p_exp, m_exp, k_exp = oracle_lib.expand_eval(big, small, fen, 0)
+            assert tuple(o["evals"][i]) == tuple(p_exp), fen
+            assert dict(zip(cm.tolist(), map(tuple, ce.tolist()))) == \
+                dict(zip(m_exp, map(tuple, G.children_from_evals(k_exp).tolist()))), fen
+            if g == 0:
+                most = max(most, len(cm))
+    assert most > 4  # (a parent with more than four king-move jobs)
