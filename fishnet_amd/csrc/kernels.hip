@@ -1015,47 +1015,98 @@ __global__ void count_children_kernel(const gn_board *__restrict__ boards, size_
   }
 }
 
-__device__ __forceinline__ bool same_placement(const gn_board &a, const gn_board &b) {
-  uint64_t x[2], y[2];
-  __builtin_memcpy(x, a.pc, 16);
-  __builtin_memcpy(y, b.pc, 16);
-  return a.occ == b.occ && x[0] == y[0] && x[1] == y[1];
-}
-
-// Children in two passes: child_moves_kernel (a thread per parent) lists the legal moves
-// and the owning parent of every child; child_boards_kernel (a thread per child) makes the
-// child, its feature-transformer delta and the chained-walk link.  A thread per parent
+// Children in two passes: child_moves_kernel (a thread per parent) lists the legal moves,
+// the owning parent of every child and the chained-walk link; child_boards_kernel (a thread
+// per child) makes the child and its feature-transformer delta.  A thread per parent
 // writing ~31 children of 58 B each left partial L2 lines to be written back (4.5x the
 // bytes); a thread per child writes every array coalesced.
+//
+// The link, next_slot[i]: the child whose placement is boards[i + 1]'s (a game's next
+// position; no two legal moves give one placement); the chained walk then starts parent
+// i + 1 from that child's accumulators, gathering one carry row per perspective instead
+// of its refresh.  Found per parent without making any child: S is the set of squares on
+// which the parent's and the next board's placements differ; a move can give the next
+// placement only when the squares it changes are exactly S, the occupancy it leaves is the
+// next board's and the piece(s) it puts down stand there in the next board -- then the two
+// placements agree on every square.  (Packing each child to compare it cost the per-child
+// pass 3.1 ms a step of its 5.8: every wave held a linked lane.)
 __global__ void child_moves_kernel(const gn_board *__restrict__ boards, size_t n, const Tables *__restrict__ tables,
                                    const uint64_t *__restrict__ offsets, uint16_t *__restrict__ moves,
-                                   uint32_t *__restrict__ owner, uint8_t *__restrict__ next_slot,
+                                   uint32_t *__restrict__ owner, uint8_t *__restrict__ next_slot, int chain_k,
                                    unsigned long long *__restrict__ rows, Board *__restrict__ unpacked) {
   __shared__ Tables T;
   load_tables(T, tables);
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  if (next_slot) next_slot[i] = 255; // child_boards_kernel overwrites it on a match
+  uint32_t slot = 255;
   Board B;
-  if (!unpack(boards[i], B)) return;
+  if (!unpack(boards[i], B)) {
+    if (next_slot) next_slot[i] = 255;
+    return;
+  }
   if (unpacked) unpacked[i] = B; // for child_boards_kernel (a valid board has children only)
-  uint64_t k = offsets[i];
+  // S (0: no link possible) and the next board's bitboards
+  Board N;
+  Bitboard S = 0;
+  if (next_slot && i + 1 < n) {
+    const gn_board nb = boards[i + 1];
+    const int pn = popcnt(nb.occ);
+    if (pn >= 2 && pn <= 32) { // a child has 2..32 pieces
+      unpack(nb, N);           // a bad piece nibble leaves its square out of N's types: in S
+      S = (B.byColor[0] ^ N.byColor[0]) | (B.byColor[1] ^ N.byColor[1]) | (B.byType[0] ^ N.byType[0]);
+#pragma unroll
+      for (int t = PAWN; t <= KING; ++t) S |= B.byType[t] ^ N.byType[t];
+    }
+  }
+  const int us = B.stm;
+  const Bitboard occ = B.byType[0];
+  const uint64_t k0 = offsets[i];
+  uint64_t k = k0;
   gen_legal(B, T, [&](uint16_t m) {
     moves[k] = m;
     owner[k] = (uint32_t)i;
+    if (S) {
+      const int from = move_from(m), to = move_to(m), type = move_type(m);
+      Bitboard sm, cocc;
+      int kto = to, rto = to;
+      if (type == MT_CASTLING) {
+        const int kside = to > from;
+        kto = rel_sq(us, kside ? 6 : 2), rto = rel_sq(us, kside ? 5 : 3);
+        sm = (kto != from ? sqbb(from) | sqbb(kto) : 0) | (rto != to ? sqbb(to) | sqbb(rto) : 0);
+        cocc = (occ ^ sqbb(from) ^ sqbb(to)) | sqbb(kto) | sqbb(rto);
+      } else {
+        const int capsq = type == MT_EN_PASSANT ? to - (us == WHITE ? 8 : -8) : to;
+        sm = sqbb(from) | sqbb(to) | sqbb(capsq);
+        cocc = (occ & ~(sqbb(from) | sqbb(capsq))) | sqbb(to);
+      }
+      if (sm == S && cocc == N.byType[0]) { // the pieces put down
+        bool same;
+        if (type == MT_CASTLING)
+          same = (N.byType[KING] & N.byColor[us] & sqbb(kto)) && (N.byType[ROOK] & N.byColor[us] & sqbb(rto));
+        else
+          same = piece_on(N, to) ==
+                 (type == MT_PROMOTION ? make_piece(us, move_promo(m)) : piece_on(B, from));
+        if (same) slot = (uint32_t)(k - k0);
+      }
+    }
     ++k;
   });
+  if (next_slot) next_slot[i] = (uint8_t)slot;
   // feature-transformer rows the incremental evaluation will gather: the parent's
-  // refresh (both perspectives) here, each child's in child_boards_kernel
-  if (rows) atomicAdd(rows, 2ull * popcnt(B.byType[0]));
+  // refresh (both perspectives) here -- or, for a linked next board of the same chain,
+  // one carry row per perspective instead of that board's refresh -- each child's in
+  // child_boards_kernel
+  if (rows) {
+    unsigned long long r = 2ull * popcnt(occ);
+    if (slot != 255 && chain_k > 1 && (i + 1) % (size_t)chain_k != 0) r -= 2ull * popcnt(N.byType[0]) - 2;
+    atomicAdd(rows, r); // modulo 2^64: the sum over all threads is the count
+  }
 }
 
-__global__ void child_boards_kernel(const gn_board *__restrict__ boards, size_t n,
-                                    const uint64_t *__restrict__ offsets, size_t c0, size_t nc,
+__global__ void child_boards_kernel(const gn_board *__restrict__ boards, size_t c0, size_t nc,
                                     const uint16_t *__restrict__ moves, const uint32_t *__restrict__ owner,
                                     gn_board *__restrict__ children, ChildDelta *__restrict__ deltas,
-                                    uint8_t *__restrict__ next_slot, int chain_k, unsigned long long *__restrict__ rows,
-                                    const Board *__restrict__ unpacked) {
+                                    unsigned long long *__restrict__ rows, const Board *__restrict__ unpacked) {
   const size_t c = c0 + (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   unsigned long long nr = 0;
   if (c < c0 + nc) {
@@ -1065,26 +1116,10 @@ __global__ void child_boards_kernel(const gn_board *__restrict__ boards, size_t 
     else unpack(boards[i], B);     // valid: an invalid parent has no children
     Dirty d;
     const Board C = do_move(B, moves[c], &d);
-    // the packed child: stored when the caller keeps the boards (children != NULL), and
-    // compared with the next board when its occupancy matches (the chained walk's link)
-    const bool link = next_slot && (size_t)i + 1 < n && C.byType[0] == boards[i + 1].occ;
-    gn_board pb;
-    if (children || link) pack(C, pb);
-    if (children) children[c] = pb;
+    if (children) pack(C, children[c]); // stored when the caller keeps the boards
     if (deltas) deltas[c] = make_child_delta(B, C, d);
     // per child either the delta rows or a refresh of the perspective whose king moved
     nr = d.king_moved ? popcnt(C.byType[0]) + d.n_rem + d.n_add : 2 * (d.n_rem + d.n_add);
-    // next_slot[i]: the child whose placement is boards[i + 1]'s (a game's next position;
-    // no two legal moves give one placement); the chained walk then starts parent i + 1
-    // from that child's accumulators, gathering one carry row per perspective instead of
-    // its refresh
-    if (link) {
-      const gn_board nb = boards[i + 1];
-      if (same_placement(pb, nb)) {
-        next_slot[i] = (uint8_t)(c - offsets[i]);
-        if (chain_k > 1 && ((size_t)i + 1) % (size_t)chain_k != 0) nr -= 2ull * popcnt(nb.occ) - 2;
-      }
-    }
   }
   if (rows) { // one atomic per workgroup
     __shared__ unsigned long long part[4];
@@ -1280,10 +1315,10 @@ hipError_t launch_write_children(const gn_board *boards, size_t n, const Tables 
   if (!n) return hipSuccess;
   if (!moves || !owner) return hipErrorInvalidValue;
   hipLaunchKernelGGL(child_moves_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, boards, n, tables, offsets, moves,
-                     owner, next_slot, rows, unpacked);
+                     owner, next_slot, chain_k, rows, unpacked);
   if (nc)
-    hipLaunchKernelGGL(child_boards_kernel, dim3(blocks_for(nc, 256)), dim3(256), 0, s, boards, n, offsets, c0, nc,
-                       moves, owner, children, deltas, next_slot, chain_k, rows, unpacked);
+    hipLaunchKernelGGL(child_boards_kernel, dim3(blocks_for(nc, 256)), dim3(256), 0, s, boards, c0, nc, moves, owner,
+                       children, deltas, rows, unpacked);
   return hipGetLastError();
 }
 

@@ -304,3 +304,40 @@ def test_king_walk_games_vs_oracle(gpu_ctx, oracle_nets, oracle_lib):
             if g == 0:
                 most = max(most, len(cm))
     assert most > 4  # (a parent with more than four king-move jobs)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("chain", [-81, -2])
+def test_chained_links_of_special_moves_vs_oracle(gpu_ctx, oracle_nets, oracle_lib, chain):
+    """The chained walk's link -- the child of position i whose placement is position i + 1's,
+    found in child_moves_kernel from the squares the two placements differ on -- across every
+    move kind: under-promotions with and without capture (four children change the same
+    squares), en passant, castling in both notations, and Chess960 castling where the king
+    stays, where the rook stays and where king and rook swap squares.  Exact chain lengths
+    (GN_OPT_CHAIN < 0): one chain over whole games, and pairs; every position and child vs
+    the oracle (a wrong link starts the next position from the wrong accumulators)."""
+    from fishnet_amd import gpu_nnue as G
+    big, small = oracle_nets
+    games = [(START, "e2e4 a7a6 e4e5 d7d5 e5d6 c7d6 g2g4 h7h5 g4h5 g7g5 h5g6 a6a5 g6g7 a5a4 g7h8n"),
+             (START, "b2b4 a7a5 b4a5 b7b5 a5b6 c7c5 b6b7 c5c4 b7a8r c4c3 a8b8 d8a5 b8c8 a5d8"),
+             ("8/P6k/8/8/8/8/p6K/8 w - - 0 1", "a7a8b a2a1n a8b7 a1b3"),
+             (C960_CASTLE, "e1g1 e8b8"), (C960_CASTLE, "e1b1 e8g8"),
+             ("6kr/8/8/8/8/8/8/6KR w Hh - 0 1", "g1h1 g8h8"),       # the king stays
+             ("k7/8/8/8/8/8/8/4KR2 w F - 0 1", "e1f1 a8b8"),        # the rook stays
+             ("k7/8/8/8/8/8/8/5KR1 w G - 0 1", "f1g1 a8a7"),        # king and rook swap
+             ("r3k2r/8/8/8/8/8/8/R3K2R w KQkq - 0 1", "e1c1 e8g8"),
+             ("r3k2r/8/8/8/8/8/8/R3K2R w KQkq - 0 1", "e1a1 e8h8")]
+    gpu_ctx.set_option(G.OPT_CHAIN, chain)
+    try:
+        out = gpu_ctx.evaluate_games([(r, m, []) for r, m in games], 0, children=True)
+    finally:
+        gpu_ctx.set_option(G.OPT_CHAIN, 81)
+    for (root, moves), o in zip(games, out):
+        assert o["status"] == 0, (root, moves)
+        fens, _ = oracle_lib.replay_game(root, moves)
+        for i, fen in enumerate(fens):
+            cm, ce = o["children"][i]
+            p_exp, m_exp, k_exp = oracle_lib.expand_eval(big, small, fen, 0)
+            assert tuple(o["evals"][i]) == tuple(p_exp), fen
+            assert dict(zip(cm.tolist(), map(tuple, ce.tolist()))) == \
+                dict(zip(m_exp, map(tuple, G.children_from_evals(k_exp).tolist()))), fen
