@@ -127,7 +127,7 @@ def host_threads():
     return max(1, min(aff, int(omp))) if omp.isdigit() and int(omp) > 0 else aff
 
 
-def roofline(alg_bytes, kern_ms, kernel, pmc):
+def roofline(alg_bytes, kern_ms, kernel, pmc, launches=1):
     """Hierarchical memory ceiling of the FT row gather: every gathered row byte passes
     the L2 (34.5 TB/s), the bytes past L2 (PMC traffic) come from the Infinity Cache /
     HBM (8.6 TB/s for gathered rows); the kernel cannot beat the slower of the two.
@@ -137,9 +137,11 @@ def roofline(alg_bytes, kern_ms, kernel, pmc):
     t_l2 = alg_bytes / (L2_PEAK_GBS * 1e9)
     r = {"bound": "hbm", "kernel": kernel, "achieved": round(achieved, 1), "unit": "GB/s",
          "traffic": None, "alg_bytes_per_launch": int(alg_bytes), "kernel_ms_per_launch": round(kern_ms, 4),
+         "launches_per_step": launches,
          "peak_model": "alg_bytes / max(alg_bytes / 34.5 TB/s (L2), traffic / 7.9 TB/s (gathered rows past L2, "
-                       "151 MB table row of MI355X_MICROARCH.md)); "
-                       "achieved = kernel-counted FT rows x (2*L1 + 4) B (row + its 4-B list entry) / kernel time"}
+                       "151 MB table row of MI355X_MICROARCH.md)); achieved = kernel-counted FT rows x "
+                       "(2*L1/S + 4) B (the launch's S-th of the row + its 4-B list entry; S = launches_per_step "
+                       "column slices) / the launch's time"}
     if pmc:
         traffic = float(pmc["hbm_side_bytes_per_launch"])
         t_ic = traffic / (IC_GATHER_GBS * 1e9)
@@ -278,11 +280,15 @@ def run_expand(c: Ctx, wl: dict, games: int, steps: int, warmup: int, check: int
     sums = (nn.checksum_device(out["po"], n * G.EVAL_SIZE), nn.checksum_device(out["co"], children * G.EVAL_SIZE),
             nn.checksum_device(out["mv"], children * 2), nn.checksum_device(out["off"], (n + 1) * 4))
     planned = stream_ms > 0
+    # the column-sliced stream (GN_OPT_STREAM_SLICES 3): three launches per step, each over a
+    # third of every row's columns; the roofline is per launch (= rocprofv3's per-dispatch view)
+    sl = 3 if planned and wl["l1"] == 3072 and nn.get_option(G.OPT_STREAM_SLICES) == 3 else 1
     r = dict(value=c.world * (n + children) * steps / wall, wall=wall, stage=stage,
-             kern_ms=stream_ms if planned else stage[5 if mode != 2 else 4], plan_ms=plan_ms,
-             alg=rows * (2 * wl["l1"] + 4), rows=rows, parents=parents, n=n,
+             kern_ms=(stream_ms / sl) if planned else stage[5 if mode != 2 else 4], plan_ms=plan_ms,
+             alg=rows * (2 * wl["l1"] // sl + 4), rows=rows, parents=parents, n=n, launches=sl,
              children=children, gen_s=gen_s, checksum=sums[0] ^ sums[1], scratch_pads=scratch_pads,
-             kernel=f"stream_eval_kernel<{wl['l1']}>" if wl["l1"] != 128 else f"expand_eval<{wl['l1']}>")
+             kernel=(f"stream_eval_kernel<{wl['l1']}, 3> (3 column-slice launches per step)" if sl == 3 else
+                     f"stream_eval_kernel<{wl['l1']}>") if wl["l1"] != 128 else f"expand_eval<{wl['l1']}>")
     if check:
         ver = {}
         # (1) sampled parents of the timed outputs, with all their children, against the oracle
@@ -686,12 +692,15 @@ def cpu_baseline_expand(c: Ctx, parents, mode, budget_s):
                       f"{th} threads = this GPU's share of the host ({os.cpu_count()} logical CPUs), {info['model']}"}
 
 
-def load_pmc(workload, n):
+def load_pmc(workload, n, launches=1):
+    """The last profile round's PMC figures of this workload's dominant kernel, when they were
+    taken on the same shape (positions, ABI, launches per step: 3 for the column-sliced stream)."""
     p = os.path.join(ROOT, "profiles", "latest_pmc.json")
     if not os.path.exists(p):
         return None
     e = json.load(open(p)).get(workload)
-    return e if e and e.get("positions") == n and e.get("abi", 1) >= 3 else None
+    ok = e and e.get("positions") == n and e.get("abi", 1) >= 3 and e.get("launches_per_step", 1) == launches
+    return e if ok else None
 
 
 def _free_port() -> int:
@@ -803,7 +812,8 @@ def main():
         data = f"synthetic: seeded random-playout positions generated on the GPU; nets {c.net_label}"
     cfg.update({"mode": ["full", "big", "small"][mode], "parallelism": f"dp{c.world} (sharded, no collective)",
                 "options": c.options})
-    roof = roofline(r["alg"], r["kern_ms"], r["kernel"], load_pmc(args.workload, n))
+    roof = roofline(r["alg"], r["kern_ms"], r["kernel"], load_pmc(args.workload, n, r.get("launches", 1)),
+                    r.get("launches", 1))
     roof["stage_ms"] = {k: round(v, 4) for k, v in zip(stage_names, r["stage"])}
     if r.get("plan_ms"):
         roof["plan_kernel_ms"] = round(r["plan_ms"], 4)

@@ -211,6 +211,7 @@ struct Dev {
   DevBuf<uint8_t> p_nsm, p_nbg;  // parent-side net selection during expansion
   DevBuf<unsigned long long> sum;
   DevBuf<uint8_t> nslot; // chained walk: child of parent i that is parent i + 1 (255: none)
+  DevBuf<int32_t> part;  // column-sliced stream: fc_0 partial sums of slices 0, 1 (2 x positions x 16)
   int chain_k = 1;          // block length of the current expansion (1: no chaining)
   // planned expansion (stream.hip): per-parent entry bounds and their scan, the entry
   // lists, tile descriptors, the scratch-slot pool and the error word
@@ -332,6 +333,7 @@ struct gn_ctx {
   int king_sort = 1;        // GN_OPT_KING_SORT (1: batches of >= KING_SORT_MIN positions, 2: all)
   int chain = 81;           // GN_OPT_CHAIN (blocks of consecutive parents per workgroup)
   bool king_cache = true;   // GN_OPT_KING_CACHE
+  int stream_slices = 3;    // GN_OPT_STREAM_SLICES (3 or 1)
   int64_t chunk_parents = 0; // GN_OPT_CHUNK_PARENTS (0: automatic)
   int l1[2] = {0, 0};
   uint32_t hash[2] = {0, 0};
@@ -776,8 +778,10 @@ static int expand_evaluate(gn_ctx *ctx, Dev &d, const gn_board *parents, size_t 
       HIP_TRY(d.ent.ensure(d.etot + 16 * (nblk + 1)));
       HIP_TRY(d.tiles.ensure((n + total) / 16 + (K + 2) * nblk + 2));
       HIP_TRY(d.btiles.ensure(nblk + 1));
-      HIP_TRY(d.pool.ensure(72)); // 8 XCDs x 8 words of scratch-slot bits, then 8 block claim counters
-      HIP_TRY(hipMemsetAsync(d.pool.p, 0, 72 * sizeof(uint32_t), s));
+      HIP_TRY(d.pool.ensure(88)); // 8 XCDs x 8 words of scratch-slot bits, then 8 block claim counters
+      HIP_TRY(hipMemsetAsync(d.pool.p, 0, 88 * sizeof(uint32_t), s)); // per stream launch (<= 3)
+      const int slices = d.net[BIG].L1 == 3072 && ctx->stream_slices == 3 ? 3 : 1;
+      if (slices > 1) HIP_TRY(d.part.ensure(2 * 16 * (n + total)));
       // XCD-local block order
       const uint32_t *order = nullptr;
       if (ctx->king_sort && nblk > 1) {
@@ -793,7 +797,8 @@ static int expand_evaluate(gn_ctx *ctx, Dev &d, const gn_board *parents, size_t 
                                  d.p_obg.p, d.obg.p, (ctx->swizzle >> 2) & 1 ? 1 : (ctx->swizzle >> 3) & 1 ? 2 : 0,
                                  d.chain_k > 1 ? d.nslot.p : nullptr, d.chain_k,
                                  ctx->king_cache ? 1 : 0, d.eoff.p, d.ent.p, d.tiles.p, d.btiles.p, d.pool.p, d.perr.p,
-                                 rows_out, d.pstat.p, 0, nblk, order, ev ? ev[4] : nullptr, s));
+                                 rows_out, d.pstat.p, 0, nblk, order, ev ? ev[4] : nullptr, s, slices,
+                                 slices > 1 ? d.part.p : nullptr, n + total));
     } else { // a 128-wide net loaded as the big net
       HIP_TRY(launch_expand_net(d.net[BIG], parents, n, off, children, dl, f ? d.p_nbg.p : nullptr,
                                 f ? d.nbg.p : nullptr, d.p_obg.p, d.obg.p, ctx->swizzle & 1, s));
@@ -2281,6 +2286,10 @@ int gn_set_option(gn_ctx *ctx, int option, int64_t value) {
     if (value < -(1 << 20) || value > (1 << 20)) return fail(GN_E_INVALID, "chain length out of range");
     ctx->chain = (int)value;
     return GN_OK;
+  case GN_OPT_STREAM_SLICES:
+    if (value != 1 && value != 3) return fail(GN_E_INVALID, "stream slices must be 1 or 3");
+    ctx->stream_slices = (int)value;
+    return GN_OK;
   case GN_OPT_CHUNK_PARENTS:
     if (value < 0) return fail(GN_E_INVALID, "chunk size < 0");
     ctx->chunk_parents = value;
@@ -2310,6 +2319,9 @@ int gn_get_option(const gn_ctx *ctx, int option, int64_t *value) {
     return GN_OK;
   case GN_OPT_CHAIN:
     *value = ctx->chain;
+    return GN_OK;
+  case GN_OPT_STREAM_SLICES:
+    *value = ctx->stream_slices;
     return GN_OK;
   case GN_OPT_CHUNK_PARENTS:
     *value = ctx->chunk_parents;

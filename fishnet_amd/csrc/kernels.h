@@ -76,19 +76,23 @@ static_assert(sizeof(TileDesc) == 192, "TileDesc is 192 bytes");
 // of them), entries at ent + eoff[pbeg] + 16 * block (list 0 upward, list 1 downward from
 // the region's end, eoff = exclusive scan of write_children's per-parent entry bounds).
 // One call plans and evaluates blocks [b0, b1) of the n parents (every index absolute, so
-// block ranges can run as a pipeline on different streams).  pool: 65 words (scratch-slot
-// bits, then the stream's block claim counter), zeroed by the caller before each call; err: bit 0 entry overflow, bit 1 no scratch slot, bit 2 a
+// block ranges can run as a pipeline on different streams).  pool: 88 words (scratch-slot
+// bits, then 8 block claim counters per stream launch), zeroed by the caller before each call; err: bit 0 entry overflow, bit 1 no scratch slot, bit 2 a
 // king-cache load closer than GN_SCR_GAP entries to its list's last store to scratch.
 // rows_out: += FT rows the stream gathers (bias, carry and king-cache rows included);
 // pads_out (optional): += no-op entries the plan inserted to keep GN_SCR_GAP.
 // order: block order of the stream (block_order) or NULL; mid: recorded between the kernels.
+// slices == 3 (L1 3072; part non-null): the stream runs as three launches over 1,024 columns
+// each (stream_eval_kernel<3072, 3>), part = 2 x npos x 16 int32 fc_0 partial sums, npos =
+// n + the children; otherwise one launch over whole rows.
 hipError_t launch_plan_stream(const NetDevice &net, const gn_board *parents, size_t n, const uint64_t *offsets,
                               const ChildDelta *deltas, const uint8_t *need_parent, const uint8_t *need_child,
                               int2 *out_parent, int2 *out_child, int swz, const uint8_t *next_slot, int chain_k,
                               int kc, const uint64_t *eoff, uint64_t *ent, TileDesc *tiles, uint32_t *btiles,
                               uint32_t *pool, uint32_t *err, unsigned long long *rows_out,
                               unsigned long long *pads_out, size_t b0, size_t b1, const uint32_t *order,
-                              hipEvent_t mid, hipStream_t s);
+                              hipEvent_t mid, hipStream_t s, int slices = 1, int32_t *part = nullptr,
+                              size_t npos = 0);
 // GN_MODE_FULL preparation: need_small = valid && |simple_eval| > threshold,
 // need_big = valid && !need_small.
 hipError_t launch_classify(const gn_board *boards, size_t n, const gn_eval_params &P, uint8_t *need_small,

@@ -52,6 +52,9 @@
 #ifndef GN_PLAN_WPE
 #define GN_PLAN_WPE 4 // <= 128 VGPRs, no spills (round 3: 3 waves at 168 VGPRs beat 4 with spills; round 4 fits 4)
 #endif
+#ifndef GN_SLICE_WPE // the column-sliced stream (2-wave workgroups): 3 waves per SIMD (125 VGPRs)
+#define GN_SLICE_WPE 3 // measured 157.1 ms per expansion; 4 (109 VGPRs, 8 workgroups per CU): 160.4 ms
+#endif
 #ifndef GN_EXPAND_WPE
 #define GN_EXPAND_WPE (GN_RING == 4 ? 5 : 4)
 #endif
@@ -715,20 +718,31 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
 }
 
 // ----------------------------------------------------------------- stream --
-template <int L1>
-__global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_EXPAND_WPE)))
+// SL > 1: the accumulator columns split over SL launches (slice = 0 .. SL - 1), each walking
+// every entry of the plan over its own L1 / SL columns (pairs j, j + L1 / 2 of the transform
+// together), so that an XCD's L2 holds the slice's rows of the king buckets in flight (the
+// whole 3072-wide rows of one bucket pair, 8.6 MB, exceed its 4 MB).  A slice's fc_0 sums are
+// partial: slices 0 .. SL - 2 store them (part[slice][position][16], position = the output
+// index: parent P, or np + child), the last slice adds them to its own (wrapping int32 adds,
+// as the LDS atomics: the sum is the whole-row kernel's exactly) and finishes the layer stack.
+template <int L1, int SL = 1>
+__global__ void __launch_bounds__(L1 / SL / 8) __attribute__((amdgpu_waves_per_eu(SL > 1 ? GN_SLICE_WPE : GN_EXPAND_WPE)))
     stream_eval_kernel(NetDevice net, const uint64_t *__restrict__ offsets, uint32_t np, uint32_t K, uint32_t b0,
                        uint32_t b1, int swz,
                        const uint64_t *__restrict__ eoff, const uint64_t *__restrict__ ent,
                        const TileDesc *__restrict__ tiles, const uint32_t *__restrict__ btiles,
                        const uint32_t *__restrict__ order, int2 *__restrict__ out_parent, int2 *__restrict__ out_child,
                        uint32_t *__restrict__ pool, int use_scr, uint32_t *__restrict__ err,
-                       uint32_t *__restrict__ claim) {
+                       uint32_t *__restrict__ claim, int slice, int32_t *__restrict__ part, uint64_t npos) {
   using namespace ps;
-  constexpr int G = L1 / 16; // threads per perspective group (whole waves)
-  constexpr int NT = 2 * G, NW = NT / 64, TILE = 16, XS = L1 + 16, KS = L1 / 64, KPW = KS / NW;
+  constexpr int LC = L1 / SL; // this launch's columns
+  constexpr int G = LC / 16;  // threads per perspective group (whole waves)
+  constexpr int NT = 2 * G, NW = NT / 64, TILE = 16, XS = LC + 16, KS = LC / 64, KPW = KS / NW;
+  constexpr int KSF = L1 / 64; // fc_0 k-steps of the whole net
   constexpr uint32_t RS = ft_row_stride(L1);
-  static_assert(G % 64 == 0 && KS % NW == 0 && KPW % 2 == 0, "geometry");
+  static_assert(G % 64 == 0 && KS % NW == 0 && KPW % 2 == 0 && L1 % SL == 0, "geometry");
+  // the slice's first column pair in bytes (its low columns; the high ones L1 bytes further)
+  const uint32_t cofs = SL > 1 ? (uint32_t)slice * (uint32_t)LC : 0u;
   __shared__ __attribute__((aligned(16))) uint8_t xt[TILE * XS];
   // fc_0 partial sums [position][output], rows padded to 20 dwords: the 4 lane groups of an
   // atomic (kg) then fall on different banks (a 16-dword row put all 4 on the same bank)
@@ -860,7 +874,7 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
   int tl0 = tid;
   asm volatile("" : "+v"(tl0));
   const int jt = tl0 % G;
-  const uint32_t j16 = 16 * jt;
+  const uint32_t j16 = 16 * jt + cofs;
   typedef int sq4 __attribute__((ext_vector_type(4)));
   const uint64_t ftp = (uint64_t)(uintptr_t)net.ft;
   const sq4 rsq = {__builtin_amdgcn_readfirstlane((int)(uint32_t)ftp),
@@ -918,7 +932,7 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
     }
     if (h & H_LAST) {
       const int sl = (h >> H_SLOT_SH) & 15, side = (h >> H_SIDE_SH) & 1;
-      *reinterpret_cast<uint2 *>(xt + sl * XS + side * (L1 / 2) + 8 * jt) = transform8(lo, hi);
+      *reinterpret_cast<uint2 *>(xt + sl * XS + side * (LC / 2) + 8 * jt) = transform8(lo, hi);
       if (h & H_PAR_E) {
         asm volatile("");
         pacc_lo = lo, pacc_hi = hi;
@@ -1016,7 +1030,10 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
       {
         const uint8_t *xa = xt + row * XS + kg * 16 + 64 * KPW * wave;
         // (w0f: the k-step's 64 lanes x 16 B are one contiguous 1 KiB)
-        const int8_t *wb = net.w0f + (((size_t)b * KS + KPW * wave) * 64 + ln) * 16;
+        // (SL > 1: wave w of perspective h covers the net's k-steps of its slice of that side)
+        constexpr int WH = NW / 2;
+        const int wsl = SL > 1 ? (wave / WH) * WH * SL + slice * WH + wave % WH : wave;
+        const int8_t *wb = net.w0f + (((size_t)b * KSF + KPW * wsl) * 64 + ln) * 16;
         int4v acc = {0, 0, 0, 0};
         // (batches of FB k-steps: the next tile's rows stay in flight in registers meanwhile)
         // (`stop`, always 0, is opaque to the compiler: without a runtime exit test it schedules the
@@ -1039,7 +1056,30 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
         for (int i = 0; i < 4; ++i) atomicAdd(&acc0[buf][(4 * kg + i) * AS + row], acc[i]);
       }
       __syncthreads();
-      if (wave == (int)(bq % NW)) { // fc_0 activations, fc_1, fc_2, outputs of bucket b
+      // a position's output index (parent P, or np + its child index) and whether it is evaluated
+      // in bucket b
+      auto present = [&](int pos) -> bool {
+        const uint32_t m = (mw[pos >> 2] >> (8 * (pos & 3))) & 0xFF;
+        return (m & 1) && (int)((m >> 1) & 7) == b;
+      };
+      auto out_index = [&](int pos, int adjv) -> uint64_t {
+        const uint32_t P = p_first + (uint32_t)__builtin_popcount(pm & ((2u << pos) - 1)) - (pm & 1);
+        return ((pm >> pos) & 1) ? (uint64_t)P : (uint64_t)np + (u0 + pos - P - 1 + adjv);
+      };
+      bool partial_only = false;
+      if constexpr (SL > 1) partial_only = slice < SL - 1;
+      if (partial_only) {
+        if (wave == (int)(bq % NW)) { // this slice's fc_0 sums of bucket b to its partial array
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int pos = 4 * kg + i;
+            if (present(pos))
+              part[((uint64_t)slice * npos + out_index(pos, D->adj[pos])) * 16 + row] = acc0[buf][pos * AS + row];
+          }
+#pragma unroll
+          for (int i = 0; i < 4; ++i) acc0[buf][(4 * kg + i) * AS + row] = 0; // free for bucket bq + 2
+        }
+      } else if (wave == (int)(bq % NW)) { // fc_0 activations, fc_1, fc_2, outputs of bucket b
         // the finishing step's scalar weights and the tile's PSQT first (one wait for memory)
         const int32_t bias0 = net.b0[b * 16 + row];
         const int32_t b1l = net.b1[b * 32 + row], b1h = net.b1[b * 32 + 16 + row];
@@ -1051,10 +1091,22 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
 #pragma unroll
           for (int i = 0; i < 4; ++i) pq[i] = *reinterpret_cast<const int2 *>(D->psq[4 * kg + i]), adj[i] = D->adj[4 * kg + i];
         }
+        int32_t sp[4] = {0, 0, 0, 0}; // SL > 1: the other slices' fc_0 sums
+        if constexpr (SL > 1) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int pos = 4 * kg + i;
+            if (present(pos)) {
+              const uint64_t q = out_index(pos, D->adj[pos]) * 16 + row;
+#pragma unroll
+              for (int t = 0; t < SL - 1; ++t) sp[i] = wadd(sp[i], part[(uint64_t)t * npos * 16 + q]);
+            }
+          }
+        }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int pos = 4 * kg + i;
-          const int32_t vv = wadd(acc0[buf][pos * AS + row], bias0);
+          const int32_t vv = wadd(wadd(acc0[buf][pos * AS + row], sp[i]), bias0);
           if (row < 15) {
             const long long s2 = ((long long)vv * vv) >> 19;
             in1[buf][pos][row] = (uint8_t)(s2 < 127 ? s2 : 127);
@@ -1077,23 +1129,23 @@ __global__ void __launch_bounds__(L1 / 8) __attribute__((amdgpu_waves_per_eu(GN_
         if (kg < 2) a1 = *reinterpret_cast<const int4v *>(&in1[buf][row][kg * 16]);
         const int4v cl = __builtin_amdgcn_mfma_i32_16x16x64_i8(a1, wl, zero, 0, 0, 0);
         const int4v ch = __builtin_amdgcn_mfma_i32_16x16x64_i8(a1, wh, zero, 0, 0, 0);
-        int32_t part[4];
+        int32_t l2[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int32_t l = clampi(wadd(cl[i], b1l) >> 6, 0, 127), hh = clampi(wadd(ch[i], b1h) >> 6, 0, 127);
-          part[i] = w2l * l + w2h * hh;
+          l2[i] = w2l * l + w2h * hh;
         }
 #pragma unroll
         for (int off = 8; off; off >>= 1)
 #pragma unroll
-          for (int i = 0; i < 4; ++i) part[i] = wadd(part[i], __shfl_xor(part[i], off, 16));
+          for (int i = 0; i < 4; ++i) l2[i] = wadd(l2[i], __shfl_xor(l2[i], off, 16));
         if (row == 0) {
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const int pos = 4 * kg + i;
             const uint32_t m = (mw[pos >> 2] >> (8 * (pos & 3))) & 0xFF;
             if ((m & 1) && (int)((m >> 1) & 7) == b) {
-              const int32_t positional = wadd(wadd(b2v, part[i]), fwd[buf][pos]);
+              const int32_t positional = wadd(wadd(b2v, l2[i]), fwd[buf][pos]);
               const int32_t psqt = (int32_t)((uint32_t)pq[i].x - (uint32_t)pq[i].y) / 2;
               const int2 val = make_int2(psqt / 16, positional / 16);
               const uint32_t P = p_first + (uint32_t)__builtin_popcount(pm & ((2u << pos) - 1)) - (pm & 1);
@@ -1145,7 +1197,7 @@ hipError_t launch_plan_stream(const NetDevice &net, const gn_board *parents, siz
                               int kc, const uint64_t *eoff, uint64_t *ent, TileDesc *tiles, uint32_t *btiles,
                               uint32_t *pool, uint32_t *err, unsigned long long *rows_out,
                               unsigned long long *pads_out, size_t b0, size_t b1, const uint32_t *order,
-                              hipEvent_t mid, hipStream_t s) {
+                              hipEvent_t mid, hipStream_t s, int slices, int32_t *part, size_t npos) {
   if (!n || b1 <= b0) return hipSuccess;
   if (n >= 0x80000000ull) return hipErrorInvalidValue; // 32-bit parent indices in the kernels
   const uint32_t K = chain_k > 1 && next_slot ? (uint32_t)chain_k : 1u;
@@ -1158,15 +1210,23 @@ hipError_t launch_plan_stream(const NetDevice &net, const gn_board *parents, siz
                        need_child, K > 1 ? next_slot : nullptr, (uint32_t)n, K, B0, B1, K > 1 ? kc : 0, eoff, ent,
                        tiles, btiles, rows_out, pads_out, err);
     if (mid) (void)hipEventRecord(mid, s);
-    hipLaunchKernelGGL((stream_eval_kernel<3072>), dim3(g), dim3(384), 0, s, net, offsets, (uint32_t)n, K, B0, B1,
-                       swz, eoff, ent, tiles, btiles, order, out_parent, out_child, pool, scr, err, pool + 64);
+    if (slices == 3 && part) // three launches over 1,024 columns each (claim counters pool[64 + 8 slice ..])
+      for (int sl = 0; sl < 3; ++sl)
+        hipLaunchKernelGGL((stream_eval_kernel<3072, 3>), dim3(g), dim3(128), 0, s, net, offsets, (uint32_t)n, K, B0,
+                           B1, swz, eoff, ent, tiles, btiles, order, out_parent, out_child, pool, scr, err,
+                           pool + 64 + 8 * sl, sl, part, (uint64_t)npos);
+    else
+      hipLaunchKernelGGL((stream_eval_kernel<3072>), dim3(g), dim3(384), 0, s, net, offsets, (uint32_t)n, K, B0, B1,
+                         swz, eoff, ent, tiles, btiles, order, out_parent, out_child, pool, scr, err, pool + 64, 0,
+                         nullptr, (uint64_t)0);
   } else if (net.L1 == 1024) {
     hipLaunchKernelGGL((plan_kernel<1024>), dim3(pg), dim3(256), 0, s, net, parents, offsets, deltas, need_parent,
                        need_child, K > 1 ? next_slot : nullptr, (uint32_t)n, K, B0, B1, K > 1 ? kc : 0, eoff, ent,
                        tiles, btiles, rows_out, pads_out, err);
     if (mid) (void)hipEventRecord(mid, s);
     hipLaunchKernelGGL((stream_eval_kernel<1024>), dim3(g), dim3(128), 0, s, net, offsets, (uint32_t)n, K, B0, B1,
-                       swz, eoff, ent, tiles, btiles, order, out_parent, out_child, pool, scr, err, pool + 64);
+                       swz, eoff, ent, tiles, btiles, order, out_parent, out_child, pool, scr, err, pool + 64, 0,
+                       nullptr, (uint64_t)0);
   } else {
     return hipErrorInvalidValue;
   }

@@ -113,6 +113,12 @@ extern "C" {
                                          Shortened when the blocks would not fill the GPU;
                                          -k: exactly k.  0, 1 or -1: every parent
                                          refreshes.  Results are identical either way.    */
+#define GN_OPT_STREAM_SLICES 8        /* expansion with a 3072-wide big net: 3 (default): the
+                                         accumulator columns in three slices of 1,024, one
+                                         stream launch each over every entry, so that an
+                                         XCD's L2 holds the slice's rows of the king buckets
+                                         in flight; 1: one launch over whole rows.  Results
+                                         are identical either way.                        */
 
 /* read-only statistics (gn_get_option) */
 #define GN_STAT_PLAN_NS 101           /* the last gn_time_expand_device's planned big net

@@ -35,6 +35,7 @@ pub const GN_OPT_CHAIN: c_int = 4;
 pub const GN_OPT_KING_CACHE: c_int = 5;
 pub const GN_OPT_CHUNK_PARENTS: c_int = 6;
 pub const GN_OPT_COALESCE: c_int = 7;
+pub const GN_OPT_STREAM_SLICES: c_int = 8;
 // read-only statistics (gn_get_option)
 pub const GN_STAT_PLAN_NS: c_int = 101;
 pub const GN_STAT_STREAM_NS: c_int = 102;

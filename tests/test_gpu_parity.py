@@ -834,3 +834,55 @@ def test_eval_params_keep_child_cp_in_24_bits(gpu_ctx):
     assert e.value.code == G.E_INVALID
     gpu_ctx.set_eval_params(p)
     assert gpu_ctx.eval_params().wdl_a[3] == p.wdl_a[3]
+
+
+@pytest.mark.gpu
+def test_stream_column_slices_equal_whole_rows(gpu_ctx, oracle_nets, oracle_lib):
+    """GN_OPT_STREAM_SLICES: the big net's stream as three launches over 1,024 accumulator
+    columns each (fc_0 partial sums of slices 0 and 1 added by the last one) gives every output
+    of the one-launch whole-row stream, with the chained walk and king cache on and off;
+    sampled parents with all their children against the oracle."""
+    from fishnet_amd import gpu_nnue as G
+    games, plies = 1200, 80
+    n = games * (plies + 1)
+    d_b = gpu_ctx.alloc(n * 32)
+    gpu_ctx.random_games_device(0x5EED0000 + 1200, 0, games, plies, d_b)
+    gpu_ctx.synchronize()
+    _, total, _, _ = gpu_ctx.time_expand_device(d_b, n, 1, 1)
+    out = {"po": gpu_ctx.alloc(n * G.EVAL_SIZE), "off": gpu_ctx.alloc((n + 1) * 4), "mv": gpu_ctx.alloc(total * 2),
+           "co": gpu_ctx.alloc(total * G.EVAL_SIZE), "cap": total}
+
+    def run(slices, k, kc):
+        gpu_ctx.set_option(G.OPT_STREAM_SLICES, slices)
+        gpu_ctx.set_option(G.OPT_CHAIN, k)
+        gpu_ctx.set_option(G.OPT_KING_CACHE, kc)
+        _, t, _, _ = gpu_ctx.time_expand_device(d_b, n, 1, 1, outputs=out)
+        assert t == total
+        return tuple(gpu_ctx.checksum_device(out[b], nb) for b, nb in
+                     (("po", n * G.EVAL_SIZE), ("co", t * G.EVAL_SIZE)))
+
+    assert gpu_ctx.get_option(G.OPT_STREAM_SLICES) == 3
+    try:
+        for k, kc in ((81, 1), (1, 0)):
+            whole = run(1, k, kc)
+            assert run(3, k, kc) == whole, (k, kc)
+        with pytest.raises(G.GnError):
+            gpu_ctx.set_option(G.OPT_STREAM_SLICES, 2)
+    finally:
+        gpu_ctx.set_option(G.OPT_STREAM_SLICES, 3)
+        gpu_ctx.set_option(G.OPT_CHAIN, 81)
+        gpu_ctx.set_option(G.OPT_KING_CACHE, 1)
+    run(3, 81, 1)
+    big, small = oracle_nets
+    boards = d_b.download(G.BOARD_DTYPE, n)
+    offs = out["off"].download(np.uint32, n + 1)
+    pev = out["po"].download(G.EVAL_DTYPE, n)
+    rng = np.random.default_rng(3)
+    for i in rng.choice(n, 48, replace=False):
+        fen = G.board_to_fen(boards[i])
+        lo, hi = int(offs[i]), int(offs[i + 1])
+        mv = out["mv"].download(np.uint16, hi - lo, offset=lo)
+        ev = out["co"].download(G.EVAL_DTYPE, hi - lo, offset=lo)
+        p_exp, m_exp, k_exp = oracle_lib.expand_eval(big, small, fen, 1, incremental=True)
+        assert tuple(pev[i]) == p_exp, fen
+        assert dict(zip(mv.tolist(), map(tuple, ev.tolist()))) == dict(zip(m_exp, map(tuple, k_exp.tolist()))), fen

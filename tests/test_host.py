@@ -260,8 +260,9 @@ def test_rust_patches_apply_to_reference(tmp_path):
 
 
 def test_stream_kernel_does_not_spill(tmp_path):
-    """The expansion's dominant kernel (stream_eval_kernel<3072>) keeps its 96 VGPRs (5 waves per
-    SIMD, three 6-wave workgroups per CU) without spilling: a spill of its ring registers cost 3 %
+    """The expansion's dominant kernel keeps its registers without spilling: the whole-row
+    stream_eval_kernel<3072> 96 VGPRs (5 waves per SIMD, three 6-wave workgroups per CU), the
+    column-sliced stream_eval_kernel<3072, 3> at most 128; a spill of the ring registers cost 3 %
     of the stream once (round 4), invisible to every correctness test."""
     import re
     import shutil
@@ -272,8 +273,9 @@ def test_stream_kernel_does_not_spill(tmp_path):
     p = subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "--cuda-device-only", "-c", src, "-o",
                         str(tmp_path / "s.o"), "-Rpass-analysis=kernel-resource-usage"], capture_output=True, text=True,
                        check=True)
-    block = p.stderr.split("stream_eval_kernelILi3072", 1)[1]
-    vgprs = int(re.search(r"VGPRs: (\d+)", block).group(1))
-    spill = int(re.search(r"VGPRs Spill: (\d+)", block).group(1))
-    scratch = int(re.search(r"ScratchSize \[bytes/lane\]: (\d+)", block).group(1))
-    assert vgprs <= 96 and spill == 0 and scratch == 0, (vgprs, spill, scratch)
+    for name, most in (("stream_eval_kernelILi3072ELi1E", 96), ("stream_eval_kernelILi3072ELi3E", 128)):
+        block = p.stderr.split(name, 1)[1]
+        vgprs = int(re.search(r"VGPRs: (\d+)", block).group(1))
+        spill = int(re.search(r"VGPRs Spill: (\d+)", block).group(1))
+        scratch = int(re.search(r"ScratchSize \[bytes/lane\]: (\d+)", block).group(1))
+        assert vgprs <= most and spill == 0 and scratch == 0, (name, vgprs, spill, scratch)

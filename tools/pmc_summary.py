@@ -36,13 +36,16 @@ def find(pattern):
     return hits[-1] if hits else None
 
 
-def counters(path, kname):
-    """{counter: [value per dispatch]} of the dispatches whose name contains kname."""
+def counters(path, kname, names=None):
+    """{counter: [value per dispatch]} of the dispatches whose name contains kname (their
+    names added to `names`)."""
     per = defaultdict(lambda: defaultdict(float))
     with open(path) as f:
         for r in csv.DictReader(f):
             if kname in r["Kernel_Name"]:
                 per[r["Counter_Name"]][r["Dispatch_Id"]] += float(r["Counter_Value"])
+                if names is not None:
+                    names.add(r["Kernel_Name"])
     return {k: list(v.values()) for k, v in per.items()}
 
 
@@ -57,11 +60,11 @@ def main(tag):
     latest_p = os.path.join(ROOT, "profiles", "latest_pmc.json")
     latest = json.load(open(latest_p)) if os.path.exists(latest_p) else {}
     for wl, kname in DOMINANT.items():
-        vals = {}
+        vals, names = {}, set()
         for grp in ("fetch", "write", "mfma", "l2"):
             p = find(os.path.join(src, f"pmc_{grp}_{wl}", "**", "*counter_collection.csv"))
             if p:
-                vals.update(counters(p, kname))
+                vals.update(counters(p, kname, names))
                 shutil.copy(p, os.path.join(dst, f"pmc_{grp}_{wl}.csv"))
         if "FETCH_SIZE" not in vals:
             continue
@@ -70,7 +73,10 @@ def main(tag):
         bl = json.load(open(bench_p)) if os.path.exists(bench_p) else None
         fetch = avg["FETCH_SIZE"] * 1024 * 2
         write = avg.get("WRITE_SIZE", 0.0) * 1024
-        s = {"kernel": kname, "launches": len(vals["FETCH_SIZE"]), "abi": 4,
+        # the column-sliced stream (stream_eval_kernel<3072, 3>): three launches per step, the
+        # counters per launch as the bench's roofline (per dispatch)
+        sl = 3 if any("3072, 3>" in x for x in names) else 1
+        s = {"kernel": kname, "launches": len(vals["FETCH_SIZE"]), "launches_per_step": sl, "abi": 4,
              "FETCH_SIZE_kB": avg["FETCH_SIZE"], "WRITE_SIZE_kB": avg.get("WRITE_SIZE"),
              "hbm_side_bytes_per_launch": fetch + write,
              "correction": "bytes = FETCH_SIZE kB x 1024 x 2 (gfx950 wide reads) + WRITE_SIZE kB x 1024; "
