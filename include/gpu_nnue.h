@@ -125,7 +125,8 @@ extern "C" {
                                          (max over devices, per iteration, nanoseconds):
                                          plan_kernel (lists, tiles, PSQT) ...            */
 #define GN_STAT_STREAM_NS 102         /* ... and stream_eval_kernel (row stream + layer
-                                         stack), the expansion's dominant kernel         */
+                                         stack; all its launches: three column slices by
+                                         default), the expansion's dominant kernel       */
 #define GN_STAT_SCRATCH_PADS 103      /* no-op entries the last planned expansion inserted
                                          (per device, summed) so that every king-cache load
                                          sits >= ring depth (4) list entries after the
