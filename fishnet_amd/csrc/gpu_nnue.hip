@@ -211,7 +211,8 @@ struct Dev {
   DevBuf<uint8_t> p_nsm, p_nbg;  // parent-side net selection during expansion
   DevBuf<unsigned long long> sum;
   DevBuf<uint8_t> nslot; // chained walk: child of parent i that is parent i + 1 (255: none)
-  DevBuf<int32_t> part;  // column-sliced stream: fc_0 partial sums of slices 0, 1 (2 x positions x 16)
+  DevBuf<int32_t> part;  // column-sliced stream: fc_0 partial sums of the 3 slices (3 x positions x 16)
+  DevBuf<int2> pinfo;    // ... and each position's (PSQT value, bucket) for the finish
   int chain_k = 1;          // block length of the current expansion (1: no chaining)
   // planned expansion (stream.hip): per-parent entry bounds and their scan, the entry
   // lists, tile descriptors, the scratch-slot pool and the error word
@@ -781,7 +782,10 @@ static int expand_evaluate(gn_ctx *ctx, Dev &d, const gn_board *parents, size_t 
       HIP_TRY(d.pool.ensure(88)); // 8 XCDs x 8 words of scratch-slot bits, then 8 block claim counters
       HIP_TRY(hipMemsetAsync(d.pool.p, 0, 88 * sizeof(uint32_t), s)); // per stream launch (<= 3)
       const int slices = d.net[BIG].L1 == 3072 && ctx->stream_slices == 3 ? 3 : 1;
-      if (slices > 1) HIP_TRY(d.part.ensure(2 * 16 * (n + total)));
+      if (slices > 1) {
+        HIP_TRY(d.part.ensure(3 * 16 * (n + total)));
+        HIP_TRY(d.pinfo.ensure(n + total));
+      }
       // XCD-local block order
       const uint32_t *order = nullptr;
       if (ctx->king_sort && nblk > 1) {
@@ -798,7 +802,7 @@ static int expand_evaluate(gn_ctx *ctx, Dev &d, const gn_board *parents, size_t 
                                  d.chain_k > 1 ? d.nslot.p : nullptr, d.chain_k,
                                  ctx->king_cache ? 1 : 0, d.eoff.p, d.ent.p, d.tiles.p, d.btiles.p, d.pool.p, d.perr.p,
                                  rows_out, d.pstat.p, 0, nblk, order, ev ? ev[4] : nullptr, s, slices,
-                                 slices > 1 ? d.part.p : nullptr, n + total));
+                                 slices > 1 ? d.part.p : nullptr, n + total, slices > 1 ? d.pinfo.p : nullptr));
     } else { // a 128-wide net loaded as the big net
       HIP_TRY(launch_expand_net(d.net[BIG], parents, n, off, children, dl, f ? d.p_nbg.p : nullptr,
                                 f ? d.nbg.p : nullptr, d.p_obg.p, d.obg.p, ctx->swizzle & 1, s));

@@ -52,9 +52,10 @@
 #ifndef GN_PLAN_WPE
 #define GN_PLAN_WPE 4 // <= 128 VGPRs, no spills (round 3: 3 waves at 168 VGPRs beat 4 with spills; round 4 fits 4)
 #endif
-#ifndef GN_SLICE_WPE // the column-sliced stream (2-wave workgroups): 3 waves per SIMD (125 VGPRs)
-#define GN_SLICE_WPE 3 // measured 157.1 ms per expansion; 4 (109 VGPRs, 8 workgroups per CU): 160.4 ms
-#endif
+#ifndef GN_SLICE_WPE // the column-sliced stream (2-wave workgroups): at least 3 waves per SIMD; without the
+#define GN_SLICE_WPE 3 // finish (slice_finish_kernel) it needs 108 VGPRs and gets 4 (with the finish in the
+#endif                 // last slice: 125 + 8 AGPRs, 3 per SIMD 157.1 ms, forced to 4 160.4 ms; now padding
+                       // the LDS tile to hold it at 3 per SIMD (GN_SLICE_XPAD 192) is 2.6 % slower)
 #ifndef GN_EXPAND_WPE
 #define GN_EXPAND_WPE (GN_RING == 4 ? 5 : 4)
 #endif
@@ -722,9 +723,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
 // every entry of the plan over its own L1 / SL columns (pairs j, j + L1 / 2 of the transform
 // together), so that an XCD's L2 holds the slice's rows of the king buckets in flight (the
 // whole 3072-wide rows of one bucket pair, 8.6 MB, exceed its 4 MB).  A slice's fc_0 sums are
-// partial: slices 0 .. SL - 2 store them (part[slice][position][16], position = the output
-// index: parent P, or np + child), the last slice adds them to its own (wrapping int32 adds,
-// as the LDS atomics: the sum is the whole-row kernel's exactly) and finishes the layer stack.
+// partial: every slice stores them (part[slice][position][16], position = the output index:
+// parent P, or np + child) and slice 0 the position's PSQT value and layer-stack bucket
+// (pinfo[position]); slice_finish_kernel adds the SL sums (wrapping int32 adds, as the LDS
+// atomics: the sum is the whole-row kernel's exactly) and runs the rest of the layer stack.
+// (The last slice finishing in its own launch, one of its two waves per bucket, took 59.6 ms
+// against 49 for the others.)
 template <int L1, int SL = 1>
 __global__ void __launch_bounds__(L1 / SL / 8) __attribute__((amdgpu_waves_per_eu(SL > 1 ? GN_SLICE_WPE : GN_EXPAND_WPE)))
     stream_eval_kernel(NetDevice net, const uint64_t *__restrict__ offsets, uint32_t np, uint32_t K, uint32_t b0,
@@ -733,11 +737,16 @@ __global__ void __launch_bounds__(L1 / SL / 8) __attribute__((amdgpu_waves_per_e
                        const TileDesc *__restrict__ tiles, const uint32_t *__restrict__ btiles,
                        const uint32_t *__restrict__ order, int2 *__restrict__ out_parent, int2 *__restrict__ out_child,
                        uint32_t *__restrict__ pool, int use_scr, uint32_t *__restrict__ err,
-                       uint32_t *__restrict__ claim, int slice, int32_t *__restrict__ part, uint64_t npos) {
+                       uint32_t *__restrict__ claim, int slice, int32_t *__restrict__ part, uint64_t npos,
+                       int2 *__restrict__ pinfo) {
   using namespace ps;
   constexpr int LC = L1 / SL; // this launch's columns
   constexpr int G = LC / 16;  // threads per perspective group (whole waves)
-  constexpr int NT = 2 * G, NW = NT / 64, TILE = 16, XS = LC + 16, KS = LC / 64, KPW = KS / NW;
+#ifndef GN_SLICE_XPAD // A/B: LDS bytes added per tile row of the sliced stream (fewer workgroups per CU)
+#define GN_SLICE_XPAD 0
+#endif
+  constexpr int NT = 2 * G, NW = NT / 64, TILE = 16, XS = LC + 16 + (SL > 1 ? GN_SLICE_XPAD : 0), KS = LC / 64,
+                KPW = KS / NW;
   constexpr int KSF = L1 / 64; // fc_0 k-steps of the whole net
   constexpr uint32_t RS = ft_row_stride(L1);
   static_assert(G % 64 == 0 && KS % NW == 0 && KPW % 2 == 0 && L1 % SL == 0, "geometry");
@@ -1066,15 +1075,19 @@ __global__ void __launch_bounds__(L1 / SL / 8) __attribute__((amdgpu_waves_per_e
         const uint32_t P = p_first + (uint32_t)__builtin_popcount(pm & ((2u << pos) - 1)) - (pm & 1);
         return ((pm >> pos) & 1) ? (uint64_t)P : (uint64_t)np + (u0 + pos - P - 1 + adjv);
       };
-      bool partial_only = false;
-      if constexpr (SL > 1) partial_only = slice < SL - 1;
-      if (partial_only) {
+      if constexpr (SL > 1) {
         if (wave == (int)(bq % NW)) { // this slice's fc_0 sums of bucket b to its partial array
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const int pos = 4 * kg + i;
-            if (present(pos))
-              part[((uint64_t)slice * npos + out_index(pos, D->adj[pos])) * 16 + row] = acc0[buf][pos * AS + row];
+            if (present(pos)) {
+              const uint64_t q = out_index(pos, D->adj[pos]);
+              part[((uint64_t)slice * npos + q) * 16 + row] = acc0[buf][pos * AS + row];
+              if (slice == 0 && row == 0) {
+                const int2 pq = *reinterpret_cast<const int2 *>(D->psq[pos]);
+                pinfo[q] = make_int2((int32_t)((uint32_t)pq.x - (uint32_t)pq.y) / 2, b);
+              }
+            }
           }
 #pragma unroll
           for (int i = 0; i < 4; ++i) acc0[buf][(4 * kg + i) * AS + row] = 0; // free for bucket bq + 2
@@ -1091,22 +1104,10 @@ __global__ void __launch_bounds__(L1 / SL / 8) __attribute__((amdgpu_waves_per_e
 #pragma unroll
           for (int i = 0; i < 4; ++i) pq[i] = *reinterpret_cast<const int2 *>(D->psq[4 * kg + i]), adj[i] = D->adj[4 * kg + i];
         }
-        int32_t sp[4] = {0, 0, 0, 0}; // SL > 1: the other slices' fc_0 sums
-        if constexpr (SL > 1) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int pos = 4 * kg + i;
-            if (present(pos)) {
-              const uint64_t q = out_index(pos, D->adj[pos]) * 16 + row;
-#pragma unroll
-              for (int t = 0; t < SL - 1; ++t) sp[i] = wadd(sp[i], part[(uint64_t)t * npos * 16 + q]);
-            }
-          }
-        }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int pos = 4 * kg + i;
-          const int32_t vv = wadd(wadd(acc0[buf][pos * AS + row], sp[i]), bias0);
+          const int32_t vv = wadd(acc0[buf][pos * AS + row], bias0);
           if (row < 15) {
             const long long s2 = ((long long)vv * vv) >> 19;
             in1[buf][pos][row] = (uint8_t)(s2 < 127 ? s2 : 127);
@@ -1191,13 +1192,72 @@ __global__ void __launch_bounds__(L1 / SL / 8) __attribute__((amdgpu_waves_per_e
 #endif
 }
 
+// The column-sliced stream's finish (a thread per position): the SL slices' fc_0 sums + bias,
+// the activations, fc_1, fc_2 and the outputs -- the whole-row kernel's finishing step in scalar
+// integer arithmetic (exact: every sum is an integer sum, the wrapping adds as there).  pinfo.y
+// < 0: a position the big net does not evaluate (left as it is).
+template <int SL>
+__global__ void __launch_bounds__(256) slice_finish_kernel(NetDevice net, const int32_t *__restrict__ part,
+                                                           const int2 *__restrict__ pinfo, uint64_t npos, uint32_t np,
+                                                           int2 *__restrict__ out_parent, int2 *__restrict__ out_child) {
+  // the 8 buckets' fc_1 weights (32 outputs x 32 int8, as 8 dwords per output) in LDS
+  __shared__ int4v w1s[8 * 32 * 2];
+  for (int i = threadIdx.x; i < 8 * 32 * 2; i += 256) w1s[i] = reinterpret_cast<const int4v *>(net.w1)[i];
+  __syncthreads();
+  const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= npos) return;
+  const int2 info = pinfo[q];
+  if (info.y < 0) return;
+  const int b = info.y & 7;
+  int32_t v[16];
+#pragma unroll
+  for (int r = 0; r < 16; r += 4) {
+    int4v a = *reinterpret_cast<const int4v *>(part + q * 16 + r);
+#pragma unroll
+    for (int t = 1; t < SL; ++t) {
+      const int4v c = *reinterpret_cast<const int4v *>(part + ((uint64_t)t * npos + q) * 16 + r);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) a[k] = wadd(a[k], c[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[r + k] = wadd(a[k], net.b0[b * 16 + r + k]);
+  }
+  // fc_1's 32 inputs as int8 packed 4 per dword: 15 squared, 15 clipped, 2 zero
+  uint32_t x[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+  for (int r = 0; r < 15; ++r) {
+    const long long s2 = ((long long)v[r] * v[r]) >> 19;
+    const uint32_t a = s2 < 127 ? (uint32_t)s2 : 127u, c = (uint32_t)clampi(v[r] >> 6, 0, 127);
+    x[r >> 2] |= a << (8 * (r & 3));
+    x[(15 + r) >> 2] |= c << (8 * ((15 + r) & 3));
+  }
+  const int32_t fwd = wmul(v[15], 600 * 16) / (127 * 64);
+  int32_t sum = 0;
+#pragma unroll 4
+  for (int o = 0; o < 32; ++o) {
+    const int4v wa = w1s[(b * 32 + o) * 2], wb = w1s[(b * 32 + o) * 2 + 1];
+    int32_t acc = 0;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) acc = __builtin_amdgcn_sdot4((int)x[d], wa[d], acc, false);
+#pragma unroll
+    for (int d = 0; d < 4; ++d) acc = __builtin_amdgcn_sdot4((int)x[4 + d], wb[d], acc, false);
+    const int32_t l = clampi(wadd(acc, net.b1[b * 32 + o]) >> 6, 0, 127);
+    sum = wadd(sum, (int32_t)net.w2[b * 32 + o] * l);
+  }
+  const int32_t positional = wadd(wadd(net.b2[b], sum), fwd);
+  const int2 val = make_int2(info.x / 16, positional / 16);
+  if (q < np) out_parent[q] = val;
+  else out_child[q - np] = val;
+}
+
 hipError_t launch_plan_stream(const NetDevice &net, const gn_board *parents, size_t n, const uint64_t *offsets,
                               const ChildDelta *deltas, const uint8_t *need_parent, const uint8_t *need_child,
                               int2 *out_parent, int2 *out_child, int swz, const uint8_t *next_slot, int chain_k,
                               int kc, const uint64_t *eoff, uint64_t *ent, TileDesc *tiles, uint32_t *btiles,
                               uint32_t *pool, uint32_t *err, unsigned long long *rows_out,
                               unsigned long long *pads_out, size_t b0, size_t b1, const uint32_t *order,
-                              hipEvent_t mid, hipStream_t s, int slices, int32_t *part, size_t npos) {
+                              hipEvent_t mid, hipStream_t s, int slices, int32_t *part, size_t npos,
+                              int2 *pinfo) {
   if (!n || b1 <= b0) return hipSuccess;
   if (n >= 0x80000000ull) return hipErrorInvalidValue; // 32-bit parent indices in the kernels
   const uint32_t K = chain_k > 1 && next_slot ? (uint32_t)chain_k : 1u;
@@ -1210,15 +1270,21 @@ hipError_t launch_plan_stream(const NetDevice &net, const gn_board *parents, siz
                        need_child, K > 1 ? next_slot : nullptr, (uint32_t)n, K, B0, B1, K > 1 ? kc : 0, eoff, ent,
                        tiles, btiles, rows_out, pads_out, err);
     if (mid) (void)hipEventRecord(mid, s);
-    if (slices == 3 && part) // three launches over 1,024 columns each (claim counters pool[64 + 8 slice ..])
+    if (slices == 3 && part && pinfo) { // three launches over 1,024 columns each (claim counters
+      // pool[64 + 8 slice ..]), then the finish
+      hipError_t e = hipMemsetAsync(pinfo, 0xFF, npos * sizeof(int2), s);
+      if (e != hipSuccess) return e;
       for (int sl = 0; sl < 3; ++sl)
         hipLaunchKernelGGL((stream_eval_kernel<3072, 3>), dim3(g), dim3(128), 0, s, net, offsets, (uint32_t)n, K, B0,
                            B1, swz, eoff, ent, tiles, btiles, order, out_parent, out_child, pool, scr, err,
-                           pool + 64 + 8 * sl, sl, part, (uint64_t)npos);
-    else
+                           pool + 64 + 8 * sl, sl, part, (uint64_t)npos, pinfo);
+      hipLaunchKernelGGL((slice_finish_kernel<3>), dim3((unsigned)((npos + 255) / 256)), dim3(256), 0, s, net, part,
+                         pinfo, (uint64_t)npos, (uint32_t)n, out_parent, out_child);
+    } else {
       hipLaunchKernelGGL((stream_eval_kernel<3072>), dim3(g), dim3(384), 0, s, net, offsets, (uint32_t)n, K, B0, B1,
                          swz, eoff, ent, tiles, btiles, order, out_parent, out_child, pool, scr, err, pool + 64, 0,
-                         nullptr, (uint64_t)0);
+                         nullptr, (uint64_t)0, nullptr);
+    }
   } else if (net.L1 == 1024) {
     hipLaunchKernelGGL((plan_kernel<1024>), dim3(pg), dim3(256), 0, s, net, parents, offsets, deltas, need_parent,
                        need_child, K > 1 ? next_slot : nullptr, (uint32_t)n, K, B0, B1, K > 1 ? kc : 0, eoff, ent,
@@ -1226,7 +1292,7 @@ hipError_t launch_plan_stream(const NetDevice &net, const gn_board *parents, siz
     if (mid) (void)hipEventRecord(mid, s);
     hipLaunchKernelGGL((stream_eval_kernel<1024>), dim3(g), dim3(128), 0, s, net, offsets, (uint32_t)n, K, B0, B1,
                        swz, eoff, ent, tiles, btiles, order, out_parent, out_child, pool, scr, err, pool + 64, 0,
-                       nullptr, (uint64_t)0);
+                       nullptr, (uint64_t)0, nullptr);
   } else {
     return hipErrorInvalidValue;
   }
