@@ -276,6 +276,7 @@ def run_expand(c: Ctx, wl: dict, games: int, steps: int, warmup: int, check: int
     # the big net's two kernels timed apart (HIP events on the library's stream, inside the
     # timed region): the roofline's dominant kernel is stream_eval_kernel alone
     plan_ms, stream_ms = nn.get_option(G.STAT_PLAN_NS) / 1e6, nn.get_option(G.STAT_STREAM_NS) / 1e6
+    finish_ms = nn.get_option(G.STAT_FINISH_NS) / 1e6  # the sliced stream's slice_finish_kernel
     parents = d_p.download(G.BOARD_DTYPE, n)
     sums = (nn.checksum_device(out["po"], n * G.EVAL_SIZE), nn.checksum_device(out["co"], children * G.EVAL_SIZE),
             nn.checksum_device(out["mv"], children * 2), nn.checksum_device(out["off"], (n + 1) * 4))
@@ -285,6 +286,7 @@ def run_expand(c: Ctx, wl: dict, games: int, steps: int, warmup: int, check: int
     sl = 3 if planned and wl["l1"] == 3072 and nn.get_option(G.OPT_STREAM_SLICES) == 3 else 1
     r = dict(value=c.world * (n + children) * steps / wall, wall=wall, stage=stage,
              kern_ms=(stream_ms / sl) if planned else stage[5 if mode != 2 else 4], plan_ms=plan_ms,
+             finish_ms=finish_ms,
              alg=rows * (2 * wl["l1"] // sl + 4), rows=rows, parents=parents, n=n, launches=sl,
              children=children, gen_s=gen_s, checksum=sums[0] ^ sums[1], scratch_pads=scratch_pads,
              kernel=(f"stream_eval_kernel<{wl['l1']}, 3> (3 column-slice launches per step)" if sl == 3 else
@@ -817,6 +819,8 @@ def main():
     roof["stage_ms"] = {k: round(v, 4) for k, v in zip(stage_names, r["stage"])}
     if r.get("plan_ms"):
         roof["plan_kernel_ms"] = round(r["plan_ms"], 4)
+    if r.get("finish_ms"):
+        roof["finish_kernel_ms"] = round(r["finish_ms"], 4)
     line = {
         "metric": METRIC, "value": round(r["value"], 1), "unit": "evals/s", "n_gpus": c.world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(r["wall"] * 1e3 / args.steps, 3),

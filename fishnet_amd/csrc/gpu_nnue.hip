@@ -233,7 +233,8 @@ struct Dev {
   // caller stream and return while their kernels are still queued).
   hipEvent_t done = nullptr;
   hipStream_t done_on = nullptr;
-  float plan_ms = 0, stream_ms = 0; // the last timed planned expansion (GN_STAT_PLAN_NS / _STREAM_NS)
+  float plan_ms = 0, stream_ms = 0, finish_ms = 0; // the last timed planned expansion (GN_STAT_PLAN_NS /
+                                                    // _STREAM_NS / _FINISH_NS)
   // the score rule's two levels of in-check replies (resolve_scores): selection, the selected
   // positions, their replies and the replies' records / rule values
   struct ScoreLevel {
@@ -802,7 +803,8 @@ static int expand_evaluate(gn_ctx *ctx, Dev &d, const gn_board *parents, size_t 
                                  d.chain_k > 1 ? d.nslot.p : nullptr, d.chain_k,
                                  ctx->king_cache ? 1 : 0, d.eoff.p, d.ent.p, d.tiles.p, d.btiles.p, d.pool.p, d.perr.p,
                                  rows_out, d.pstat.p, 0, nblk, order, ev ? ev[4] : nullptr, s, slices,
-                                 slices > 1 ? d.part.p : nullptr, n + total, slices > 1 ? d.pinfo.p : nullptr));
+                                 slices > 1 ? d.part.p : nullptr, n + total, slices > 1 ? d.pinfo.p : nullptr,
+                                 ev ? ev[6] : nullptr));
     } else { // a 128-wide net loaded as the big net
       HIP_TRY(launch_expand_net(d.net[BIG], parents, n, off, children, dl, f ? d.p_nbg.p : nullptr,
                                 f ? d.nbg.p : nullptr, d.p_obg.p, d.obg.p, ctx->swizzle & 1, s));
@@ -2159,8 +2161,9 @@ int gn_time_expand_device(gn_ctx *ctx, int device_slot, const gn_board *d_parent
   SeqGuard sg(*d, s);
   HIP_TRY(sg.e);
   // start, [count+scan], [total read], [write], [classify], [small], [big], [finalize], the
-  // planned big net's plan -> stream boundary, and [score rule] (ends at e[9])
-  const int NE = 10;
+  // planned big net's plan -> stream boundary, [score rule] (ends at e[9]), and the stream ->
+  // finish boundary (e[10])
+  const int NE = 11;
   std::vector<hipEvent_t> ev((size_t)iters * NE + 2, nullptr);
   auto cleanup = [&] {
     for (auto &e : ev)
@@ -2216,15 +2219,16 @@ int gn_time_expand_device(gn_ctx *ctx, int device_slot, const gn_board *d_parent
     for (int k = 0; k < 8; ++k) stage_ms[k] = acc[k] / (float)iters;
   }
   if (rc == GN_OK && he == hipSuccess && d->planned) { // the big net's two kernels apart
-    float pl = 0, st = 0;
+    float pl = 0, st = 0, fi = 0;
     for (int it = 0; it < iters && he == hipSuccess; ++it) {
-      float a = 0, b = 0;
+      float a = 0, b = 0, c = 0;
       const size_t o = 2 + (size_t)NE * it;
       he = hipEventElapsedTime(&a, ev[o + 5], ev[o + 8]);
-      if (he == hipSuccess) he = hipEventElapsedTime(&b, ev[o + 8], ev[o + 6]);
-      pl += a, st += b;
+      if (he == hipSuccess) he = hipEventElapsedTime(&b, ev[o + 8], ev[o + 10]); // the stream launches
+      if (he == hipSuccess) he = hipEventElapsedTime(&c, ev[o + 10], ev[o + 6]);  // the sliced stream's finish
+      pl += a, st += b, fi += c;
     }
-    d->plan_ms = pl / (float)iters, d->stream_ms = st / (float)iters;
+    d->plan_ms = pl / (float)iters, d->stream_ms = st / (float)iters, d->finish_ms = fi / (float)iters;
   }
   cleanup();
   *total = t;
@@ -2341,9 +2345,13 @@ int gn_get_option(const gn_ctx *ctx, int option, int64_t *value) {
     return GN_OK;
   }
   case GN_STAT_PLAN_NS:
-  case GN_STAT_STREAM_NS: { // read-only: the last gn_time_expand_device's planned kernels (max over devices)
+  case GN_STAT_STREAM_NS:
+  case GN_STAT_FINISH_NS: { // read-only: the last gn_time_expand_device's planned kernels (max over devices)
     float m = 0;
-    for (auto &dp : ctx->devs) m = std::max(m, option == GN_STAT_PLAN_NS ? dp->plan_ms : dp->stream_ms);
+    for (auto &dp : ctx->devs)
+      m = std::max(m, option == GN_STAT_PLAN_NS     ? dp->plan_ms
+                      : option == GN_STAT_STREAM_NS ? dp->stream_ms
+                                                    : dp->finish_ms);
     *value = (int64_t)((double)m * 1e6);
     return GN_OK;
   }

@@ -85,7 +85,8 @@ static_assert(sizeof(TileDesc) == 192, "TileDesc is 192 bytes");
 // slices == 3 (L1 3072; part, pinfo non-null): the stream runs as three launches over 1,024
 // columns each (stream_eval_kernel<3072, 3>) and slice_finish_kernel; part = 3 x npos x 16 int32
 // fc_0 partial sums, pinfo = npos (PSQT value, bucket) pairs, npos = n + the children;
-// otherwise one launch over whole rows.
+// otherwise one launch over whole rows.  fin (optional): recorded after the stream launches
+// (before the finish).
 hipError_t launch_plan_stream(const NetDevice &net, const gn_board *parents, size_t n, const uint64_t *offsets,
                               const ChildDelta *deltas, const uint8_t *need_parent, const uint8_t *need_child,
                               int2 *out_parent, int2 *out_child, int swz, const uint8_t *next_slot, int chain_k,
@@ -93,7 +94,7 @@ hipError_t launch_plan_stream(const NetDevice &net, const gn_board *parents, siz
                               uint32_t *pool, uint32_t *err, unsigned long long *rows_out,
                               unsigned long long *pads_out, size_t b0, size_t b1, const uint32_t *order,
                               hipEvent_t mid, hipStream_t s, int slices = 1, int32_t *part = nullptr,
-                              size_t npos = 0, int2 *pinfo = nullptr);
+                              size_t npos = 0, int2 *pinfo = nullptr, hipEvent_t fin = nullptr);
 // GN_MODE_FULL preparation: need_small = valid && |simple_eval| > threshold,
 // need_big = valid && !need_small.
 hipError_t launch_classify(const gn_board *boards, size_t n, const gn_eval_params &P, uint8_t *need_small,

@@ -1257,7 +1257,7 @@ hipError_t launch_plan_stream(const NetDevice &net, const gn_board *parents, siz
                               uint32_t *pool, uint32_t *err, unsigned long long *rows_out,
                               unsigned long long *pads_out, size_t b0, size_t b1, const uint32_t *order,
                               hipEvent_t mid, hipStream_t s, int slices, int32_t *part, size_t npos,
-                              int2 *pinfo) {
+                              int2 *pinfo, hipEvent_t fin) {
   if (!n || b1 <= b0) return hipSuccess;
   if (n >= 0x80000000ull) return hipErrorInvalidValue; // 32-bit parent indices in the kernels
   const uint32_t K = chain_k > 1 && next_slot ? (uint32_t)chain_k : 1u;
@@ -1278,12 +1278,14 @@ hipError_t launch_plan_stream(const NetDevice &net, const gn_board *parents, siz
         hipLaunchKernelGGL((stream_eval_kernel<3072, 3>), dim3(g), dim3(128), 0, s, net, offsets, (uint32_t)n, K, B0,
                            B1, swz, eoff, ent, tiles, btiles, order, out_parent, out_child, pool, scr, err,
                            pool + 64 + 8 * sl, sl, part, (uint64_t)npos, pinfo);
+      if (fin) (void)hipEventRecord(fin, s);
       hipLaunchKernelGGL((slice_finish_kernel<3>), dim3((unsigned)((npos + 255) / 256)), dim3(256), 0, s, net, part,
                          pinfo, (uint64_t)npos, (uint32_t)n, out_parent, out_child);
     } else {
       hipLaunchKernelGGL((stream_eval_kernel<3072>), dim3(g), dim3(384), 0, s, net, offsets, (uint32_t)n, K, B0, B1,
                          swz, eoff, ent, tiles, btiles, order, out_parent, out_child, pool, scr, err, pool + 64, 0,
                          nullptr, (uint64_t)0, nullptr);
+      if (fin) (void)hipEventRecord(fin, s);
     }
   } else if (net.L1 == 1024) {
     hipLaunchKernelGGL((plan_kernel<1024>), dim3(pg), dim3(256), 0, s, net, parents, offsets, deltas, need_parent,
@@ -1293,6 +1295,7 @@ hipError_t launch_plan_stream(const NetDevice &net, const gn_board *parents, siz
     hipLaunchKernelGGL((stream_eval_kernel<1024>), dim3(g), dim3(128), 0, s, net, offsets, (uint32_t)n, K, B0, B1,
                        swz, eoff, ent, tiles, btiles, order, out_parent, out_child, pool, scr, err, pool + 64, 0,
                        nullptr, (uint64_t)0, nullptr);
+    if (fin) (void)hipEventRecord(fin, s);
   } else {
     return hipErrorInvalidValue;
   }

@@ -51,7 +51,7 @@ EXPORTS = ["gn_load_net", "gn_load_net_memory", "gn_free", "gn_last_error", "gn_
            "gn_random_games_uci"]
 OPT_INCREMENTAL_CHILDREN, OPT_XCD_SWIZZLE, OPT_KING_SORT, OPT_CHAIN, OPT_KING_CACHE = 1, 2, 3, 4, 5
 OPT_CHUNK_PARENTS, OPT_COALESCE, OPT_STREAM_SLICES = 6, 7, 8
-STAT_PLAN_NS, STAT_STREAM_NS, STAT_SCRATCH_PADS = 101, 102, 103
+STAT_PLAN_NS, STAT_STREAM_NS, STAT_SCRATCH_PADS, STAT_FINISH_NS = 101, 102, 103, 104
 STAT_BATCH_LAUNCHES, STAT_BATCH_CALLS = 117, 118
 HOST_STAGES = {"parse": 110, "upload": 111, "replay": 112, "compute": 113, "download": 114, "tail": 115, "total": 116}
 EXPAND_STAGES = ["count_scan", "total_readback", "write_children", "classify", "small_net", "big_net", "finalize",

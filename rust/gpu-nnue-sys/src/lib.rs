@@ -40,6 +40,7 @@ pub const GN_OPT_STREAM_SLICES: c_int = 8;
 pub const GN_STAT_PLAN_NS: c_int = 101;
 pub const GN_STAT_STREAM_NS: c_int = 102;
 pub const GN_STAT_SCRATCH_PADS: c_int = 103;
+pub const GN_STAT_FINISH_NS: c_int = 104;
 pub const GN_STAT_HOST_PARSE_NS: c_int = 110;
 pub const GN_STAT_HOST_UPLOAD_NS: c_int = 111;
 pub const GN_STAT_HOST_REPLAY_NS: c_int = 112;
