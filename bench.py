@@ -343,21 +343,31 @@ def run_expand(c: Ctx, wl: dict, games: int, steps: int, warmup: int, check: int
     return r
 
 
+def gather_records(c, out, n, children):
+    """Every rank's records of one expansion to rank 0 (ShardComm.gather_tensor: RCCL on device
+    tensors, gloo on CPU tensors; the lengths differ per rank): parent gn_eval records, the child
+    offsets, child moves and child gn_eval records.  Returns ({part: list of every rank's bytes
+    on rank 0, None elsewhere}, bytes of all ranks)."""
+    es = c.G.EVAL_SIZE
+    parts = (("po", n * es), ("off", (n + 1) * 4), ("mv", children * 2), ("co", children * es))
+    got = {k: c.comm.gather_tensor(out[k].tensor[:nb]) for k, nb in parts}
+    if out["po"].tensor.is_cuda:
+        c.torch.cuda.synchronize()
+    return got, sum(c.comm.gather_i64(sum(nb for _, nb in parts)))
+
+
 def gather_results(c: Ctx, out, n, children, games, mode, check):
     """The result gather of DESIGN.md section 6 (N > 1): every rank's parent / child records, child
     moves and offsets of the timed step to rank 0 over RCCL (torch.distributed gather on the
     records' device memory), outside the timed region and timed on its own; rank 0 then checks
     sampled parents of every rank, with all their children, against the oracle."""
-    G, T = c.G, c.torch
+    G = c.G
     es = G.EVAL_SIZE
-    parts = (("po", n * es), ("off", (n + 1) * 4), ("mv", children * 2), ("co", children * es))
     c.barrier_sync()
     t0 = time.perf_counter()
-    got = {k: c.comm.gather_tensor(out[k].tensor[:nb]) for k, nb in parts}
-    T.cuda.synchronize()
+    got, nbytes = gather_records(c, out, n, children)
     c.barrier_sync()
     ms = c.comm.max(time.perf_counter() - t0) * 1e3
-    nbytes = sum(c.comm.gather_i64(sum(nb for _, nb in parts)))
     r = {"bytes_all_ranks": nbytes, "ms": round(ms, 2), "GBps_into_rank0": round(nbytes / ms / 1e6, 1),
          "how": "torch.distributed.gather (RCCL over xGMI) of each rank's gn_eval records, child moves and offsets "
                 "to rank 0's device memory, after the timed steps"}
@@ -727,6 +737,13 @@ def launch_ranks(gpus: int, argv) -> int | None:
         return None
     if gpus <= 1:
         return None
+    # build the HIP library and the oracle once, here, before any rank exists (hipcc and gcc need
+    # no GPU): N ranks finding a stale build would otherwise compile the same files at once
+    if not os.environ.get("GPU_NNUE_LIB"):
+        from fishnet_amd import build
+        build.build()
+    from oracle import oracle as O
+    O.build()
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *argv]
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))

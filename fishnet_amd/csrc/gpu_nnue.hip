@@ -782,10 +782,13 @@ static int expand_evaluate(gn_ctx *ctx, Dev &d, const gn_board *parents, size_t 
       HIP_TRY(d.btiles.ensure(nblk + 1));
       HIP_TRY(d.pool.ensure(88)); // 8 XCDs x 8 words of scratch-slot bits, then 8 block claim counters
       HIP_TRY(hipMemsetAsync(d.pool.p, 0, 88 * sizeof(uint32_t), s)); // per stream launch (<= 3)
-      const int slices = d.net[BIG].L1 == 3072 && ctx->stream_slices == 3 ? 3 : 1;
-      if (slices > 1) {
-        HIP_TRY(d.part.ensure(3 * 16 * (n + total)));
-        HIP_TRY(d.pinfo.ensure(n + total));
+      int slices = d.net[BIG].L1 == 3072 && ctx->stream_slices == 3 ? 3 : 1;
+      // the sliced stream's partial sums cost 200 B per position (include/gpu_nnue.h,
+      // GN_OPT_STREAM_SLICES); when they do not fit, the whole-row stream gives the same results
+      if (slices > 1 && (d.part.ensure(3 * 16 * (n + total)) != hipSuccess || d.pinfo.ensure(n + total) != hipSuccess)) {
+        (void)hipGetLastError(); // (the failed allocation's error is not the call's)
+        d.part.release(), d.pinfo.release();
+        slices = 1;
       }
       // XCD-local block order
       const uint32_t *order = nullptr;
@@ -978,16 +981,40 @@ static int evaluate_coalesced(gn_ctx *ctx, const gn_board *boards, size_t n, int
   auto &C = ctx->co;
   BatchReq me{boards, n, mode, out};
   std::unique_lock<std::mutex> lk(C.mu);
-  C.q.push_back(&me);
+  try {
+    C.q.push_back(&me);
+  } catch (const std::bad_alloc &) {
+    return fail(GN_E_NOMEM, "host allocation failed");
+  }
+  // every exit (an exception included) takes this call's request off the queue, so that no
+  // later leader touches it after this stack frame is gone
+  struct Dequeue {
+    decltype(C) &c;
+    BatchReq *me;
+    ~Dequeue() {
+      for (size_t i = 0; i < c.q.size(); ++i)
+        if (c.q[i] == me) {
+          c.q.erase(c.q.begin() + (ptrdiff_t)i);
+          break;
+        }
+    }
+  } dq{C, &me};
   while (!me.done) {
     if (C.busy) {
       C.cv.wait(lk);
       continue;
     }
-    C.busy = true;
+    // the queue is split before the context is marked busy: an allocation failure here leaves
+    // the context free and this call off the queue (Dequeue)
     std::vector<BatchReq *> mine, rest;
+    try {
+      mine.reserve(C.q.size()), rest.reserve(C.q.size());
+    } catch (const std::bad_alloc &) {
+      return fail(GN_E_NOMEM, "host allocation failed");
+    }
     for (BatchReq *r : C.q) (r->mode == mode ? mine : rest).push_back(r);
     C.q.swap(rest);
+    C.busy = true;
     lk.unlock();
     int rc = GN_OK;
     std::string err;
@@ -1782,11 +1809,11 @@ int gn_set_eval_params(gn_ctx *ctx, const gn_eval_params *p) {
                 (int)VALUE_MATE_IN_MAX_PLY);
   // to_cp's a(material) >= 1 wherever it is evaluated (every clamped material value), so that
   // |final_cp| <= 100 * value_clamp < 2^23 fits gn_child's 24-bit field (defaults: a ~ 370-400)
-  for (int mc = p->wdl_material_min; mc <= p->wdl_material_max; ++mc) {
+  for (int64_t mc = p->wdl_material_min; mc <= (int64_t)p->wdl_material_max; ++mc) { // (int64: max may be INT_MAX)
 #pragma clang fp contract(off)
     const double m = (double)mc / (double)p->wdl_material_anchor;
     const double a = ((p->wdl_a[0] * m + p->wdl_a[1]) * m + p->wdl_a[2]) * m + p->wdl_a[3];
-    if (!(a >= 1.0)) return fail(GN_E_INVALID, "win-rate model a(material %d) = %g < 1", mc, a);
+    if (!(a >= 1.0)) return fail(GN_E_INVALID, "win-rate model a(material %lld) = %g < 1", (long long)mc, a);
   }
   ctx->P = *p;
   return GN_OK;

@@ -121,7 +121,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
                 const uint8_t *__restrict__ need_child, const uint8_t *__restrict__ next_slot, uint32_t np, uint32_t K,
                 uint32_t b0, uint32_t b1, int kc, const uint64_t *__restrict__ eoff, uint64_t *__restrict__ ent, TileDesc *__restrict__ tiles,
                 uint32_t *__restrict__ btiles, unsigned long long *__restrict__ rows_out,
-                unsigned long long *__restrict__ pads_out, uint32_t *__restrict__ err) {
+                unsigned long long *__restrict__ pads_out, uint32_t *__restrict__ err, int2 *__restrict__ pinfo) {
   using namespace ps;
   __shared__ uint32_t ksnap[4][128][8]; // per wave: placement (64 nibbles) of each king-cache row
   __shared__ uint16_t prow_s[4][2][32];
@@ -486,6 +486,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
       const bool nx = q == nxpos;
       // ---- PSQT of the slot by side (a king-move perspective: its job's sum), slot metadata
       if (in && live) {
+        int32_t sv[2] = {0, 0}; // the slot's PSQT at its bucket by side (0: the side to move)
 #pragma unroll
         for (int hh = 0; hh < 2; ++hh) {
           const int kd = hh ? kinds >> 2 : kinds & 3;
@@ -495,9 +496,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
             const int32_t d1 = (hh ? s1 : s0) >= 2 ? -dq[hh][1] : dq[hh][1];
             v = wadd(pp[hh][bk == bp ? 0 : 1], wadd(wadd(-dq[hh][0], d1), wadd(dq[hh][2], dq[hh][3])));
           }
-          *reinterpret_cast<int32_t *>(tf(tk0 + tix, offsetof(TileDesc, psq) + 8 * t + 4 * (hh != cst))) =
-              kd == 2 ? jsum : v;
+          v = kd == 2 ? jsum : v;
+          *reinterpret_cast<int32_t *>(tf(tk0 + tix, offsetof(TileDesc, psq) + 8 * t + 4 * (hh != cst))) = v;
+          sv[hh != cst] = v;
         }
+        // the column-sliced stream's finish takes each evaluated position's PSQT value and
+        // bucket from here (Network::evaluate's psqt term, a15 / a17), by output index
+        if (pinfo && vld)
+          pinfo[q == 0 ? (uint64_t)p : (uint64_t)np + off + (uint64_t)child_of(q)] =
+              make_int2((int32_t)((uint32_t)sv[0] - (uint32_t)sv[1]) / 2, bk);
       }
       if (in) {
         *tf(tk0 + tix, offsetof(TileDesc, meta) + t) = (char)((live && vld ? 1 : 0) | bk << 1 | (q == 0 ? 16 : 0) | cst << 5);
@@ -871,6 +878,36 @@ __global__ void __launch_bounds__(L1 / SL / 8) __attribute__((amdgpu_waves_per_e
   ushort8 rlo[RD], rhi[RD];
   uint32_t eh[RD]; // hi words of the entries in flight
   uint32_t bq = 0; // buckets done (acc0 / in1 / fwd buffer parity)
+  // SL > 1: this wave's fc_0 weights of one bucket (its 8 k-steps of the slice, in the MFMA's
+  // operand order) stay in registers across tiles (a game's bucket changes rarely); a tile whose
+  // first bucket is not the cached one loads it at the tile's start, so that the loads are older
+  // than the ring's row loads of the tile's last entries and the layer stack waits for them alone
+  // (vmcnt counts in issue order: loads issued at the layer stack wait behind the ring's 8)
+  int4v wc[8]; // (no initial value: read only after a fill)
+  int cb = 8; // the cached bucket (8: none)
+  const __amdgpu_buffer_rsrc_t w0r = __builtin_amdgcn_make_buffer_rsrc(
+      (void *)net.w0f, 0, (int)((size_t)PSQT_BUCKETS * KSF * 1024), 0x00020000);
+  const uint32_t wl16 = (uint32_t)(threadIdx.x & 63) * 16;
+  // the 8 k-steps of bucket b for this wave (side = the wave's perspective group, the slice's
+  // k-steps of that side): invisible to the compiler's waits like the ring (wc_wait below)
+  auto wc_load = [&](int b) {
+    const uint32_t so = ((uint32_t)b * KSF + (uint32_t)(24 * HU + 8 * slice)) * 1024u;
+    asm volatile("buffer_load_dwordx4 %0, %8, %9, %10 offen\n\t"
+                 "buffer_load_dwordx4 %1, %8, %9, %10 offen offset:1024\n\t"
+                 "buffer_load_dwordx4 %2, %8, %9, %10 offen offset:2048\n\t"
+                 "buffer_load_dwordx4 %3, %8, %9, %10 offen offset:3072\n\t"
+                 "buffer_load_dwordx4 %4, %8, %9, %11 offen\n\t"
+                 "buffer_load_dwordx4 %5, %8, %9, %11 offen offset:1024\n\t"
+                 "buffer_load_dwordx4 %6, %8, %9, %11 offen offset:2048\n\t"
+                 "buffer_load_dwordx4 %7, %8, %9, %11 offen offset:3072"
+                 : "+v"(wc[0]), "+v"(wc[1]), "+v"(wc[2]), "+v"(wc[3]), "+v"(wc[4]), "+v"(wc[5]), "+v"(wc[6]),
+                   "+v"(wc[7]) // ("+v": the fill overwrites the cache's own registers, no copies)
+                 : "v"(wl16), "s"(w0r), "s"(so), "s"(so + 4096u));
+  };
+  // wait for the cache's loads: vmcnt(8) when at least 8 vector-memory operations were issued
+  // after them (the ring's loads of the tile's last 4 entries: in-order completion), else all
+#define GN_WC_WAIT(N) asm volatile("s_waitcnt vmcnt(" #N ")" : "+v"(wc[0]), "+v"(wc[1]), "+v"(wc[2]), "+v"(wc[3]), \
+                                   "+v"(wc[4]), "+v"(wc[5]), "+v"(wc[6]), "+v"(wc[7]))
   typedef uint32_t u8e __attribute__((ext_vector_type(2 * RD), aligned(8)));
   typedef const __attribute__((address_space(4))) u8e cu8e;
   typedef const __attribute__((address_space(4))) uint64_t cu64;
@@ -915,6 +952,10 @@ __global__ void __launch_bounds__(L1 / SL / 8) __attribute__((amdgpu_waves_per_e
   // entries of the last revolution and the earlier ones of this one were issued since); any
   // other memory operation in between (a drained store, the layer stack's loads) only makes
   // vmcnt(6) wait for more.  The "+v" ties the row registers to the wait: no use before it.
+  // (one wait form only: a second form behind a branch made the compiler copy ring registers
+  // before their wait at the join -- tests/test_host.py::test_ring_registers_untouched_in_flight.
+  // A weight-cache fill at a tile's start is younger than the RD entries then in flight, so the
+  // next waits also wait for its loads: once per bucket change)
   auto ring_wait = [&](int r) {
     asm volatile("s_waitcnt vmcnt(" GN_STR(GN_RING_WAIT) ")" : "+v"(rlo[r]), "+v"(rhi[r]));
   };
@@ -941,7 +982,11 @@ __global__ void __launch_bounds__(L1 / SL / 8) __attribute__((amdgpu_waves_per_e
     }
     if (h & H_LAST) {
       const int sl = (h >> H_SLOT_SH) & 15, side = (h >> H_SIDE_SH) & 1;
+#ifdef GN_AB_NO_TRANSFORM // timing diagnostics only (wrong results): the accumulator's low bytes, untransformed
+      *reinterpret_cast<uint2 *>(xt + sl * XS + side * (LC / 2) + 8 * jt) = make_uint2(lo[0] | (uint32_t)hi[0] << 16, lo[1]);
+#else
       *reinterpret_cast<uint2 *>(xt + sl * XS + side * (LC / 2) + 8 * jt) = transform8(lo, hi);
+#endif
       if (h & H_PAR_E) {
         asm volatile("");
         pacc_lo = lo, pacc_hi = hi;
@@ -993,6 +1038,29 @@ __global__ void __launch_bounds__(L1 / SL / 8) __attribute__((amdgpu_waves_per_e
 #pragma unroll
     for (int i = 0; i < 4; ++i)
       mw[i] = (uint32_t)__builtin_amdgcn_readfirstlane((int)reinterpret_cast<const uint32_t *>(D->meta)[i]);
+    uint32_t bm = 0, pm = 0; // the tile's buckets, its parent slots
+#pragma unroll
+    for (int sl = 0; sl < TILE; ++sl) {
+      const uint32_t m = (mw[sl >> 2] >> (8 * (sl & 3))) & 0xFF;
+      if (m & 1) bm |= 1u << ((m >> 1) & 7);
+      if (m & 16) pm |= 1u << sl;
+    }
+#ifdef GN_AB_NO_LS // timing diagnostics only (no outputs): the stream without its layer stack
+    bm = 0;
+#endif
+    bool wpend = false; // (SL > 1) the cache was loaded at this tile's start
+    const uint32_t pos0 = pos;
+#ifndef GN_NO_WCACHE // A/B: round 4's layer stack (every tile's weights loaded at the layer stack)
+    if constexpr (SL > 1) {
+#else
+    if constexpr (false) {
+#endif
+      if (bm && !((bm >> cb) & 1)) {
+        cb = __builtin_ctz(bm);
+        wc_load(cb);
+        wpend = true;
+      }
+    }
     // ---- the row stream of this group's list segment [pos, e_end): ring slot r holds entry i
     // with i % 4 == r, so a tile may begin and end anywhere in a revolution of 4 entries (a
     // revolution starts at a multiple of 4: it waits for its prefetched group of entries,
@@ -1016,33 +1084,68 @@ __global__ void __launch_bounds__(L1 / SL / 8) __attribute__((amdgpu_waves_per_e
     }
     asm volatile("" ::: "memory");
     const unsigned long long t1 = SP_T();
+#ifndef GN_AB_NO_BARRIER // timing diagnostics only (racy, wrong results): the layer stack without barriers
     __syncthreads();
+#endif
     const unsigned long long t2 = SP_T();
     sp_s += t1 - t0, sp_w += t2 - t1;
     // ---- layer stack: per bucket of the tile, fc_0 by all waves (int8 MFMA over this wave's
     // k-steps, partial sums by LDS integer atomics, exact), then one wave finishes it
-    uint32_t bm = 0, pm = 0;
-#pragma unroll
-    for (int sl = 0; sl < TILE; ++sl) {
-      const uint32_t m = (mw[sl >> 2] >> (8 * (sl & 3))) & 0xFF;
-      if (m & 1) bm |= 1u << ((m >> 1) & 7);
-      if (m & 16) pm |= 1u << sl;
-    }
     const uint64_t u0 = us_b + first;
+    if constexpr (SL > 1) {
+      // the cache's loads (issued before the tile's entries) are complete once at most the 8
+      // youngest operations are outstanding: the ring's loads of this list's last RD entries,
+      // when the tile had RD entries or more since the fill; otherwise wait for everything.
+      // The tied wait is unconditional (no join of two paths after it, where the compiler could
+      // copy the registers before the wait)
+      if (wpend && pos - pos0 < (uint32_t)RD) __builtin_amdgcn_s_waitcnt(0x0F70); // vmcnt(0)
+      GN_WC_WAIT(8);
+    }
+    // (SL > 1: the cached bucket first, as bit 8 of mm; the others load the cache when they come)
+    uint32_t mm = SL > 1 && ((bm >> cb) & 1) ? (bm ^ (1u << cb)) | 256u : bm;
 #pragma unroll 1
-    for (uint32_t mm = bm; mm; mm &= mm - 1) {
-      const int b = __builtin_ctz(mm);
+    while (mm) {
+      int b;
+      if (mm & 256u) b = cb, mm ^= 256u;
+      else b = __builtin_ctz(mm), mm &= mm - 1;
       const int buf = (int)(bq & 1);
       int tl = tid;
       asm volatile("" : "+v"(tl));
       const int ln = tl & 63, row = ln & 15, kg = ln >> 4;
-      {
+      if constexpr (SL > 1) {
+        if (b != cb) { // a tile's second bucket: the cache's fill now, behind the ring's loads
+          cb = b;
+          wc_load(b);
+          GN_WC_WAIT(0);
+        }
+        const uint8_t *xa = xt + row * XS + kg * 16 + 64 * KPW * wave;
+        int4v acc = {0, 0, 0, 0};
+        constexpr int FB = 2;
+        int stop = 0;
+        asm volatile("" : "+s"(stop));
+#pragma unroll
+        for (int k0 = 0; k0 < KPW && !stop; k0 += FB) {
+          int4v av[FB];
+#pragma unroll
+          for (int j = 0; j < FB; ++j) av[j] = *reinterpret_cast<const int4v *>(xa + 64 * (k0 + j));
+#pragma unroll
+          for (int j = 0; j < FB; ++j) acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(av[j], wc[k0 + j], acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) atomicAdd(&acc0[buf][(4 * kg + i) * AS + row], acc[i]);
+      } else {
         const uint8_t *xa = xt + row * XS + kg * 16 + 64 * KPW * wave;
         // (w0f: the k-step's 64 lanes x 16 B are one contiguous 1 KiB)
         // (SL > 1: wave w of perspective h covers the net's k-steps of its slice of that side)
         constexpr int WH = NW / 2;
         const int wsl = SL > 1 ? (wave / WH) * WH * SL + slice * WH + wave % WH : wave;
+#ifdef GN_AB_W0_FIXED // timing diagnostics only (wrong results): every k-step's weights from one 1-KiB block
+        const int8_t *wb = net.w0f + (size_t)ln * 16;
+        constexpr int WSTEP = 0;
+#else
         const int8_t *wb = net.w0f + (((size_t)b * KSF + KPW * wsl) * 64 + ln) * 16;
+        constexpr int WSTEP = 1024;
+#endif
         int4v acc = {0, 0, 0, 0};
         // (batches of FB k-steps: the next tile's rows stay in flight in registers meanwhile)
         // (`stop`, always 0, is opaque to the compiler: without a runtime exit test it schedules the
@@ -1055,7 +1158,7 @@ __global__ void __launch_bounds__(L1 / SL / 8) __attribute__((amdgpu_waves_per_e
         for (int k0 = 0; k0 < KPW && !stop; k0 += FB) {
           int4v wv[FB], av[FB];
 #pragma unroll
-          for (int j = 0; j < FB; ++j) wv[j] = *reinterpret_cast<const int4v *>(wb + 1024 * (k0 + j));
+          for (int j = 0; j < FB; ++j) wv[j] = *reinterpret_cast<const int4v *>(wb + WSTEP * (k0 + j));
 #pragma unroll
           for (int j = 0; j < FB; ++j) av[j] = *reinterpret_cast<const int4v *>(xa + 64 * (k0 + j));
 #pragma unroll
@@ -1064,7 +1167,9 @@ __global__ void __launch_bounds__(L1 / SL / 8) __attribute__((amdgpu_waves_per_e
 #pragma unroll
         for (int i = 0; i < 4; ++i) atomicAdd(&acc0[buf][(4 * kg + i) * AS + row], acc[i]);
       }
+#ifndef GN_AB_NO_BARRIER
       __syncthreads();
+#endif
       // a position's output index (parent P, or np + its child index) and whether it is evaluated
       // in bucket b
       auto present = [&](int pos) -> bool {
@@ -1077,16 +1182,23 @@ __global__ void __launch_bounds__(L1 / SL / 8) __attribute__((amdgpu_waves_per_e
       };
       if constexpr (SL > 1) {
         if (wave == (int)(bq % NW)) { // this slice's fc_0 sums of bucket b to its partial array
+          // the tile's 16 adj values by one scalar load (the descriptor is in the scalar cache
+          // since the tile's start): a vector load here would make the compiler wait for every
+          // vector load in flight, i.e. the ring's next entries (in-order vmcnt)
+          typedef const __attribute__((address_space(4))) uint32_t cu32;
+          const cu32 *aw = (const cu32 *)reinterpret_cast<const uint32_t *>(D->adj);
+          uint32_t a8[8];
+#pragma unroll
+          for (int i = 0; i < 8; ++i) a8[i] = aw[i];
+          const uint32_t alo = kg == 0 ? a8[0] : kg == 1 ? a8[2] : kg == 2 ? a8[4] : a8[6];
+          const uint32_t ahi = kg == 0 ? a8[1] : kg == 1 ? a8[3] : kg == 2 ? a8[5] : a8[7];
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const int pos = 4 * kg + i;
             if (present(pos)) {
-              const uint64_t q = out_index(pos, D->adj[pos]);
+              const uint32_t aword = i < 2 ? alo : ahi;
+              const uint64_t q = out_index(pos, (int)(int16_t)(aword >> (16 * (i & 1))));
               part[((uint64_t)slice * npos + q) * 16 + row] = acc0[buf][pos * AS + row];
-              if (slice == 0 && row == 0) {
-                const int2 pq = *reinterpret_cast<const int2 *>(D->psq[pos]);
-                pinfo[q] = make_int2((int32_t)((uint32_t)pq.x - (uint32_t)pq.y) / 2, b);
-              }
             }
           }
 #pragma unroll
@@ -1266,14 +1378,17 @@ hipError_t launch_plan_stream(const NetDevice &net, const gn_board *parents, siz
   const uint32_t nb = (uint32_t)(b1 - b0), B0 = (uint32_t)b0, B1 = (uint32_t)b1;
   const unsigned pg = (nb + 3) / 4, g = swz == 1 ? 8 * ((nb + 7) / 8) : nb + nb / 16 + 8; // (stream_eval_kernel: claims)
   if (net.L1 == 3072) {
-    hipLaunchKernelGGL((plan_kernel<3072>), dim3(pg), dim3(256), 0, s, net, parents, offsets, deltas, need_parent,
-                       need_child, K > 1 ? next_slot : nullptr, (uint32_t)n, K, B0, B1, K > 1 ? kc : 0, eoff, ent,
-                       tiles, btiles, rows_out, pads_out, err);
-    if (mid) (void)hipEventRecord(mid, s);
-    if (slices == 3 && part && pinfo) { // three launches over 1,024 columns each (claim counters
-      // pool[64 + 8 slice ..]), then the finish
+    const bool sliced = slices == 3 && part && pinfo;
+    if (sliced) { // (positions the big net does not evaluate keep pinfo.y < 0; the plan writes the rest)
       hipError_t e = hipMemsetAsync(pinfo, 0xFF, npos * sizeof(int2), s);
       if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL((plan_kernel<3072>), dim3(pg), dim3(256), 0, s, net, parents, offsets, deltas, need_parent,
+                       need_child, K > 1 ? next_slot : nullptr, (uint32_t)n, K, B0, B1, K > 1 ? kc : 0, eoff, ent,
+                       tiles, btiles, rows_out, pads_out, err, sliced ? pinfo : nullptr);
+    if (mid) (void)hipEventRecord(mid, s);
+    if (sliced) { // three launches over 1,024 columns each (claim counters pool[64 + 8 slice ..]),
+      // then the finish
       for (int sl = 0; sl < 3; ++sl)
         hipLaunchKernelGGL((stream_eval_kernel<3072, 3>), dim3(g), dim3(128), 0, s, net, offsets, (uint32_t)n, K, B0,
                            B1, swz, eoff, ent, tiles, btiles, order, out_parent, out_child, pool, scr, err,
@@ -1290,7 +1405,7 @@ hipError_t launch_plan_stream(const NetDevice &net, const gn_board *parents, siz
   } else if (net.L1 == 1024) {
     hipLaunchKernelGGL((plan_kernel<1024>), dim3(pg), dim3(256), 0, s, net, parents, offsets, deltas, need_parent,
                        need_child, K > 1 ? next_slot : nullptr, (uint32_t)n, K, B0, B1, K > 1 ? kc : 0, eoff, ent,
-                       tiles, btiles, rows_out, pads_out, err);
+                       tiles, btiles, rows_out, pads_out, err, nullptr);
     if (mid) (void)hipEventRecord(mid, s);
     hipLaunchKernelGGL((stream_eval_kernel<1024>), dim3(g), dim3(128), 0, s, net, offsets, (uint32_t)n, K, B0, B1,
                        swz, eoff, ent, tiles, btiles, order, out_parent, out_child, pool, scr, err, pool + 64, 0,

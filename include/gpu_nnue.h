@@ -118,7 +118,11 @@ extern "C" {
                                          stream launch each over every entry, so that an
                                          XCD's L2 holds the slice's rows of the king buckets
                                          in flight; 1: one launch over whole rows.  Results
-                                         are identical either way.                        */
+                                         are identical either way.  The slices' fc_0 partial
+                                         sums take 200 B of device memory per evaluated
+                                         position (parents + children of a call or chunk);
+                                         when that allocation fails the call runs the
+                                         whole-row stream instead.                        */
 
 /* read-only statistics (gn_get_option) */
 #define GN_STAT_PLAN_NS 101           /* the last gn_time_expand_device's planned big net

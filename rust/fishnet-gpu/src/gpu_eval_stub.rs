@@ -41,8 +41,12 @@ fn replay_to_fen(pos: &Position) -> Option<Fen> {
 /// move lists are prefixes of the longest one (IncomingBatch::from_acquired makes position i
 /// = root + moves[..i], queue.rs:605-637), so replaying the longest list once yields every
 /// position's FEN (O(L) moves instead of the O(L^2) of a replay per position); a position
-/// outside that pattern is replayed on its own.  None: a move that does not replay.
+/// outside that pattern is replayed on its own.  None: a move that does not replay; an empty
+/// chunk gives an empty list.
 fn replay_chunk(positions: &[Position]) -> Option<Vec<Fen>> {
+    if positions.is_empty() {
+        return Some(Vec::new()); // an empty chunk is an empty result, not a failed replay
+    }
     let longest = positions.iter().max_by_key(|p| p.moves.len())?;
     let mut board: Chess = longest.root_fen.clone().into_position(CastlingMode::Chess960).ok()?;
     let mut line = vec![Fen::from_position(board.clone(), EnPassantMode::Legal)];

@@ -135,3 +135,73 @@ def test_bench_world_size_mismatch_fails():
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     p = _bench(["--gpus", "1", "--launch-check"], env)  # one rank, no launcher: runs in place
     assert p.returncode == 0 and '"world": 1' in p.stdout
+
+
+def _gather_worker(rank, world, port, q):
+    """One rank of the world-size-4 record gather: this rank's expansion outputs as CPU tensors of
+    the sizes the library writes (gn_eval records, u32 offsets, u16 moves), a different number of
+    parents and children per rank, through bench.gather_records (ShardComm.gather_tensor over
+    gloo; RCCL on device tensors in an 8-GPU run)."""
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path.insert(0, ROOT)
+    try:
+        import types
+        import torch
+        import bench
+        from fishnet_amd import gpu_nnue as G
+        from fishnet_amd.dist import ShardComm
+        comm = ShardComm("gloo")
+        n, children = _gather_shape(rank)
+        out = {k: types.SimpleNamespace(tensor=torch.from_numpy(v.copy())) for k, v in _gather_bytes(rank).items()}
+        c = types.SimpleNamespace(G=G, torch=torch, comm=comm)
+        got, nbytes = bench.gather_records(c, out, n, children)
+        comm.close()
+        q.put((rank, nbytes, None if got["po"] is None else
+               {k: [t.numpy().tobytes() for t in v] for k, v in got.items()}))
+    except Exception as e:  # surface the failure to the parent
+        q.put((rank, "error", repr(e)))
+
+
+def _gather_shape(rank):
+    return 81 * (rank + 1) + 7 * rank, 2_000 + 977 * rank  # (parents, children) of this rank
+
+
+def _gather_bytes(rank):
+    """Deterministic record bytes of one rank (the library's record sizes, ABI v4)."""
+    from fishnet_amd import gpu_nnue as G
+    n, ch = _gather_shape(rank)
+    rng = np.random.default_rng(900 + rank)
+    return {"po": rng.integers(0, 256, n * G.EVAL_SIZE, dtype=np.uint8),
+            "off": np.sort(rng.integers(0, ch + 1, n + 1)).astype(np.uint32).view(np.uint8),
+            "mv": rng.integers(0, 256, ch * 2, dtype=np.uint8),
+            "co": rng.integers(0, 256, ch * G.EVAL_SIZE, dtype=np.uint8)}
+
+
+def test_four_rank_gloo_record_gather():
+    """bench.py's result gather (gather_records, the code an N-GPU run executes
+    after its timed steps) at world size 4 with a different record count per rank: rank 0 gets
+    every rank's parent records, offsets, child moves and child records byte for byte, the
+    other ranks None, and every rank the total byte count."""
+    import multiprocessing as mp
+    world = 4
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_gather_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = {}
+    for _ in range(world):
+        item = q.get(timeout=240)
+        res[item[0]] = item
+    for p in ps:
+        p.join(timeout=60)
+    assert all(r[1] != "error" for r in res.values()), res
+    exp = [_gather_bytes(r) for r in range(world)]
+    total = sum(len(v) for e in exp for v in e.values())
+    for r in range(world):
+        assert res[r][1] == total
+        assert (res[r][2] is None) == (r != 0)
+    for k in ("po", "off", "mv", "co"):
+        assert res[0][2][k] == [exp[r][k].tobytes() for r in range(world)], k

@@ -839,9 +839,11 @@ def test_eval_params_keep_child_cp_in_24_bits(gpu_ctx):
 @pytest.mark.gpu
 def test_stream_column_slices_equal_whole_rows(gpu_ctx, oracle_nets, oracle_lib):
     """GN_OPT_STREAM_SLICES: the big net's stream as three launches over 1,024 accumulator
-    columns each (fc_0 partial sums of slices 0 and 1 added by the last one) gives every output
-    of the one-launch whole-row stream, with the chained walk and king cache on and off;
-    sampled parents with all their children against the oracle."""
+    columns each (every slice stores its fc_0 partial sums; slice_finish_kernel adds the three and
+    runs the rest of the layer stack) gives every output of the one-launch whole-row stream, with
+    the chained walk and king cache on and off, in mode BIG (every position on the big net) and
+    mode FULL (the big net on the positions the small net hands over: gaps in the slices' position
+    lists); sampled parents with all their children against the oracle."""
     from fishnet_amd import gpu_nnue as G
     games, plies = 1200, 80
     n = games * (plies + 1)
@@ -852,20 +854,20 @@ def test_stream_column_slices_equal_whole_rows(gpu_ctx, oracle_nets, oracle_lib)
     out = {"po": gpu_ctx.alloc(n * G.EVAL_SIZE), "off": gpu_ctx.alloc((n + 1) * 4), "mv": gpu_ctx.alloc(total * 2),
            "co": gpu_ctx.alloc(total * G.EVAL_SIZE), "cap": total}
 
-    def run(slices, k, kc):
+    def run(slices, k, kc, mode=1):
         gpu_ctx.set_option(G.OPT_STREAM_SLICES, slices)
         gpu_ctx.set_option(G.OPT_CHAIN, k)
         gpu_ctx.set_option(G.OPT_KING_CACHE, kc)
-        _, t, _, _ = gpu_ctx.time_expand_device(d_b, n, 1, 1, outputs=out)
+        _, t, _, _ = gpu_ctx.time_expand_device(d_b, n, mode, 1, outputs=out)
         assert t == total
         return tuple(gpu_ctx.checksum_device(out[b], nb) for b, nb in
                      (("po", n * G.EVAL_SIZE), ("co", t * G.EVAL_SIZE)))
 
     assert gpu_ctx.get_option(G.OPT_STREAM_SLICES) == 3
     try:
-        for k, kc in ((81, 1), (1, 0)):
-            whole = run(1, k, kc)
-            assert run(3, k, kc) == whole, (k, kc)
+        for k, kc, mode in ((81, 1, 1), (1, 0, 1), (81, 1, 0), (1, 0, 0)):
+            whole = run(1, k, kc, mode)
+            assert run(3, k, kc, mode) == whole, (k, kc, mode)
         with pytest.raises(G.GnError):
             gpu_ctx.set_option(G.OPT_STREAM_SLICES, 2)
     finally:

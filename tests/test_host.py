@@ -279,3 +279,115 @@ def test_stream_kernel_does_not_spill(tmp_path):
         spill = int(re.search(r"VGPRs Spill: (\d+)", block).group(1))
         scratch = int(re.search(r"ScratchSize \[bytes/lane\]: (\d+)", block).group(1))
         assert vgprs <= most and spill == 0 and scratch == 0, (name, vgprs, spill, scratch)
+
+
+def _stream_isa(tmp_path):
+    """stream_eval_kernel<3072, 3>'s ISA lines (hipcc -S of stream.hip)."""
+    import subprocess
+    src = os.path.join(ROOT, "fishnet_amd", "csrc", "stream.hip")
+    asm = tmp_path / "s.s"
+    subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "--cuda-device-only", "-S", src, "-o",
+                    str(asm)], capture_output=True, text=True, check=True)
+    text = asm.read_text()
+    start = text.index("\n_ZN2gn18stream_eval_kernelILi3072ELi3E")
+    start = text.index("\n", start + 1)
+    return text[start:text.index(".Lfunc_end", start)].splitlines()
+
+
+def _vregs(operands):
+    import re
+    out = set()
+    for a, b, c in re.findall(r"v\[(\d+):(\d+)\]|\bv(\d+)\b", operands):
+        out |= {int(c)} if c else set(range(int(a), int(b) + 1))
+    return out
+
+
+def _asm_blocks(body, n_loads):
+    """(line, destination registers) of every inline-asm block of n_loads buffer_load_dwordx4."""
+    out, i = [], 0
+    while i < len(body):
+        if "ASMSTART" in body[i]:
+            j = i + 1
+            while "ASMEND" not in body[j]:
+                j += 1
+            blk = body[i + 1:j]
+            if len(blk) == n_loads and all("buffer_load_dwordx4" in x for x in blk):
+                out.append((i, set().union(*(_vregs(x.split(None, 2)[1].split(",")[0]) for x in blk))))
+            i = j
+        i += 1
+    return out
+
+
+def _group_regions(body):
+    """The kernel's two perspective-group instantiations (run_group<0>, run_group<1>) as line
+    ranges: each begins with its ring prologue, four 2-load asm blocks within a few lines."""
+    ring = [i for i, _ in _asm_blocks(body, 2)]
+    starts = [i for j, i in enumerate(ring) if j + 3 < len(ring) and ring[j + 3] - i < 60
+              and (j == 0 or i - ring[j - 1] > 60)]
+    assert len(starts) == 2, starts
+    return [(0, starts[1]), (starts[1], len(body))]
+
+
+def _touches(body, regs, lo=0, hi=None):
+    for k, line in enumerate(body[lo:hi], lo):
+        s = line.strip()
+        if not s or s.startswith((";", ".")) or s.endswith(":") or " " not in s:
+            continue
+        op, rest = s.split(None, 1)
+        if _vregs(rest.split(";")[0]) & regs:
+            yield k, op, s
+
+
+def test_ring_registers_untouched_in_flight(tmp_path):
+    """The stream's row ring is filled by inline-asm loads (issue()) that the compiler cannot see
+    complete; each entry's wait (ring_wait) ties its two registers.  A compiler copy of a ring
+    register between its load and its wait reads stale data (round 5: a two-armed wait made the
+    compiler do exactly that at the join).  In stream_eval_kernel<3072, 3>'s ISA a ring register
+    is read only by the consume step's multiply-adds, or as a temporary the same basic block
+    wrote first (the register is free between its entry's consume and its next load): no copy,
+    store or other read of its loaded value."""
+    import shutil
+    if not shutil.which("hipcc"):
+        pytest.skip("hipcc not available")
+    body = _stream_isa(tmp_path)
+    for lo, hi in _group_regions(body):
+        ring = set().union(*(r for i, r in _asm_blocks(body, 2) if lo <= i < hi))
+        assert len(ring) == 32, sorted(ring)  # 4 entries x (lo, hi) x 4 VGPRs
+        bad, temp = [], set()
+        for k in range(lo, hi):
+            s = body[k].strip()
+            if s.endswith(":") or s.startswith(".LBB") or "ASMSTART" in s:
+                temp = set()  # (a new basic block, or an asm block: nothing is known to be a temporary)
+                continue
+            if not s or s.startswith((";", ".")) or " " not in s:
+                continue
+            op, rest = s.split(None, 1)
+            ops = [x.strip() for x in rest.split(";")[0].split(",")]
+            dst = _vregs(ops[0]) if op.startswith("v_") else set()
+            src = set().union(*(_vregs(x) for x in ops[1:])) if op.startswith("v_") else _vregs(",".join(ops))
+            if op.startswith(("buffer_load", "global_load", "ds_read")):
+                src, dst = set().union(*(_vregs(x) for x in ops[1:])), _vregs(ops[0])
+            if (src & ring) - temp and op not in ("v_pk_mad_u16", "v_pk_mul_lo_u16"):
+                bad.append((k, s))
+            temp |= dst & ring
+        assert not bad, bad[:8]
+
+
+def test_weight_cache_registers_untouched_in_flight(tmp_path):
+    """The sliced stream's fc_0 weight cache is filled by inline-asm loads whose completion the
+    compiler cannot see (stream.hip, wc_load / GN_WC_WAIT): a copy of those registers made by the
+    compiler between the fill and the wait would read stale data.  In the kernel's ISA the fill's
+    destination registers are touched only by the fills and the MFMAs (after the wait) -- no
+    move, spill or other read anywhere else."""
+    import shutil
+    if not shutil.which("hipcc"):
+        pytest.skip("hipcc not available")
+    body = _stream_isa(tmp_path)
+    fills = _asm_blocks(body, 8)
+    assert len(fills) in (2, 4), len(fills)  # per perspective group: the tile-start fill (+ the second bucket's)
+    for lo, hi in _group_regions(body):
+        wc = set().union(*(r for i, r in fills if lo <= i < hi))
+        assert len(wc) == 32, sorted(wc)  # (both fill sites of a group write the same registers)
+        bad = [(k, s) for k, op, s in _touches(body, wc, lo, hi)
+               if not ((op == "buffer_load_dwordx4" and any(f <= k <= f + 9 for f, _ in fills)) or op.startswith("v_mfma"))]
+        assert not bad, bad[:8]
