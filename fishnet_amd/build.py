@@ -14,6 +14,10 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIBDIR = os.path.join(HERE, "lib")
 LIB = os.path.join(LIBDIR, "libgpu_nnue.so")
+# test-only variant: the plan reports an entry overflow for block 1 on its first launch in a process
+# (stream.hip GN_FAULT_PLAN_BLOCK; tests/test_gpu_parity.py::test_plan_overflow_fails_the_call_then_recovers)
+FAULT_LIB = os.path.join(LIBDIR, "libgpu_nnue_fault.so")
+FAULT_DEFINES = ("-DGN_FAULT_PLAN_BLOCK=1",)
 SOURCES = ["gpu_nnue.hip", "kernels.hip", "stream.hip"]
 HEADERS = ["chess.h", "host_board.h", "nnue.h", "kernels.h", "sha256.h", "device_util.h", "archive.h"]
 ARCH = "gfx950"
@@ -68,6 +72,11 @@ def build(force: bool = False, verbose: bool = False, defines=(), out: str | Non
     for o in objs:
         os.remove(o)
     return lib
+
+
+def build_fault(force: bool = False, verbose: bool = False) -> str:
+    """The fault-injection library (never loaded by the product path or the bench)."""
+    return build(force=force, verbose=verbose, defines=FAULT_DEFINES, out=FAULT_LIB)
 
 
 if __name__ == "__main__":

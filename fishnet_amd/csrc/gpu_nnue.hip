@@ -785,7 +785,7 @@ static int expand_evaluate(gn_ctx *ctx, Dev &d, const gn_board *parents, size_t 
       int slices = d.net[BIG].L1 == 3072 && ctx->stream_slices == 3 ? 3 : 1;
       // the sliced stream's partial sums cost 200 B per position (include/gpu_nnue.h,
       // GN_OPT_STREAM_SLICES); when they do not fit, the whole-row stream gives the same results
-      if (slices > 1 && (d.part.ensure(3 * 16 * (n + total)) != hipSuccess || d.pinfo.ensure(n + total) != hipSuccess)) {
+      if (slices > 1 && (d.part.ensure((size_t)GN_PART_SLICES * 16 * (n + total)) != hipSuccess || d.pinfo.ensure(n + total) != hipSuccess)) {
         (void)hipGetLastError(); // (the failed allocation's error is not the call's)
         d.part.release(), d.pinfo.release();
         slices = 1;

@@ -26,6 +26,18 @@
 #define GN_SCR_GAP GN_RING
 #endif
 
+// The column-sliced stream's fc_0 partial sums: one array per slice (default), which
+// slice_finish_kernel adds; or, with -DGN_PART_INPLACE (A/B only), one array that each slice
+// s > 0 adds its sums to in place, reading slice s - 1's at the tile's start.  In place measured
+// slower (round 5: finish 5.44 -> 2.75 ms, but each later stream launch +2.1 ms: the prefetch
+// misses to HBM and, vector-memory completion being in order, holds up the ring's next loads).
+// GN_PART_SLICES: the arrays launch_plan_stream's part holds.
+#ifdef GN_PART_INPLACE
+#define GN_PART_SLICES 1
+#else
+#define GN_PART_SLICES 3
+#endif
+
 namespace gn {
 
 // NetworkOutput {psqt / 16, positional / 16} for every position whose
@@ -83,8 +95,9 @@ static_assert(sizeof(TileDesc) == 192, "TileDesc is 192 bytes");
 // pads_out (optional): += no-op entries the plan inserted to keep GN_SCR_GAP.
 // order: block order of the stream (block_order) or NULL; mid: recorded between the kernels.
 // slices == 3 (L1 3072; part, pinfo non-null): the stream runs as three launches over 1,024
-// columns each (stream_eval_kernel<3072, 3>) and slice_finish_kernel; part = 3 x npos x 16 int32
-// fc_0 partial sums, pinfo = npos (PSQT value, bucket) pairs, npos = n + the children;
+// columns each (stream_eval_kernel<3072, 3>) and slice_finish_kernel; part = GN_PART_SLICES x npos
+// x 16 int32 fc_0 partial sums, pinfo = npos (PSQT value, bucket) pairs (written by the plan),
+// npos = n + the children;
 // otherwise one launch over whole rows.  fin (optional): recorded after the stream launches
 // (before the finish).
 hipError_t launch_plan_stream(const NetDevice &net, const gn_board *parents, size_t n, const uint64_t *offsets,

@@ -52,10 +52,15 @@
 #ifndef GN_PLAN_WPE
 #define GN_PLAN_WPE 4 // <= 128 VGPRs, no spills (round 3: 3 waves at 168 VGPRs beat 4 with spills; round 4 fits 4)
 #endif
-#ifndef GN_SLICE_WPE // the column-sliced stream (2-wave workgroups): at least 3 waves per SIMD; without the
-#define GN_SLICE_WPE 3 // finish (slice_finish_kernel) it needs 108 VGPRs and gets 4 (with the finish in the
-#endif                 // last slice: 125 + 8 AGPRs, 3 per SIMD 157.1 ms, forced to 4 160.4 ms; now padding
-                       // the LDS tile to hold it at 3 per SIMD (GN_SLICE_XPAD 192) is 2.6 % slower)
+#ifndef GN_SLICE_WPE // the column-sliced stream (2-wave workgroups): 4 waves per SIMD (<= 128 VGPRs; LDS holds
+#define GN_SLICE_WPE 4 // 8 workgroups per CU).  Round 5's weight cache and partial-sum prefetch need 126 at that
+#endif                 // bound (130 unbounded, i.e. 3 per SIMD).  (Round 4: with the finish in the last slice,
+                       // 125 + 8 AGPRs, 3 per SIMD 157.1 ms, forced to 4 160.4 ms)
+#define GN_PART_N GN_PART_SLICES
+#ifndef GN_WCACHE // the sliced stream's per-wave fc_0 weight cache (0: weights loaded at each layer stack)
+#define GN_WCACHE 1
+#endif
+#define GN_PV_WAIT GN_RING_WAIT_PV
 #ifndef GN_EXPAND_WPE
 #define GN_EXPAND_WPE (GN_RING == 4 ? 5 : 4)
 #endif
@@ -63,8 +68,10 @@
 #define GN_STR(x) GN_STR2(x)
 #if GN_RING == 4
 #define GN_RING_WAIT 6 // the 3 later entries' 2 loads each
+#define GN_RING_WAIT_PV 8 // the layer stack: every load older than the ring's RD entries (2 loads each)
 #else
 #define GN_RING_WAIT 14
+#define GN_RING_WAIT_PV 16
 #endif
 
 #ifdef GN_STREAM_PROF
@@ -92,6 +99,12 @@ __device__ unsigned long long gn_pp[4];
 // diagnostics build only: per XCD, [x] the last workgroup end and [8 + x] the first start
 // (s_memrealtime, 100 MHz, chip-wide), [16 + x] entries streamed, [24 + x] workgroups
 __device__ unsigned long long gn_xp[32] = {0, 0, 0, 0, 0, 0, 0, 0, ~0ull, ~0ull, ~0ull, ~0ull, ~0ull, ~0ull, ~0ull, ~0ull};
+#endif
+
+#ifdef GN_FAULT_PLAN_BLOCK
+// fault-injection build only (fishnet_amd/build.py FAULT_LIB; tests/test_gpu_parity.py
+// ::test_plan_overflow_fails_the_call_then_recovers): armed once per process
+__device__ int gn_fault_armed = 1;
 #endif
 
 namespace gn {
@@ -710,6 +723,18 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
     }
   }
   if (t_fill) flush();
+#ifdef GN_FAULT_PLAN_BLOCK
+  // the first plan launch of the process reports an entry overflow for this block (err bit 0) and
+  // leaves its last tile's list ends past the block's entry region, as round 4's plan bug did:
+  // the stream must clamp them (elim) and stay inside the region, and the call must fail
+  if (blk == (uint32_t)(GN_FAULT_PLAN_BLOCK) && tile_k > 0) {
+    int armed = lane == 0 ? atomicExch(&gn_fault_armed, 0) : 0;
+    if (__builtin_amdgcn_readfirstlane(armed)) {
+      if (lane == 0) *reinterpret_cast<uint2 *>(tf(tile_k - 1, 0)) = make_uint2(rtot + 4096u, rtot + 4096u);
+      bad |= 1u;
+    }
+  }
+#endif
   if (lane == 0) btiles[blk] = tile_k;
   // error bits: 1 entries beyond the block's region (eoff under-counted), 4 a scratch-row load
   // closer than GN_SCR_GAP to its list's last scratch store; neither can happen by construction
@@ -763,7 +788,7 @@ __global__ void __launch_bounds__(L1 / SL / 8) __attribute__((amdgpu_waves_per_e
   // fc_0 partial sums [position][output], rows padded to 20 dwords: the 4 lane groups of an
   // atomic (kg) then fall on different banks (a 16-dword row put all 4 on the same bank)
   constexpr int AS = 20;
-  __shared__ int32_t acc0[2][16 * AS];
+  __shared__ __attribute__((aligned(16))) int32_t acc0[2][16 * AS];
   __shared__ __attribute__((aligned(16))) uint8_t in1[2][TILE][32];
   __shared__ int32_t fwd[2][TILE];
   __shared__ uint32_t sslot, sblk;
@@ -906,7 +931,7 @@ __global__ void __launch_bounds__(L1 / SL / 8) __attribute__((amdgpu_waves_per_e
   };
   // wait for the cache's loads: vmcnt(8) when at least 8 vector-memory operations were issued
   // after them (the ring's loads of the tile's last 4 entries: in-order completion), else all
-#define GN_WC_WAIT(N) asm volatile("s_waitcnt vmcnt(" #N ")" : "+v"(wc[0]), "+v"(wc[1]), "+v"(wc[2]), "+v"(wc[3]), \
+#define GN_WC_WAIT(N) asm volatile("s_waitcnt vmcnt(" GN_STR(N) ")" : "+v"(wc[0]), "+v"(wc[1]), "+v"(wc[2]), "+v"(wc[3]), \
                                    "+v"(wc[4]), "+v"(wc[5]), "+v"(wc[6]), "+v"(wc[7]))
   typedef uint32_t u8e __attribute__((ext_vector_type(2 * RD), aligned(8)));
   typedef const __attribute__((address_space(4))) u8e cu8e;
@@ -1018,6 +1043,19 @@ __global__ void __launch_bounds__(L1 / SL / 8) __attribute__((amdgpu_waves_per_e
     for (int r = 0; r < RD; ++r) issue(r, elo(g0, r), ehi(g0, r));
   }
 
+  // tile slot sl's adj value (TileDesc.adj, the chained walk's output reorder) for a lane-varying
+  // slot: the 8 words by scalar loads (no vector load: it would make the compiler wait for the
+  // ring's loads in flight), into lanes 0..7 of one register, each lane fetching its word by
+  // ds_bpermute (an 8-way select would keep 7 lane masks in SGPRs: spills)
+  auto adj_of = [&](const TileDesc *Dt, int sl) -> int {
+    typedef const __attribute__((address_space(4))) uint32_t cu32;
+    const cu32 *aw = (const cu32 *)reinterpret_cast<const uint32_t *>(Dt->adj);
+    int vx = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(vx) : "s"((int)aw[i]), "i"(i));
+    const uint32_t w = (uint32_t)__builtin_amdgcn_ds_bpermute((sl >> 1) << 2, vx);
+    return (int)(int16_t)(w >> (16 * (sl & 1)));
+  };
   unsigned long long sp_s = 0, sp_w = 0, sp_l = 0, sp_m = 0, sp_n = 0;
   uint32_t sp_e0 = 0, sp_e1 = 0;
 #pragma unroll 1
@@ -1050,16 +1088,26 @@ __global__ void __launch_bounds__(L1 / SL / 8) __attribute__((amdgpu_waves_per_e
 #endif
     bool wpend = false; // (SL > 1) the cache was loaded at this tile's start
     const uint32_t pos0 = pos;
-#ifndef GN_NO_WCACHE // A/B: round 4's layer stack (every tile's weights loaded at the layer stack)
-    if constexpr (SL > 1) {
-#else
-    if constexpr (false) {
-#endif
+    if constexpr (SL > 1 && GN_WCACHE) {
       if (bm && !((bm >> cb) & 1)) {
         cb = __builtin_ctz(bm);
         wc_load(cb);
         wpend = true;
       }
+    }
+    // (SL > 1, slice > 0, in-place partial sums) this lane's 16 B of the previous slices' sums:
+    // position wp of the tile, outputs 4 wj .. 4 wj + 3 (the writer's lane layout below); an
+    // unevaluated slot reads position 0 (ignored).  Unconditional asm, waited with the cache
+    // (no path join between the load and its wait)
+    int4v pv;
+    if constexpr (SL > 1 && GN_PART_N == 1) {
+      const int ln = tid & 63, wp = ln >> 2, wj = ln & 3;
+      const int adjv = adj_of(D, wp);
+      const uint32_t m = (mw[wp >> 2] >> (8 * (wp & 3))) & 0xFF;
+      const uint32_t P = p_first + (uint32_t)__builtin_popcount(pm & ((2u << wp) - 1)) - (pm & 1);
+      const uint64_t q = !(m & 1) ? 0ull : ((pm >> wp) & 1) ? (uint64_t)P : (uint64_t)np + (us_b + first + wp - P - 1 + adjv);
+      const int32_t *src = part + q * 16 + 4 * wj;
+      if (slice > 0) asm volatile("global_load_dwordx4 %0, %1, off" : "=&v"(pv) : "v"(src));
     }
     // ---- the row stream of this group's list segment [pos, e_end): ring slot r holds entry i
     // with i % 4 == r, so a tile may begin and end anywhere in a revolution of 4 entries (a
@@ -1098,8 +1146,10 @@ __global__ void __launch_bounds__(L1 / SL / 8) __attribute__((amdgpu_waves_per_e
       // when the tile had RD entries or more since the fill; otherwise wait for everything.
       // The tied wait is unconditional (no join of two paths after it, where the compiler could
       // copy the registers before the wait)
-      if (wpend && pos - pos0 < (uint32_t)RD) __builtin_amdgcn_s_waitcnt(0x0F70); // vmcnt(0)
-      GN_WC_WAIT(8);
+      if ((wpend || (GN_PART_N == 1 && slice > 0)) && pos - pos0 < (uint32_t)RD)
+        __builtin_amdgcn_s_waitcnt(0x0F70); // vmcnt(0)
+      if constexpr (GN_WCACHE) GN_WC_WAIT(GN_RING_WAIT_PV);
+      if constexpr (GN_PART_N == 1) asm volatile("s_waitcnt vmcnt(" GN_STR(GN_PV_WAIT) ")" : "+v"(pv));
     }
     // (SL > 1: the cached bucket first, as bit 8 of mm; the others load the cache when they come)
     uint32_t mm = SL > 1 && ((bm >> cb) & 1) ? (bm ^ (1u << cb)) | 256u : bm;
@@ -1112,7 +1162,7 @@ __global__ void __launch_bounds__(L1 / SL / 8) __attribute__((amdgpu_waves_per_e
       int tl = tid;
       asm volatile("" : "+v"(tl));
       const int ln = tl & 63, row = ln & 15, kg = ln >> 4;
-      if constexpr (SL > 1) {
+      if constexpr (SL > 1 && GN_WCACHE) {
         if (b != cb) { // a tile's second bucket: the cache's fill now, behind the ring's loads
           cb = b;
           wc_load(b);
@@ -1185,24 +1235,22 @@ __global__ void __launch_bounds__(L1 / SL / 8) __attribute__((amdgpu_waves_per_e
           // the tile's 16 adj values by one scalar load (the descriptor is in the scalar cache
           // since the tile's start): a vector load here would make the compiler wait for every
           // vector load in flight, i.e. the ring's next entries (in-order vmcnt)
-          typedef const __attribute__((address_space(4))) uint32_t cu32;
-          const cu32 *aw = (const cu32 *)reinterpret_cast<const uint32_t *>(D->adj);
-          uint32_t a8[8];
+          // lane = (position wp, outputs 4 wj .. 4 wj + 3): one 16-B load of the sums and one
+          // 16-B store per lane (a store is a vector-memory operation younger than the ring's
+          // entries in flight, which the next entries' waits then also wait for: one, not four)
+          const int wp = ln >> 2, wj = ln & 3;
+          const int adjv = adj_of(D, wp);
+          int4v *src = reinterpret_cast<int4v *>(&acc0[buf][wp * AS + 4 * wj]);
+          if (present(wp)) {
+            const uint64_t q = out_index(wp, adjv);
+            int4v v = *src;
+            if (GN_PART_N == 1 && slice > 0) {
 #pragma unroll
-          for (int i = 0; i < 8; ++i) a8[i] = aw[i];
-          const uint32_t alo = kg == 0 ? a8[0] : kg == 1 ? a8[2] : kg == 2 ? a8[4] : a8[6];
-          const uint32_t ahi = kg == 0 ? a8[1] : kg == 1 ? a8[3] : kg == 2 ? a8[5] : a8[7];
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int pos = 4 * kg + i;
-            if (present(pos)) {
-              const uint32_t aword = i < 2 ? alo : ahi;
-              const uint64_t q = out_index(pos, (int)(int16_t)(aword >> (16 * (i & 1))));
-              part[((uint64_t)slice * npos + q) * 16 + row] = acc0[buf][pos * AS + row];
+              for (int k = 0; k < 4; ++k) v[k] = wadd(v[k], pv[k]); // (wrapping, as the LDS atomics)
             }
+            *reinterpret_cast<int4v *>(part + ((uint64_t)(GN_PART_N == 1 ? 0 : slice) * npos + q) * 16 + 4 * wj) = v;
           }
-#pragma unroll
-          for (int i = 0; i < 4; ++i) acc0[buf][(4 * kg + i) * AS + row] = 0; // free for bucket bq + 2
+          *src = int4v{0, 0, 0, 0}; // free for bucket bq + 2
         }
       } else if (wave == (int)(bq % NW)) { // fc_0 activations, fc_1, fc_2, outputs of bucket b
         // the finishing step's scalar weights and the tile's PSQT first (one wait for memory)
@@ -1326,7 +1374,7 @@ __global__ void __launch_bounds__(256) slice_finish_kernel(NetDevice net, const 
   for (int r = 0; r < 16; r += 4) {
     int4v a = *reinterpret_cast<const int4v *>(part + q * 16 + r);
 #pragma unroll
-    for (int t = 1; t < SL; ++t) {
+    for (int t = 1; t < GN_PART_N; ++t) { // (in place: the last slice's sums are the totals)
       const int4v c = *reinterpret_cast<const int4v *>(part + ((uint64_t)t * npos + q) * 16 + r);
 #pragma unroll
       for (int k = 0; k < 4; ++k) a[k] = wadd(a[k], c[k]);

@@ -23,7 +23,7 @@ FLAG_IN_CHECK, FLAG_SMALLNET, FLAG_BAD_FEN, FLAG_REEVAL, FLAG_SKIPPED = 1, 2, 4,
 FLAG_MATE, FLAG_NO_SCORE, FLAG_SEARCHED, FLAG_NO_MOVES = 32, 64, 128, 256
 ERRORS = {-1: "INVALID", -2: "IO", -3: "FORMAT", -4: "HIP", -5: "NOMEM", -6: "CAPACITY",
           -7: "NODEVICE", -8: "NONET", -9: "ILLEGAL_MOVE"}
-E_INVALID, E_IO, E_FORMAT, E_CAPACITY, E_ILLEGAL_MOVE = -1, -2, -3, -6, -9
+E_INVALID, E_IO, E_FORMAT, E_HIP, E_NOMEM, E_CAPACITY, E_NODEVICE, E_NONET, E_ILLEGAL_MOVE = -1, -2, -3, -4, -5, -6, -7, -8, -9
 
 # gn_eval (ABI v3): the static evaluation, and the score fishnet posts (gpu_nnue.h)
 EVAL_DTYPE = np.dtype([("psqt", "<i4"), ("positional", "<i4"), ("final_v", "<i4"), ("final_cp", "<i4"),

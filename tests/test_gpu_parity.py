@@ -888,3 +888,108 @@ def test_stream_column_slices_equal_whole_rows(gpu_ctx, oracle_nets, oracle_lib)
         p_exp, m_exp, k_exp = oracle_lib.expand_eval(big, small, fen, 1, incremental=True)
         assert tuple(pev[i]) == p_exp, fen
         assert dict(zip(mv.tolist(), map(tuple, ev.tolist()))) == dict(zip(m_exp, map(tuple, k_exp.tolist()))), fen
+
+
+_FAULT_CHILD = r"""
+import json, sys
+import numpy as np
+from fishnet_amd import gpu_nnue as G
+big, small, games = sys.argv[1], sys.argv[2], int(sys.argv[3])
+ctx = G.GpuNnue(big, small, devices=[0])
+n = games * 81
+d_b = ctx.alloc(n * 32)
+ctx.random_games_device(0x5EED0FA1, 0, games, 80, d_b)
+ctx.synchronize()
+ctx.set_option(G.OPT_CHAIN, -81)  # one block per game: block 1 exists
+res = {}
+try:
+    ctx.time_expand_device(d_b, n, G.MODE_BIG, 1)
+    res["first"] = "ok"
+except G.GnError as e:
+    res["first"] = [e.code, str(e)]
+_, total, _, _ = ctx.time_expand_device(d_b, n, G.MODE_BIG, 1)
+out = {"po": ctx.alloc(n * G.EVAL_SIZE), "off": ctx.alloc((n + 1) * 4), "mv": ctx.alloc(total * 2),
+       "co": ctx.alloc(total * G.EVAL_SIZE), "cap": total}
+_, t, _, _ = ctx.time_expand_device(d_b, n, G.MODE_BIG, 1, outputs=out)
+res["second"] = [ctx.checksum_device(out[b], nb) for b, nb in
+                 (("po", n * G.EVAL_SIZE), ("off", (n + 1) * 4), ("mv", t * 2), ("co", t * G.EVAL_SIZE))]
+ctx.close()
+print(json.dumps(res), flush=True)
+"""
+
+
+def test_plan_overflow_fails_the_call_then_recovers(gpu_ctx, synth_big_path, synth_small_path):
+    """round 4's plan bug made the plan overflow its lists; the plan reported it
+    (err bit 0) but the stream, launched before the host reads the error word, followed the bad
+    tile ends and faulted.  The stream now clamps every tile end to the block's entry region.
+    The fault-injection build (fishnet_amd/build.py FAULT_LIB, -DGN_FAULT_PLAN_BLOCK=1) has the
+    plan report an overflow for block 1 on its first launch and leave that block's last tile ends
+    4,096 entries past the region: in a process of its own (the variant library), the expansion
+    returns GN_E_HIP naming error bit 0 -- no fault -- and the next expansion on the same context
+    returns exactly the normal library's records (device checksums of every output)."""
+    import subprocess
+    import sys
+    from fishnet_amd import build, gpu_nnue as G
+    assert os.path.exists(build.FAULT_LIB), "run __graft_entry__.build() (builds the fault-injection library)"
+    games = 6
+    env = dict(os.environ, GPU_NNUE_LIB=build.FAULT_LIB)
+    p = subprocess.run([sys.executable, "-c", _FAULT_CHILD, synth_big_path, synth_small_path, str(games)],
+                       env=env, cwd=os.path.dirname(HERE), capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr[-3000:]
+    res = json.loads(p.stdout.strip().splitlines()[-1])
+    assert res["first"][0] == G.E_HIP and "0x1" in res["first"][1], res["first"]
+    # the same expansion with the normal library, in this process
+    n = games * 81
+    d_b = gpu_ctx.alloc(n * 32)
+    gpu_ctx.random_games_device(0x5EED0FA1, 0, games, 80, d_b)
+    gpu_ctx.synchronize()
+    try:
+        gpu_ctx.set_option(G.OPT_CHAIN, -81)
+        _, total, _, _ = gpu_ctx.time_expand_device(d_b, n, G.MODE_BIG, 1)
+        out = {"po": gpu_ctx.alloc(n * G.EVAL_SIZE), "off": gpu_ctx.alloc((n + 1) * 4), "mv": gpu_ctx.alloc(total * 2),
+               "co": gpu_ctx.alloc(total * G.EVAL_SIZE), "cap": total}
+        _, t, _, _ = gpu_ctx.time_expand_device(d_b, n, G.MODE_BIG, 1, outputs=out)
+    finally:
+        gpu_ctx.set_option(G.OPT_CHAIN, 81)
+    exp = [gpu_ctx.checksum_device(out[b], nb) for b, nb in
+           (("po", n * G.EVAL_SIZE), ("off", (n + 1) * 4), ("mv", t * 2), ("co", t * G.EVAL_SIZE))]
+    assert res["second"] == exp
+
+
+def test_two_device_slots_games_at_scale(synth_big_path, synth_small_path, oracle_nets, oracle_lib):
+    """the in-process multi-device path (one host thread per device slot,
+    INTEGRATION.md section 5) at the bench's shape -- 1,024 lichess-shaped 80-ply games through
+    gn_evaluate_games(with_children) with the column-sliced stream on two device slots (both on
+    GPU 0 here: gn_partition gives each slot 512 whole games, each runs its own chained walk,
+    king cache and three slice launches) -- returns byte for byte the single-slot records, and
+    sampled positions with all their children equal the oracle."""
+    from fishnet_amd import gpu_nnue as G
+    start = "rnbqkbnr/pppppppp/8/8/8/8/PPPPPPPP/RNBQKBNR w KQkq - 0 1"
+    games = [(start, u, (5,) if g % 7 == 0 else ()) for g, u in enumerate(G.random_games_uci(0x5EED2D2D, 0, 1024, 80))]
+    arr, keep = G._games_array(games)
+    res = []
+    for devs in ([0], [0, 0]):
+        ctx = G.GpuNnue(synth_big_path, synth_small_path, devices=devs)
+        try:
+            assert ctx.get_option(G.OPT_STREAM_SLICES) == 3
+            res.append([np.copy(x) for x in ctx.evaluate_games_arrays(arr, len(games), G.MODE_BIG, children=True)[:6]])
+        finally:
+            ctx.close()
+    for a, b in zip(*res):
+        assert a.tobytes() == b.tobytes()
+    offs, status, pos, coffs, cmoves, kids = res[1]
+    npos = int(offs[-1])  # (a random game may end early, at mate or a draw)
+    assert not status.any() and npos > 1024 * 70 and int(coffs[npos]) > npos * 20
+    big, _ = oracle_nets
+    rng = np.random.default_rng(11)
+    for g in rng.choice(len(games), 4, replace=False):
+        fens = oracle_lib.replay_game(start, games[g][1])[0]
+        ng = int(offs[g + 1] - offs[g])
+        assert ng == len(fens)
+        for i in (0, ng // 2, ng - 1):
+            k = int(offs[g]) + i
+            p_exp, m_exp, k_exp = oracle_lib.expand_eval(big, None, fens[i], G.MODE_BIG)
+            assert tuple(pos[k]) == p_exp, (g, i)
+            lo, hi = int(coffs[k]), int(coffs[k + 1])
+            got = dict(zip(cmoves[lo:hi].tolist(), map(tuple, G.decode_children(kids[lo:hi]).tolist())))
+            assert got == dict(zip(m_exp, map(tuple, G.children_from_evals(k_exp).tolist()))), (g, i)

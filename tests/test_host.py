@@ -281,13 +281,13 @@ def test_stream_kernel_does_not_spill(tmp_path):
         assert vgprs <= most and spill == 0 and scratch == 0, (name, vgprs, spill, scratch)
 
 
-def _stream_isa(tmp_path):
+def _stream_isa(tmp_path, defines=()):
     """stream_eval_kernel<3072, 3>'s ISA lines (hipcc -S of stream.hip)."""
     import subprocess
     src = os.path.join(ROOT, "fishnet_amd", "csrc", "stream.hip")
     asm = tmp_path / "s.s"
-    subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "--cuda-device-only", "-S", src, "-o",
-                    str(asm)], capture_output=True, text=True, check=True)
+    subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "--cuda-device-only", *defines, "-S", src,
+                    "-o", str(asm)], capture_output=True, text=True, check=True)
     text = asm.read_text()
     start = text.index("\n_ZN2gn18stream_eval_kernelILi3072ELi3E")
     start = text.index("\n", start + 1)
@@ -302,8 +302,8 @@ def _vregs(operands):
     return out
 
 
-def _asm_blocks(body, n_loads):
-    """(line, destination registers) of every inline-asm block of n_loads buffer_load_dwordx4."""
+def _asm_blocks(body, n_loads, op="buffer_load_dwordx4"):
+    """(line, destination registers) of every inline-asm block of n_loads `op` loads."""
     out, i = [], 0
     while i < len(body):
         if "ASMSTART" in body[i]:
@@ -311,7 +311,7 @@ def _asm_blocks(body, n_loads):
             while "ASMEND" not in body[j]:
                 j += 1
             blk = body[i + 1:j]
-            if len(blk) == n_loads and all("buffer_load_dwordx4" in x for x in blk):
+            if len(blk) == n_loads and all(op in x for x in blk):
                 out.append((i, set().union(*(_vregs(x.split(None, 2)[1].split(",")[0]) for x in blk))))
             i = j
         i += 1
@@ -390,4 +390,25 @@ def test_weight_cache_registers_untouched_in_flight(tmp_path):
         assert len(wc) == 32, sorted(wc)  # (both fill sites of a group write the same registers)
         bad = [(k, s) for k, op, s in _touches(body, wc, lo, hi)
                if not ((op == "buffer_load_dwordx4" and any(f <= k <= f + 9 for f, _ in fills)) or op.startswith("v_mfma"))]
+        assert not bad, bad[:8]
+
+
+def test_partial_sum_prefetch_registers_untouched_in_flight(tmp_path):
+    """The in-place slice partial sums (kernels.h, -DGN_PART_INPLACE, an A/B build): slice s > 0
+    reads slice s - 1's sums at the tile's start by an inline-asm load waited at the layer stack.
+    Its destination registers are read only by the writer's wrapping adds (v_add_u32) after that
+    wait: no copy or other read while the load is in flight (as the ring and the weight cache)."""
+    import shutil
+    if not shutil.which("hipcc"):
+        pytest.skip("hipcc not available")
+    body = _stream_isa(tmp_path, ("-DGN_PART_INPLACE",))
+    for lo, hi in _group_regions(body):
+        loads = [(i, r) for i, r in _asm_blocks(body, 1, "global_load_dwordx4") if lo <= i < hi]
+        assert len(loads) == 1, loads
+        i0, pv = loads[0]
+        assert len(pv) == 4
+        bad = [(k, s) for k, op, s in _touches(body, pv, lo, hi)
+               if k != i0 + 1 and not (op.startswith("v_add_u32") and s.split(",")[0].split()[-1] not in
+                                       {f"v{r}" for r in pv})
+               and not (op.startswith("buffer_load_dwordx4") and k - 1 in {i for i, _ in _asm_blocks(body, 2)})]
         assert not bad, bad[:8]
