@@ -992,6 +992,8 @@ __global__ void __launch_bounds__(L1 / SL / 8) __attribute__((amdgpu_waves_per_e
     // sg (1, 0xFFFF = -1, 0) the low half of h as the instruction's scalar operand; src is
     // the accumulator, or (PRE) 0 / the parent / the sibling base at a slot's first entry
     // (wrapping int16, as the accumulators)
+    const unsigned short sg = (unsigned short)h;
+#ifndef GN_PRE_MAD // (GN_PRE_MAD: one multiply-add per source, below: 11 VGPRs spilled with the revolution loop)
     if (h & H_PRE) {
       const uint32_t init = (h >> H_INIT_SH) & 3;
       asm volatile("");
@@ -999,12 +1001,32 @@ __global__ void __launch_bounds__(L1 / SL / 8) __attribute__((amdgpu_waves_per_e
       else if (init == 3) lo = base_lo, hi = base_hi;
       else lo = ushort8{}, hi = ushort8{};
     }
-    const unsigned short sg = (unsigned short)h;
     lo = rlo[r] * sg + lo, hi = rhi[r] * sg + hi;
     if ((h & (H_PRE | 3u << H_INIT_SH)) == (H_PRE | 2u << H_INIT_SH)) {
       asm volatile("");
       base_lo = lo, base_hi = hi;
     }
+#else
+    // each source has its own multiply-add (no copy of the source first; the copies and the
+    // merged paths cost ~10 scalar instructions and 4 branches per PRE entry)
+    if (!(h & H_PRE)) {
+      lo = rlo[r] * sg + lo, hi = rhi[r] * sg + hi;
+    } else {
+      const uint32_t init = (h >> H_INIT_SH) & 3;
+      asm volatile("");
+      if (init == 2) {
+        lo = rlo[r] * sg + pacc_lo, hi = rhi[r] * sg + pacc_hi;
+        asm volatile("");
+        base_lo = lo, base_hi = hi;
+      } else if (init == 3) {
+        asm volatile("");
+        lo = rlo[r] * sg + base_lo, hi = rhi[r] * sg + base_hi;
+      } else {
+        asm volatile("");
+        lo = rlo[r] * sg, hi = rhi[r] * sg;
+      }
+    }
+#endif
     if (h & H_LAST) {
       const int sl = (h >> H_SLOT_SH) & 15, side = (h >> H_SIDE_SH) & 1;
 #ifdef GN_AB_NO_TRANSFORM // timing diagnostics only (wrong results): the accumulator's low bytes, untransformed
@@ -1112,23 +1134,61 @@ __global__ void __launch_bounds__(L1 / SL / 8) __attribute__((amdgpu_waves_per_e
     // ---- the row stream of this group's list segment [pos, e_end): ring slot r holds entry i
     // with i % 4 == r, so a tile may begin and end anywhere in a revolution of 4 entries (a
     // revolution starts at a multiple of 4: it waits for its prefetched group of entries,
-    // whose rows it issues, and prefetches the next); every step is guarded by uniform tests
+    // whose rows it issues, and prefetches the next); the steps of a partial revolution are
+    // guarded by uniform tests, whole revolutions run unguarded (sliced stream)
+#ifdef GN_AB_GUARDED // A/B (round 4): every entry behind its own guard
+    constexpr bool REV = false;
+#else
+    constexpr bool REV = SL > 1; // (the whole-row stream, at its 96-VGPR cap, spills with it)
+#endif
+    // the tile's first partial revolution (guarded), then whole revolutions without per-entry
+    // guards (each took 7 scalar instructions and a branch), then the last partial one (guarded)
+    if constexpr (REV) {
+      {
+        const uint32_t r0 = pos & (RD - 1);
+        if (r0 != 0) {
+#pragma unroll
+          for (int r = 1; r < RD; ++r)
+            if (r0 <= (uint32_t)r && pos < e_end) consume(r), issue(r, elo(gw, r), ehi(gw, r)), ++pos;
+        }
+      }
 #pragma unroll 1
-    while (pos < e_end) {
-      const uint32_t r0 = pos & (RD - 1);
-      if (r0 == 0) {
-        // scalar loads complete out of order, so any use waits for all of them: wait once
-        // here (lgkmcnt(0): the prefetch of the previous revolution), take this revolution's
-        // entries, and only then prefetch the next group, which nothing uses before the next
+      while (pos + RD <= e_end) {
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        gw = gp;
+        gp = group(pos + 2 * RD);
+#pragma unroll
+        for (int r = 0; r < RD; ++r) consume(r), issue(r, elo(gw, r), ehi(gw, r));
+        pos += RD;
+      }
+      if (pos < e_end) {
         __builtin_amdgcn_s_waitcnt(0xC07F);
         gw = gp;
         gp = group(pos + 2 * RD);
         consume(0), issue(0, elo(gw, 0), ehi(gw, 0));
         ++pos;
-      }
 #pragma unroll
-      for (int r = 1; r < RD; ++r)
-        if (r0 <= (uint32_t)r && pos < e_end) consume(r), issue(r, elo(gw, r), ehi(gw, r)), ++pos;
+        for (int r = 1; r < RD - 1; ++r)
+          if (pos < e_end) consume(r), issue(r, elo(gw, r), ehi(gw, r)), ++pos;
+      }
+    } else {
+#pragma unroll 1
+      while (pos < e_end) {
+        const uint32_t r0 = pos & (RD - 1);
+        if (r0 == 0) {
+          // scalar loads complete out of order, so any use waits for all of them: wait once
+          // here (lgkmcnt(0): the prefetch of the previous revolution), take this revolution's
+          // entries, and only then prefetch the next group, which nothing uses before the next
+          __builtin_amdgcn_s_waitcnt(0xC07F);
+          gw = gp;
+          gp = group(pos + 2 * RD);
+          consume(0), issue(0, elo(gw, 0), ehi(gw, 0));
+          ++pos;
+        }
+#pragma unroll
+        for (int r = 1; r < RD; ++r)
+          if (r0 <= (uint32_t)r && pos < e_end) consume(r), issue(r, elo(gw, r), ehi(gw, r)), ++pos;
+      }
     }
     asm volatile("" ::: "memory");
     const unsigned long long t1 = SP_T();
