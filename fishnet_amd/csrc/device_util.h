@@ -298,4 +298,57 @@ __device__ __forceinline__ int32_t wave_sum_dpp(int32_t v) {
   return __builtin_amdgcn_readlane((int)scan_add((uint32_t)v), 63);
 }
 
+// ---- the column-sliced stream's finishing step for one position (slice_finish_kernel, and
+// finalize_kernel when it takes the big net's outputs from the partial sums itself): the NPART
+// slices' fc_0 sums (part[t * npos + q][16]) + bias, the activations, fc_1, fc_2 -- the
+// whole-row kernel's finishing step in scalar integer arithmetic (exact: every sum is an
+// integer sum, the wrapping adds as there).  info = pinfo[q] (PSQT value, bucket >= 0).
+// w1s: the 8 buckets' fc_1 weights (32 outputs x 32 int8, 8 dwords per output) staged in LDS
+// by stage_fc1 (8 KiB).
+__device__ __forceinline__ void stage_fc1(int4v *w1s, const NetDevice &net) {
+  for (int i = threadIdx.x; i < 8 * 32 * 2; i += blockDim.x) w1s[i] = reinterpret_cast<const int4v *>(net.w1)[i];
+}
+template <int NPART>
+__device__ __forceinline__ int2 slice_finish_one(const NetDevice &net, const int4v *w1s, const int32_t *__restrict__ part,
+                                                 uint64_t npos, uint64_t q, int2 info) {
+  const int b = info.y & 7;
+  int32_t v[16];
+#pragma unroll
+  for (int r = 0; r < 16; r += 4) {
+    int4v a = *reinterpret_cast<const int4v *>(part + q * 16 + r);
+#pragma unroll
+    for (int t = 1; t < NPART; ++t) { // (one array: the last slice's sums are the totals)
+      const int4v c = *reinterpret_cast<const int4v *>(part + ((uint64_t)t * npos + q) * 16 + r);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) a[k] = wadd(a[k], c[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[r + k] = wadd(a[k], net.b0[b * 16 + r + k]);
+  }
+  // fc_1's 32 inputs as int8 packed 4 per dword: 15 squared, 15 clipped, 2 zero
+  uint32_t x[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+  for (int r = 0; r < 15; ++r) {
+    const long long s2 = ((long long)v[r] * v[r]) >> 19;
+    const uint32_t a = s2 < 127 ? (uint32_t)s2 : 127u, c = (uint32_t)clampi(v[r] >> 6, 0, 127);
+    x[r >> 2] |= a << (8 * (r & 3));
+    x[(15 + r) >> 2] |= c << (8 * ((15 + r) & 3));
+  }
+  const int32_t fwd = wmul(v[15], 600 * 16) / (127 * 64);
+  int32_t sum = 0;
+#pragma unroll 4
+  for (int o = 0; o < 32; ++o) {
+    const int4v wa = w1s[(b * 32 + o) * 2], wb = w1s[(b * 32 + o) * 2 + 1];
+    int32_t acc = 0;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) acc = __builtin_amdgcn_sdot4((int)x[d], wa[d], acc, false);
+#pragma unroll
+    for (int d = 0; d < 4; ++d) acc = __builtin_amdgcn_sdot4((int)x[4 + d], wb[d], acc, false);
+    const int32_t l = clampi(wadd(acc, net.b1[b * 32 + o]) >> 6, 0, 127);
+    sum = wadd(sum, (int32_t)net.w2[b * 32 + o] * l);
+  }
+  const int32_t positional = wadd(wadd(net.b2[b], sum), fwd);
+  return make_int2(info.x / 16, positional / 16);
+}
+
 } // namespace gn

@@ -632,18 +632,22 @@ static bool plan_path(const gn_ctx *ctx, const Dev &d, int mode) {
 
 // finalize of the n parents and total children (their net outputs in the Dev buffers)
 // (score_parents: the parents are positions with the score rule; the children are child records)
+// (sliced: the big net's outputs are the sliced stream's partial sums, positions = parents then
+// children, which finalize finishes itself)
 static int finalize_all(gn_ctx *ctx, Dev &d, const gn_board *parents, const gn_board *children, int mode,
                         gn_eval *parent_out, gn_eval *child_out, size_t n, size_t total, hipStream_t s,
-                        bool score_parents) {
+                        bool score_parents, bool sliced = false) {
   const gn_eval_params &P = ctx->P;
+  const SlicedOut sc = {&d.net[BIG], d.part.p, d.pinfo.p, (uint64_t)(n + total), (uint64_t)n},
+                  sp = {&d.net[BIG], d.part.p, d.pinfo.p, (uint64_t)(n + total), 0};
   // children from their parents as write_children unpacked them
   const bool fast = d.child_moves != nullptr;
   HIP_TRY(launch_finalize(children, total, mode, d.osm.p, d.obg.p, d.nsm.p, d.nbg.p, P, d.tables, child_out, s, 0,
                           nullptr, fast ? d.owner.p : nullptr, fast ? d.child_moves : nullptr,
-                          fast ? d.unpacked.p : nullptr));
+                          fast ? d.unpacked.p : nullptr, sliced ? &sc : nullptr));
   if (parent_out) // the parents' legal-move counts are generate_children's
     HIP_TRY(launch_finalize(parents, n, mode, d.p_osm.p, d.p_obg.p, d.p_nsm.p, d.p_nbg.p, P, d.tables, parent_out, s,
-                            score_parents ? 1 : 0, d.counts.p));
+                            score_parents ? 1 : 0, d.counts.p, nullptr, nullptr, nullptr, sliced ? &sp : nullptr));
   return GN_OK;
 }
 
@@ -773,6 +777,7 @@ static int expand_evaluate(gn_ctx *ctx, Dev &d, const gn_board *parents, size_t 
     }
   }
   HIP_TRY(mark(1));
+  bool fused = false; // the sliced stream's finish runs inside finalize
   if (mode != GN_MODE_SMALL) {
     const bool f = mode == GN_MODE_FULL;
     if (d.planned) {
@@ -801,20 +806,23 @@ static int expand_evaluate(gn_ctx *ctx, Dev &d, const gn_board *parents, size_t 
                             d.sort_tmp, d.sort_bytes, s));
         order = d.border.p;
       }
+#ifndef GN_AB_FINISH_SEPARATE // A/B (round 4): slice_finish_kernel, then finalize
+      fused = slices > 1;
+#endif
       HIP_TRY(launch_plan_stream(d.net[BIG], parents, n, off, dl, f ? d.p_nbg.p : nullptr, f ? d.nbg.p : nullptr,
                                  d.p_obg.p, d.obg.p, (ctx->swizzle >> 2) & 1 ? 1 : (ctx->swizzle >> 3) & 1 ? 2 : 0,
                                  d.chain_k > 1 ? d.nslot.p : nullptr, d.chain_k,
                                  ctx->king_cache ? 1 : 0, d.eoff.p, d.ent.p, d.tiles.p, d.btiles.p, d.pool.p, d.perr.p,
                                  rows_out, d.pstat.p, 0, nblk, order, ev ? ev[4] : nullptr, s, slices,
                                  slices > 1 ? d.part.p : nullptr, n + total, slices > 1 ? d.pinfo.p : nullptr,
-                                 ev ? ev[6] : nullptr));
+                                 ev ? ev[6] : nullptr, !fused));
     } else { // a 128-wide net loaded as the big net
       HIP_TRY(launch_expand_net(d.net[BIG], parents, n, off, children, dl, f ? d.p_nbg.p : nullptr,
                                 f ? d.nbg.p : nullptr, d.p_obg.p, d.obg.p, ctx->swizzle & 1, s));
     }
   }
   HIP_TRY(mark(2));
-  int rc = finalize_all(ctx, d, parents, children, mode, parent_out, child_out, n, total, s, score_parents);
+  int rc = finalize_all(ctx, d, parents, children, mode, parent_out, child_out, n, total, s, score_parents, fused);
   if (rc) return rc;
   HIP_TRY(mark(3));
   return GN_OK;

@@ -99,7 +99,9 @@ static_assert(sizeof(TileDesc) == 192, "TileDesc is 192 bytes");
 // x 16 int32 fc_0 partial sums, pinfo = npos (PSQT value, bucket) pairs (written by the plan),
 // npos = n + the children;
 // otherwise one launch over whole rows.  fin (optional): recorded after the stream launches
-// (before the finish).
+// (before the finish).  finish false (sliced stream): no slice_finish_kernel, out_parent /
+// out_child stay unwritten: the caller's launch_finalize takes the big net's outputs from part
+// and pinfo itself.
 hipError_t launch_plan_stream(const NetDevice &net, const gn_board *parents, size_t n, const uint64_t *offsets,
                               const ChildDelta *deltas, const uint8_t *need_parent, const uint8_t *need_child,
                               int2 *out_parent, int2 *out_child, int swz, const uint8_t *next_slot, int chain_k,
@@ -107,7 +109,7 @@ hipError_t launch_plan_stream(const NetDevice &net, const gn_board *parents, siz
                               uint32_t *pool, uint32_t *err, unsigned long long *rows_out,
                               unsigned long long *pads_out, size_t b0, size_t b1, const uint32_t *order,
                               hipEvent_t mid, hipStream_t s, int slices = 1, int32_t *part = nullptr,
-                              size_t npos = 0, int2 *pinfo = nullptr, hipEvent_t fin = nullptr);
+                              size_t npos = 0, int2 *pinfo = nullptr, hipEvent_t fin = nullptr, bool finish = true);
 // GN_MODE_FULL preparation: need_small = valid && |simple_eval| > threshold,
 // need_big = valid && !need_small.
 hipError_t launch_classify(const gn_board *boards, size_t n, const gn_eval_params &P, uint8_t *need_small,
@@ -121,11 +123,20 @@ hipError_t launch_reeval(const int2 *out_small, const uint8_t *need_small, size_
 // otherwise, which resolve_scores replaces for the in-check ones).
 // owner / moves / unpacked (optional, children only): board i is unpacked[owner[i]] after
 // moves[i] (the parents write_children unpacked), instead of unpacking boards[i].
+// sliced (optional): the column-sliced stream's partial sums of the big net; position i's big-net
+// output is then slice_finish_one of pinfo[qoff + i] (out_big[i] where pinfo.y < 0)
+struct SlicedOut {
+  const NetDevice *net;
+  const int32_t *part;
+  const int2 *pinfo;
+  uint64_t npos, qoff;
+};
 hipError_t launch_finalize(const gn_board *boards, size_t n, int mode, const int2 *out_small,
                            const int2 *out_big, const uint8_t *need_small, const uint8_t *need_big,
                            const gn_eval_params &P, const Tables *tables, gn_eval *out, hipStream_t s,
                            int score, const uint64_t *counts = nullptr, const uint32_t *owner = nullptr,
-                           const uint16_t *moves = nullptr, const Board *unpacked = nullptr);
+                           const uint16_t *moves = nullptr, const Board *unpacked = nullptr,
+                           const SlicedOut *sliced = nullptr);
 // The score rule's in-check positions (include/gpu_nnue.h gn_eval.score): select (sel[n + 1],
 // 1 for a scored position in check with a legal move), gather (idx / boards of the selected,
 // pos = exclusive scan of sel), reduce (max over each selected position's replies

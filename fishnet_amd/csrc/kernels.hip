@@ -744,9 +744,22 @@ __global__ void finalize_kernel(const gn_board *__restrict__ boards, size_t n, i
                                 const uint8_t *__restrict__ need_small, const uint8_t *__restrict__ need_big,
                                 gn_eval_params P, const Tables *__restrict__ tables, gn_eval *__restrict__ out,
                                 const uint32_t *__restrict__ owner, const uint16_t *__restrict__ moves,
-                                const Board *__restrict__ unpacked, int score, const uint64_t *__restrict__ counts) {
+                                const Board *__restrict__ unpacked, int score, const uint64_t *__restrict__ counts,
+                                NetDevice bnet, const int32_t *__restrict__ part, const int2 *__restrict__ pinfo,
+                                uint64_t npos, uint64_t qoff) {
   __shared__ Tables T;
+  // (part: the big net's outputs from the sliced stream's partial sums, slice_finish_one --
+  // its reads then overlap this kernel's arithmetic instead of running as a kernel of their own)
+  __shared__ int4v w1s[8 * 32 * 2];
+  if (part) stage_fc1(w1s, bnet);
   load_tables(T, tables);
+  auto big_out = [&](size_t i) -> int2 {
+    if (part) {
+      const int2 info = pinfo[qoff + i];
+      if (info.y >= 0) return slice_finish_one<GN_PART_SLICES>(bnet, w1s, part, npos, qoff + i, info);
+    }
+    return out_big[i];
+  };
   // a bounded grid striding over the positions: the 4 KiB table load and its barrier once
   // per workgroup and many positions, not once per 256 (480 k workgroups per expansion)
   const size_t stride = (size_t)gridDim.x * blockDim.x;
@@ -767,11 +780,11 @@ __global__ void finalize_kernel(const gn_board *__restrict__ boards, size_t n, i
     if (mode == GN_MODE_SMALL) {
       small = true, o = out_small[i];
     } else if (mode == GN_MODE_BIG) {
-      small = false, o = out_big[i];
+      small = false, o = big_out(i);
     } else if (need_small[i] && !need_big[i]) {
       small = true, o = out_small[i];
     } else {
-      small = false, o = out_big[i];
+      small = false, o = big_out(i);
       if (need_small[i]) flags |= GN_FLAG_REEVAL;
     }
     int32_t nnue = wadd(wmul(P.psqt_weight, o.x), wmul(P.positional_weight, o.y)) / 128;
@@ -934,14 +947,19 @@ hipError_t launch_reeval(const int2 *out_small, const uint8_t *need_small, size_
 hipError_t launch_finalize(const gn_board *boards, size_t n, int mode, const int2 *out_small, const int2 *out_big,
                            const uint8_t *need_small, const uint8_t *need_big, const gn_eval_params &P,
                            const Tables *tables, gn_eval *out, hipStream_t s, int score, const uint64_t *counts,
-                           const uint32_t *owner, const uint16_t *moves, const Board *unpacked) {
+                           const uint32_t *owner, const uint16_t *moves, const Board *unpacked,
+                           const SlicedOut *sliced) {
   if (!n) return hipSuccess;
+  NetDevice bnet = {};
+  if (sliced) bnet = *sliced->net;
   // a bounded grid striding over the positions: each workgroup copies the movegen tables to
   // LDS once (8,192 workgroups: 2.55 -> 2.36 ms per expansion against one per 256 positions)
   constexpr size_t max_blocks = 8192;
   const size_t blocks = std::min<size_t>(blocks_for(n, 256), max_blocks);
   hipLaunchKernelGGL(finalize_kernel, dim3(blocks), dim3(256), 0, s, boards, n, mode, out_small, out_big, need_small,
-                     need_big, P, tables, out, owner, moves, unpacked, score, counts);
+                     need_big, P, tables, out, owner, moves, unpacked, score, counts, bnet,
+                     sliced ? sliced->part : nullptr, sliced ? sliced->pinfo : nullptr, sliced ? sliced->npos : 0,
+                     sliced ? sliced->qoff : 0);
   return hipGetLastError();
 }
 

@@ -1412,60 +1412,20 @@ __global__ void __launch_bounds__(L1 / SL / 8) __attribute__((amdgpu_waves_per_e
 #endif
 }
 
-// The column-sliced stream's finish (a thread per position): the SL slices' fc_0 sums + bias,
-// the activations, fc_1, fc_2 and the outputs -- the whole-row kernel's finishing step in scalar
-// integer arithmetic (exact: every sum is an integer sum, the wrapping adds as there).  pinfo.y
-// < 0: a position the big net does not evaluate (left as it is).
+// The column-sliced stream's finish when finalize does not take it over (a thread per position,
+// slice_finish_one).  pinfo.y < 0: a position the big net does not evaluate (left as it is).
 template <int SL>
 __global__ void __launch_bounds__(256) slice_finish_kernel(NetDevice net, const int32_t *__restrict__ part,
                                                            const int2 *__restrict__ pinfo, uint64_t npos, uint32_t np,
                                                            int2 *__restrict__ out_parent, int2 *__restrict__ out_child) {
-  // the 8 buckets' fc_1 weights (32 outputs x 32 int8, as 8 dwords per output) in LDS
   __shared__ int4v w1s[8 * 32 * 2];
-  for (int i = threadIdx.x; i < 8 * 32 * 2; i += 256) w1s[i] = reinterpret_cast<const int4v *>(net.w1)[i];
+  stage_fc1(w1s, net);
   __syncthreads();
   const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= npos) return;
   const int2 info = pinfo[q];
   if (info.y < 0) return;
-  const int b = info.y & 7;
-  int32_t v[16];
-#pragma unroll
-  for (int r = 0; r < 16; r += 4) {
-    int4v a = *reinterpret_cast<const int4v *>(part + q * 16 + r);
-#pragma unroll
-    for (int t = 1; t < GN_PART_N; ++t) { // (in place: the last slice's sums are the totals)
-      const int4v c = *reinterpret_cast<const int4v *>(part + ((uint64_t)t * npos + q) * 16 + r);
-#pragma unroll
-      for (int k = 0; k < 4; ++k) a[k] = wadd(a[k], c[k]);
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) v[r + k] = wadd(a[k], net.b0[b * 16 + r + k]);
-  }
-  // fc_1's 32 inputs as int8 packed 4 per dword: 15 squared, 15 clipped, 2 zero
-  uint32_t x[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#pragma unroll
-  for (int r = 0; r < 15; ++r) {
-    const long long s2 = ((long long)v[r] * v[r]) >> 19;
-    const uint32_t a = s2 < 127 ? (uint32_t)s2 : 127u, c = (uint32_t)clampi(v[r] >> 6, 0, 127);
-    x[r >> 2] |= a << (8 * (r & 3));
-    x[(15 + r) >> 2] |= c << (8 * ((15 + r) & 3));
-  }
-  const int32_t fwd = wmul(v[15], 600 * 16) / (127 * 64);
-  int32_t sum = 0;
-#pragma unroll 4
-  for (int o = 0; o < 32; ++o) {
-    const int4v wa = w1s[(b * 32 + o) * 2], wb = w1s[(b * 32 + o) * 2 + 1];
-    int32_t acc = 0;
-#pragma unroll
-    for (int d = 0; d < 4; ++d) acc = __builtin_amdgcn_sdot4((int)x[d], wa[d], acc, false);
-#pragma unroll
-    for (int d = 0; d < 4; ++d) acc = __builtin_amdgcn_sdot4((int)x[4 + d], wb[d], acc, false);
-    const int32_t l = clampi(wadd(acc, net.b1[b * 32 + o]) >> 6, 0, 127);
-    sum = wadd(sum, (int32_t)net.w2[b * 32 + o] * l);
-  }
-  const int32_t positional = wadd(wadd(net.b2[b], sum), fwd);
-  const int2 val = make_int2(info.x / 16, positional / 16);
+  const int2 val = slice_finish_one<GN_PART_N>(net, w1s, part, npos, q, info);
   if (q < np) out_parent[q] = val;
   else out_child[q - np] = val;
 }
@@ -1477,7 +1437,7 @@ hipError_t launch_plan_stream(const NetDevice &net, const gn_board *parents, siz
                               uint32_t *pool, uint32_t *err, unsigned long long *rows_out,
                               unsigned long long *pads_out, size_t b0, size_t b1, const uint32_t *order,
                               hipEvent_t mid, hipStream_t s, int slices, int32_t *part, size_t npos,
-                              int2 *pinfo, hipEvent_t fin) {
+                              int2 *pinfo, hipEvent_t fin, bool finish) {
   if (!n || b1 <= b0) return hipSuccess;
   if (n >= 0x80000000ull) return hipErrorInvalidValue; // 32-bit parent indices in the kernels
   const uint32_t K = chain_k > 1 && next_slot ? (uint32_t)chain_k : 1u;
@@ -1502,8 +1462,9 @@ hipError_t launch_plan_stream(const NetDevice &net, const gn_board *parents, siz
                            B1, swz, eoff, ent, tiles, btiles, order, out_parent, out_child, pool, scr, err,
                            pool + 64 + 8 * sl, sl, part, (uint64_t)npos, pinfo);
       if (fin) (void)hipEventRecord(fin, s);
-      hipLaunchKernelGGL((slice_finish_kernel<3>), dim3((unsigned)((npos + 255) / 256)), dim3(256), 0, s, net, part,
-                         pinfo, (uint64_t)npos, (uint32_t)n, out_parent, out_child);
+      if (finish) // (otherwise the caller's finalize takes the outputs from part itself)
+        hipLaunchKernelGGL((slice_finish_kernel<3>), dim3((unsigned)((npos + 255) / 256)), dim3(256), 0, s, net, part,
+                           pinfo, (uint64_t)npos, (uint32_t)n, out_parent, out_child);
     } else {
       hipLaunchKernelGGL((stream_eval_kernel<3072>), dim3(g), dim3(384), 0, s, net, offsets, (uint32_t)n, K, B0, B1,
                          swz, eoff, ent, tiles, btiles, order, out_parent, out_child, pool, scr, err, pool + 64, 0,
