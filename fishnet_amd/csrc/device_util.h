@@ -308,23 +308,28 @@ __device__ __forceinline__ int32_t wave_sum_dpp(int32_t v) {
 __device__ __forceinline__ void stage_fc1(int4v *w1s, const NetDevice &net) {
   for (int i = threadIdx.x; i < 8 * 32 * 2; i += blockDim.x) w1s[i] = reinterpret_cast<const int4v *>(net.w1)[i];
 }
+// a position's fc_0 sums over the NPART slices (sums[k]: outputs 4k .. 4k + 3, bias not added),
+// read by its own lane (wrapping int32 adds, as the LDS atomics)
 template <int NPART>
-__device__ __forceinline__ int2 slice_finish_one(const NetDevice &net, const int4v *w1s, const int32_t *__restrict__ part,
-                                                 uint64_t npos, uint64_t q, int2 info) {
+__device__ __forceinline__ void slice_sums(const int32_t *__restrict__ part, uint64_t npos, uint64_t q, int4v (&sums)[4]) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    sums[r] = *reinterpret_cast<const int4v *>(part + q * 16 + 4 * r);
+#pragma unroll
+    for (int t = 1; t < NPART; ++t) { // (one array: the last slice's sums are the totals)
+      const int4v c = *reinterpret_cast<const int4v *>(part + ((uint64_t)t * npos + q) * 16 + 4 * r);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) sums[r][k] = wadd(sums[r][k], c[k]);
+    }
+  }
+}
+// ... and the finishing step from them
+__device__ __forceinline__ int2 slice_finish_from(const NetDevice &net, const int4v *w1s, const int4v (&sums)[4],
+                                                  int2 info) {
   const int b = info.y & 7;
   int32_t v[16];
 #pragma unroll
-  for (int r = 0; r < 16; r += 4) {
-    int4v a = *reinterpret_cast<const int4v *>(part + q * 16 + r);
-#pragma unroll
-    for (int t = 1; t < NPART; ++t) { // (one array: the last slice's sums are the totals)
-      const int4v c = *reinterpret_cast<const int4v *>(part + ((uint64_t)t * npos + q) * 16 + r);
-#pragma unroll
-      for (int k = 0; k < 4; ++k) a[k] = wadd(a[k], c[k]);
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) v[r + k] = wadd(a[k], net.b0[b * 16 + r + k]);
-  }
+  for (int r = 0; r < 16; ++r) v[r] = wadd(sums[r >> 2][r & 3], net.b0[b * 16 + r]);
   // fc_1's 32 inputs as int8 packed 4 per dword: 15 squared, 15 clipped, 2 zero
   uint32_t x[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
@@ -349,6 +354,13 @@ __device__ __forceinline__ int2 slice_finish_one(const NetDevice &net, const int
   }
   const int32_t positional = wadd(wadd(net.b2[b], sum), fwd);
   return make_int2(info.x / 16, positional / 16);
+}
+template <int NPART>
+__device__ __forceinline__ int2 slice_finish_one(const NetDevice &net, const int4v *w1s, const int32_t *__restrict__ part,
+                                                 uint64_t npos, uint64_t q, int2 info) {
+  int4v sums[4];
+  slice_sums<NPART>(part, npos, q, sums);
+  return slice_finish_from(net, w1s, sums, info);
 }
 
 } // namespace gn

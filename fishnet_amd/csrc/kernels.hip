@@ -753,21 +753,40 @@ __global__ void finalize_kernel(const gn_board *__restrict__ boards, size_t n, i
   __shared__ int4v w1s[8 * 32 * 2];
   if (part) stage_fc1(w1s, bnet);
   load_tables(T, tables);
-  auto big_out = [&](size_t i) -> int2 {
-    if (part) {
-      const int2 info = pinfo[qoff + i];
-      if (info.y >= 0) return slice_finish_one<GN_PART_SLICES>(bnet, w1s, part, npos, qoff + i, info);
-    }
-    return out_big[i];
-  };
   // a bounded grid striding over the positions: the 4 KiB table load and its barrier once
   // per workgroup and many positions, not once per 256 (480 k workgroups per expansion)
   const size_t stride = (size_t)gridDim.x * blockDim.x;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+#ifdef GN_AB_FIN_LATE_SUMS // A/B: the sums loaded where the output is needed (after the board)
+    auto big_out = [&](size_t j) -> int2 {
+      if (part) {
+        const int2 info = pinfo[qoff + j];
+        if (info.y >= 0) return slice_finish_one<GN_PART_SLICES>(bnet, w1s, part, npos, qoff + j, info);
+      }
+      return out_big[j];
+    };
+    const uint32_t ow = unpacked ? owner[i] : 0u;
+    const uint16_t mv = unpacked ? moves[i] : (uint16_t)0;
+#else
+    // the owner and move, then (part) the position's slice sums, all loaded before anything waits:
+    // the sums' HBM round trip runs beside the owner -> parent board chain instead of after the
+    // board work (owner, parent, pinfo, sums were three round trips in a row)
+    const uint32_t ow = unpacked ? owner[i] : 0u;
+    const uint16_t mv = unpacked ? moves[i] : (uint16_t)0;
+    int2 info = make_int2(0, -1);
+    int4v sums[4];
+    if (part) {
+      info = pinfo[qoff + i];
+      slice_sums<GN_PART_SLICES>(part, npos, qoff + i, sums);
+    }
+    auto big_out = [&](size_t j) -> int2 {
+      return part && info.y >= 0 ? slice_finish_from(bnet, w1s, sums, info) : out_big[j];
+    };
+#endif
     Board B;
     gn_eval e = {0, 0, 0, 0, 0, 0, 0};
     if (unpacked) {
-      B = do_move(unpacked[owner[i]], moves[i], nullptr); // a legal child of a valid parent
+      B = do_move(unpacked[ow], mv, nullptr); // a legal child of a valid parent
     } else if (!unpack(boards[i], B)) {
       e.flags = GN_FLAG_BAD_FEN | GN_FLAG_NO_SCORE;
       out[i] = e;
