@@ -132,7 +132,9 @@ extern "C" {
                                          stack; all its launches: three column slices by
                                          default), the expansion's dominant kernel ...   */
 #define GN_STAT_FINISH_NS 104         /* ... and the column-sliced stream's layer-stack
-                                         finish (slice_finish_kernel; 0 with one launch) */
+                                         finish (slice_finish_kernel; ~0 by default, where
+                                         finalize computes each output itself, and with
+                                         one launch)                                       */
 #define GN_STAT_SCRATCH_PADS 103      /* no-op entries the last planned expansion inserted
                                          (per device, summed) so that every king-cache load
                                          sits >= ring depth (4) list entries after the
