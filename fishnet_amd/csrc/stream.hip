@@ -993,7 +993,8 @@ __global__ void __launch_bounds__(L1 / SL / 8) __attribute__((amdgpu_waves_per_e
     // the accumulator, or (PRE) 0 / the parent / the sibling base at a slot's first entry
     // (wrapping int16, as the accumulators)
     const unsigned short sg = (unsigned short)h;
-#ifndef GN_PRE_MAD // (GN_PRE_MAD: one multiply-add per source, below: 11 VGPRs spilled with the revolution loop)
+    // (the source copied first, then one multiply-add: a multiply-add per source, with no copy,
+    // spilled 11 VGPRs in the sliced stream's revolution loop)
     if (h & H_PRE) {
       const uint32_t init = (h >> H_INIT_SH) & 3;
       asm volatile("");
@@ -1006,27 +1007,6 @@ __global__ void __launch_bounds__(L1 / SL / 8) __attribute__((amdgpu_waves_per_e
       asm volatile("");
       base_lo = lo, base_hi = hi;
     }
-#else
-    // each source has its own multiply-add (no copy of the source first; the copies and the
-    // merged paths cost ~10 scalar instructions and 4 branches per PRE entry)
-    if (!(h & H_PRE)) {
-      lo = rlo[r] * sg + lo, hi = rhi[r] * sg + hi;
-    } else {
-      const uint32_t init = (h >> H_INIT_SH) & 3;
-      asm volatile("");
-      if (init == 2) {
-        lo = rlo[r] * sg + pacc_lo, hi = rhi[r] * sg + pacc_hi;
-        asm volatile("");
-        base_lo = lo, base_hi = hi;
-      } else if (init == 3) {
-        asm volatile("");
-        lo = rlo[r] * sg + base_lo, hi = rhi[r] * sg + base_hi;
-      } else {
-        asm volatile("");
-        lo = rlo[r] * sg, hi = rhi[r] * sg;
-      }
-    }
-#endif
     if (h & H_LAST) {
       const int sl = (h >> H_SLOT_SH) & 15, side = (h >> H_SIDE_SH) & 1;
 #ifdef GN_AB_NO_TRANSFORM // timing diagnostics only (wrong results): the accumulator's low bytes, untransformed
