@@ -248,7 +248,7 @@ def run_eval(c: Ctx, wl: dict, n: int, steps: int, warmup: int, max_plies: int, 
     return r
 
 
-def run_expand(c: Ctx, wl: dict, games: int, steps: int, warmup: int, check: int):
+def run_expand(c: Ctx, wl: dict, games: int, steps: int, warmup: int, check: int, gather: bool | None = None):
     """Games x 81 parents, every legal child, incremental evaluation; verifies the timed outputs."""
     G, nn, mode = c.G, c.nn, wl["mode"]
     n = games * (PLIES + 1)
@@ -334,7 +334,7 @@ def run_expand(c: Ctx, wl: dict, games: int, steps: int, warmup: int, check: int
                                 "checksum_plain": f"{ref[0] ^ ref[1]:016x}",
                                 "plain_path": "GN_OPT_CHAIN=1, GN_OPT_KING_CACHE=0 (refresh-started parents)"}
         r["oracle_check"] = ver
-    if c.world > 1:
+    if c.world > 1 if gather is None else gather:  # (gather=True: also at N = 1, tests)
         r["gather"] = gather_results(c, out, n, children, games, mode, check)
     for b in ("po", "off", "mv", "co"):
         out[b].free()

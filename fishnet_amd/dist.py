@@ -8,18 +8,22 @@ import os
 
 
 class ShardComm:
-    def __init__(self, backend: str | None = None):
+    """collectives: run the torch.distributed collectives (default: only when world > 1; True
+    at world 1 drives a one-rank RCCL group through the same calls, tests/test_bench_gpu.py)."""
+
+    def __init__(self, backend: str | None = None, collectives: bool | None = None):
         import torch
         import torch.distributed as dist
         self.torch, self.dist = torch, dist
         self.rank = int(os.environ.get("RANK", "0"))
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.coll = self.world > 1 if collectives is None else collectives
         self.backend = backend or ("nccl" if torch.cuda.is_available() else "gloo")
         self.device = torch.device("cuda", self.local) if self.backend == "nccl" else torch.device("cpu")
         if self.backend == "nccl":
             torch.cuda.set_device(self.local)
-        if self.world > 1 and not dist.is_initialized():
+        if self.coll and not dist.is_initialized():
             kw = {"device_id": self.device} if self.backend == "nccl" else {}
             dist.init_process_group(self.backend, **kw)
 
@@ -40,7 +44,7 @@ class ShardComm:
 
     # ---- collectives ---------------------------------------------------------
     def broadcast_bytes(self, data: bytes, src: int = 0) -> bytes:
-        if self.world == 1:
+        if not self.coll:
             return data
         torch, dist = self.torch, self.dist
         ln = torch.tensor([len(data)], dtype=torch.int64, device=self.device)
@@ -53,25 +57,25 @@ class ShardComm:
         return t.cpu().numpy().tobytes()
 
     def broadcast_obj(self, obj, src: int = 0):
-        if self.world == 1:
+        if not self.coll:
             return obj
         lst = [obj]
         self.dist.broadcast_object_list(lst, src)
         return lst[0]
 
     def barrier(self):
-        if self.world > 1:
+        if self.coll:
             self.dist.barrier()
 
     def max(self, x: float) -> float:
-        if self.world == 1:
+        if not self.coll:
             return x
         t = self.torch.tensor([x], dtype=self.torch.float64, device=self.device)
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
         return float(t.item())
 
     def gather_i64(self, x: int) -> list[int]:
-        if self.world == 1:
+        if not self.coll:
             return [x]
         t = self.torch.tensor([x & 0x7FFFFFFFFFFFFFFF], dtype=self.torch.int64, device=self.device)
         lst = [self.torch.zeros_like(t) for _ in range(self.world)]
@@ -82,7 +86,7 @@ class ShardComm:
         """Gathers numpy arrays of one dtype (e.g. gn_eval records; lengths may differ per
         rank) to dst: the list of every rank's array on dst, None elsewhere."""
         import numpy as np
-        if self.world == 1:
+        if not self.coll:
             return [arr]
         torch, dist = self.torch, self.dist
         data = np.ascontiguousarray(arr).tobytes()
@@ -107,7 +111,7 @@ class ShardComm:
         """Gathers a 1-D tensor (device tensors over RCCL, CPU tensors over gloo; the length may
         differ per rank) to dst: dst gets the list of every rank's tensor, the others None.
         This is the result gather of DESIGN.md section 6 (gn_eval records, moves, offsets)."""
-        if self.world == 1:
+        if not self.coll:
             return [t]
         torch, dist = self.torch, self.dist
         sizes = self.gather_i64(int(t.numel()))
@@ -123,6 +127,6 @@ class ShardComm:
         return None if outs is None else [o[:n] for o, n in zip(outs, sizes)]
 
     def close(self):
-        if self.world > 1 and self.dist.is_initialized():
+        if self.coll and self.dist.is_initialized():
             self.dist.barrier()
             self.dist.destroy_process_group()

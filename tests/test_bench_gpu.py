@@ -8,6 +8,8 @@ under RCCL).  torch is imported first, as bench.py does, so that its HIP runtime
 libgpu_nnue binds to."""
 import argparse
 import copy
+import json
+import os
 
 import numpy as np
 import torch  # (before libgpu_nnue, as in bench.py)
@@ -103,3 +105,46 @@ def test_evaluate_device_blocks_until_written(gpu_ctx):
     gpu_ctx.evaluate_device(d_b, len(boards), G.MODE_FULL, d_o, stream=s.cuda_stream)
     assert s.query()
     assert np.array_equal(d_o.download(G.EVAL_DTYPE, len(boards)), ref)
+
+
+_ONE_RANK = r"""
+import argparse, json, sys
+import torch
+sys.path.insert(0, sys.argv[1])
+import bench
+from fishnet_amd.dist import ShardComm
+comm = ShardComm("nccl", collectives=True)  # a one-rank RCCL group, every collective real
+c = bench.Ctx(argparse.Namespace(swizzle=-1, king_sort=-1, chain=None, king_cache=None), comm=comm)
+r = bench.run_expand(c, bench.WORKLOADS["expand"], 48, 1, 0, 8, gather=True)
+print(json.dumps({"oracle": r["oracle_check"]["oracle"]["mismatching_parents"],
+                  "plain": r["oracle_check"]["vs_plain_path"]["equal"], "gather": r["gather"]}))
+c.nn.close()
+comm.close()
+"""
+
+
+def test_rccl_result_gather_one_rank(tmp_path):
+    """The result gather's RCCL transport on the GPU (it had never executed): one rank
+    in a "nccl" process group with its collectives on (ShardComm(collectives=True)), so the
+    nets' broadcast, the length all_gather and the records' torch.distributed.gather all run
+    through RCCL on device memory; rank 0 then checks sampled parents of the gathered records,
+    with all their children, against the oracle.  In a child process: the process group must
+    not outlive the test."""
+    import socket
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    script = tmp_path / "one_rank.py"
+    script.write_text(_ONE_RANK)
+    p = subprocess.run([sys.executable, str(script), root], env=env, capture_output=True, text=True, timeout=110)
+    assert p.returncode == 0, p.stderr[-3000:]
+    d = json.loads(p.stdout.strip().splitlines()[-1])
+    assert d["oracle"] == 0 and d["plain"]
+    g = d["gather"]
+    assert g["oracle_check"]["ranks"] == 1 and g["oracle_check"]["mismatching_parents"] == 0
+    assert g["oracle_check"]["parents"] == 32 and g["bytes_all_ranks"] > 0
