@@ -319,7 +319,8 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR) __attribute__((amdgpu_wav
           for (int i = 0; i < D; ++i) ps += (uint32_t)pt[ft_row(rr[k + i])];
         }
 #pragma unroll
-        for (int i = 0; i < D; i += 2) lo += a[i] + a[i + 1], hi += b[i] + b[i + 1];
+        for (int i = 0; i + 1 < D; i += 2) lo += a[i] + a[i + 1], hi += b[i] + b[i + 1];
+        if constexpr (D % 2) lo += a[D - 1], hi += b[D - 1]; // (an odd depth's last row)
       }
       if (k < cnt) { // tail of 1 .. D - 1 rows (indices past the end repeat row k, not added)
         ushort8 a[D - 1], b[D - 1];
