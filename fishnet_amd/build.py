@@ -74,6 +74,31 @@ def build(force: bool = False, verbose: bool = False, defines=(), out: str | Non
     return lib
 
 
+def build_rev(rev: str, out: str, defines=()) -> str:
+    """A/B baseline: the library as of git revision `rev` (its csrc/ and include/ extracted into a
+    temporary tree), into lib/<out>.  Used on the CPU before an A/B run; never by the product."""
+    import shutil
+    import tempfile
+    tmp = tempfile.mkdtemp(prefix="gn_rev_")
+    try:
+        arch = subprocess.run(["git", "-C", ROOT, "archive", rev, "fishnet_amd/csrc", "include"],
+                              check=True, capture_output=True).stdout
+        subprocess.run(["tar", "-x", "-C", tmp], input=arch, check=True)
+        objs = []
+        for src in SOURCES:
+            obj = os.path.join(tmp, src.replace(".hip", ".o"))
+            subprocess.run(["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden",
+                            "-w", *defines, "-c", os.path.join(tmp, "fishnet_amd", "csrc", src), "-o", obj],
+                           check=True)
+            objs.append(obj)
+        lib = os.path.join(LIBDIR, out)
+        subprocess.run(["hipcc", f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib] + objs + ["-lpthread"],
+                       check=True)
+        return lib
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
 def build_fault(force: bool = False, verbose: bool = False) -> str:
     """The fault-injection library (never loaded by the product path or the bench)."""
     return build(force=force, verbose=verbose, defines=FAULT_DEFINES, out=FAULT_LIB)
@@ -82,5 +107,9 @@ def build_fault(force: bool = False, verbose: bool = False) -> str:
 if __name__ == "__main__":
     defs = [a for a in sys.argv[1:] if a.startswith("-D")]
     outs = [a[len("--out="):] for a in sys.argv[1:] if a.startswith("--out=")]
+    revs = [a[len("--rev="):] for a in sys.argv[1:] if a.startswith("--rev=")]
+    if revs:
+        print(build_rev(revs[0], outs[0] if outs else f"libgpu_nnue_{revs[0]}.so", defines=defs))
+        sys.exit(0)
     print(build(force="--force" in sys.argv, verbose=True, defines=defs,
                 out=os.path.join(LIBDIR, outs[0]) if outs else None))

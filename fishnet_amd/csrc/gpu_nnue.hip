@@ -10,6 +10,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <memory>
@@ -185,6 +186,52 @@ struct DevBuf {
   }
 };
 
+// The net outputs / selections of one evaluation (evaluate_on)
+struct EvalBufs {
+  DevBuf<int2> osm, obg;
+  DevBuf<uint8_t> nsm, nbg;
+  void release() { osm.release(), obg.release(), nsm.release(), nbg.release(); }
+};
+
+// ---- the drop-in's small batches ------------------------------------
+// fishnet's GPU backend sends one game per gn_evaluate_batch (/root/reference/src/stockfish.rs:
+// 36-47, src/main.rs:306-338: a chunk per worker call), ~80 positions, a few of them in check.
+// The general path costs ~20 launches and three host round trips per call (the score rule's
+// reply counts); on a one-device context a batch of <= 4,096 positions runs instead as one
+// captured HIP graph per (size class, mode): upload from pinned memory, the evaluation, both
+// levels of the in-check replies (reply_level_kernel: one workgroup selects, counts, scans and
+// makes a level's replies; every launch after it is sized by the level's capacity, its unused
+// slots empty boards, so nothing waits for a count), the two reductions, and the download of
+// the records with the overflow flag behind them.  One synchronisation per call.  A level with
+// more replies than its capacity (2 nb + 256, nb + 256: far beyond a game's) sets the flag and
+// the call reruns on the general path.  Positions beyond n are empty boards (BAD_FEN records,
+// never read back).
+constexpr size_t FAST_NB0 = 128, FAST_MAX = 4096;
+struct FastBatch {
+  size_t nb = 0, c1 = 0, c2 = 0;
+  int mode = -1;
+  uint64_t gen = 0;
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t exec = nullptr;
+  gn_board *h_in = nullptr; // pinned: nb boards
+  gn_eval *h_out = nullptr; // pinned: nb records + one holding the overflow flag
+  DevBuf<gn_board> in, r1, r2;
+  DevBuf<gn_eval> out, e1, e2;
+  DevBuf<uint64_t> off0, off1;
+  DevBuf<uint16_t> m1, m2;
+  DevBuf<int32_t> sv1, sv2;
+  EvalBufs eb;
+  ~FastBatch() {
+    if (exec) (void)hipGraphExecDestroy(exec);
+    if (graph) (void)hipGraphDestroy(graph);
+    if (h_in) (void)hipHostFree(h_in);
+    if (h_out) (void)hipHostFree(h_out);
+    in.release(), r1.release(), r2.release(), out.release(), e1.release(), e2.release();
+    off0.release(), off1.release(), m1.release(), m2.release(), sv1.release(), sv2.release();
+    eb.release();
+  }
+};
+
 struct Dev {
   int id = 0;
   hipStream_t stream = nullptr;
@@ -192,8 +239,9 @@ struct Dev {
   NetDevice net[2] = {};
   bool has[2] = {false, false};
   Tables *tables = nullptr;
-  DevBuf<int2> osm, obg;
-  DevBuf<uint8_t> nsm, nbg;
+  EvalBufs eb; // evaluate_on's outputs
+  DevBuf<int2> &osm = eb.osm, &obg = eb.obg;
+  DevBuf<uint8_t> &nsm = eb.nsm, &nbg = eb.nbg;
   DevBuf<gn_board> io_boards, frontier[2];
   DevBuf<gn_eval> io_out, io_out2;
   DevBuf<uint64_t> counts, offsets;
@@ -264,6 +312,8 @@ struct Dev {
   DevBuf<uint32_t> gidx;
   // stage times of the last host-buffer call on this device (GN_STAT_HOST_*), ms
   double t_upload = 0, t_replay = 0, t_compute = 0, t_download = 0, t_tail = 0;
+  // the drop-in's small-batch graphs (FastBatch): one per size class (128 << k positions) and mode
+  std::unique_ptr<FastBatch> fast[6][3];
   std::mutex mu;
 };
 
@@ -328,6 +378,10 @@ struct gn_ctx {
     uint64_t launches = 0, calls = 0;
   } co;
   bool coalesce = true;
+  bool fast_batch = true;                  // GN_OPT_FAST_BATCH
+  std::atomic<uint64_t> graph_gen{0};      // bumped by every option / parameter change: the small-
+                                           // batch graphs captured before it are rebuilt
+  std::atomic<uint64_t> fast_runs{0}, fast_fallbacks{0};
   gn_eval_params P;
   bool incremental = true; // GN_OPT_INCREMENTAL_CHILDREN
   int swizzle = 9;          // GN_OPT_XCD_SWIZZLE bit mask: 1 small-net expansion, 2 batch evaluation,
@@ -445,6 +499,8 @@ static void destroy(gn_ctx *ctx) {
     d.pstat.release();
     d.bkeys.release(), d.bkeys2.release(), d.bidx.release(), d.border.release();
     d.lv[0].release(), d.lv[1].release();
+    for (auto &row : d.fast)
+      for (auto &f : row) f.reset();
     for (int i = 0; i < 2; ++i) {
       d.po2[i].release(), d.co2[i].release(), d.cc2[i].release(), d.mv2[i].release();
       if (d.cev[i]) (void)hipEventDestroy(d.cev[i]);
@@ -536,28 +592,33 @@ struct KernelTimes {
 // the stages [classify(+)] [small net (+reeval)] [big net] [finalize].
 // score: the records are positions (the score rule's static part; resolve_scores does the
 // in-check ones) rather than child records; counts (optional): their legal-move counts.
+// eb (optional): the net outputs and selections in these buffers instead of the device's (the
+// drop-in's captured small-batch graphs own theirs, FastBatch); sort false: no king sort.
 static int evaluate_on(gn_ctx *ctx, Dev &d, const gn_board *b, size_t n, int mode, gn_eval *out, hipStream_t s,
                        hipEvent_t *ev, unsigned long long *rows_out = nullptr, int score = 1,
-                       const uint64_t *counts = nullptr) {
+                       const uint64_t *counts = nullptr, EvalBufs *eb = nullptr, bool sort = true) {
   if (mode < GN_MODE_FULL || mode > GN_MODE_SMALL) return fail(GN_E_INVALID, "bad mode %d", mode);
   if ((mode != GN_MODE_SMALL && !d.has[BIG]) || (mode != GN_MODE_BIG && !d.has[SMALL]))
     return fail(GN_E_NONET, "mode %d needs a network that is not loaded", mode);
   if (!n) return GN_OK;
-  if (mode != GN_MODE_BIG) HIP_TRY(d.osm.ensure(n));
-  if (mode != GN_MODE_SMALL) HIP_TRY(d.obg.ensure(n));
+  EvalBufs &B = eb ? *eb : d.eb;
+  DevBuf<int2> &osm = B.osm, &obg = B.obg;
+  DevBuf<uint8_t> &nsm = B.nsm, &nbg = B.nbg;
+  if (mode != GN_MODE_BIG) HIP_TRY(osm.ensure(n));
+  if (mode != GN_MODE_SMALL) HIP_TRY(obg.ensure(n));
   if (mode == GN_MODE_FULL) {
-    HIP_TRY(d.nsm.ensure(n));
-    HIP_TRY(d.nbg.ensure(n));
+    HIP_TRY(nsm.ensure(n));
+    HIP_TRY(nbg.ensure(n));
   }
   auto mark = [&](int k) -> hipError_t { return ev ? hipEventRecord(ev[k], s) : hipSuccess; };
   const gn_eval_params &P = ctx->P;
   HIP_TRY(mark(0));
-  if (mode == GN_MODE_FULL) HIP_TRY(launch_classify(b, n, P, d.nsm.p, d.nbg.p, s));
+  if (mode == GN_MODE_FULL) HIP_TRY(launch_classify(b, n, P, nsm.p, nbg.p, s));
   const uint32_t *perm = nullptr;
   // a small batch (one game, a handful of in-check replies) gains nothing from the order and
   // would pay the sort's launches on its latency (bench.py secondary.dropin)
   constexpr size_t KING_SORT_MIN = 1024;
-  if (ctx->king_sort == 2 || (ctx->king_sort == 1 && n >= KING_SORT_MIN)) {
+  if (sort && (ctx->king_sort == 2 || (ctx->king_sort == 1 && n >= KING_SORT_MIN))) {
     if (n > 0x7FFFFFFFull) return fail(GN_E_INVALID, "king sort supports < 2^31 positions per call");
     HIP_TRY(d.kkeys.ensure(n));
     HIP_TRY(d.kkeys2.ensure(n));
@@ -570,15 +631,15 @@ static int evaluate_on(gn_ctx *ctx, Dev &d, const gn_board *b, size_t n, int mod
   const int swz = (ctx->swizzle >> 1) & 1;
   HIP_TRY(mark(1));
   if (mode != GN_MODE_BIG)
-    HIP_TRY(launch_eval_net(d.net[SMALL], b, mode == GN_MODE_FULL ? d.nsm.p : nullptr, n, d.osm.p, perm, swz, s,
+    HIP_TRY(launch_eval_net(d.net[SMALL], b, mode == GN_MODE_FULL ? nsm.p : nullptr, n, osm.p, perm, swz, s,
                             mode == GN_MODE_SMALL ? rows_out : nullptr));
-  if (mode == GN_MODE_FULL) HIP_TRY(launch_reeval(d.osm.p, d.nsm.p, n, P, d.nbg.p, s));
+  if (mode == GN_MODE_FULL) HIP_TRY(launch_reeval(osm.p, nsm.p, n, P, nbg.p, s));
   HIP_TRY(mark(2));
   if (mode != GN_MODE_SMALL)
-    HIP_TRY(launch_eval_net(d.net[BIG], b, mode == GN_MODE_FULL ? d.nbg.p : nullptr, n, d.obg.p, perm, swz, s,
+    HIP_TRY(launch_eval_net(d.net[BIG], b, mode == GN_MODE_FULL ? nbg.p : nullptr, n, obg.p, perm, swz, s,
                             rows_out));
   HIP_TRY(mark(3));
-  HIP_TRY(launch_finalize(b, n, mode, d.osm.p, d.obg.p, d.nsm.p, d.nbg.p, P, d.tables, out, s, score, counts));
+  HIP_TRY(launch_finalize(b, n, mode, osm.p, obg.p, nsm.p, nbg.p, P, d.tables, out, s, score, counts));
   HIP_TRY(mark(4));
   return GN_OK;
 }
@@ -947,9 +1008,112 @@ static int for_each_device(gn_ctx *ctx, F &&f) {
   return GN_OK;
 }
 
+// A FastBatch for nb positions in mode: buffers, pinned staging, the captured graph (d.mu held).
+static int fast_build(gn_ctx *ctx, Dev &d, FastBatch &f, size_t nb, int mode) {
+  f.nb = nb, f.c1 = 2 * nb + 256, f.c2 = nb + 256, f.mode = mode, f.gen = ctx->graph_gen.load();
+  const size_t ne = std::max(nb, f.c1);
+  HIP_TRY(hipHostMalloc((void **)&f.h_in, nb * sizeof(gn_board), hipHostMallocDefault));
+  HIP_TRY(hipHostMalloc((void **)&f.h_out, (nb + 1) * sizeof(gn_eval), hipHostMallocDefault));
+  HIP_TRY(f.in.ensure(nb));
+  HIP_TRY(f.out.ensure(nb + 1));
+  HIP_TRY(f.r1.ensure(f.c1));
+  HIP_TRY(f.e1.ensure(f.c1));
+  HIP_TRY(f.m1.ensure(f.c1));
+  HIP_TRY(f.sv1.ensure(f.c1));
+  HIP_TRY(f.r2.ensure(f.c2));
+  HIP_TRY(f.e2.ensure(f.c2));
+  HIP_TRY(f.m2.ensure(f.c2));
+  HIP_TRY(f.sv2.ensure(f.c2));
+  HIP_TRY(f.off0.ensure(nb + 1));
+  HIP_TRY(f.off1.ensure(f.c1 + 1));
+  HIP_TRY(f.eb.osm.ensure(ne));
+  HIP_TRY(f.eb.obg.ensure(ne));
+  HIP_TRY(f.eb.nsm.ensure(ne));
+  HIP_TRY(f.eb.nbg.ensure(ne));
+  const hipStream_t s = d.stream;
+  uint32_t *flag = reinterpret_cast<uint32_t *>(f.out.p + nb);
+  HIP_TRY(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+  auto seq = [&]() -> int {
+    HIP_TRY(hipMemcpyAsync(f.in.p, f.h_in, nb * sizeof(gn_board), hipMemcpyHostToDevice, s));
+    int rc = evaluate_on(ctx, d, f.in.p, nb, mode, f.out.p, s, nullptr, nullptr, 1, nullptr, &f.eb, false);
+    if (rc) return rc;
+    // level 1: the replies of the in-check positions; level 2: those of the replies in check
+    HIP_TRY(launch_reply_level(f.in.p, f.out.p, nb, d.tables, f.off0.p, f.c1, f.r1.p, f.m1.p, flag, 1, s));
+    if ((rc = evaluate_on(ctx, d, f.r1.p, f.c1, mode, f.e1.p, s, nullptr, nullptr, 1, nullptr, &f.eb, false))) return rc;
+    HIP_TRY(launch_reply_level(f.r1.p, f.e1.p, f.c1, d.tables, f.off1.p, f.c2, f.r2.p, f.m2.p, flag, 0, s));
+    if ((rc = evaluate_on(ctx, d, f.r2.p, f.c2, mode, f.e2.p, s, nullptr, nullptr, 1, nullptr, &f.eb, false))) return rc;
+    HIP_TRY(launch_score_reduce(f.r1.p, f.c1, nullptr, f.off1.p, f.m2.p, f.e2.p, f.sv2.p, ctx->P, f.e1.p, f.sv1.p, s));
+    HIP_TRY(launch_score_reduce(f.in.p, nb, nullptr, f.off0.p, f.m1.p, f.e1.p, f.sv1.p, ctx->P, f.out.p, nullptr, s));
+    HIP_TRY(hipMemcpyAsync(f.h_out, f.out.p, (nb + 1) * sizeof(gn_eval), hipMemcpyDeviceToHost, s));
+    return GN_OK;
+  };
+  const int rc = seq();
+  hipGraph_t g = nullptr;
+  const hipError_t ec = hipStreamEndCapture(s, &g);
+  if (rc) {
+    if (g) (void)hipGraphDestroy(g);
+    return rc;
+  }
+  HIP_TRY(ec);
+  f.graph = g;
+  HIP_TRY(hipGraphInstantiate(&f.exec, f.graph, nullptr, nullptr, 0));
+  return GN_OK;
+}
+
+// One small batch through its graph (one device, d.mu held).  *done = false: a reply level
+// overflowed and nothing was written (the caller runs the general path).
+static int fast_run(gn_ctx *ctx, Dev &d, const gn_board *boards, size_t n, int mode, gn_eval *out, bool *done) {
+  *done = false;
+  size_t nb = FAST_NB0;
+  int k = 0;
+  while (nb < n) nb <<= 1, ++k;
+  std::unique_ptr<FastBatch> &fp = d.fast[k][mode];
+  HIP_TRY(hipSetDevice(d.id));
+  if (!fp || fp->gen != ctx->graph_gen.load()) {
+    if (fp) HIP_TRY(hipStreamSynchronize(d.stream)); // (its last launch is done: the call synchronised)
+    fp.reset(new FastBatch());
+    const int rc = fast_build(ctx, d, *fp, nb, mode);
+    if (rc) {
+      fp.reset();
+      return rc;
+    }
+  }
+  FastBatch &f = *fp;
+  memcpy(f.h_in, boards, n * sizeof(gn_board));
+  if (nb > n) memset(f.h_in + n, 0, (nb - n) * sizeof(gn_board));
+  {
+    SeqGuard sg(d, d.stream);
+    HIP_TRY(sg.e);
+    HIP_TRY(hipGraphLaunch(f.exec, d.stream));
+    HIP_TRY(sg.finish());
+  }
+  uint32_t flag;
+  memcpy(&flag, f.h_out + nb, sizeof(flag));
+  ++ctx->fast_runs;
+  if (flag) {
+    ++ctx->fast_fallbacks;
+    return GN_OK;
+  }
+  memcpy(out, f.h_out, n * sizeof(gn_eval));
+  *done = true;
+  return GN_OK;
+}
+
 // Host boards -> device(s) -> gn_eval: contiguous shards, one host thread per device.
 static int evaluate_boards_host(gn_ctx *ctx, const gn_board *boards, size_t n, int mode, gn_eval *out) {
   if (!n) return GN_OK;
+  if (ctx->fast_batch && n <= FAST_MAX && ctx->devs.size() == 1 && mode >= GN_MODE_FULL && mode <= GN_MODE_SMALL) {
+    Dev &d = *ctx->devs[0];
+    std::lock_guard<std::mutex> lk(d.mu);
+    bool done = false;
+    int rc;
+    try {
+      rc = fast_run(ctx, d, boards, n, mode, out, &done);
+    } catch (const std::bad_alloc &) {
+      rc = fail(GN_E_NOMEM, "host allocation failed");
+    }
+    if (rc || done) return rc;
+  }
   try {
     std::vector<size_t> b(ctx->devs.size() + 1);
     partition(nullptr, n, (int)ctx->devs.size(), b.data());
@@ -1824,6 +1988,7 @@ int gn_set_eval_params(gn_ctx *ctx, const gn_eval_params *p) {
     if (!(a >= 1.0)) return fail(GN_E_INVALID, "win-rate model a(material %lld) = %g < 1", (long long)mc, a);
   }
   ctx->P = *p;
+  ++ctx->graph_gen; // (the small-batch graphs hold the parameters they were captured with)
   return GN_OK;
 }
 
@@ -2311,6 +2476,7 @@ int gn_random_games_device(gn_ctx *ctx, int device_slot, uint64_t seed, size_t f
 
 int gn_set_option(gn_ctx *ctx, int option, int64_t value) {
   if (!ctx) return fail(GN_E_INVALID, "ctx is NULL");
+  ++ctx->graph_gen; // (the small-batch graphs hold the options they were captured with)
   switch (option) {
   case GN_OPT_INCREMENTAL_CHILDREN:
     ctx->incremental = value != 0;
@@ -2339,6 +2505,9 @@ int gn_set_option(gn_ctx *ctx, int option, int64_t value) {
     return GN_OK;
   case GN_OPT_COALESCE:
     ctx->coalesce = value != 0;
+    return GN_OK;
+  case GN_OPT_FAST_BATCH:
+    ctx->fast_batch = value != 0;
     return GN_OK;
   default:
     return fail(GN_E_INVALID, "unknown option %d", option);
@@ -2371,6 +2540,15 @@ int gn_get_option(const gn_ctx *ctx, int option, int64_t *value) {
     return GN_OK;
   case GN_OPT_COALESCE:
     *value = ctx->coalesce;
+    return GN_OK;
+  case GN_OPT_FAST_BATCH:
+    *value = ctx->fast_batch;
+    return GN_OK;
+  case GN_STAT_FAST_BATCHES:
+    *value = (int64_t)ctx->fast_runs.load();
+    return GN_OK;
+  case GN_STAT_FAST_FALLBACKS:
+    *value = (int64_t)ctx->fast_fallbacks.load();
     return GN_OK;
   case GN_STAT_BATCH_LAUNCHES:
   case GN_STAT_BATCH_CALLS: { // cumulative since load (the coalescer's counters)

@@ -906,7 +906,9 @@ __global__ void score_reduce_kernel(const gn_board *__restrict__ sb, size_t m, c
                                     const gn_eval *__restrict__ ce, const int32_t *__restrict__ csv,
                                     gn_eval_params P, gn_eval *__restrict__ out, int32_t *__restrict__ sv) {
   const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= m) return;
+  // (idx NULL: every position j of sb, those without replies left as they are -- the drop-in's
+  // small-batch path, reply_level_kernel, keeps positions in place instead of compacting them)
+  if (j >= m || off[j] == off[j + 1]) return;
   int32_t best = INT32_MIN;
   uint32_t bm = 0xFFFFu;
   for (uint64_t c = off[j]; c < off[j + 1]; ++c) {
@@ -917,7 +919,7 @@ __global__ void score_reduce_kernel(const gn_board *__restrict__ sb, size_t m, c
   }
   Board B;
   unpack(sb[j], B);
-  const uint32_t i = idx[j];
+  const uint32_t i = idx ? idx[j] : (uint32_t)j;
   gn_eval e = out[i];
   uint32_t fl = (e.flags | GN_FLAG_SEARCHED) & ~GN_FLAG_MATE;
   e.score = rule_score(best, wdl_material(B, P), P, fl);
@@ -1011,6 +1013,85 @@ hipError_t launch_score_replies_fill(const uint32_t *idx, size_t m, const uint64
   if (!m) return hipSuccess;
   hipLaunchKernelGGL(score_replies_kernel, dim3(blocks_for(m, 256)), dim3(256), 0, s, idx, m, off, coff, rec, moves,
                      unpacked, tables, ce, cb, cm);
+  return hipGetLastError();
+}
+
+// One level of the score rule's replies for a small batch (the drop-in's gn_evaluate_batch,
+// gpu_nnue.hip FastBatch), as one workgroup and no host round trip: position i of boards (records
+// ev) is selected as score_select_kernel does (scored, in check, a legal move); off[i] = the
+// exclusive prefix of the selected positions' legal-move counts (off[n] = their total); the
+// replies, in gen_legal order, are rb / rm [off[i], off[i + 1]) -- the boards write_children
+// would make -- and every slot from the total to cap is an empty board (an invalid position for
+// the evaluation that follows, so that launches sized by cap need no count).  A total beyond cap
+// sets *flag (the caller then takes the general path); first: *flag is set, else or'd.
+// Positions per thread <= 4 (n <= 4096).
+__global__ void __launch_bounds__(1024) reply_level_kernel(const gn_board *__restrict__ boards,
+                                                           const gn_eval *__restrict__ ev, uint32_t n,
+                                                           const Tables *__restrict__ tables, uint64_t *__restrict__ off,
+                                                           uint32_t cap, gn_board *__restrict__ rb,
+                                                           uint16_t *__restrict__ rm, uint32_t *__restrict__ flag,
+                                                           int first) {
+  __shared__ Tables T;
+  __shared__ uint32_t part[1024];
+  load_tables(T, tables);
+  constexpr uint32_t NT = 1024, QMAX = 4;
+  const uint32_t t = threadIdx.x, q = (n + NT - 1) / NT, lo = t * q, hi = lo + q < n ? lo + q : n;
+  uint32_t cnt[QMAX] = {0, 0, 0, 0}, c = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < QMAX; ++k) {
+    const uint32_t i = lo + k;
+    if (k < q && i < hi) {
+      const uint32_t f = ev[i].flags;
+      if ((f & GN_FLAG_IN_CHECK) && !(f & (GN_FLAG_NO_MOVES | GN_FLAG_NO_SCORE | GN_FLAG_BAD_FEN))) {
+        Board B;
+        if (unpack(boards[i], B)) gen_legal(B, T, [&](uint16_t) { ++cnt[k]; });
+      }
+      c += cnt[k];
+    }
+  }
+  part[t] = c;
+  __syncthreads();
+  for (uint32_t d = 1; d < NT; d <<= 1) { // inclusive scan of the per-thread totals (Hillis-Steele)
+    const uint32_t v = t >= d ? part[t - d] : 0u;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  const uint32_t total = part[NT - 1];
+  uint32_t base = part[t] - c;
+#pragma unroll
+  for (uint32_t k = 0; k < QMAX; ++k) {
+    const uint32_t i = lo + k;
+    if (k < q && i < hi) {
+      off[i] = base;
+      if (cnt[k]) {
+        Board B;
+        unpack(boards[i], B);
+        uint32_t r = base;
+        gen_legal(B, T, [&](uint16_t m) {
+          if (r < cap) {
+            pack(do_move(B, m, nullptr), rb[r]);
+            rm[r] = m;
+          }
+          ++r;
+        });
+      }
+      base += cnt[k];
+    }
+  }
+  if (t == 0) {
+    off[n] = total;
+    if (first) *flag = total > cap ? 1u : 0u;
+    else if (total > cap) atomicOr(flag, 1u);
+  }
+  for (uint32_t r = total + t; r < cap; r += NT) rb[r] = gn_board{};
+}
+
+hipError_t launch_reply_level(const gn_board *boards, const gn_eval *ev, size_t n, const Tables *tables, uint64_t *off,
+                              size_t cap, gn_board *rb, uint16_t *rm, uint32_t *flag, int first, hipStream_t s) {
+  if (!n || n > 4096 || cap >= 0x80000000ull) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(reply_level_kernel, dim3(1), dim3(1024), 0, s, boards, ev, (uint32_t)n, tables, off,
+                     (uint32_t)cap, rb, rm, flag, first);
   return hipGetLastError();
 }
 

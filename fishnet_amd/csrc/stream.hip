@@ -23,18 +23,25 @@
 //                       fc_1 / fc_2 and writes the outputs while the others stream on.
 //
 // Entry (u64, built by the plan kernel in the form the stream consumes):
-//   lo = the row's byte offset: an FT row, the zero row, or (hi SCR) a row of the
+//   lo = the row's byte offset: an FT row, the zero row, or (bit 31, SCR) a row of the
 //        workgroup's scratch slot counted from its first row (2 + 64 h + ksq: the
-//        king-cache row of (h, ksq)); the workgroup adds its slot's offset
+//        king-cache row of (h, ksq)); the workgroup adds its slot's offset (the FT table is
+//        < 2^28 bytes, so bit 31 is free)
 //   hi = [15:0] the 16-bit multiplier of the row (1 add, 0xFFFF subtract, 0 no-op; a
 //        store-only KST entry loads the zero row and has its target scratch row here),
-//        [16] PRE (an init before the entry), [18:17] the init kind (1 ZERO: acc = row,
-//        2 PACC: acc = parent - row, saved as the sibling base, 3 BASE: acc = base +- row),
-//        [19] LAST entry of its slot, [23:20] slot in tile, [24] side (0: the perspective
-//        to move), [25] PAR_E (the slot's accumulator becomes pacc: a parent, or the child
-//        that is the next parent), [27] KST (store the slot's accumulator to the scratch row
-//        of this entry), [31] SCR
-// so the stream's common entry is a multiply-add with hi as its scalar operand and two bit tests.
+//        [17:16] the init before the entry (0 none, 1 ZERO: acc = row, 2 PACC: acc = parent
+//        - row, saved as the sibling base, 3 BASE: acc = base +- row), [18] LAST entry of its
+//        slot, [19] X (PAR_E or KST), [20] PAR_E (the slot's accumulator becomes pacc: a
+//        parent, or the child that is the next parent), [21] KST (store the slot's
+//        accumulator to the scratch row of this entry), [31:22] where the slot's features go
+//        in the LDS tile: (slot in tile) * xu + (side) * hu, side 0 the perspective to move,
+//        in the stream's units (plan_kernel's xu / hu: 16-B units of the tile row XS and of
+//        the half LC / 2 for the column-sliced and 1024-wide streams; slot * 2 + side for
+//        the whole-row 3072 stream)
+// Round 6: each test the stream makes is one bit or one field of hi, nested so that an entry
+// runs only the tests of its kind (round 5's decode ran ~25 scalar instructions per entry, the
+// scalar unit's issue being the larger part of the stream's issue floor), and the LDS address
+// of the features is a shift of hi.
 // The ring issues a row load 4 entries before it
 // consumes it, so an entry that loads a scratch row sits at least GN_SCR_GAP (= 4) entries
 // after the last store to scratch in its list (no-op entries are inserted when needed): the
@@ -109,16 +116,33 @@ __device__ int gn_fault_armed = 1;
 
 namespace gn {
 namespace ps {
-constexpr uint32_t H_PRE = 1u << 16, H_INIT_SH = 17, H_LAST = 1u << 19, H_SLOT_SH = 20, H_SIDE_SH = 24,
-                   H_PAR_E = 1u << 25, H_KST = 1u << 27, H_SCR = 1u << 31;
+constexpr uint32_t H_K0 = 1u << 16, H_K1 = 1u << 17, H_KM = H_K0 | H_K1, H_LAST = 1u << 18, H_X = 1u << 19,
+                   H_PAR_E = H_X | 1u << 20, H_KST = H_X | 1u << 21, H_LDS_SH = 22;
+constexpr uint32_t L_SCR = 1u << 31; // (in lo)
 // Each put site knows its entry's kind, so hi is a constant mask or'd with the slot / side
-// bits (round 3 built a u32 entry and decoded it per put: ~25 VALU per entry in an
+// field (round 3 built a u32 entry and decoded it per put: ~25 VALU per entry in an
 // issue-bound kernel).
 constexpr uint32_t M_ADD = 1u, M_SUB = 0xFFFFu;
-constexpr uint32_t HZ = H_PRE | 1u << H_INIT_SH, HP = H_PRE | 2u << H_INIT_SH, HB = H_PRE | 3u << H_INIT_SH;
-__device__ __forceinline__ uint32_t hs(int slot, int side) {
-  return (uint32_t)slot << H_SLOT_SH | (uint32_t)side << H_SIDE_SH;
+constexpr uint32_t HZ = 1u << 16, HP = 2u << 16, HB = 3u << 16;
+// the slot's LDS field (xu / hu: plan_kernel's arguments, see above)
+__device__ __forceinline__ uint32_t hs(int slot, int side, uint32_t xu, uint32_t hu) {
+  return ((uint32_t)slot * xu + (uint32_t)side * hu) << H_LDS_SH;
 }
+// a stream whose tile rows (XS bytes) and halves (LC / 2) are whole 16-B units that fit the
+// 10-bit field for 16 slots takes its LDS offset as field << 4; otherwise the field is slot * 2
+// + side
+constexpr bool lds_field16(int XS, int LC) {
+  return XS % 16 == 0 && (LC / 2) % 16 == 0 && 15 * (XS / 16) + LC / 32 < 1024;
+}
+#ifndef GN_SLICE_XPAD // A/B: LDS bytes added per tile row of the sliced stream (fewer workgroups per CU)
+#define GN_SLICE_XPAD 0
+#endif
+// the stream's LDS tile row (bytes) for L1 / SL columns, and the plan's (xu, hu) for it
+constexpr int tile_xs(int L1, int SL) { return L1 / SL + 16 + (SL > 1 ? GN_SLICE_XPAD : 0); }
+constexpr uint32_t field_xu(int L1, int SL) {
+  return lds_field16(tile_xs(L1, SL), L1 / SL) ? (uint32_t)tile_xs(L1, SL) / 16 : 2u;
+}
+constexpr uint32_t field_hu(int L1, int SL) { return lds_field16(tile_xs(L1, SL), L1 / SL) ? (uint32_t)(L1 / SL) / 32 : 1u; }
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -134,7 +158,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
                 const uint8_t *__restrict__ need_child, const uint8_t *__restrict__ next_slot, uint32_t np, uint32_t K,
                 uint32_t b0, uint32_t b1, int kc, const uint64_t *__restrict__ eoff, uint64_t *__restrict__ ent, TileDesc *__restrict__ tiles,
                 uint32_t *__restrict__ btiles, unsigned long long *__restrict__ rows_out,
-                unsigned long long *__restrict__ pads_out, uint32_t *__restrict__ err, int2 *__restrict__ pinfo) {
+                unsigned long long *__restrict__ pads_out, uint32_t *__restrict__ err, int2 *__restrict__ pinfo,
+                uint32_t xu, uint32_t hu) {
   using namespace ps;
   __shared__ uint32_t ksnap[4][128][8]; // per wave: placement (64 nibbles) of each king-cache row
   __shared__ uint16_t prow_s[4][2][32];
@@ -164,7 +189,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
   uint32_t safe0 = 0, safe1 = 0; // first index of each list at which a scratch row may be loaded
   constexpr uint32_t RS = ft_row_stride(L1);
   constexpr uint32_t LO_BIAS = (uint32_t)FT_BIAS_ROW * RS, LO_ZERO = (uint32_t)ZERO_ROW * RS;
-  auto lo_scr = [](uint32_t r) -> uint32_t { return ((uint32_t)FT_ROWS + r) * RS; }; // scratch row r
+  auto lo_scr = [](uint32_t r) -> uint32_t { return ((uint32_t)FT_ROWS + r) * RS | L_SCR; }; // scratch row r
   // entry i of list g: the row at byte offset lo, hi = multiplier + flags (see above)
   // One SGPR base and an unsigned 32-bit byte offset for both lists: the store is the base + a
   // VGPR offset, no 64-bit address arithmetic per entry.  Entries are only ever put below their
@@ -173,7 +198,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
   const uint32_t rlast = rtot - 1;
   auto put = [&](int g, uint32_t i, uint32_t lo, uint32_t hi) {
     // a scratch-row load must sit GN_SCR_GAP entries after the list's last scratch store
-    if ((hi & H_SCR) && i < (g ? safe1 : safe0)) bad |= 4u;
+    if ((lo & L_SCR) && i < (g ? safe1 : safe0)) bad |= 4u;
     const uint32_t ic = i < rlast ? i : rlast;
     const uint32_t x = g ? rlast - ic : ic;
     *reinterpret_cast<uint2 *>(reinterpret_cast<char *>(E) + (x << 3)) = make_uint2(lo, hi);
@@ -532,21 +557,21 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
       // at the cursor), before the jobs: a cache-row load is put while the lists' last scratch
       // stores are still the ones before it (put() checks the distance)
       if (live && q0 == 0 && lane == 0) {
-        const uint32_t t0w = hs(tf0, stm != 0), t1w = hs(tf0, stm != 1);
+        const uint32_t t0w = hs(tf0, stm != 0, xu, hu), t1w = hs(tf0, stm != 1, xu, hu);
         if (have) { // the parent is its predecessor's last child: pacc, one entry per list
           put(0, len0, LO_ZERO, M_SUB | HP | t0w | H_PAR_E | H_LAST);
           put(1, len1, LO_ZERO, M_SUB | HP | t1w | H_PAR_E | H_LAST);
         } else { // bias entry or the cache row; the rest follows (lane = square / row)
-          put(0, len0, pnd[0] >= 0 ? lo_scr(2 + pkq[0]) : LO_BIAS, M_ADD | HZ | t0w | H_PAR_E | (pnd[0] >= 0 ? H_SCR : 0u));
+          put(0, len0, pnd[0] >= 0 ? lo_scr(2 + pkq[0]) : LO_BIAS, M_ADD | HZ | t0w | H_PAR_E);
           put(1, len1, pnd[1] >= 0 ? lo_scr(2 + 64 + pkq[1]) : LO_BIAS,
-              M_ADD | HZ | t1w | H_PAR_E | (pnd[1] >= 0 ? H_SCR : 0u));
+              M_ADD | HZ | t1w | H_PAR_E);
         }
       }
       if (live && q0 == 0 && !have) {
         const uint64_t lt2 = (1ull << lane) - 1;
 #pragma unroll 1
         for (int hh = 0; hh < 2; ++hh) {
-          const uint32_t tp = hs(tf0, stm != hh), b0 = (hh ? len1 : len0) + 1;
+          const uint32_t tp = hs(tf0, stm != hh, xu, hu), b0 = (hh ? len1 : len0) + 1;
           const uint32_t kr = (uint32_t)(2 + 64 * hh + pkq[hh]); // the cache row (scratch row index)
           if (pnd[hh] >= 0) { // the cache row's differences: removed pieces, then added ones
             int spc;
@@ -623,7 +648,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
           row = king_move_row_pc(ppc, hh, sq01 & 0xFFFF, kt, sq23 & 0xFFFF, sq23 >> 16, lane, pos, cpc);
         }
         ++ji;
-        const uint32_t tw = hs(tl, hh != st);
+        const uint32_t tw = hs(tl, hh != st, xu, hu);
         bool kuse = kc && ((jd >> 21) & 1); // not castling
         const int kci = 64 * hh + kt;
         const int kst = kuse ? kstate_of(hh, kt) : 0;
@@ -652,7 +677,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
           const int nd = popcnt(bs) + popcnt(ba);
           ne = nd + 2;
           const int ps = 1 + popcnt(bs & lt), pa = 1 + popcnt(bs) + popcnt(ba & lt);
-          if (lane == 0) put(g, base, lo_scr(kr), M_ADD | HZ | tw | H_SCR);
+          if (lane == 0) put(g, base, lo_scr(kr), M_ADD | HZ | tw);
           if ((bs >> lane) & 1) put(g, base + ps, (uint32_t)feature_index(hh, lane, spc, kt) * RS, M_SUB | tw);
           if ((ba >> lane) & 1) put(g, base + pa, (uint32_t)row * RS, M_ADD | tw);
           if (lane == 0) put(g, base + ne - 1, LO_ZERO, kr | tw | H_KST | L);
@@ -685,7 +710,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
         const uint32_t rel = exc - (uint32_t)__shfl((int)exc, tile_lane0(tix)); // (no borrow: prefix sums)
         const uint32_t at0 = (uint32_t)__shfl((int)ts0, tix) + (rel & 0xFFFF);
         const uint32_t at1 = (uint32_t)__shfl((int)ts1, tix) + (rel >> 16);
-        const uint32_t t0w = hs(t, cst != 0), t1w = hs(t, cst != 1);
+        const uint32_t t0w = hs(t, cst != 0, xu, hu), t1w = hs(t, cst != 1, xu, hu);
         if (in && live) {
           auto delta = [&](int g, uint32_t at, uint32_t lo2, uint32_t hi2, int s, int n, bool hit, uint32_t tw,
                            uint32_t L) {
@@ -774,10 +799,7 @@ __global__ void __launch_bounds__(L1 / SL / 8) __attribute__((amdgpu_waves_per_e
   using namespace ps;
   constexpr int LC = L1 / SL; // this launch's columns
   constexpr int G = LC / 16;  // threads per perspective group (whole waves)
-#ifndef GN_SLICE_XPAD // A/B: LDS bytes added per tile row of the sliced stream (fewer workgroups per CU)
-#define GN_SLICE_XPAD 0
-#endif
-  constexpr int NT = 2 * G, NW = NT / 64, TILE = 16, XS = LC + 16 + (SL > 1 ? GN_SLICE_XPAD : 0), KS = LC / 64,
+  constexpr int NT = 2 * G, NW = NT / 64, TILE = 16, XS = tile_xs(L1, SL), KS = LC / 64,
                 KPW = KS / NW;
   constexpr int KSF = L1 / 64; // fc_0 k-steps of the whole net
   constexpr uint32_t RS = ft_row_stride(L1);
@@ -897,7 +919,9 @@ __global__ void __launch_bounds__(L1 / SL / 8) __attribute__((amdgpu_waves_per_e
   // groups of 4 ahead, so waiting for an entry never waits for the row loads in flight;
   // rows are loaded one group of 4 ahead of consumption, also across tile boundaries
   // (the next tile's first rows are in flight during this tile's layer stack).
-  ushort8 pacc_lo = {}, pacc_hi = {}, base_lo = {}, base_hi = {};
+  // the accumulator (A), the parent accumulator (PA) and the sibling base (BA) of this lane's 16
+  // columns as 8 dwords each (the low half's 8 columns, then the high half's)
+  uint32_t PA[8] = {0, 0, 0, 0, 0, 0, 0, 0}, BA[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   constexpr int RD = GN_RING;
   static_assert(RD == 4 || RD == 8, "ring depth");
   ushort8 rlo[RD], rhi[RD];
@@ -951,13 +975,15 @@ __global__ void __launch_bounds__(L1 / SL / 8) __attribute__((amdgpu_waves_per_e
   const sq4 rsq = {__builtin_amdgcn_readfirstlane((int)(uint32_t)ftp),
                    __builtin_amdgcn_readfirstlane((int)(uint32_t)(ftp >> 32) & 0xFFFF),
                    (int)(((size_t)ZERO_ROW + 1) * RS), 0x00020000};
-  const uint32_t scr_off = (scr - (uint32_t)FT_ROWS) * RS; // this slot's rows from the first scratch row
+  // this slot's rows from the first scratch row, less the SCR bit the entry carries in lo
+  const uint32_t scr_off = (scr - (uint32_t)FT_ROWS) * RS - L_SCR;
   auto offset = [&](uint32_t lo, uint32_t h) -> uint32_t {
+    (void)h;
 #ifdef GN_ABLATE_ROWS
     (void)lo, (void)h;
     return (uint32_t)FT_BIAS_ROW * RS; // timing diagnostics build only: every row from L1 / L2
 #else
-    return lo + ((uint32_t)((int32_t)h >> 31) & scr_off);
+    return lo + ((uint32_t)((int32_t)lo >> 31) & scr_off);
 #endif
   };
   auto issue = [&](int r, uint32_t lo, uint32_t h) {
@@ -984,41 +1010,106 @@ __global__ void __launch_bounds__(L1 / SL / 8) __attribute__((amdgpu_waves_per_e
   auto ring_wait = [&](int r) {
     asm volatile("s_waitcnt vmcnt(" GN_STR(GN_RING_WAIT) ")" : "+v"(rlo[r]), "+v"(rhi[r]));
   };
-  ushort8 lo = {}, hi = {};
+  uint32_t A[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   auto consume = [&](int r) {
     ring_wait(r);
     const uint32_t h = eh[r];
+#ifdef GN_AB_SALU_PLUS // timing diagnostics only: N extra independent scalar ALU instructions per entry
+    {
+      uint32_t d0, d1;
+      asm volatile(".rept " GN_STR(GN_AB_SALU_PLUS) " / 2\n\ts_add_u32 %0, %2, 1\n\ts_add_u32 %1, %2, 2\n\t.endr"
+                   : "=&s"(d0), "=&s"(d1) : "s"(h));
+    }
+#endif
+#ifdef GN_AB_VALU_PLUS // timing diagnostics only: N extra independent vector ALU instructions per entry
+    {
+      uint32_t d0, d1;
+      asm volatile(".rept " GN_STR(GN_AB_VALU_PLUS) " / 2\n\tv_mov_b32 %0, %2\n\tv_mov_b32 %1, %2\n\t.endr"
+                   : "=&v"(d0), "=&v"(d1) : "v"(j16));
+    }
+#endif
     // every entry is one 16-bit multiply-add per dword, acc = src + sg * row, its multiplier
     // sg (1, 0xFFFF = -1, 0) the low half of h as the instruction's scalar operand; src is
-    // the accumulator, or (PRE) 0 / the parent / the sibling base at a slot's first entry
-    // (wrapping int16, as the accumulators)
-    const unsigned short sg = (unsigned short)h;
-    // (the source copied first, then one multiply-add: a multiply-add per source, with no copy,
-    // spilled 11 VGPRs in the sliced stream's revolution loop)
-    if (h & H_PRE) {
-      const uint32_t init = (h >> H_INIT_SH) & 3;
-      asm volatile("");
-      if (init == 2) lo = pacc_lo, hi = pacc_hi;
-      else if (init == 3) lo = base_lo, hi = base_hi;
-      else lo = ushort8{}, hi = ushort8{};
-    }
-    lo = rlo[r] * sg + lo, hi = rhi[r] * sg + hi;
-    if ((h & (H_PRE | 3u << H_INIT_SH)) == (H_PRE | 2u << H_INIT_SH)) {
-      asm volatile("");
-      base_lo = lo, base_hi = hi;
+    // the accumulator, or (an init) 0 / the parent / the sibling base at a slot's first entry
+    // (wrapping int16, as the accumulators).  The decode is a branch tree on h's init field, one
+    // test per branch, each kind with its own multiply-adds (the compiler's version of this tree
+    // copied the source registers on every path and spilled): a plain entry costs two scalar
+    // instructions, an init five to seven.
+    {
+      const uint4 rl = __builtin_bit_cast(uint4, rlo[r]), rh = __builtin_bit_cast(uint4, rhi[r]);
+      uint32_t t;
+#define GN_MAD8(SRC)                                                                                        \
+  "v_pk_mad_u16 %[a0], %[r0], %[h], %[" SRC "0] op_sel_hi:[1,0,1]\n\t"                                       \
+  "v_pk_mad_u16 %[a1], %[r1], %[h], %[" SRC "1] op_sel_hi:[1,0,1]\n\t"                                       \
+  "v_pk_mad_u16 %[a2], %[r2], %[h], %[" SRC "2] op_sel_hi:[1,0,1]\n\t"                                       \
+  "v_pk_mad_u16 %[a3], %[r3], %[h], %[" SRC "3] op_sel_hi:[1,0,1]\n\t"                                       \
+  "v_pk_mad_u16 %[a4], %[r4], %[h], %[" SRC "4] op_sel_hi:[1,0,1]\n\t"                                       \
+  "v_pk_mad_u16 %[a5], %[r5], %[h], %[" SRC "5] op_sel_hi:[1,0,1]\n\t"                                       \
+  "v_pk_mad_u16 %[a6], %[r6], %[h], %[" SRC "6] op_sel_hi:[1,0,1]\n\t"                                       \
+  "v_pk_mad_u16 %[a7], %[r7], %[h], %[" SRC "7] op_sel_hi:[1,0,1]\n\t"
+      asm volatile("s_and_b32 %[t], %[h], 0x30000\n\t"
+                   "s_cbranch_scc0 .Lgn_plain%=\n\t"
+                   "s_bitcmp1_b32 %[h], 17\n\t"
+                   "s_cbranch_scc0 .Lgn_zero%=\n\t"
+                   "s_bitcmp1_b32 %[h], 16\n\t"
+                   "s_cbranch_scc0 .Lgn_pacc%=\n\t"
+                   GN_MAD8("b")
+                   "s_branch .Lgn_end%=\n"
+                   ".Lgn_pacc%=:\n\t"
+                   GN_MAD8("p")
+                   "v_mov_b32 %[b0], %[a0]\n\t"
+                   "v_mov_b32 %[b1], %[a1]\n\t"
+                   "v_mov_b32 %[b2], %[a2]\n\t"
+                   "v_mov_b32 %[b3], %[a3]\n\t"
+                   "v_mov_b32 %[b4], %[a4]\n\t"
+                   "v_mov_b32 %[b5], %[a5]\n\t"
+                   "v_mov_b32 %[b6], %[a6]\n\t"
+                   "v_mov_b32 %[b7], %[a7]\n\t"
+                   "s_branch .Lgn_end%=\n"
+                   ".Lgn_zero%=:\n\t"
+                   "v_pk_mul_lo_u16 %[a0], %[r0], %[h] op_sel_hi:[1,0]\n\t"
+                   "v_pk_mul_lo_u16 %[a1], %[r1], %[h] op_sel_hi:[1,0]\n\t"
+                   "v_pk_mul_lo_u16 %[a2], %[r2], %[h] op_sel_hi:[1,0]\n\t"
+                   "v_pk_mul_lo_u16 %[a3], %[r3], %[h] op_sel_hi:[1,0]\n\t"
+                   "v_pk_mul_lo_u16 %[a4], %[r4], %[h] op_sel_hi:[1,0]\n\t"
+                   "v_pk_mul_lo_u16 %[a5], %[r5], %[h] op_sel_hi:[1,0]\n\t"
+                   "v_pk_mul_lo_u16 %[a6], %[r6], %[h] op_sel_hi:[1,0]\n\t"
+                   "v_pk_mul_lo_u16 %[a7], %[r7], %[h] op_sel_hi:[1,0]\n\t"
+                   "s_branch .Lgn_end%=\n"
+                   ".Lgn_plain%=:\n\t"
+                   GN_MAD8("a")
+                   ".Lgn_end%=:"
+                   : [a0] "+v"(A[0]), [a1] "+v"(A[1]), [a2] "+v"(A[2]), [a3] "+v"(A[3]), [a4] "+v"(A[4]),
+                     [a5] "+v"(A[5]), [a6] "+v"(A[6]), [a7] "+v"(A[7]), [b0] "+v"(BA[0]), [b1] "+v"(BA[1]),
+                     [b2] "+v"(BA[2]), [b3] "+v"(BA[3]), [b4] "+v"(BA[4]), [b5] "+v"(BA[5]), [b6] "+v"(BA[6]),
+                     [b7] "+v"(BA[7]), [t] "=&s"(t)
+                   : [h] "s"(h), [p0] "v"(PA[0]), [p1] "v"(PA[1]), [p2] "v"(PA[2]), [p3] "v"(PA[3]),
+                     [p4] "v"(PA[4]), [p5] "v"(PA[5]), [p6] "v"(PA[6]), [p7] "v"(PA[7]), [r0] "v"(rl.x),
+                     [r1] "v"(rl.y), [r2] "v"(rl.z), [r3] "v"(rl.w), [r4] "v"(rh.x), [r5] "v"(rh.y),
+                     [r6] "v"(rh.z), [r7] "v"(rh.w)
+                   : "scc");
+#undef GN_MAD8
     }
     if (h & H_LAST) {
-      const int sl = (h >> H_SLOT_SH) & 15, side = (h >> H_SIDE_SH) & 1;
+      const ushort8 lo = __builtin_bit_cast(ushort8, make_uint4(A[0], A[1], A[2], A[3]));
+      const ushort8 hi = __builtin_bit_cast(ushort8, make_uint4(A[4], A[5], A[6], A[7]));
+      // the slot's LDS offset: a shift of hi (slot * XS + side * LC / 2 in 16-B units), or for the
+      // whole-row 3072 stream slot * 2 + side
+      constexpr bool FIELD16 = lds_field16(XS, LC);
+      const uint32_t la = FIELD16 ? (h >> H_LDS_SH) << 4
+                                  : (h >> (H_LDS_SH + 1)) * (uint32_t)XS + ((h >> H_LDS_SH) & 1) * (uint32_t)(LC / 2);
 #ifdef GN_AB_NO_TRANSFORM // timing diagnostics only (wrong results): the accumulator's low bytes, untransformed
-      *reinterpret_cast<uint2 *>(xt + sl * XS + side * (LC / 2) + 8 * jt) = make_uint2(lo[0] | (uint32_t)hi[0] << 16, lo[1]);
+      *reinterpret_cast<uint2 *>(xt + la + 8 * jt) = make_uint2(lo[0] | (uint32_t)hi[0] << 16, lo[1]);
 #else
-      *reinterpret_cast<uint2 *>(xt + sl * XS + side * (LC / 2) + 8 * jt) = transform8(lo, hi);
+      *reinterpret_cast<uint2 *>(xt + la + 8 * jt) = transform8(lo, hi);
 #endif
-      if (h & H_PAR_E) {
+      if (h & H_X) {
+      if (h & (H_PAR_E & ~H_X)) {
         asm volatile("");
-        pacc_lo = lo, pacc_hi = hi;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) PA[i] = A[i];
       }
-      if (h & H_KST) { // the accumulator to its king-cache row
+      if (h & (H_KST & ~H_X)) { // the accumulator to its king-cache row
         asm volatile("");
         const uint32_t so = (scr + (h & 0xFFFFu)) * RS;
 #ifndef GN_KC_POLICY
@@ -1033,6 +1124,7 @@ __global__ void __launch_bounds__(L1 / SL / 8) __attribute__((amdgpu_waves_per_e
         // outstanding (loads complete in order, so >= 2 of the >= 4 completions it waits for are
         // that entry's loads), and a later load of the row is issued after the store in program
         // order by the same lanes (the plan keeps it >= 4 entries behind)
+      }
       }
     }
   };
@@ -1433,7 +1525,8 @@ hipError_t launch_plan_stream(const NetDevice &net, const gn_board *parents, siz
     }
     hipLaunchKernelGGL((plan_kernel<3072>), dim3(pg), dim3(256), 0, s, net, parents, offsets, deltas, need_parent,
                        need_child, K > 1 ? next_slot : nullptr, (uint32_t)n, K, B0, B1, K > 1 ? kc : 0, eoff, ent,
-                       tiles, btiles, rows_out, pads_out, err, sliced ? pinfo : nullptr);
+                       tiles, btiles, rows_out, pads_out, err, sliced ? pinfo : nullptr,
+                       sliced ? ps::field_xu(3072, 3) : ps::field_xu(3072, 1), sliced ? ps::field_hu(3072, 3) : ps::field_hu(3072, 1));
     if (mid) (void)hipEventRecord(mid, s);
     if (sliced) { // three launches over 1,024 columns each (claim counters pool[64 + 8 slice ..]),
       // then the finish
@@ -1454,7 +1547,7 @@ hipError_t launch_plan_stream(const NetDevice &net, const gn_board *parents, siz
   } else if (net.L1 == 1024) {
     hipLaunchKernelGGL((plan_kernel<1024>), dim3(pg), dim3(256), 0, s, net, parents, offsets, deltas, need_parent,
                        need_child, K > 1 ? next_slot : nullptr, (uint32_t)n, K, B0, B1, K > 1 ? kc : 0, eoff, ent,
-                       tiles, btiles, rows_out, pads_out, err, nullptr);
+                       tiles, btiles, rows_out, pads_out, err, nullptr, ps::field_xu(1024, 1), ps::field_hu(1024, 1));
     if (mid) (void)hipEventRecord(mid, s);
     hipLaunchKernelGGL((stream_eval_kernel<1024>), dim3(g), dim3(128), 0, s, net, offsets, (uint32_t)n, K, B0, B1,
                        swz, eoff, ent, tiles, btiles, order, out_parent, out_child, pool, scr, err, pool + 64, 0,

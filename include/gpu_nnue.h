@@ -77,6 +77,13 @@ extern "C" {
                                          call of its mode; a lone call runs at once, no
                                          timer); 0: calls run one after another.  Results
                                          are identical either way.                        */
+#define GN_OPT_FAST_BATCH 9           /* 1 (default): a gn_evaluate_batch of <= 4,096 positions on
+                                         a one-device context runs as one captured HIP graph
+                                         (upload, evaluation, both levels of the score rule's
+                                         in-check replies, download: one host synchronisation
+                                         per call); 0: the general path (a launch sequence with
+                                         a host round trip per reply level).  Results are
+                                         identical either way.                              */
 #define GN_OPT_INCREMENTAL_CHILDREN 1 /* 1 (default): children from the parent accumulators
                                          by add/sub deltas; 0: full refresh per child    */
 #define GN_OPT_XCD_SWIZZLE 2          /* bit mask, default 9: each XCD takes a contiguous
@@ -154,6 +161,10 @@ extern "C" {
 #define GN_STAT_HOST_TOTAL_NS 116     /* the whole call                                    */
 #define GN_STAT_BATCH_LAUNCHES 117    /* merged gn_evaluate_batch launches since load ...   */
 #define GN_STAT_BATCH_CALLS 118       /* ... and the calls they served (GN_OPT_COALESCE)    */
+#define GN_STAT_FAST_BATCHES 119      /* evaluations run by the captured small-batch graphs
+                                         (GN_OPT_FAST_BATCH) since load ...                 */
+#define GN_STAT_FAST_FALLBACKS 120    /* ... and those rerun on the general path because a
+                                         reply level exceeded the graph's capacity          */
 
 /* per-position flags */
 #define GN_FLAG_IN_CHECK 1u /* side to move in check: Stockfish has no static eval

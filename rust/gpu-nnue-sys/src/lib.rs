@@ -36,6 +36,7 @@ pub const GN_OPT_KING_CACHE: c_int = 5;
 pub const GN_OPT_CHUNK_PARENTS: c_int = 6;
 pub const GN_OPT_COALESCE: c_int = 7;
 pub const GN_OPT_STREAM_SLICES: c_int = 8;
+pub const GN_OPT_FAST_BATCH: c_int = 9;
 // read-only statistics (gn_get_option)
 pub const GN_STAT_PLAN_NS: c_int = 101;
 pub const GN_STAT_STREAM_NS: c_int = 102;
@@ -50,6 +51,8 @@ pub const GN_STAT_HOST_TAIL_NS: c_int = 115;
 pub const GN_STAT_HOST_TOTAL_NS: c_int = 116;
 pub const GN_STAT_BATCH_LAUNCHES: c_int = 117;
 pub const GN_STAT_BATCH_CALLS: c_int = 118;
+pub const GN_STAT_FAST_BATCHES: c_int = 119;
+pub const GN_STAT_FAST_FALLBACKS: c_int = 120;
 
 // per-position flags
 pub const GN_FLAG_IN_CHECK: u16 = 1;

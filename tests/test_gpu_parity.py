@@ -993,3 +993,46 @@ def test_two_device_slots_games_at_scale(synth_big_path, synth_small_path, oracl
             lo, hi = int(coffs[k]), int(coffs[k + 1])
             got = dict(zip(cmoves[lo:hi].tolist(), map(tuple, G.decode_children(kids[lo:hi]).tolist())))
             assert got == dict(zip(m_exp, map(tuple, G.children_from_evals(k_exp).tolist()))), (g, i)
+
+
+def test_fast_batch_graph_equals_general_path(gpu_ctx, oracle_nets, oracle_lib):
+    """The drop-in's small-batch graphs (GN_OPT_FAST_BATCH, gpu_nnue.hip FastBatch): one lichess
+    game per call as GpuEvalStub sends it, batches at the size-class edges, every mode, a batch
+    whose in-check replies overflow the graph's capacity (rerun on the general path), and new
+    eval params (the graphs are recaptured) -- every record equal to the general path's, and a
+    sample of games against the oracle."""
+    from fishnet_amd import gpu_nnue as G
+    start = "rnbqkbnr/pppppppp/8/8/8/8/PPPPPPPP/RNBQKBNR w KQkq - 0 1"
+    games = [G.boards_to_fens(G.replay_game(start, u)[0]) for u in G.random_games_uci(0x5EED0A00, 0, 24, 80)]
+    big, small = oracle_nets
+    pool = random_fens(4200, 0x5EED0A01) + special_fens()
+    fl = gpu_ctx.evaluate_batch(pool, 1)["flags"]
+    checks = [f for f, x in zip(pool, fl) if x & G.FLAG_IN_CHECK and not x & G.FLAG_NO_MOVES]
+    assert len(checks) >= 50
+    batches = games + [pool[:1], pool[:127], pool[:128], pool[:129], pool[:1000], pool[:4096], pool[:4097]]
+    overflow = (checks * 40)[:600]  # ~600 in-check positions: their replies exceed 2 * 1024 + 256
+
+    def run(fens, mode, fast):
+        gpu_ctx.set_option(G.OPT_FAST_BATCH, fast)
+        return gpu_ctx.evaluate_batch(fens, mode)
+
+    try:
+        for mode in (0, 1, 2):
+            f0, fb0 = gpu_ctx.get_option(G.STAT_FAST_BATCHES), gpu_ctx.get_option(G.STAT_FAST_FALLBACKS)
+            for fens in batches + [overflow]:
+                assert np.array_equal(run(fens, mode, 1), run(fens, mode, 0)), (mode, len(fens))
+            # every batch but the 4,097 ran a graph, and the overflowing one fell back
+            assert gpu_ctx.get_option(G.STAT_FAST_BATCHES) - f0 == len(batches) - 1 + 1
+            assert gpu_ctx.get_option(G.STAT_FAST_FALLBACKS) - fb0 == 1
+            for fens in games[:4]:
+                _cmp(run(fens, mode, 1), oracle_lib.eval_fens(big, small, fens, mode), fens)
+        p = gpu_ctx.eval_params()
+        q = gpu_ctx.eval_params()
+        q.psqt_weight, q.rule50_div = 111, 150
+        gpu_ctx.set_eval_params(q)
+        for fens in games[:3] + [pool[:300]]:
+            assert np.array_equal(run(fens, 0, 1), run(fens, 0, 0))
+        gpu_ctx.set_eval_params(p)
+        assert np.array_equal(run(games[0], 0, 1), run(games[0], 0, 0))
+    finally:
+        gpu_ctx.set_option(G.OPT_FAST_BATCH, 1)
