@@ -739,11 +739,13 @@ def launch_ranks(gpus: int, argv) -> int | None:
         return None
     # build the HIP library and the oracle once, here, before any rank exists (hipcc and gcc need
     # no GPU): N ranks finding a stale build would otherwise compile the same files at once
-    if not os.environ.get("GPU_NNUE_LIB"):
-        from fishnet_amd import build
-        build.build()
-    from oracle import oracle as O
-    O.build()
+    # (--launch-check: no GPU work and no library, so the CPU launcher test needs no ROCm toolchain)
+    if "--launch-check" not in argv:
+        if not os.environ.get("GPU_NNUE_LIB"):
+            from fishnet_amd import build
+            build.build()
+        from oracle import oracle as O
+        O.build()
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *argv]
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))

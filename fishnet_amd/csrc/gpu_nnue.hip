@@ -363,7 +363,7 @@ struct BatchReq {
   gn_eval *out;
   int rc = GN_OK;
   bool done = false;
-  std::string err;
+  char err[256] = ""; // (fixed size: copied while another caller's launch is marked busy, noexcept)
 };
 
 struct gn_ctx {
@@ -1188,8 +1188,10 @@ static int evaluate_coalesced(gn_ctx *ctx, const gn_board *boards, size_t n, int
     C.q.swap(rest);
     C.busy = true;
     lk.unlock();
+    // from here to the re-lock nothing may throw outside the try block: C.busy is true and only
+    // this thread clears it
     int rc = GN_OK;
-    std::string err;
+    char err[256] = "";
     try {
       if (mine.size() == 1) {
         rc = evaluate_boards_host(ctx, me.boards, me.n, mode, me.out);
@@ -1210,15 +1212,20 @@ static int evaluate_coalesced(gn_ctx *ctx, const gn_board *boards, size_t n, int
     } catch (...) {
       rc = fail(GN_E_INVALID, "unexpected exception");
     }
-    if (rc) err = g_err;
+    if (rc) snprintf(err, sizeof err, "%s", g_err.c_str());
     lk.lock();
-    for (BatchReq *r : mine) r->rc = rc, r->err = err, r->done = true;
+    for (BatchReq *r : mine) r->rc = rc, memcpy(r->err, err, sizeof err), r->done = true;
     ++C.launches, C.calls += mine.size();
     C.busy = false;
     C.cv.notify_all();
   }
   const int rc = me.rc;
-  if (rc) g_err = me.err;
+  if (rc) {
+    try {
+      g_err = me.err;
+    } catch (...) {
+    }
+  }
   return rc;
 }
 

@@ -160,7 +160,7 @@ hipError_t launch_score_reduce(const gn_board *sb, size_t m, const uint32_t *idx
                                const uint16_t *moves, const gn_eval *ce, const int32_t *csv, const gn_eval_params &P,
                                gn_eval *out, int32_t *sv, hipStream_t s);
 // One level of the score rule's replies for a small batch in one launch (reply_level_kernel,
-// kernels.hip): n <= 4096 positions; replies into rb / rm [0, cap) (empty boards after the last),
+// kernels.hip): n <= 16,384 positions; replies into rb / rm [0, cap) (empty boards after the last),
 // off = n + 1 offsets; *flag set (first) / or'd when the replies exceed cap.
 hipError_t launch_reply_level(const gn_board *boards, const gn_eval *ev, size_t n, const Tables *tables, uint64_t *off,
                               size_t cap, gn_board *rb, uint16_t *rm, uint32_t *flag, int first, hipStream_t s);

@@ -778,7 +778,9 @@ __global__ void finalize_kernel(const gn_board *__restrict__ boards, size_t n, i
     int4v sums[4];
     if (part) {
       info = pinfo[qoff + i];
-      slice_sums<GN_PART_SLICES>(part, npos, qoff + i, sums);
+      // (mode FULL: only the positions the big net evaluates have sums -- the small net's read
+      // none; mode BIG: every position, with no load in front of the sums')
+      if (mode == GN_MODE_BIG || (mode == GN_MODE_FULL && need_big[i])) slice_sums<GN_PART_SLICES>(part, npos, qoff + i, sums);
     }
     auto big_out = [&](size_t j) -> int2 {
       return part && info.y >= 0 ? slice_finish_from(bnet, w1s, sums, info) : out_big[j];
@@ -1024,7 +1026,8 @@ hipError_t launch_score_replies_fill(const uint32_t *idx, size_t m, const uint64
 // would make -- and every slot from the total to cap is an empty board (an invalid position for
 // the evaluation that follows, so that launches sized by cap need no count).  A total beyond cap
 // sets *flag (the caller then takes the general path); first: *flag is set, else or'd.
-// Positions per thread <= 4 (n <= 4096).
+// Positions per thread <= 16 (n <= 16,384: level 2 takes level 1's capacity, 2 * 4,096 + 256).
+// A thread's counts wait in off[] (its own entries) between the two passes.
 __global__ void __launch_bounds__(1024) reply_level_kernel(const gn_board *__restrict__ boards,
                                                            const gn_eval *__restrict__ ev, uint32_t n,
                                                            const Tables *__restrict__ tables, uint64_t *__restrict__ off,
@@ -1034,20 +1037,19 @@ __global__ void __launch_bounds__(1024) reply_level_kernel(const gn_board *__res
   __shared__ Tables T;
   __shared__ uint32_t part[1024];
   load_tables(T, tables);
-  constexpr uint32_t NT = 1024, QMAX = 4;
+  constexpr uint32_t NT = 1024;
   const uint32_t t = threadIdx.x, q = (n + NT - 1) / NT, lo = t * q, hi = lo + q < n ? lo + q : n;
-  uint32_t cnt[QMAX] = {0, 0, 0, 0}, c = 0;
-#pragma unroll
-  for (uint32_t k = 0; k < QMAX; ++k) {
-    const uint32_t i = lo + k;
-    if (k < q && i < hi) {
-      const uint32_t f = ev[i].flags;
-      if ((f & GN_FLAG_IN_CHECK) && !(f & (GN_FLAG_NO_MOVES | GN_FLAG_NO_SCORE | GN_FLAG_BAD_FEN))) {
-        Board B;
-        if (unpack(boards[i], B)) gen_legal(B, T, [&](uint16_t) { ++cnt[k]; });
-      }
-      c += cnt[k];
+  uint32_t c = 0;
+#pragma unroll 1
+  for (uint32_t i = lo; i < hi; ++i) {
+    uint32_t cnt = 0;
+    const uint32_t f = ev[i].flags;
+    if ((f & GN_FLAG_IN_CHECK) && !(f & (GN_FLAG_NO_MOVES | GN_FLAG_NO_SCORE | GN_FLAG_BAD_FEN))) {
+      Board B;
+      if (unpack(boards[i], B)) gen_legal(B, T, [&](uint16_t) { ++cnt; });
     }
+    off[i] = cnt;
+    c += cnt;
   }
   part[t] = c;
   __syncthreads();
@@ -1059,25 +1061,23 @@ __global__ void __launch_bounds__(1024) reply_level_kernel(const gn_board *__res
   }
   const uint32_t total = part[NT - 1];
   uint32_t base = part[t] - c;
-#pragma unroll
-  for (uint32_t k = 0; k < QMAX; ++k) {
-    const uint32_t i = lo + k;
-    if (k < q && i < hi) {
-      off[i] = base;
-      if (cnt[k]) {
-        Board B;
-        unpack(boards[i], B);
-        uint32_t r = base;
-        gen_legal(B, T, [&](uint16_t m) {
-          if (r < cap) {
-            pack(do_move(B, m, nullptr), rb[r]);
-            rm[r] = m;
-          }
-          ++r;
-        });
-      }
-      base += cnt[k];
+#pragma unroll 1
+  for (uint32_t i = lo; i < hi; ++i) {
+    const uint32_t cnt = (uint32_t)off[i];
+    off[i] = base;
+    if (cnt) {
+      Board B;
+      unpack(boards[i], B);
+      uint32_t r = base;
+      gen_legal(B, T, [&](uint16_t m) {
+        if (r < cap) {
+          pack(do_move(B, m, nullptr), rb[r]);
+          rm[r] = m;
+        }
+        ++r;
+      });
     }
+    base += cnt;
   }
   if (t == 0) {
     off[n] = total;
@@ -1089,7 +1089,7 @@ __global__ void __launch_bounds__(1024) reply_level_kernel(const gn_board *__res
 
 hipError_t launch_reply_level(const gn_board *boards, const gn_eval *ev, size_t n, const Tables *tables, uint64_t *off,
                               size_t cap, gn_board *rb, uint16_t *rm, uint32_t *flag, int first, hipStream_t s) {
-  if (!n || n > 4096 || cap >= 0x80000000ull) return hipErrorInvalidValue;
+  if (!n || n > 16384 || cap >= 0x80000000ull) return hipErrorInvalidValue;
   hipLaunchKernelGGL(reply_level_kernel, dim3(1), dim3(1024), 0, s, boards, ev, (uint32_t)n, tables, off,
                      (uint32_t)cap, rb, rm, flag, first);
   return hipGetLastError();

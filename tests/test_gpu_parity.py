@@ -839,8 +839,9 @@ def test_eval_params_keep_child_cp_in_24_bits(gpu_ctx):
 @pytest.mark.gpu
 def test_stream_column_slices_equal_whole_rows(gpu_ctx, oracle_nets, oracle_lib):
     """GN_OPT_STREAM_SLICES: the big net's stream as three launches over 1,024 accumulator
-    columns each (every slice stores its fc_0 partial sums; slice_finish_kernel adds the three and
-    runs the rest of the layer stack) gives every output of the one-launch whole-row stream, with
+    columns each (every slice stores its fc_0 partial sums; finalize adds the three where it reads
+    each big-net output and runs the rest of the layer stack, slice_finish_one -- the separate
+    slice_finish_kernel runs only in the -DGN_AB_FINISH_SEPARATE A/B build) gives every output of the one-launch whole-row stream, with
     the chained walk and king cache on and off, in mode BIG (every position on the big net) and
     mode FULL (the big net on the positions the small net hands over: gaps in the slices' position
     lists); sampled parents with all their children against the oracle."""
