@@ -18,6 +18,11 @@ LIB = os.path.join(LIBDIR, "libgpu_nnue.so")
 # (stream.hip GN_FAULT_PLAN_BLOCK; tests/test_gpu_parity.py::test_plan_overflow_fails_the_call_then_recovers)
 FAULT_LIB = os.path.join(LIBDIR, "libgpu_nnue_fault.so")
 FAULT_DEFINES = ("-DGN_FAULT_PLAN_BLOCK=1",)
+# test-only variant: eval_net<128>'s gather at an odd depth (5 rows in flight; the default is 4), so
+# that the odd depth's last-row add and its tail are exercised (ADVICE r5;
+# tests/test_gpu_parity.py::test_small_net_odd_gather_depth_vs_oracle)
+ODD_LIB = os.path.join(LIBDIR, "libgpu_nnue_d5.so")
+ODD_DEFINES = ("-DGN_SMALL_DEPTH=5",)
 SOURCES = ["gpu_nnue.hip", "kernels.hip", "stream.hip"]
 HEADERS = ["chess.h", "host_board.h", "nnue.h", "kernels.h", "sha256.h", "device_util.h", "archive.h"]
 ARCH = "gfx950"
@@ -102,6 +107,11 @@ def build_rev(rev: str, out: str, defines=()) -> str:
 def build_fault(force: bool = False, verbose: bool = False) -> str:
     """The fault-injection library (never loaded by the product path or the bench)."""
     return build(force=force, verbose=verbose, defines=FAULT_DEFINES, out=FAULT_LIB)
+
+
+def build_odd(force: bool = False, verbose: bool = False) -> str:
+    """The odd-gather-depth library (test only; never loaded by the product path or the bench)."""
+    return build(force=force, verbose=verbose, defines=ODD_DEFINES, out=ODD_LIB)
 
 
 if __name__ == "__main__":

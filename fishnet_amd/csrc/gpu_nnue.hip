@@ -843,7 +843,7 @@ static int expand_evaluate(gn_ctx *ctx, Dev &d, const gn_board *parents, size_t 
     const bool f = mode == GN_MODE_FULL;
     if (d.planned) {
       const size_t K = (size_t)std::max(1, d.chain_k), nblk = (n + K - 1) / K;
-      HIP_TRY(d.ent.ensure(d.etot + 16 * (nblk + 1)));
+      HIP_TRY(d.ent.ensure(d.etot + (size_t)ENT_SPARE * (nblk + 1)));
       HIP_TRY(d.tiles.ensure((n + total) / 16 + (K + 2) * nblk + 2));
       HIP_TRY(d.btiles.ensure(nblk + 1));
       HIP_TRY(d.pool.ensure(88)); // 8 XCDs x 8 words of scratch-slot bits, then 8 block claim counters

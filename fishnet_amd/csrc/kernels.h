@@ -22,9 +22,17 @@
 #ifndef GN_RING
 #define GN_RING 4
 #endif
-#ifndef GN_SCR_GAP
-#define GN_SCR_GAP GN_RING
+// the column-sliced stream's ring (stream_eval_kernel<3072, 3>): 4, 5 or 6 entries per wave
+#ifndef GN_SLICE_RING
+#define GN_SLICE_RING 4
 #endif
+#ifndef GN_SCR_GAP // (the plan serves both streams: the deeper ring's distance)
+#define GN_SCR_GAP (GN_RING > GN_SLICE_RING ? GN_RING : GN_SLICE_RING)
+#endif
+// Spare entries at the end of each block's entry region (plan_kernel, stream_eval_kernel): the
+// stream's scalar prefetch of the entries two ring revolutions ahead reads up to 2 * ring + 8 - 1
+// entries past its position, so a list ending at the region less the spares never reads past it.
+constexpr unsigned ENT_SPARE = 32;
 
 // The column-sliced stream's fc_0 partial sums: one array per slice (default), which
 // slice_finish_kernel adds; or, with -DGN_PART_INPLACE (A/B only), one array that each slice

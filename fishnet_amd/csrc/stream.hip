@@ -67,19 +67,11 @@
 #ifndef GN_WCACHE // the sliced stream's per-wave fc_0 weight cache (0: weights loaded at each layer stack)
 #define GN_WCACHE 1
 #endif
-#define GN_PV_WAIT GN_RING_WAIT_PV
 #ifndef GN_EXPAND_WPE
 #define GN_EXPAND_WPE (GN_RING == 4 ? 5 : 4)
 #endif
 #define GN_STR2(x) #x
 #define GN_STR(x) GN_STR2(x)
-#if GN_RING == 4
-#define GN_RING_WAIT 6 // the 3 later entries' 2 loads each
-#define GN_RING_WAIT_PV 8 // the layer stack: every load older than the ring's RD entries (2 loads each)
-#else
-#define GN_RING_WAIT 14
-#define GN_RING_WAIT_PV 16
-#endif
 
 #ifdef GN_STREAM_PROF
 // diagnostics build only: per-phase s_memtime cycles summed over waves, and list balance
@@ -89,7 +81,7 @@ __device__ unsigned long long gn_sp[8]; // [0] stream [1] barrier wait [2] layer
 #define SP_ADD(k, v) atomicAdd(&gn_sp[k], (unsigned long long)(v))
 #else
 #define SP_T() 0ull
-#define SP_ADD(k, v) (void)0
+#define SP_ADD(k, v) (void)(v)
 #endif
 #ifdef GN_PLAN_PROF
 // diagnostics build only: plan_kernel cycles (s_memtime) per section, summed over waves:
@@ -100,7 +92,7 @@ __device__ unsigned long long gn_pp[4];
 #define PP_ADD(k, v) atomicAdd(&gn_pp[k], (unsigned long long)(v))
 #else
 #define PP_T() 0ull
-#define PP_ADD(k, v) (void)0
+#define PP_ADD(k, v) (void)(v)
 #endif
 #ifdef GN_XCD_PROF
 // diagnostics build only: per XCD, [x] the last workgroup end and [8 + x] the first start
@@ -116,7 +108,7 @@ __device__ int gn_fault_armed = 1;
 
 namespace gn {
 namespace ps {
-constexpr uint32_t H_K0 = 1u << 16, H_K1 = 1u << 17, H_KM = H_K0 | H_K1, H_LAST = 1u << 18, H_X = 1u << 19,
+constexpr uint32_t H_K0 = 1u << 16, H_K1 = 1u << 17, H_LAST = 1u << 18, H_X = 1u << 19,
                    H_PAR_E = H_X | 1u << 20, H_KST = H_X | 1u << 21, H_LDS_SH = 22;
 constexpr uint32_t L_SCR = 1u << 31; // (in lo)
 // Each put site knows its entry's kind, so hi is a constant mask or'd with the slot / side
@@ -179,7 +171,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
   };
   const uint32_t pbeg = blk * K, pend = pbeg + K < np ? pbeg + K : np;
   const uint64_t us_b = pbeg + offsets[pbeg];
-  const uint64_t rbeg = eoff[pbeg] + 16ull * blk, rend = eoff[pend] + 16ull * (blk + 1);
+  const uint64_t rbeg = eoff[pbeg] + (uint64_t)ENT_SPARE * blk, rend = eoff[pend] + (uint64_t)ENT_SPARE * (blk + 1);
   uint2 *E = reinterpret_cast<uint2 *>(ent + rbeg); // list 0 from E[0] up, list 1 from E[rtot - 1] down
   const uint32_t rtot = (uint32_t)(rend - rbeg); // the block's entry region (both lists; < 2^32)
   uint32_t bad = 0;                  // this lane's error bits (reported once per wave)
@@ -765,7 +757,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
   // closer than GN_SCR_GAP to its list's last scratch store; neither can happen by construction
   const uint32_t werr = __ballot(bad & 1u) ? 1u : 0u, werr4 = __ballot(bad & 4u) ? 4u : 0u;
   if (lane == 0) {
-    if ((uint64_t)len0 + len1 > (uint64_t)rtot || werr) atomicOr(err, 1u);
+    if ((uint64_t)len0 + len1 > (uint64_t)(rtot - ENT_SPARE) || werr) atomicOr(err, 1u);
     if (werr4) atomicOr(err, 4u);
     if (rows_out) atomicAdd(rows_out, (unsigned long long)rows);
     if (pads_out && pads) atomicAdd(pads_out, (unsigned long long)pads);
@@ -869,12 +861,12 @@ __global__ void __launch_bounds__(L1 / SL / 8) __attribute__((amdgpu_waves_per_e
   const uint64_t us_b = pbeg + offsets[pbeg];
   const uint32_t ntiles = btiles[blk];
   const TileDesc *T = tiles + us_b / 16 + (uint64_t)(K + 2) * blk; // as plan_kernel
-  const uint64_t rbeg = eoff[pbeg] + 16ull * blk, rend = eoff[pend] + 16ull * (blk + 1);
-  // a list never ends past the block's entry bound (the region less its 16 spare entries): a
+  const uint64_t rbeg = eoff[pbeg] + (uint64_t)ENT_SPARE * blk, rend = eoff[pend] + (uint64_t)ENT_SPARE * (blk + 1);
+  // a list never ends past the block's entry bound (the region less its ENT_SPARE entries): a
   // tile end beyond it can only come from a plan that overflowed, which the plan reports (err
   // bit 0, the call fails); clamped, the entry loads (and their prefetch, 8 ahead) stay inside
   // the region whatever the descriptors say
-  const uint32_t elim = (uint32_t)(rend - rbeg) - 16u;
+  const uint32_t elim = (uint32_t)(rend - rbeg) - ENT_SPARE;
 #ifdef GN_XCD_PROF
   const unsigned long long xp_t0 = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -922,8 +914,13 @@ __global__ void __launch_bounds__(L1 / SL / 8) __attribute__((amdgpu_waves_per_e
   // the accumulator (A), the parent accumulator (PA) and the sibling base (BA) of this lane's 16
   // columns as 8 dwords each (the low half's 8 columns, then the high half's)
   uint32_t PA[8] = {0, 0, 0, 0, 0, 0, 0, 0}, BA[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  constexpr int RD = GN_RING;
-  static_assert(RD == 4 || RD == 8, "ring depth");
+  constexpr int RD = SL > 1 ? GN_SLICE_RING : GN_RING;
+  static_assert(RD == 4 || RD == 5 || RD == 6 || RD == 8, "ring depth");
+  // the ring's waits: before an entry is consumed, its two loads are older than the RD - 1 later
+  // entries' (2 loads each); the layer stack waits for every load older than the ring's RD entries
+  constexpr int RWAIT = 2 * (RD - 1), RWAIT_PV = 2 * RD;
+  // entries per scalar group load: 4 (s_load_dwordx8) or 8 (x16; rings of 5 or 6 use the first RD)
+  constexpr int GV = RD;
   ushort8 rlo[RD], rhi[RD];
   uint32_t eh[RD]; // hi words of the entries in flight
   uint32_t bq = 0; // buckets done (acc0 / in1 / fwd buffer parity)
@@ -955,17 +952,17 @@ __global__ void __launch_bounds__(L1 / SL / 8) __attribute__((amdgpu_waves_per_e
   };
   // wait for the cache's loads: vmcnt(8) when at least 8 vector-memory operations were issued
   // after them (the ring's loads of the tile's last 4 entries: in-order completion), else all
-#define GN_WC_WAIT(N) asm volatile("s_waitcnt vmcnt(" GN_STR(N) ")" : "+v"(wc[0]), "+v"(wc[1]), "+v"(wc[2]), "+v"(wc[3]), \
-                                   "+v"(wc[4]), "+v"(wc[5]), "+v"(wc[6]), "+v"(wc[7]))
-  typedef uint32_t u8e __attribute__((ext_vector_type(2 * RD), aligned(8)));
+#define GN_WC_WAIT(N) asm volatile("s_waitcnt vmcnt(%8)" : "+v"(wc[0]), "+v"(wc[1]), "+v"(wc[2]), "+v"(wc[3]), \
+                                   "+v"(wc[4]), "+v"(wc[5]), "+v"(wc[6]), "+v"(wc[7]) : "n"(N))
+  typedef uint32_t u8e __attribute__((ext_vector_type(2 * GV), aligned(8)));
   typedef const __attribute__((address_space(4))) u8e cu8e;
   typedef const __attribute__((address_space(4))) uint64_t cu64;
   cu64 *EL = (cu64 *)(HU ? ent + rend : ent + rbeg);
-  // entries i .. i + 3 of this group's list by one s_load_dwordx8 (list 1 is stored
-  // downward: its 4 entries arrive reversed, see elo / ehi)
-  auto group = [&](uint32_t i) -> u8e { return *(cu8e *)(HU ? EL - RD - i : EL + i); };
-  auto elo = [&](const u8e v, int r) -> uint32_t { return HU ? v[2 * (RD - 1 - r)] : v[2 * r]; };
-  auto ehi = [&](const u8e v, int r) -> uint32_t { return HU ? v[2 * (RD - 1 - r) + 1] : v[2 * r + 1]; };
+  // entries i .. i + GV - 1 of this group's list by one s_load_dwordx8 / x16 (list 1 is stored
+  // downward: its entries arrive reversed, see elo / ehi)
+  auto group = [&](uint32_t i) -> u8e { return *(cu8e *)(HU ? EL - GV - i : EL + i); };
+  auto elo = [&](const u8e v, int r) -> uint32_t { return HU ? v[2 * (GV - 1 - r)] : v[2 * r]; };
+  auto ehi = [&](const u8e v, int r) -> uint32_t { return HU ? v[2 * (GV - 1 - r) + 1] : v[2 * r + 1]; };
   int tl0 = tid;
   asm volatile("" : "+v"(tl0));
   const int jt = tl0 % G;
@@ -1008,7 +1005,7 @@ __global__ void __launch_bounds__(L1 / SL / 8) __attribute__((amdgpu_waves_per_e
   // A weight-cache fill at a tile's start is younger than the RD entries then in flight, so the
   // next waits also wait for its loads: once per bucket change)
   auto ring_wait = [&](int r) {
-    asm volatile("s_waitcnt vmcnt(" GN_STR(GN_RING_WAIT) ")" : "+v"(rlo[r]), "+v"(rhi[r]));
+    asm volatile("s_waitcnt vmcnt(%2)" : "+v"(rlo[r]), "+v"(rhi[r]) : "n"(RWAIT));
   };
   uint32_t A[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   auto consume = [&](int r) {
@@ -1217,7 +1214,7 @@ __global__ void __launch_bounds__(L1 / SL / 8) __attribute__((amdgpu_waves_per_e
     // guards (each took 7 scalar instructions and a branch), then the last partial one (guarded)
     if constexpr (REV) {
       {
-        const uint32_t r0 = pos & (RD - 1);
+        const uint32_t r0 = pos % RD;
         if (r0 != 0) {
 #pragma unroll
           for (int r = 1; r < RD; ++r)
@@ -1246,7 +1243,7 @@ __global__ void __launch_bounds__(L1 / SL / 8) __attribute__((amdgpu_waves_per_e
     } else {
 #pragma unroll 1
       while (pos < e_end) {
-        const uint32_t r0 = pos & (RD - 1);
+        const uint32_t r0 = pos % RD;
         if (r0 == 0) {
           // scalar loads complete out of order, so any use waits for all of them: wait once
           // here (lgkmcnt(0): the prefetch of the previous revolution), take this revolution's
@@ -1280,8 +1277,8 @@ __global__ void __launch_bounds__(L1 / SL / 8) __attribute__((amdgpu_waves_per_e
       // copy the registers before the wait)
       if ((wpend || (GN_PART_N == 1 && slice > 0)) && pos - pos0 < (uint32_t)RD)
         __builtin_amdgcn_s_waitcnt(0x0F70); // vmcnt(0)
-      if constexpr (GN_WCACHE) GN_WC_WAIT(GN_RING_WAIT_PV);
-      if constexpr (GN_PART_N == 1) asm volatile("s_waitcnt vmcnt(" GN_STR(GN_PV_WAIT) ")" : "+v"(pv));
+      if constexpr (GN_WCACHE) GN_WC_WAIT(RWAIT_PV);
+      if constexpr (GN_PART_N == 1) asm volatile("s_waitcnt vmcnt(%1)" : "+v"(pv) : "n"(RWAIT_PV));
     }
     // (SL > 1: the cached bucket first, as bit 8 of mm; the others load the cache when they come)
     uint32_t mm = SL > 1 && ((bm >> cb) & 1) ? (bm ^ (1u << cb)) | 256u : bm;

@@ -1006,12 +1006,15 @@ def test_fast_batch_graph_equals_general_path(gpu_ctx, oracle_nets, oracle_lib):
     start = "rnbqkbnr/pppppppp/8/8/8/8/PPPPPPPP/RNBQKBNR w KQkq - 0 1"
     games = [G.boards_to_fens(G.replay_game(start, u)[0]) for u in G.random_games_uci(0x5EED0A00, 0, 24, 80)]
     big, small = oracle_nets
-    pool = random_fens(4200, 0x5EED0A01) + special_fens()
+    # (positions of random games: ~4 % are in check; gn_random_positions gave none of 4,200 in
+    # check, the oracle agrees)
+    pool = [f for u in G.random_games_uci(0x5EED0A01, 0, 60, 80) for f in G.boards_to_fens(G.replay_game(start, u)[0])]
+    pool = pool[:4200] + special_fens()
     fl = gpu_ctx.evaluate_batch(pool, 1)["flags"]
     checks = [f for f, x in zip(pool, fl) if x & G.FLAG_IN_CHECK and not x & G.FLAG_NO_MOVES]
     assert len(checks) >= 50
     batches = games + [pool[:1], pool[:127], pool[:128], pool[:129], pool[:1000], pool[:4096], pool[:4097]]
-    overflow = (checks * 40)[:600]  # ~600 in-check positions: their replies exceed 2 * 1024 + 256
+    overflow = (checks * 40)[:1000]  # 1,000 in-check positions: their replies exceed 2 * 1024 + 256
 
     def run(fens, mode, fast):
         gpu_ctx.set_option(G.OPT_FAST_BATCH, fast)
@@ -1037,3 +1040,40 @@ def test_fast_batch_graph_equals_general_path(gpu_ctx, oracle_nets, oracle_lib):
         assert np.array_equal(run(games[0], 0, 1), run(games[0], 0, 0))
     finally:
         gpu_ctx.set_option(G.OPT_FAST_BATCH, 1)
+
+
+_ODD_CHILD = r"""
+import sys
+import numpy as np
+from fishnet_amd import gpu_nnue as G
+big, small, n, out = sys.argv[1], sys.argv[2], int(sys.argv[3]), sys.argv[4]
+fens = [G.board_to_fen(b) for b in G.random_positions(0x5EED0DD5, 0, n, 160)]
+ctx = G.GpuNnue(big, small, devices=[0])
+np.save(out, np.stack([ctx.evaluate_batch(fens, m) for m in (G.MODE_SMALL, G.MODE_FULL)]))
+ctx.close()
+"""
+
+
+def test_small_net_odd_gather_depth_vs_oracle(gpu_ctx, synth_big_path, synth_small_path, oracle_nets, oracle_lib,
+                                              tmp_path):
+    """eval_net<128>'s gather keeps GN_SMALL_DEPTH rows in flight (default 4); an odd
+    depth adds its last row on its own and takes a tail of up to D - 1 rows.  The variant library
+    built with depth 5 (fishnet_amd/build.py ODD_LIB), in a process of its own, evaluates 4,096
+    random-playout positions (2..32 pieces: every remainder of the row count mod 5) in modes SMALL
+    and FULL: equal to the oracle and to the default library."""
+    import subprocess
+    import sys
+    from fishnet_amd import build, gpu_nnue as G
+    assert os.path.exists(build.ODD_LIB), "run __graft_entry__.build() (builds the odd-depth library)"
+    n = 4096
+    dst = str(tmp_path / "odd.npy")
+    env = dict(os.environ, GPU_NNUE_LIB=build.ODD_LIB)
+    p = subprocess.run([sys.executable, "-c", _ODD_CHILD, synth_big_path, synth_small_path, str(n), dst],
+                       env=env, cwd=os.path.dirname(HERE), capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr[-3000:]
+    got = np.load(dst)
+    fens = [G.board_to_fen(b) for b in G.random_positions(0x5EED0DD5, 0, n, 160)]
+    big, small = oracle_nets
+    for k, m in enumerate((G.MODE_SMALL, G.MODE_FULL)):
+        assert np.array_equal(got[k], gpu_ctx.evaluate_batch(fens, m)), m
+        assert np.array_equal(got[k], oracle_lib.eval_fens(big, small, fens, m)), m
