@@ -183,10 +183,13 @@ class Ctx:
             self.nn.set_option(G.OPT_CHAIN, args.chain)
         if args.king_cache is not None:
             self.nn.set_option(G.OPT_KING_CACHE, args.king_cache)
+        if args.pipeline is not None:
+            self.nn.set_option(G.OPT_EXPAND_PIPELINE, args.pipeline)
         self.options = {"xcd_swizzle": self.nn.get_option(G.OPT_XCD_SWIZZLE),
                         "king_sort": self.nn.get_option(G.OPT_KING_SORT),
                         "incremental_children": self.nn.get_option(G.OPT_INCREMENTAL_CHILDREN),
-                        "chain": self.nn.get_option(G.OPT_CHAIN), "king_cache": self.nn.get_option(G.OPT_KING_CACHE)}
+                        "chain": self.nn.get_option(G.OPT_CHAIN), "king_cache": self.nn.get_option(G.OPT_KING_CACHE),
+                        "expand_pipeline": self.nn.get_option(G.OPT_EXPAND_PIPELINE)}
         self._onets = None
 
     def oracle_nets(self):
@@ -787,6 +790,7 @@ def main():
     ap.add_argument("--king-sort", type=int, default=-1, help="GN_OPT_KING_SORT (-1: library default)")
     ap.add_argument("--chain", type=int, default=None, help="GN_OPT_CHAIN (None: library default; -k: exactly k)")
     ap.add_argument("--king-cache", type=int, default=None, help="GN_OPT_KING_CACHE (None: library default)")
+    ap.add_argument("--pipeline", type=int, default=None, help="GN_OPT_EXPAND_PIPELINE (None: library default)")
     ap.add_argument("--abi-games", type=int, default=0,
                     help="only the secondary.abi_games line with this many games per GPU (A/B runs)")
     ap.add_argument("--launch-check", action="store_true", help=argparse.SUPPRESS)

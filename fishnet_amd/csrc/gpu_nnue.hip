@@ -232,6 +232,35 @@ struct FastBatch {
   }
 };
 
+// The buffers one expansion's front half (child generation, classify, small net, plan) writes and
+// its back half (row stream, finalize, score rule) reads: the expansion pipeline (expand_pipeline
+// below) runs expansion k + 1's front on the device's second stream while expansion k's back
+// runs, in the other set (swap_sets: the Dev's own fields are always the current set).
+struct ExpSet {
+  DevBuf<uint64_t> counts, offsets;
+  DevBuf<uint32_t> owner;
+  DevBuf<Board> unpacked;
+  DevBuf<uint16_t> moves_tmp;
+  const uint16_t *child_moves = nullptr;
+  DevBuf<int2> pinfo, p_osm, p_obg;
+  DevBuf<uint8_t> p_nsm, p_nbg;
+  EvalBufs eb;
+  DevBuf<gn_board> children;
+  int chain_k = 1, slices = 1;
+  bool planned = false;
+  uint64_t etot = 0;
+  void *scan_tmp = nullptr, *sort_tmp = nullptr; // (the two streams' scans / sorts run at once)
+  size_t scan_bytes = 0, sort_bytes = 0;
+  void release() {
+    counts.release(), offsets.release(), owner.release(), unpacked.release(), moves_tmp.release();
+    pinfo.release(), p_osm.release(), p_obg.release(), p_nsm.release(), p_nbg.release(), eb.release();
+    children.release();
+    if (scan_tmp) (void)hipFree(scan_tmp);
+    if (sort_tmp) (void)hipFree(sort_tmp);
+    scan_tmp = sort_tmp = nullptr, scan_bytes = sort_bytes = 0;
+  }
+};
+
 struct Dev {
   int id = 0;
   hipStream_t stream = nullptr;
@@ -262,6 +291,7 @@ struct Dev {
   DevBuf<int32_t> part;  // column-sliced stream: fc_0 partial sums of the 3 slices (3 x positions x 16)
   DevBuf<int2> pinfo;    // ... and each position's (PSQT value, bucket) for the finish
   int chain_k = 1;          // block length of the current expansion (1: no chaining)
+  int slices = 1;           // the current expansion's stream: column slices (3) or whole rows (1)
   // planned expansion (stream.hip): per-parent entry bounds and their scan, the entry
   // lists, tile descriptors, the scratch-slot pool and the error word
   DevBuf<uint64_t> ebound, eoff;
@@ -314,8 +344,29 @@ struct Dev {
   double t_upload = 0, t_replay = 0, t_compute = 0, t_download = 0, t_tail = 0;
   // the drop-in's small-batch graphs (FastBatch): one per size class (128 << k positions) and mode
   std::unique_ptr<FastBatch> fast[6][3];
+  // the expansion pipeline: the other buffer set, the front's stream and its two events (the
+  // back's row stream done: the front may overwrite the plan's lists; the plan done)
+  ExpSet alt;
+  hipStream_t front = nullptr;
+  hipEvent_t ev_streamed = nullptr, ev_planned = nullptr;
   std::mutex mu;
 };
+
+// The Dev's current expansion buffers <-> its other set (host-side pointers only: launches already
+// queued keep the buffers they were given).
+static void swap_sets(Dev &d) {
+  ExpSet &x = d.alt;
+  std::swap(d.counts, x.counts), std::swap(d.offsets, x.offsets), std::swap(d.owner, x.owner);
+  std::swap(d.unpacked, x.unpacked), std::swap(d.moves_tmp, x.moves_tmp), std::swap(d.child_moves, x.child_moves);
+  std::swap(d.pinfo, x.pinfo), std::swap(d.p_osm, x.p_osm), std::swap(d.p_obg, x.p_obg);
+  std::swap(d.p_nsm, x.p_nsm), std::swap(d.p_nbg, x.p_nbg);
+  std::swap(d.eb.osm, x.eb.osm), std::swap(d.eb.obg, x.eb.obg), std::swap(d.eb.nsm, x.eb.nsm), std::swap(d.eb.nbg, x.eb.nbg);
+  std::swap(d.frontier[1], x.children);
+  std::swap(d.chain_k, x.chain_k), std::swap(d.slices, x.slices), std::swap(d.planned, x.planned);
+  std::swap(d.etot, x.etot);
+  std::swap(d.scan_tmp, x.scan_tmp), std::swap(d.scan_bytes, x.scan_bytes);
+  std::swap(d.sort_tmp, x.sort_tmp), std::swap(d.sort_bytes, x.sort_bytes);
+}
 
 // Called under d.mu before a launch sequence on stream s / after it.
 static hipError_t seq_begin(Dev &d, hipStream_t s) {
@@ -379,6 +430,7 @@ struct gn_ctx {
   } co;
   bool coalesce = true;
   bool fast_batch = true;                  // GN_OPT_FAST_BATCH
+  bool pipeline = true;                    // GN_OPT_EXPAND_PIPELINE
   std::atomic<uint64_t> graph_gen{0};      // bumped by every option / parameter change: the small-
                                            // batch graphs captured before it are rebuilt
   std::atomic<uint64_t> fast_runs{0}, fast_fallbacks{0};
@@ -491,6 +543,10 @@ static void destroy(gn_ctx *ctx) {
     d.off32.release(), d.moves.release(), d.sum.release(), d.deltas.release();
     d.moves_tmp.release(), d.owner.release(), d.unpacked.release();
     d.p_osm.release(), d.p_obg.release(), d.p_nsm.release(), d.p_nbg.release();
+    d.part.release(), d.pinfo.release(), d.alt.release();
+    if (d.front) (void)hipStreamSynchronize(d.front), (void)hipStreamDestroy(d.front);
+    if (d.ev_streamed) (void)hipEventDestroy(d.ev_streamed);
+    if (d.ev_planned) (void)hipEventDestroy(d.ev_planned);
     if (d.scan_tmp) (void)hipFree(d.scan_tmp);
     if (d.sort_tmp) (void)hipFree(d.sort_tmp);
     d.kkeys.release(), d.kkeys2.release(), d.kidx.release(), d.kperm.release();
@@ -549,6 +605,9 @@ static int create(const uint8_t *big, size_t big_len, const uint8_t *small, size
     HIP_TRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
     HIP_TRY(hipEventCreateWithFlags(&d.done, hipEventDisableTiming));
     HIP_TRY(hipStreamCreateWithFlags(&d.copy, hipStreamNonBlocking));
+    HIP_TRY(hipStreamCreateWithFlags(&d.front, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreateWithFlags(&d.ev_streamed, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&d.ev_planned, hipEventDisableTiming));
     for (int i = 0; i < 2; ++i) HIP_TRY(hipEventCreateWithFlags(&d.cev[i], hipEventDisableTiming));
 #ifdef GN_AB_AUX_STREAMS // A/B only: two extra streams, as the removed range pipeline had
     {
@@ -789,13 +848,20 @@ static int generate_children(Dev &d, const gn_board *parents, size_t n, gn_board
 // after the big net, after finalize, and (planned path) between its plan and stream kernels.
 // score_parents: the parents are positions (the score rule's static part; callers run
 // resolve_scores on them) rather than child records (depth 2's level 2).
+// phases: EXP_FRONT (classify, the small net, the big net's plan) and / or EXP_BACK (the big net's
+// row stream, finalize); the expansion pipeline runs the two on different streams.  ev (optional):
+// [0] after classify, [1] after the small net, [2] after the big net, [3] after finalize, [4] the
+// plan -> stream boundary, [6] after the stream launches, [7] (EXP_BACK alone) the stream's start.
+constexpr int EXP_FRONT = 1, EXP_BACK = 2;
 static int expand_evaluate(gn_ctx *ctx, Dev &d, const gn_board *parents, size_t n, const gn_board *children,
                            size_t total, int mode, gn_eval *parent_out, gn_eval *child_out, hipStream_t s,
-                           hipEvent_t *ev, unsigned long long *rows_out = nullptr, bool score_parents = true) {
+                           hipEvent_t *ev, unsigned long long *rows_out = nullptr, bool score_parents = true,
+                           int phases = EXP_FRONT | EXP_BACK) {
   if (mode < GN_MODE_FULL || mode > GN_MODE_SMALL) return fail(GN_E_INVALID, "bad mode %d", mode);
   if ((mode != GN_MODE_SMALL && !d.has[BIG]) || (mode != GN_MODE_BIG && !d.has[SMALL]))
     return fail(GN_E_NONET, "mode %d needs a network that is not loaded", mode);
   if (!ctx->incremental) {
+    if (!(phases & EXP_BACK)) return GN_OK; // (no front half: every child is a full refresh)
     if (total) {
       int rc = evaluate_on(ctx, d, children, total, mode, child_out, s, nullptr, nullptr, 0);
       if (rc) return rc;
@@ -804,50 +870,47 @@ static int expand_evaluate(gn_ctx *ctx, Dev &d, const gn_board *parents, size_t 
                                     d.counts.p)
                       : GN_OK;
   }
-  const size_t nt = std::max<size_t>(total, 1);
-  if (mode != GN_MODE_BIG) {
-    HIP_TRY(d.osm.ensure(nt));
-    HIP_TRY(d.p_osm.ensure(n));
-  }
-  if (mode != GN_MODE_SMALL) {
-    HIP_TRY(d.obg.ensure(nt));
-    HIP_TRY(d.p_obg.ensure(n));
-  }
-  if (mode == GN_MODE_FULL) {
-    HIP_TRY(d.nsm.ensure(nt));
-    HIP_TRY(d.nbg.ensure(nt));
-    HIP_TRY(d.p_nsm.ensure(n));
-    HIP_TRY(d.p_nbg.ensure(n));
-  }
   auto mark = [&](int k) -> hipError_t { return ev ? hipEventRecord(ev[k], s) : hipSuccess; };
   const gn_eval_params &P = ctx->P;
   const uint64_t *off = d.offsets.p;
   const ChildDelta *dl = d.deltas.p;
-  if (mode == GN_MODE_FULL) {
-    HIP_TRY(launch_classify(parents, n, P, d.p_nsm.p, d.p_nbg.p, s));
-    HIP_TRY(launch_classify(children, total, P, d.nsm.p, d.nbg.p, s));
-  }
-  HIP_TRY(mark(0));
-  if (mode != GN_MODE_BIG) {
-    const bool f = mode == GN_MODE_FULL;
-    HIP_TRY(launch_expand_net(d.net[SMALL], parents, n, off, children, dl, f ? d.p_nsm.p : nullptr,
-                              f ? d.nsm.p : nullptr, d.p_osm.p, d.osm.p, ctx->swizzle & 1, s));
-    if (f) {
-      HIP_TRY(launch_reeval(d.p_osm.p, d.p_nsm.p, n, P, d.p_nbg.p, s));
-      HIP_TRY(launch_reeval(d.osm.p, d.nsm.p, total, P, d.nbg.p, s));
+  const bool f = mode == GN_MODE_FULL;
+  const size_t K = (size_t)std::max(1, d.chain_k), nblk = (n + K - 1) / K;
+  // ---- the front half: selections, the small net, the plan (the stream's lists and tiles)
+  if (phases & EXP_FRONT) {
+    const size_t nt = std::max<size_t>(total, 1);
+    if (mode != GN_MODE_BIG) {
+      HIP_TRY(d.osm.ensure(nt));
+      HIP_TRY(d.p_osm.ensure(n));
     }
-  }
-  HIP_TRY(mark(1));
-  bool fused = false; // the sliced stream's finish runs inside finalize
-  if (mode != GN_MODE_SMALL) {
-    const bool f = mode == GN_MODE_FULL;
-    if (d.planned) {
-      const size_t K = (size_t)std::max(1, d.chain_k), nblk = (n + K - 1) / K;
+    if (mode != GN_MODE_SMALL) {
+      HIP_TRY(d.obg.ensure(nt));
+      HIP_TRY(d.p_obg.ensure(n));
+    }
+    if (f) {
+      HIP_TRY(d.nsm.ensure(nt));
+      HIP_TRY(d.nbg.ensure(nt));
+      HIP_TRY(d.p_nsm.ensure(n));
+      HIP_TRY(d.p_nbg.ensure(n));
+      HIP_TRY(launch_classify(parents, n, P, d.p_nsm.p, d.p_nbg.p, s));
+      HIP_TRY(launch_classify(children, total, P, d.nsm.p, d.nbg.p, s));
+    }
+    HIP_TRY(mark(0));
+    if (mode != GN_MODE_BIG) {
+      HIP_TRY(launch_expand_net(d.net[SMALL], parents, n, off, children, dl, f ? d.p_nsm.p : nullptr,
+                                f ? d.nsm.p : nullptr, d.p_osm.p, d.osm.p, ctx->swizzle & 1, s));
+      if (f) {
+        HIP_TRY(launch_reeval(d.p_osm.p, d.p_nsm.p, n, P, d.p_nbg.p, s));
+        HIP_TRY(launch_reeval(d.osm.p, d.nsm.p, total, P, d.nbg.p, s));
+      }
+    }
+    HIP_TRY(mark(1));
+    d.slices = 1;
+    if (mode != GN_MODE_SMALL && d.planned) {
       HIP_TRY(d.ent.ensure(d.etot + (size_t)ENT_SPARE * (nblk + 1)));
       HIP_TRY(d.tiles.ensure((n + total) / 16 + (K + 2) * nblk + 2));
       HIP_TRY(d.btiles.ensure(nblk + 1));
       HIP_TRY(d.pool.ensure(88)); // 8 XCDs x 8 words of scratch-slot bits, then 8 block claim counters
-      HIP_TRY(hipMemsetAsync(d.pool.p, 0, 88 * sizeof(uint32_t), s)); // per stream launch (<= 3)
       int slices = d.net[BIG].L1 == 3072 && ctx->stream_slices == 3 ? 3 : 1;
       // the sliced stream's partial sums cost 200 B per position (include/gpu_nnue.h,
       // GN_OPT_STREAM_SLICES); when they do not fit, the whole-row stream gives the same results
@@ -856,8 +919,8 @@ static int expand_evaluate(gn_ctx *ctx, Dev &d, const gn_board *parents, size_t 
         d.part.release(), d.pinfo.release();
         slices = 1;
       }
+      d.slices = slices;
       // XCD-local block order
-      const uint32_t *order = nullptr;
       if (ctx->king_sort && nblk > 1) {
         HIP_TRY(d.bkeys.ensure(nblk));
         HIP_TRY(d.bkeys2.ensure(nblk));
@@ -865,18 +928,34 @@ static int expand_evaluate(gn_ctx *ctx, Dev &d, const gn_board *parents, size_t 
         HIP_TRY(d.border.ensure(nblk));
         HIP_TRY(block_order(parents, n, (uint32_t)K, (uint32_t)nblk, d.bkeys.p, d.bidx.p, d.bkeys2.p, d.border.p,
                             d.sort_tmp, d.sort_bytes, s));
-        order = d.border.p;
       }
+      HIP_TRY(launch_plan_stream(d.net[BIG], parents, n, off, dl, f ? d.p_nbg.p : nullptr, f ? d.nbg.p : nullptr,
+                                 d.p_obg.p, d.obg.p, 0, d.chain_k > 1 ? d.nslot.p : nullptr, d.chain_k,
+                                 ctx->king_cache ? 1 : 0, d.eoff.p, d.ent.p, d.tiles.p, d.btiles.p, d.pool.p, d.perr.p,
+                                 rows_out, d.pstat.p, 0, nblk, nullptr, ev ? ev[4] : nullptr, s, slices,
+                                 slices > 1 ? d.part.p : nullptr, n + total, slices > 1 ? d.pinfo.p : nullptr,
+                                 nullptr, false, PLAN_PHASE));
+    }
+  }
+  if (!(phases & EXP_BACK)) return GN_OK;
+  // ---- the back half: the big net's row stream, finalize
+  bool fused = false; // the sliced stream's finish runs inside finalize
+  if (mode != GN_MODE_SMALL) {
+    if (d.planned) {
+      const int slices = d.slices;
+      const uint32_t *order = ctx->king_sort && nblk > 1 ? d.border.p : nullptr;
+      HIP_TRY(hipMemsetAsync(d.pool.p, 0, 88 * sizeof(uint32_t), s)); // per stream launch (<= 3)
 #ifndef GN_AB_FINISH_SEPARATE // A/B (round 4): slice_finish_kernel, then finalize
       fused = slices > 1;
 #endif
+      if (ev && (phases & EXP_FRONT) == 0) HIP_TRY(hipEventRecord(ev[7], s)); // (the pipeline: the stream's start)
       HIP_TRY(launch_plan_stream(d.net[BIG], parents, n, off, dl, f ? d.p_nbg.p : nullptr, f ? d.nbg.p : nullptr,
                                  d.p_obg.p, d.obg.p, (ctx->swizzle >> 2) & 1 ? 1 : (ctx->swizzle >> 3) & 1 ? 2 : 0,
                                  d.chain_k > 1 ? d.nslot.p : nullptr, d.chain_k,
                                  ctx->king_cache ? 1 : 0, d.eoff.p, d.ent.p, d.tiles.p, d.btiles.p, d.pool.p, d.perr.p,
-                                 rows_out, d.pstat.p, 0, nblk, order, ev ? ev[4] : nullptr, s, slices,
+                                 rows_out, d.pstat.p, 0, nblk, order, nullptr, s, slices,
                                  slices > 1 ? d.part.p : nullptr, n + total, slices > 1 ? d.pinfo.p : nullptr,
-                                 ev ? ev[6] : nullptr, !fused));
+                                 ev ? ev[6] : nullptr, !fused, STREAM_PHASE));
     } else { // a 128-wide net loaded as the big net
       HIP_TRY(launch_expand_net(d.net[BIG], parents, n, off, children, dl, f ? d.p_nbg.p : nullptr,
                                 f ? d.nbg.p : nullptr, d.p_obg.p, d.obg.p, ctx->swizzle & 1, s));
@@ -2370,7 +2449,7 @@ int gn_time_expand_device(gn_ctx *ctx, int device_slot, const gn_board *d_parent
   // start, [count+scan], [total read], [write], [classify], [small], [big], [finalize], the
   // planned big net's plan -> stream boundary, [score rule] (ends at e[9]), and the stream ->
   // finish boundary (e[10])
-  const int NE = 11;
+  const int NE = 12;
   std::vector<hipEvent_t> ev((size_t)iters * NE + 2, nullptr);
   auto cleanup = [&] {
     for (auto &e : ev)
@@ -2386,7 +2465,58 @@ int gn_time_expand_device(gn_ctx *ctx, int device_slot, const gn_board *d_parent
   HIP_TRY(d->sum.ensure(2)); // [0] rows by write_children's formula, [1] rows the row stream gathered
   HIP_TRY(hipMemsetAsync(d->sum.p, 0, 2 * sizeof(unsigned long long), s));
   hipError_t he = hipEventRecord(ev[0], s);
-  for (int it = 0; it < iters && rc == GN_OK && he == hipSuccess; ++it) {
+  // the expansion pipeline (GN_OPT_EXPAND_PIPELINE): expansion it + 1's front half (children,
+  // plan) on the device's second stream, into the other buffer set, while expansion it's finalize
+  // and score rule run; its row stream waits for that plan
+  const bool pipe = ctx->pipeline && plan_path(ctx, *d, mode) && ctx->incremental && iters > 1;
+  if (pipe && he == hipSuccess) {
+    hipStream_t B = d->front;
+    size_t tn = 0; // the children of the expansion whose front ran last
+    auto front = [&](int it) -> int {
+      hipEvent_t *e = &ev[2 + (size_t)NE * it];
+      HIP_TRY(hipEventRecord(e[0], B));
+      // (moves into the set's own buffer: the caller's is written once, after the last expansion)
+      int r = generate_children(*d, d_parents, n, nullptr, cap, nullptr, true, &tn, B, e + 1, nullptr,
+                                chain_len(ctx, *d, n), true, mode == GN_MODE_BIG);
+      if (r) return r;
+      if (d_child_out && tn > cap) return fail(GN_E_CAPACITY, "%zu children exceed capacity %zu", tn, cap);
+      r = expand_evaluate(ctx, *d, d_parents, n, d->frontier[1].p, tn, mode, nullptr, nullptr, B, e + 4,
+                          it == 0 ? d->sum.p + 1 : nullptr, true, EXP_FRONT);
+      if (r) return r;
+      HIP_TRY(hipEventRecord(d->ev_planned, B));
+      return GN_OK;
+    };
+    // the front starts after what the stream holds so far (the sequence guard's wait, the reset)
+    he = hipEventRecord(d->ev_streamed, s);
+    if (he == hipSuccess) he = hipStreamWaitEvent(B, d->ev_streamed, 0);
+    if (he == hipSuccess) rc = front(0);
+    t = tn;
+    HIP_TRY(d->io_out.ensure(n));
+    HIP_TRY(d->io_out2.ensure(std::max<size_t>(t, 1)));
+    gn_eval *po = d_parent_out ? d_parent_out : d->io_out.p, *co = d_child_out ? d_child_out : d->io_out2.p;
+    for (int it = 0; it < iters && rc == GN_OK && he == hipSuccess; ++it) {
+      hipEvent_t *e = &ev[2 + (size_t)NE * it];
+      if ((he = hipStreamWaitEvent(s, d->ev_planned, 0)) != hipSuccess) break;
+      rc = expand_evaluate(ctx, *d, d_parents, n, d->frontier[1].p, t, mode, po, co, s, e + 4, nullptr, true,
+                           EXP_BACK);
+      if (rc) break;
+      const bool more = it + 1 < iters;
+      if (more) { // the next front, after this row stream (it overwrites the plan's lists)
+        swap_sets(*d);
+        he = hipStreamWaitEvent(B, e[10], 0);
+        if (he == hipSuccess) rc = front(it + 1);
+        swap_sets(*d);
+        if (rc || he != hipSuccess) break;
+      }
+      const Replies rp{co, d->child_moves};
+      rc = resolve_scores(ctx, *d, d_parents, n, mode, po, nullptr, s, 2, &rp);
+      if (rc == GN_OK) he = hipEventRecord(e[9], s);
+      if (more) swap_sets(*d), t = tn;
+    }
+    if (rc == GN_OK && he == hipSuccess && d_moves && t)
+      he = hipMemcpyAsync(d_moves, d->child_moves, t * sizeof(uint16_t), hipMemcpyDeviceToDevice, s);
+  }
+  for (int it = 0; !pipe && it < iters && rc == GN_OK && he == hipSuccess; ++it) {
     hipEvent_t *e = &ev[2 + (size_t)NE * it];
     he = hipEventRecord(e[0], s);
     if (he != hipSuccess) break;
@@ -2414,14 +2544,21 @@ int gn_time_expand_device(gn_ctx *ctx, int device_slot, const gn_board *d_parent
   if (rc == GN_OK && he == hipSuccess) he = hipEventRecord(ev[1], s);
   if (rc == GN_OK && he == hipSuccess) he = hipEventSynchronize(ev[1]);
   if (rc == GN_OK && he == hipSuccess) he = hipEventElapsedTime(ms_total, ev[0], ev[1]);
+  // stage k from event k to k + 1 (score: 7 -> 9).  Pipelined, the front's stages are on the second
+  // stream and the big net is the plan (5 -> 8) plus the stream (11 -> 10, after its wait)
   if (rc == GN_OK && he == hipSuccess && stage_ms) {
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (int it = 0; it < iters && he == hipSuccess; ++it)
       for (int k = 0; k < 8 && he == hipSuccess; ++k) {
-        float ms = 0;
+        float ms = 0, ms2 = 0;
         const size_t o = 2 + (size_t)NE * it;
-        he = hipEventElapsedTime(&ms, ev[o + k], ev[o + (k < 7 ? k + 1 : 9)]);
-        acc[k] += ms;
+        if (pipe && k == 5) {
+          he = hipEventElapsedTime(&ms, ev[o + 5], ev[o + 8]);
+          if (he == hipSuccess) he = hipEventElapsedTime(&ms2, ev[o + 11], ev[o + 6]);
+        } else {
+          he = hipEventElapsedTime(&ms, ev[o + k], ev[o + (k < 7 ? k + 1 : 9)]);
+        }
+        acc[k] += ms + ms2;
       }
     for (int k = 0; k < 8; ++k) stage_ms[k] = acc[k] / (float)iters;
   }
@@ -2431,7 +2568,7 @@ int gn_time_expand_device(gn_ctx *ctx, int device_slot, const gn_board *d_parent
       float a = 0, b = 0, c = 0;
       const size_t o = 2 + (size_t)NE * it;
       he = hipEventElapsedTime(&a, ev[o + 5], ev[o + 8]);
-      if (he == hipSuccess) he = hipEventElapsedTime(&b, ev[o + 8], ev[o + 10]); // the stream launches
+      if (he == hipSuccess) he = hipEventElapsedTime(&b, ev[o + (pipe ? 11 : 8)], ev[o + 10]); // the stream launches
       if (he == hipSuccess) he = hipEventElapsedTime(&c, ev[o + 10], ev[o + 6]);  // the sliced stream's finish
       pl += a, st += b, fi += c;
     }
@@ -2516,6 +2653,9 @@ int gn_set_option(gn_ctx *ctx, int option, int64_t value) {
   case GN_OPT_FAST_BATCH:
     ctx->fast_batch = value != 0;
     return GN_OK;
+  case GN_OPT_EXPAND_PIPELINE:
+    ctx->pipeline = value != 0;
+    return GN_OK;
   default:
     return fail(GN_E_INVALID, "unknown option %d", option);
   }
@@ -2550,6 +2690,9 @@ int gn_get_option(const gn_ctx *ctx, int option, int64_t *value) {
     return GN_OK;
   case GN_OPT_FAST_BATCH:
     *value = ctx->fast_batch;
+    return GN_OK;
+  case GN_OPT_EXPAND_PIPELINE:
+    *value = ctx->pipeline;
     return GN_OK;
   case GN_STAT_FAST_BATCHES:
     *value = (int64_t)ctx->fast_runs.load();

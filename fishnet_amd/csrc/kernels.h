@@ -110,6 +110,10 @@ static_assert(sizeof(TileDesc) == 192, "TileDesc is 192 bytes");
 // (before the finish).  finish false (sliced stream): no slice_finish_kernel, out_parent /
 // out_child stay unwritten: the caller's launch_finalize takes the big net's outputs from part
 // and pinfo itself.
+// phases: PLAN_PHASE (the pinfo reset and plan_kernel) and / or STREAM_PHASE (the stream launches
+// and the finish), so that an expansion's plan can run on another stream than its row stream (the
+// expansion pipeline, gpu_nnue.hip): the two calls take the same arguments.
+constexpr int PLAN_PHASE = 1, STREAM_PHASE = 2;
 hipError_t launch_plan_stream(const NetDevice &net, const gn_board *parents, size_t n, const uint64_t *offsets,
                               const ChildDelta *deltas, const uint8_t *need_parent, const uint8_t *need_child,
                               int2 *out_parent, int2 *out_child, int swz, const uint8_t *next_slot, int chain_k,
@@ -117,7 +121,8 @@ hipError_t launch_plan_stream(const NetDevice &net, const gn_board *parents, siz
                               uint32_t *pool, uint32_t *err, unsigned long long *rows_out,
                               unsigned long long *pads_out, size_t b0, size_t b1, const uint32_t *order,
                               hipEvent_t mid, hipStream_t s, int slices = 1, int32_t *part = nullptr,
-                              size_t npos = 0, int2 *pinfo = nullptr, hipEvent_t fin = nullptr, bool finish = true);
+                              size_t npos = 0, int2 *pinfo = nullptr, hipEvent_t fin = nullptr, bool finish = true,
+                              int phases = PLAN_PHASE | STREAM_PHASE);
 // GN_MODE_FULL preparation: need_small = valid && |simple_eval| > threshold,
 // need_big = valid && !need_small.
 hipError_t launch_classify(const gn_board *boards, size_t n, const gn_eval_params &P, uint8_t *need_small,

@@ -1506,8 +1506,9 @@ hipError_t launch_plan_stream(const NetDevice &net, const gn_board *parents, siz
                               uint32_t *pool, uint32_t *err, unsigned long long *rows_out,
                               unsigned long long *pads_out, size_t b0, size_t b1, const uint32_t *order,
                               hipEvent_t mid, hipStream_t s, int slices, int32_t *part, size_t npos,
-                              int2 *pinfo, hipEvent_t fin, bool finish) {
+                              int2 *pinfo, hipEvent_t fin, bool finish, int phases) {
   if (!n || b1 <= b0) return hipSuccess;
+  const bool do_plan = phases & PLAN_PHASE, do_stream = phases & STREAM_PHASE;
   if (n >= 0x80000000ull) return hipErrorInvalidValue; // 32-bit parent indices in the kernels
   const uint32_t K = chain_k > 1 && next_slot ? (uint32_t)chain_k : 1u;
   const int scr = K > 1 && kc; // the king cache's rows (the chained walk itself needs no scratch)
@@ -1516,16 +1517,19 @@ hipError_t launch_plan_stream(const NetDevice &net, const gn_board *parents, siz
   const unsigned pg = (nb + 3) / 4, g = swz == 1 ? 8 * ((nb + 7) / 8) : nb + nb / 16 + 8; // (stream_eval_kernel: claims)
   if (net.L1 == 3072) {
     const bool sliced = slices == 3 && part && pinfo;
-    if (sliced) { // (positions the big net does not evaluate keep pinfo.y < 0; the plan writes the rest)
-      hipError_t e = hipMemsetAsync(pinfo, 0xFF, npos * sizeof(int2), s);
-      if (e != hipSuccess) return e;
+    if (do_plan) {
+      if (sliced) { // (positions the big net does not evaluate keep pinfo.y < 0; the plan writes the rest)
+        hipError_t e = hipMemsetAsync(pinfo, 0xFF, npos * sizeof(int2), s);
+        if (e != hipSuccess) return e;
+      }
+      hipLaunchKernelGGL((plan_kernel<3072>), dim3(pg), dim3(256), 0, s, net, parents, offsets, deltas, need_parent,
+                         need_child, K > 1 ? next_slot : nullptr, (uint32_t)n, K, B0, B1, K > 1 ? kc : 0, eoff, ent,
+                         tiles, btiles, rows_out, pads_out, err, sliced ? pinfo : nullptr,
+                         sliced ? ps::field_xu(3072, 3) : ps::field_xu(3072, 1), sliced ? ps::field_hu(3072, 3) : ps::field_hu(3072, 1));
+      if (mid) (void)hipEventRecord(mid, s);
     }
-    hipLaunchKernelGGL((plan_kernel<3072>), dim3(pg), dim3(256), 0, s, net, parents, offsets, deltas, need_parent,
-                       need_child, K > 1 ? next_slot : nullptr, (uint32_t)n, K, B0, B1, K > 1 ? kc : 0, eoff, ent,
-                       tiles, btiles, rows_out, pads_out, err, sliced ? pinfo : nullptr,
-                       sliced ? ps::field_xu(3072, 3) : ps::field_xu(3072, 1), sliced ? ps::field_hu(3072, 3) : ps::field_hu(3072, 1));
-    if (mid) (void)hipEventRecord(mid, s);
-    if (sliced) { // three launches over 1,024 columns each (claim counters pool[64 + 8 slice ..]),
+    if (!do_stream) {
+    } else if (sliced) { // three launches over 1,024 columns each (claim counters pool[64 + 8 slice ..]),
       // then the finish
       for (int sl = 0; sl < 3; ++sl)
         hipLaunchKernelGGL((stream_eval_kernel<3072, 3>), dim3(g), dim3(128), 0, s, net, offsets, (uint32_t)n, K, B0,
@@ -1542,14 +1546,18 @@ hipError_t launch_plan_stream(const NetDevice &net, const gn_board *parents, siz
       if (fin) (void)hipEventRecord(fin, s);
     }
   } else if (net.L1 == 1024) {
-    hipLaunchKernelGGL((plan_kernel<1024>), dim3(pg), dim3(256), 0, s, net, parents, offsets, deltas, need_parent,
-                       need_child, K > 1 ? next_slot : nullptr, (uint32_t)n, K, B0, B1, K > 1 ? kc : 0, eoff, ent,
-                       tiles, btiles, rows_out, pads_out, err, nullptr, ps::field_xu(1024, 1), ps::field_hu(1024, 1));
-    if (mid) (void)hipEventRecord(mid, s);
-    hipLaunchKernelGGL((stream_eval_kernel<1024>), dim3(g), dim3(128), 0, s, net, offsets, (uint32_t)n, K, B0, B1,
-                       swz, eoff, ent, tiles, btiles, order, out_parent, out_child, pool, scr, err, pool + 64, 0,
-                       nullptr, (uint64_t)0, nullptr);
-    if (fin) (void)hipEventRecord(fin, s);
+    if (do_plan) {
+      hipLaunchKernelGGL((plan_kernel<1024>), dim3(pg), dim3(256), 0, s, net, parents, offsets, deltas, need_parent,
+                         need_child, K > 1 ? next_slot : nullptr, (uint32_t)n, K, B0, B1, K > 1 ? kc : 0, eoff, ent,
+                         tiles, btiles, rows_out, pads_out, err, nullptr, ps::field_xu(1024, 1), ps::field_hu(1024, 1));
+      if (mid) (void)hipEventRecord(mid, s);
+    }
+    if (do_stream) {
+      hipLaunchKernelGGL((stream_eval_kernel<1024>), dim3(g), dim3(128), 0, s, net, offsets, (uint32_t)n, K, B0, B1,
+                         swz, eoff, ent, tiles, btiles, order, out_parent, out_child, pool, scr, err, pool + 64, 0,
+                         nullptr, (uint64_t)0, nullptr);
+      if (fin) (void)hipEventRecord(fin, s);
+    }
   } else {
     return hipErrorInvalidValue;
   }

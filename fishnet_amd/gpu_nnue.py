@@ -50,7 +50,7 @@ EXPORTS = ["gn_load_net", "gn_load_net_memory", "gn_free", "gn_last_error", "gn_
            "gn_boards_to_fens", "gn_load_net_archive", "gn_archive_read", "gn_expand2_device",
            "gn_random_games_uci"]
 OPT_INCREMENTAL_CHILDREN, OPT_XCD_SWIZZLE, OPT_KING_SORT, OPT_CHAIN, OPT_KING_CACHE = 1, 2, 3, 4, 5
-OPT_CHUNK_PARENTS, OPT_COALESCE, OPT_STREAM_SLICES, OPT_FAST_BATCH = 6, 7, 8, 9
+OPT_CHUNK_PARENTS, OPT_COALESCE, OPT_STREAM_SLICES, OPT_FAST_BATCH, OPT_EXPAND_PIPELINE = 6, 7, 8, 9, 10
 STAT_PLAN_NS, STAT_STREAM_NS, STAT_SCRATCH_PADS, STAT_FINISH_NS = 101, 102, 103, 104
 STAT_BATCH_LAUNCHES, STAT_BATCH_CALLS, STAT_FAST_BATCHES, STAT_FAST_FALLBACKS = 117, 118, 119, 120
 HOST_STAGES = {"parse": 110, "upload": 111, "replay": 112, "compute": 113, "download": 114, "tail": 115, "total": 116}

@@ -37,6 +37,7 @@ pub const GN_OPT_CHUNK_PARENTS: c_int = 6;
 pub const GN_OPT_COALESCE: c_int = 7;
 pub const GN_OPT_STREAM_SLICES: c_int = 8;
 pub const GN_OPT_FAST_BATCH: c_int = 9;
+pub const GN_OPT_EXPAND_PIPELINE: c_int = 10;
 // read-only statistics (gn_get_option)
 pub const GN_STAT_PLAN_NS: c_int = 101;
 pub const GN_STAT_STREAM_NS: c_int = 102;

@@ -1077,3 +1077,51 @@ def test_small_net_odd_gather_depth_vs_oracle(gpu_ctx, synth_big_path, synth_sma
     for k, m in enumerate((G.MODE_SMALL, G.MODE_FULL)):
         assert np.array_equal(got[k], gpu_ctx.evaluate_batch(fens, m)), m
         assert np.array_equal(got[k], oracle_lib.eval_fens(big, small, fens, m)), m
+
+
+def test_expand_pipeline_equals_serial(gpu_ctx, oracle_nets, oracle_lib):
+    """GN_OPT_EXPAND_PIPELINE: gn_time_expand_device's iterations overlapped (expansion k + 1's
+    children and plan on the second stream, in the other buffer set, while expansion k's finalize
+    and score rule run) give every output of one serial expansion -- parents, offsets, moves,
+    children -- in modes BIG and FULL, for 2 and 3 iterations (each buffer set used as the last);
+    sampled parents with all their children against the oracle."""
+    from fishnet_amd import gpu_nnue as G
+    games, plies = 300, 80
+    n = games * (plies + 1)
+    d_b = gpu_ctx.alloc(n * 32)
+    gpu_ctx.random_games_device(0x5EED0F1F, 0, games, plies, d_b)
+    gpu_ctx.synchronize()
+    _, total, _, _ = gpu_ctx.time_expand_device(d_b, n, 1, 1)
+    out = {"po": gpu_ctx.alloc(n * G.EVAL_SIZE), "off": gpu_ctx.alloc((n + 1) * 4), "mv": gpu_ctx.alloc(total * 2),
+           "co": gpu_ctx.alloc(total * G.EVAL_SIZE), "cap": total}
+
+    def run(iters, pipe, mode):
+        gpu_ctx.set_option(G.OPT_EXPAND_PIPELINE, pipe)
+        for b in ("po", "off", "mv", "co"):
+            out[b].upload(np.zeros(out[b].nbytes, np.uint8))
+        _, t, _, _ = gpu_ctx.time_expand_device(d_b, n, mode, iters, outputs=out)
+        assert t == total
+        return tuple(gpu_ctx.checksum_device(out[b], nb) for b, nb in
+                     (("po", n * G.EVAL_SIZE), ("off", (n + 1) * 4), ("mv", t * 2), ("co", t * G.EVAL_SIZE)))
+
+    assert gpu_ctx.get_option(G.OPT_EXPAND_PIPELINE) == 1
+    try:
+        for mode in (1, 0):
+            serial = run(1, 0, mode)
+            assert run(2, 1, mode) == serial, mode
+            assert run(3, 1, mode) == serial, mode
+            assert run(3, 0, mode) == serial, mode
+    finally:
+        gpu_ctx.set_option(G.OPT_EXPAND_PIPELINE, 1)
+    run(3, 1, 1)  # pipelined, mode BIG: sampled parents with all their children against the oracle
+    big, small = oracle_nets
+    parents = d_b.download(G.BOARD_DTYPE, n)
+    offs = out["off"].download(np.uint32, n + 1)
+    pev = out["po"].download(G.EVAL_DTYPE, n)
+    for i in np.random.default_rng(5).choice(n, 24, replace=False):
+        lo, hi = int(offs[i]), int(offs[i + 1])
+        mv = out["mv"].download(np.uint16, hi - lo, offset=lo)
+        ev = out["co"].download(G.EVAL_DTYPE, hi - lo, offset=lo)
+        p_exp, m_exp, k_exp = oracle_lib.expand_eval(big, small, G.board_to_fen(parents[i]), 1, incremental=True)
+        assert tuple(pev[i]) == p_exp
+        assert dict(zip(mv.tolist(), map(tuple, ev.tolist()))) == dict(zip(m_exp, map(tuple, k_exp.tolist())))
