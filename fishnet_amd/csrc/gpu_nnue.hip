@@ -251,7 +251,10 @@ struct ExpSet {
   uint64_t etot = 0;
   void *scan_tmp = nullptr, *sort_tmp = nullptr; // (the two streams' scans / sorts run at once)
   size_t scan_bytes = 0, sort_bytes = 0;
+  DevBuf<uint32_t> perr;            // the planned expansion's error word ...
+  DevBuf<unsigned long long> pstat; // ... and pad count (each expansion of the pipeline its own)
   void release() {
+    perr.release(), pstat.release();
     counts.release(), offsets.release(), owner.release(), unpacked.release(), moves_tmp.release();
     pinfo.release(), p_osm.release(), p_obg.release(), p_nsm.release(), p_nbg.release(), eb.release();
     children.release();
@@ -366,6 +369,7 @@ static void swap_sets(Dev &d) {
   std::swap(d.etot, x.etot);
   std::swap(d.scan_tmp, x.scan_tmp), std::swap(d.scan_bytes, x.scan_bytes);
   std::swap(d.sort_tmp, x.sort_tmp), std::swap(d.sort_bytes, x.sort_bytes);
+  std::swap(d.perr, x.perr), std::swap(d.pstat, x.pstat);
 }
 
 // Called under d.mu before a launch sequence on stream s / after it.
@@ -616,8 +620,11 @@ static int create(const uint8_t *big, size_t big_len, const uint8_t *small, size
     }
 #endif
     HIP_TRY(hipMalloc(&d.tables, sizeof(Tables)));
-    HIP_TRY(d.perr.ensure(1)); // the planned expansion's error word and pad count
+    HIP_TRY(d.perr.ensure(1)); // the planned expansion's error word and pad count (both sets)
     HIP_TRY(d.pstat.ensure(1));
+    HIP_TRY(d.alt.perr.ensure(1));
+    HIP_TRY(d.alt.pstat.ensure(1));
+    HIP_TRY(hipMemset(d.alt.perr.p, 0, sizeof(uint32_t)));
     HIP_TRY(hipMemcpy(d.tables, &host_tables(), sizeof(Tables), hipMemcpyHostToDevice));
     for (int w = 0; w < 2; ++w)
       if (hn[w].L1) {
@@ -852,11 +859,12 @@ static int generate_children(Dev &d, const gn_board *parents, size_t n, gn_board
 // row stream, finalize); the expansion pipeline runs the two on different streams.  ev (optional):
 // [0] after classify, [1] after the small net, [2] after the big net, [3] after finalize, [4] the
 // plan -> stream boundary, [6] after the stream launches, [7] (EXP_BACK alone) the stream's start.
+// streamed (without ev): recorded after the stream launches (the pipeline's next front waits for it).
 constexpr int EXP_FRONT = 1, EXP_BACK = 2;
 static int expand_evaluate(gn_ctx *ctx, Dev &d, const gn_board *parents, size_t n, const gn_board *children,
                            size_t total, int mode, gn_eval *parent_out, gn_eval *child_out, hipStream_t s,
                            hipEvent_t *ev, unsigned long long *rows_out = nullptr, bool score_parents = true,
-                           int phases = EXP_FRONT | EXP_BACK) {
+                           int phases = EXP_FRONT | EXP_BACK, hipEvent_t streamed = nullptr) {
   if (mode < GN_MODE_FULL || mode > GN_MODE_SMALL) return fail(GN_E_INVALID, "bad mode %d", mode);
   if ((mode != GN_MODE_SMALL && !d.has[BIG]) || (mode != GN_MODE_BIG && !d.has[SMALL]))
     return fail(GN_E_NONET, "mode %d needs a network that is not loaded", mode);
@@ -955,7 +963,7 @@ static int expand_evaluate(gn_ctx *ctx, Dev &d, const gn_board *parents, size_t 
                                  ctx->king_cache ? 1 : 0, d.eoff.p, d.ent.p, d.tiles.p, d.btiles.p, d.pool.p, d.perr.p,
                                  rows_out, d.pstat.p, 0, nblk, order, nullptr, s, slices,
                                  slices > 1 ? d.part.p : nullptr, n + total, slices > 1 ? d.pinfo.p : nullptr,
-                                 ev ? ev[6] : nullptr, !fused, STREAM_PHASE));
+                                 ev ? ev[6] : streamed, !fused, STREAM_PHASE));
     } else { // a 128-wide net loaded as the big net
       HIP_TRY(launch_expand_net(d.net[BIG], parents, n, off, children, dl, f ? d.p_nbg.p : nullptr,
                                 f ? d.nbg.p : nullptr, d.p_obg.p, d.obg.p, ctx->swizzle & 1, s));
@@ -1449,7 +1457,83 @@ static int expand_pipelined(gn_ctx *ctx, Dev &d, const gn_board *d_par, size_t m
     return r;
   };
   int rc = GN_OK;
-  for (size_t c = 0; c + 1 < chunks.size() && rc == GN_OK; ++c) {
+  auto drain_chunk = [&](int k, size_t pa, size_t mp, size_t t, uint64_t cb) {
+    drain[k] = std::thread([&, k, pa, mp, t, cb] {
+      const auto t1 = Clock::now();
+      hipError_t e = hipSetDevice(d.id);
+      if (e == hipSuccess) e = hipStreamWaitEvent(d.copy, d.cev[k], 0);
+      if (e == hipSuccess && t)
+        e = hipMemcpyAsync(child_out + cb, d.cc2[k].p, t * sizeof(gn_child), hipMemcpyDeviceToHost, d.copy);
+      if (e == hipSuccess && t)
+        e = hipMemcpyAsync(child_moves + cb, d.mv2[k].p, t * sizeof(uint16_t), hipMemcpyDeviceToHost, d.copy);
+      if (e == hipSuccess && parent_out)
+        e = hipMemcpyAsync(parent_out + pa, d.po2[k].p, mp * sizeof(gn_eval), hipMemcpyDeviceToHost, d.copy);
+      if (e == hipSuccess) e = hipStreamSynchronize(d.copy);
+      if (e != hipSuccess) drc[k] = GN_E_HIP, derr[k] = std::string("result download failed: ") + hipGetErrorString(e);
+      dms[k] = ms_since(t1);
+    });
+  };
+  // GN_OPT_EXPAND_PIPELINE: chunk c + 1's child generation and plan run on the second stream (in
+  // the other buffer set) while chunk c's finalize and score rule run
+  const bool pipe = ctx->pipeline && plan_path(ctx, d, mode) && ctx->incremental && chunks.size() > 2;
+  if (pipe) {
+    hipStream_t B = d.front;
+    auto front = [&](size_t c) -> int {
+      const int k = (int)(c & 1);
+      const size_t pa = chunks[c], mp = chunks[c + 1] - pa;
+      const uint64_t tc = off[chunks[c + 1]] - off[pa];
+      size_t t = 0;
+      int r = generate_children(d, d_par + pa, mp, nullptr, d.mv2[k].cap, d.mv2[k].p, true, &t, B, nullptr, nullptr,
+                                chain_len(ctx, d, mp), true, mode == GN_MODE_BIG);
+      if (!r && t != tc) r = fail(GN_E_HIP, "child count changed between passes (%zu != %zu)", t, (size_t)tc);
+      if (!r)
+        r = expand_evaluate(ctx, d, d_par + pa, mp, d.frontier[1].p, t, mode, nullptr, nullptr, B, nullptr, nullptr,
+                            true, EXP_FRONT);
+      if (!r && hipEventRecord(d.ev_planned, B) != hipSuccess) r = fail(GN_E_HIP, "hipEventRecord failed");
+      return r;
+    };
+    // the front starts after what the device stream holds (the parents' upload / replay)
+    if (hipEventRecord(d.ev_streamed, s) != hipSuccess || hipStreamWaitEvent(B, d.ev_streamed, 0) != hipSuccess)
+      return fail(GN_E_HIP, "hipStreamWaitEvent failed");
+    rc = front(0);
+    for (size_t c = 0; c + 1 < chunks.size() && rc == GN_OK; ++c) {
+      const int k = (int)(c & 1);
+      const size_t pa = chunks[c], mp = chunks[c + 1] - pa;
+      const uint64_t cb = off[pa], t = off[chunks[c + 1]] - cb;
+      const auto t0 = Clock::now();
+      if (hipStreamWaitEvent(s, d.ev_planned, 0) != hipSuccess) {
+        rc = fail(GN_E_HIP, "hipStreamWaitEvent failed");
+        break;
+      }
+      rc = expand_evaluate(ctx, d, d_par + pa, mp, d.frontier[1].p, t, mode, d.po2[k].p, d.co2[k].p, s, nullptr,
+                           nullptr, true, EXP_BACK, d.ev_streamed);
+      if (rc) break;
+      const bool more = c + 2 < chunks.size();
+      if (more) { // the next chunk's front (slot k ^ 1: its previous chunk downloaded first)
+        if ((rc = join(k ^ 1)) != GN_OK) break;
+        swap_sets(d);
+        if (hipStreamWaitEvent(B, d.ev_streamed, 0) != hipSuccess) rc = fail(GN_E_HIP, "hipStreamWaitEvent failed");
+        if (!rc) rc = front(c + 1);
+        swap_sets(d);
+        if (rc) break;
+      }
+      const Replies rp{d.co2[k].p, d.mv2[k].p};
+      rc = resolve_scores(ctx, d, d_par + pa, mp, mode, d.po2[k].p, nullptr, s, 2, &rp);
+      if (!rc && launch_pack_children(d.co2[k].p, t, d.cc2[k].p, s) != hipSuccess)
+        rc = fail(GN_E_HIP, "child record packing failed");
+      if (!rc) rc = check_plan(d, s); // synchronises the stream: chunk c is computed
+      if (rc) break;
+      d.t_compute += ms_since(t0);
+      if (hipEventRecord(d.cev[k], s) != hipSuccess) {
+        rc = fail(GN_E_HIP, "hipEventRecord failed");
+        break;
+      }
+      drain_chunk(k, pa, mp, t, cb);
+      if (more) swap_sets(d);
+    }
+    if (rc) (void)hipStreamSynchronize(B); // (nothing of a failed call's front may still run)
+  }
+  for (size_t c = 0; !pipe && c + 1 < chunks.size() && rc == GN_OK; ++c) {
     const int k = (int)(c & 1);
     if ((rc = join(k)) != GN_OK) break; // the slot's previous chunk is downloaded
     const size_t pa = chunks[c], mp = chunks[c + 1] - pa;
@@ -1472,20 +1556,7 @@ static int expand_pipelined(gn_ctx *ctx, Dev &d, const gn_board *d_par, size_t m
       rc = fail(GN_E_HIP, "hipEventRecord failed");
       break;
     }
-    drain[k] = std::thread([&, k, pa, mp, t, cb] {
-      const auto t1 = Clock::now();
-      hipError_t e = hipSetDevice(d.id);
-      if (e == hipSuccess) e = hipStreamWaitEvent(d.copy, d.cev[k], 0);
-      if (e == hipSuccess && t)
-        e = hipMemcpyAsync(child_out + cb, d.cc2[k].p, t * sizeof(gn_child), hipMemcpyDeviceToHost, d.copy);
-      if (e == hipSuccess && t)
-        e = hipMemcpyAsync(child_moves + cb, d.mv2[k].p, t * sizeof(uint16_t), hipMemcpyDeviceToHost, d.copy);
-      if (e == hipSuccess && parent_out)
-        e = hipMemcpyAsync(parent_out + pa, d.po2[k].p, mp * sizeof(gn_eval), hipMemcpyDeviceToHost, d.copy);
-      if (e == hipSuccess) e = hipStreamSynchronize(d.copy);
-      if (e != hipSuccess) drc[k] = GN_E_HIP, derr[k] = std::string("result download failed: ") + hipGetErrorString(e);
-      dms[k] = ms_since(t1);
-    });
+    drain_chunk(k, pa, mp, t, cb);
   }
   const auto tt = Clock::now();
   for (int k = 0; k < 2; ++k) {
@@ -2578,6 +2649,12 @@ int gn_time_expand_device(gn_ctx *ctx, int device_slot, const gn_board *d_parent
   *total = t;
   if (rc) return rc;
   if (he == hipSuccess && (rc = check_plan(*d, s)) != GN_OK) return rc;
+  if (he == hipSuccess && pipe) { // (the other set's expansion too)
+    swap_sets(*d);
+    rc = check_plan(*d, s);
+    swap_sets(*d);
+    if (rc) return rc;
+  }
   if (ft_rows && he == hipSuccess) {
     unsigned long long r[2] = {0, 0};
     he = hipMemcpy(r, d->sum.p, sizeof(r), hipMemcpyDeviceToHost);

@@ -758,7 +758,9 @@ def test_pipeline_chunks_equal_one_chunk(gpu_ctx):
     """The host-buffer expansion pipeline cut into many chunks (GN_OPT_CHUNK_PARENTS: slot reuse in
     the device output buffers, the drain threads' downloads on the copy stream, chunk cuts at game
     starts) returns byte-identical results to one chunk: gn_evaluate_games with children (cuts at
-    game starts, skipped positions inside chunks) and gn_expand_and_evaluate (cuts every 81)."""
+    game starts, skipped positions inside chunks) and gn_expand_and_evaluate (cuts every 81), with
+    the chunks overlapped (GN_OPT_EXPAND_PIPELINE, the default: chunk c + 1's children and plan on
+    the second stream while chunk c finishes) and one after another."""
     from fishnet_amd import gpu_nnue as G
     ucis = G.random_games_uci(0x5EED0123, 0, 40, 80)
     start = "rnbqkbnr/pppppppp/8/8/8/8/PPPPPPPP/RNBQKBNR w KQkq - 0 1"
@@ -767,15 +769,17 @@ def test_pipeline_chunks_equal_one_chunk(gpu_ctx):
     fens = [G.board_to_fen(b) for b in G.random_positions(0x5EED0456, 0, 700, 160)]
     try:
         out = {}
-        for chunk in (0, 100, 250):
+        for chunk, pipe in ((0, 1), (100, 1), (250, 1), (100, 0), (250, 0)):
             gpu_ctx.set_option(G.OPT_CHUNK_PARENTS, chunk)
+            gpu_ctx.set_option(G.OPT_EXPAND_PIPELINE, pipe)
             res = gpu_ctx.evaluate_games_arrays(arr, len(games), 0, children=True)
-            out[chunk] = ([np.copy(x) for x in res[:6]], [np.copy(x) for x in gpu_ctx.expand_and_evaluate(fens, 1)])
-        for chunk in (100, 250):
-            for a, b in zip(out[0][0] + out[0][1], out[chunk][0] + out[chunk][1]):
-                assert a.tobytes() == b.tobytes(), chunk
+            out[chunk, pipe] = ([np.copy(x) for x in res[:6]], [np.copy(x) for x in gpu_ctx.expand_and_evaluate(fens, 1)])
+        for key in ((100, 1), (250, 1), (100, 0), (250, 0)):
+            for a, b in zip(out[0, 1][0] + out[0, 1][1], out[key][0] + out[key][1]):
+                assert a.tobytes() == b.tobytes(), key
     finally:
         gpu_ctx.set_option(G.OPT_CHUNK_PARENTS, 0)
+        gpu_ctx.set_option(G.OPT_EXPAND_PIPELINE, 1)
 
 
 def test_concurrent_batches_coalesce(gpu_ctx):
