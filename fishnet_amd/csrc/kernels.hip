@@ -152,7 +152,7 @@ template <int L1, int PAR>
 __global__ void __launch_bounds__(2 * (L1 / 16) * PAR) __attribute__((amdgpu_waves_per_eu(PAR == 1 ? 1 : GN_SMALL_WPE)))
     eval_net_kernel(NetDevice net, const gn_board *__restrict__ boards, const uint8_t *__restrict__ need,
                     size_t n, int2 *__restrict__ out, const uint32_t *__restrict__ perm, unsigned tiles, int swz,
-                    unsigned long long *__restrict__ rows_out) {
+                    unsigned long long *__restrict__ rows_out, unsigned tn) {
   constexpr int G = L1 / 16;
   constexpr int NT = 2 * G * PAR;
   constexpr int NW = NT / 64;
@@ -191,14 +191,18 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR) __attribute__((amdgpu_wav
     tile = (blockIdx.x & 7) * t8 + (blockIdx.x >> 3);
     if (tile >= tiles) return;
   }
-  const size_t base = (size_t)tile * TILE;
-  // the tile's 16 boards to LDS by 16 lanes in one round trip (perm, need, board), instead of a
-  // dependent board load per position in each phase-0 loop below
+  // tn positions per workgroup (16; fewer for a small batch: the big net's phase 1 walks a tile's
+  // positions one after another, so a 128-position batch in 16-position tiles is 8 workgroups each
+  // 16 gathers deep -- the drop-in's latency -- while 2-position tiles are 64 workgroups 2 deep)
+  const size_t base = (size_t)tile * tn;
+  // the tile's boards to LDS by tn lanes in one round trip (perm, need, board), instead of a
+  // dependent board load per position in each phase-0 loop below (slots >= tn: empty boards)
   if (tid < TILE) {
     const size_t q = base + tid;
-    const size_t i = q < n ? (perm ? perm[q] : q) : 0;
+    const bool in = (unsigned)tid < tn && q < n;
+    const size_t i = in ? (perm ? perm[q] : q) : 0;
     gn_board b = {};
-    if (q < n && (!need || need[i])) b = boards[i];
+    if (in && (!need || need[i])) b = boards[i];
     tb[tid] = b;
     tix[tid] = (uint32_t)i;
   }
@@ -366,7 +370,7 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR) __attribute__((amdgpu_wav
   // ---- phase 2: layer stack (MFMA).  Big net: every wave takes part in each bucket's fc_0
   // (48 k-steps); small net (2 k-steps): one wave per bucket present runs the whole stack
   // (layer_stack_wave: no LDS partial sums, no further barrier), the other waves are done
-  auto valid = [&](int pos, int b) { return base + pos < n && nfeat[pos] && bkt[pos] == b; };
+  auto valid = [&](int pos, int b) { return (unsigned)pos < tn && base + pos < n && nfeat[pos] && bkt[pos] == b; };
   auto emit = [&](int pos, int2 v) { out[gidx[pos]] = v; };
   if constexpr (PAR == 1) {
     layer_stack_tile<L1, NW>(net, xt, scratch, psq, (int)threadIdx.x, bmask, valid, emit);
@@ -680,17 +684,22 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR) __attribute__((amdgpu_wav
 hipError_t launch_eval_net(const NetDevice &net, const gn_board *boards, const uint8_t *need, size_t n, int2 *out,
                            const uint32_t *perm, int swz, hipStream_t s, unsigned long long *rows_out) {
   if (!n) return hipSuccess;
-  const unsigned tiles = (unsigned)((n + 15) / 16);
+  // positions per workgroup: 16, or for a big net (positions one after another in phase 1) and a
+  // batch of fewer than 32 k positions, as few as keep >= 2,048 workgroups (>= 2)
+  unsigned tn = 16;
+  if (net.L1 != 128)
+    while (tn > 2 && (n + tn - 1) / tn < 2048) tn >>= 1;
+  const unsigned tiles = (unsigned)((n + tn - 1) / tn);
   const unsigned grid = swz ? 8 * ((tiles + 7) / 8) : tiles;
   if (net.L1 == 3072) {
     hipLaunchKernelGGL((eval_net_kernel<3072, 1>), dim3(grid), dim3(384), 0, s, net, boards, need, n, out, perm, tiles, swz,
-                       rows_out);
+                       rows_out, tn);
   } else if (net.L1 == 128) {
     hipLaunchKernelGGL((eval_net_kernel<128, 16>), dim3(grid), dim3(256), 0, s, net, boards, need, n, out, perm, tiles, swz,
-                       rows_out);
+                       rows_out, tn);
   } else if (net.L1 == 1024) {
     hipLaunchKernelGGL((eval_net_kernel<1024, 1>), dim3(grid), dim3(128), 0, s, net, boards, need, n, out, perm, tiles, swz,
-                       rows_out);
+                       rows_out, tn);
   } else {
     return hipErrorInvalidValue;
   }

@@ -13,3 +13,5 @@ for P in 1 0 1 0; do
   timeout -k 10 200 python -u tools/ab.py --out gpurun_out/r06g/ab$P --variants libgpu_nnue.so --timeout 180 -- --steps 5 --pipeline $P > gpurun_out/r06g/ab_p$P.log 2>&1; echo "pipeline $P rc=$?"; cat gpurun_out/r06g/ab_p$P.log
 done
 timeout -k 10 700 python -u -m pytest tests -m gpu -q --timeout 200 --timeout-method thread --deselect $T > gpurun_out/r06g/pytest.log 2>&1; echo "suite rc=$?"; tail -5 gpurun_out/r06g/pytest.log
+timeout -k 10 200 python -u bench.py --dropin > gpurun_out/r06g/dropin.json 2> gpurun_out/r06g/dropin.err; echo "dropin rc=$?"; cat gpurun_out/r06g/dropin.json
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r06g/dtrace -o run --output-format csv -- python bench.py --dropin > gpurun_out/r06g/dtrace.log 2>&1; echo "dtrace rc=$?"
