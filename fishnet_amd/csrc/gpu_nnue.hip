@@ -253,8 +253,14 @@ struct ExpSet {
   size_t scan_bytes = 0, sort_bytes = 0;
   DevBuf<uint32_t> perr;            // the planned expansion's error word ...
   DevBuf<unsigned long long> pstat; // ... and pad count (each expansion of the pipeline its own)
+  // the plan's output the row stream reads (GN_OPT_EXPAND_PIPELINE 2: the next plan runs beside
+  // this expansion's row stream)
+  DevBuf<uint64_t> ent, eoff;
+  DevBuf<TileDesc> tiles;
+  DevBuf<uint32_t> btiles, border;
   void release() {
     perr.release(), pstat.release();
+    ent.release(), eoff.release(), tiles.release(), btiles.release(), border.release();
     counts.release(), offsets.release(), owner.release(), unpacked.release(), moves_tmp.release();
     pinfo.release(), p_osm.release(), p_obg.release(), p_nsm.release(), p_nbg.release(), eb.release();
     children.release();
@@ -370,6 +376,8 @@ static void swap_sets(Dev &d) {
   std::swap(d.scan_tmp, x.scan_tmp), std::swap(d.scan_bytes, x.scan_bytes);
   std::swap(d.sort_tmp, x.sort_tmp), std::swap(d.sort_bytes, x.sort_bytes);
   std::swap(d.perr, x.perr), std::swap(d.pstat, x.pstat);
+  std::swap(d.ent, x.ent), std::swap(d.eoff, x.eoff), std::swap(d.tiles, x.tiles), std::swap(d.btiles, x.btiles);
+  std::swap(d.border, x.border);
 }
 
 // Called under d.mu before a launch sequence on stream s / after it.
@@ -434,7 +442,7 @@ struct gn_ctx {
   } co;
   bool coalesce = true;
   bool fast_batch = true;                  // GN_OPT_FAST_BATCH
-  bool pipeline = true;                    // GN_OPT_EXPAND_PIPELINE
+  int pipeline = 1;                        // GN_OPT_EXPAND_PIPELINE (2: the next front beside the stream)
   std::atomic<uint64_t> graph_gen{0};      // bumped by every option / parameter change: the small-
                                            // batch graphs captured before it are rebuilt
   std::atomic<uint64_t> fast_runs{0}, fast_fallbacks{0};
@@ -1512,7 +1520,8 @@ static int expand_pipelined(gn_ctx *ctx, Dev &d, const gn_board *d_par, size_t m
       if (more) { // the next chunk's front (slot k ^ 1: its previous chunk downloaded first)
         if ((rc = join(k ^ 1)) != GN_OK) break;
         swap_sets(d);
-        if (hipStreamWaitEvent(B, d.ev_streamed, 0) != hipSuccess) rc = fail(GN_E_HIP, "hipStreamWaitEvent failed");
+        if (ctx->pipeline != 2 && hipStreamWaitEvent(B, d.ev_streamed, 0) != hipSuccess)
+          rc = fail(GN_E_HIP, "hipStreamWaitEvent failed");
         if (!rc) rc = front(c + 1);
         swap_sets(d);
         if (rc) break;
@@ -2574,7 +2583,7 @@ int gn_time_expand_device(gn_ctx *ctx, int device_slot, const gn_board *d_parent
       const bool more = it + 1 < iters;
       if (more) { // the next front, after this row stream (it overwrites the plan's lists)
         swap_sets(*d);
-        he = hipStreamWaitEvent(B, e[10], 0);
+        he = ctx->pipeline == 2 ? hipSuccess : hipStreamWaitEvent(B, e[10], 0);
         if (he == hipSuccess) rc = front(it + 1);
         swap_sets(*d);
         if (rc || he != hipSuccess) break;
@@ -2731,7 +2740,8 @@ int gn_set_option(gn_ctx *ctx, int option, int64_t value) {
     ctx->fast_batch = value != 0;
     return GN_OK;
   case GN_OPT_EXPAND_PIPELINE:
-    ctx->pipeline = value != 0;
+    if (value < 0 || value > 2) return fail(GN_E_INVALID, "GN_OPT_EXPAND_PIPELINE %lld not in 0..2", (long long)value);
+    ctx->pipeline = (int)value;
     return GN_OK;
   default:
     return fail(GN_E_INVALID, "unknown option %d", option);

@@ -89,8 +89,10 @@ extern "C" {
                                          pipeline's chunks) overlap: expansion k + 1's child
                                          generation and plan run on a second stream while
                                          expansion k's finalize and score rule run (two
-                                         buffer sets); 0: one after another.  Results are
-                                         identical either way.                              */
+                                         buffer sets); 2: the next child generation and
+                                         plan start while expansion k's row stream still
+                                         runs; 0: one after another.  Results are identical
+                                         for every value.                                   */
 #define GN_OPT_INCREMENTAL_CHILDREN 1 /* 1 (default): children from the parent accumulators
                                          by add/sub deltas; 0: full refresh per child    */
 #define GN_OPT_XCD_SWIZZLE 2          /* bit mask, default 9: each XCD takes a contiguous

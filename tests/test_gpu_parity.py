@@ -769,12 +769,12 @@ def test_pipeline_chunks_equal_one_chunk(gpu_ctx):
     fens = [G.board_to_fen(b) for b in G.random_positions(0x5EED0456, 0, 700, 160)]
     try:
         out = {}
-        for chunk, pipe in ((0, 1), (100, 1), (250, 1), (100, 0), (250, 0)):
+        for chunk, pipe in ((0, 1), (100, 1), (250, 1), (100, 0), (250, 0), (100, 2)):
             gpu_ctx.set_option(G.OPT_CHUNK_PARENTS, chunk)
             gpu_ctx.set_option(G.OPT_EXPAND_PIPELINE, pipe)
             res = gpu_ctx.evaluate_games_arrays(arr, len(games), 0, children=True)
             out[chunk, pipe] = ([np.copy(x) for x in res[:6]], [np.copy(x) for x in gpu_ctx.expand_and_evaluate(fens, 1)])
-        for key in ((100, 1), (250, 1), (100, 0), (250, 0)):
+        for key in ((100, 1), (250, 1), (100, 0), (250, 0), (100, 2)):
             for a, b in zip(out[0, 1][0] + out[0, 1][1], out[key][0] + out[key][1]):
                 assert a.tobytes() == b.tobytes(), key
     finally:
@@ -1112,8 +1112,9 @@ def test_expand_pipeline_equals_serial(gpu_ctx, oracle_nets, oracle_lib):
     try:
         for mode in (1, 0):
             serial = run(1, 0, mode)
-            assert run(2, 1, mode) == serial, mode
-            assert run(3, 1, mode) == serial, mode
+            for pipe in (1, 2):  # (2: the next front beside the row stream)
+                assert run(2, pipe, mode) == serial, (mode, pipe)
+                assert run(3, pipe, mode) == serial, (mode, pipe)
             assert run(3, 0, mode) == serial, mode
     finally:
         gpu_ctx.set_option(G.OPT_EXPAND_PIPELINE, 1)
