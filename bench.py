@@ -183,7 +183,7 @@ class Ctx:
             self.nn.set_option(G.OPT_CHAIN, args.chain)
         if args.king_cache is not None:
             self.nn.set_option(G.OPT_KING_CACHE, args.king_cache)
-        if args.pipeline is not None:
+        if getattr(args, "pipeline", None) is not None:
             self.nn.set_option(G.OPT_EXPAND_PIPELINE, args.pipeline)
         self.options = {"xcd_swizzle": self.nn.get_option(G.OPT_XCD_SWIZZLE),
                         "king_sort": self.nn.get_option(G.OPT_KING_SORT),

@@ -687,8 +687,10 @@ hipError_t launch_eval_net(const NetDevice &net, const gn_board *boards, const u
   // positions per workgroup: 16, or for a big net (positions one after another in phase 1) and a
   // batch of fewer than 32 k positions, as few as keep >= 2,048 workgroups (>= 2)
   unsigned tn = 16;
+#ifndef GN_AB_TN16 // A/B: 16 positions per workgroup at every batch size
   if (net.L1 != 128)
     while (tn > 2 && (n + tn - 1) / tn < 2048) tn >>= 1;
+#endif
   const unsigned tiles = (unsigned)((n + tn - 1) / tn);
   const unsigned grid = swz ? 8 * ((tiles + 7) / 8) : tiles;
   if (net.L1 == 3072) {
@@ -1035,18 +1037,19 @@ hipError_t launch_score_replies_fill(const uint32_t *idx, size_t m, const uint64
 // would make -- and every slot from the total to cap is an empty board (an invalid position for
 // the evaluation that follows, so that launches sized by cap need no count).  A total beyond cap
 // sets *flag (the caller then takes the general path); first: *flag is set, else or'd.
-// Positions per thread <= 16 (n <= 16,384: level 2 takes level 1's capacity, 2 * 4,096 + 256).
-// A thread's counts wait in off[] (its own entries) between the two passes.
-__global__ void __launch_bounds__(1024) reply_level_kernel(const gn_board *__restrict__ boards,
+// 256 threads (a 1,024-thread version spilled 35 VGPRs around gen_legal and took 36 us per launch,
+// the drop-in's largest kernel); positions per thread <= 64 (n <= 16,384: level 2 takes level 1's
+// capacity, 2 * 4,096 + 256).  A thread's counts wait in off[] (its own entries) between the passes.
+__global__ void __launch_bounds__(256) reply_level_kernel(const gn_board *__restrict__ boards,
                                                            const gn_eval *__restrict__ ev, uint32_t n,
                                                            const Tables *__restrict__ tables, uint64_t *__restrict__ off,
                                                            uint32_t cap, gn_board *__restrict__ rb,
                                                            uint16_t *__restrict__ rm, uint32_t *__restrict__ flag,
                                                            int first) {
+  constexpr uint32_t NT = 256;
   __shared__ Tables T;
-  __shared__ uint32_t part[1024];
+  __shared__ uint32_t part[NT];
   load_tables(T, tables);
-  constexpr uint32_t NT = 1024;
   const uint32_t t = threadIdx.x, q = (n + NT - 1) / NT, lo = t * q, hi = lo + q < n ? lo + q : n;
   uint32_t c = 0;
 #pragma unroll 1
@@ -1099,7 +1102,7 @@ __global__ void __launch_bounds__(1024) reply_level_kernel(const gn_board *__res
 hipError_t launch_reply_level(const gn_board *boards, const gn_eval *ev, size_t n, const Tables *tables, uint64_t *off,
                               size_t cap, gn_board *rb, uint16_t *rm, uint32_t *flag, int first, hipStream_t s) {
   if (!n || n > 16384 || cap >= 0x80000000ull) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(reply_level_kernel, dim3(1), dim3(1024), 0, s, boards, ev, (uint32_t)n, tables, off,
+  hipLaunchKernelGGL(reply_level_kernel, dim3(1), dim3(256), 0, s, boards, ev, (uint32_t)n, tables, off,
                      (uint32_t)cap, rb, rm, flag, first);
   return hipGetLastError();
 }

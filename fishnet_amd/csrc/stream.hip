@@ -809,8 +809,6 @@ __global__ void __launch_bounds__(L1 / SL / 8) __attribute__((amdgpu_waves_per_e
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int hu = __builtin_amdgcn_readfirstlane((tid / G) & 1);
-  const __amdgpu_buffer_rsrc_t ftr = __builtin_amdgcn_make_buffer_rsrc(
-      (void *)net.ft, 0, (int)(((size_t)ZERO_ROW + 1) * RS), 0x00020000);
   for (int i = tid; i < 2 * 16 * AS; i += NT) (&acc0[0][0])[i] = 0;
   // this launch evaluates blocks [b0, b1).  swz: XCD x (= dispatch index mod 8) takes the x-th
   // contiguous eighth of them; otherwise (default) every workgroup claims the next block of the
@@ -1032,6 +1030,34 @@ __global__ void __launch_bounds__(L1 / SL / 8) __attribute__((amdgpu_waves_per_e
     // test per branch, each kind with its own multiply-adds (the compiler's version of this tree
     // copied the source registers on every path and spilled): a plain entry costs two scalar
     // instructions, an init five to seven.
+#ifdef GN_AB_WHOLE_CDECODE // diagnostics: the whole-row stream with the compiler's decode (round 5's)
+    if constexpr (SL == 1) {
+      const unsigned short sg = (unsigned short)h;
+      const uint32_t init = (h >> 16) & 3u;
+      ushort8 lo = __builtin_bit_cast(ushort8, make_uint4(A[0], A[1], A[2], A[3]));
+      ushort8 hi = __builtin_bit_cast(ushort8, make_uint4(A[4], A[5], A[6], A[7]));
+      if (init) {
+        asm volatile("");
+        if (init == 2) {
+          lo = __builtin_bit_cast(ushort8, make_uint4(PA[0], PA[1], PA[2], PA[3]));
+          hi = __builtin_bit_cast(ushort8, make_uint4(PA[4], PA[5], PA[6], PA[7]));
+        } else if (init == 3) {
+          lo = __builtin_bit_cast(ushort8, make_uint4(BA[0], BA[1], BA[2], BA[3]));
+          hi = __builtin_bit_cast(ushort8, make_uint4(BA[4], BA[5], BA[6], BA[7]));
+        } else {
+          lo = ushort8{}, hi = ushort8{};
+        }
+      }
+      lo = rlo[r] * sg + lo, hi = rhi[r] * sg + hi;
+      const uint4 l4 = __builtin_bit_cast(uint4, lo), h4 = __builtin_bit_cast(uint4, hi);
+      A[0] = l4.x, A[1] = l4.y, A[2] = l4.z, A[3] = l4.w, A[4] = h4.x, A[5] = h4.y, A[6] = h4.z, A[7] = h4.w;
+      if (init == 2) {
+        asm volatile("");
+#pragma unroll
+        for (int i = 0; i < 8; ++i) BA[i] = A[i];
+      }
+    } else
+#endif
     {
       const uint4 rl = __builtin_bit_cast(uint4, rlo[r]), rh = __builtin_bit_cast(uint4, rhi[r]);
       uint32_t t;
@@ -1076,10 +1102,13 @@ __global__ void __launch_bounds__(L1 / SL / 8) __attribute__((amdgpu_waves_per_e
                    ".Lgn_plain%=:\n\t"
                    GN_MAD8("a")
                    ".Lgn_end%=:"
-                   : [a0] "+v"(A[0]), [a1] "+v"(A[1]), [a2] "+v"(A[2]), [a3] "+v"(A[3]), [a4] "+v"(A[4]),
-                     [a5] "+v"(A[5]), [a6] "+v"(A[6]), [a7] "+v"(A[7]), [b0] "+v"(BA[0]), [b1] "+v"(BA[1]),
-                     [b2] "+v"(BA[2]), [b3] "+v"(BA[3]), [b4] "+v"(BA[4]), [b5] "+v"(BA[5]), [b6] "+v"(BA[6]),
-                     [b7] "+v"(BA[7]), [t] "=&s"(t)
+                   // (early clobbers: the tree writes a0 .. while it still reads the later inputs, so
+                   // no input may share a register with an output -- without "&" the compiler may
+                   // give an output and an input of equal value one register)
+                   : [a0] "+&v"(A[0]), [a1] "+&v"(A[1]), [a2] "+&v"(A[2]), [a3] "+&v"(A[3]), [a4] "+&v"(A[4]),
+                     [a5] "+&v"(A[5]), [a6] "+&v"(A[6]), [a7] "+&v"(A[7]), [b0] "+&v"(BA[0]), [b1] "+&v"(BA[1]),
+                     [b2] "+&v"(BA[2]), [b3] "+&v"(BA[3]), [b4] "+&v"(BA[4]), [b5] "+&v"(BA[5]), [b6] "+&v"(BA[6]),
+                     [b7] "+&v"(BA[7]), [t] "=&s"(t)
                    : [h] "s"(h), [p0] "v"(PA[0]), [p1] "v"(PA[1]), [p2] "v"(PA[2]), [p3] "v"(PA[3]),
                      [p4] "v"(PA[4]), [p5] "v"(PA[5]), [p6] "v"(PA[6]), [p7] "v"(PA[7]), [r0] "v"(rl.x),
                      [r1] "v"(rl.y), [r2] "v"(rl.z), [r3] "v"(rl.w), [r4] "v"(rh.x), [r5] "v"(rh.y),
@@ -1109,14 +1138,27 @@ __global__ void __launch_bounds__(L1 / SL / 8) __attribute__((amdgpu_waves_per_e
       if (h & (H_KST & ~H_X)) { // the accumulator to its king-cache row
         asm volatile("");
         const uint32_t so = (scr + (h & 0xFFFFu)) * RS;
-#ifndef GN_KC_POLICY
-// cache policy of the king-cache stores: 0 = default.  The same-address store -> load order
+#ifndef GN_KC_ASM_POLICY
+// cache policy of the king-cache stores: "" = default.  The same-address store -> load order
 // the reload relies on is pinned for default-policy stores only (kernels.h); non-temporal
-// (2) measured 205.5 -> 205.0 ms, within noise, so it stays an A/B build option
-#define GN_KC_POLICY 0
+// (" nt") measured 205.5 -> 205.0 ms, within noise, so it stays an A/B build option
+#define GN_KC_ASM_POLICY ""
 #endif
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(int4v, lo), ftr, j16, so, GN_KC_POLICY);
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(int4v, hi), ftr, j16 + L1, so, GN_KC_POLICY);
+        // Both halves in one asm block: the high half at the instruction's immediate offset, and a
+        // wait state after the pair before any VALU may overwrite their data registers.  (As two
+        // builtins, the whole-row kernel at its 96-VGPR cap computed the second address into a data
+        // register of the first store in the very next instruction -- `buffer_store_dwordx4
+        // v[2:5] ...; v_add_u32 v4, 0xc00, v1` -- with no wait state between: the king-cache rows
+        // then held wrong values now and then, round 6, test_stream_column_slices_equal_whole_rows.
+        // A VALU write to the data VGPRs of a > 64-bit store needs one wait state on this family.)
+        static_assert(L1 < 4096, "the high half's offset fits the 12-bit immediate");
+        asm volatile("buffer_store_dwordx4 %0, %2, %3, %4 offen" GN_KC_ASM_POLICY "\n\t"
+                     "buffer_store_dwordx4 %1, %2, %3, %4 offen offset:%5" GN_KC_ASM_POLICY "\n\t"
+                     "s_nop 0"
+                     :
+                     : "v"(__builtin_bit_cast(int4v, lo)), "v"(__builtin_bit_cast(int4v, hi)), "v"(j16), "s"(rsq),
+                       "s"(so), "n"(L1)
+                     : "memory");
         // no drain: the ring's vmcnt(6) still covers an entry's own loads with these two stores
         // outstanding (loads complete in order, so >= 2 of the >= 4 completions it waits for are
         // that entry's loads), and a later load of the row is issued after the store in program

@@ -415,3 +415,35 @@ def test_partial_sum_prefetch_registers_untouched_in_flight(tmp_path):
                and not (op.startswith("v_add_u32") and s.split(",")[0].split()[-1] not in {f"v{r}" for r in pv})
                and not (op.startswith("buffer_load_dwordx4") and k - 1 in {i for i, _ in _asm_blocks(body, 2)})]
         assert not bad, bad[:8]
+
+
+def test_no_valu_write_to_wide_store_data_in_the_next_instruction(tmp_path):
+    """Round 6: the whole-row stream's king-cache stores, compiled as two builtins, came out as
+    `buffer_store_dwordx4 v[2:5] ...` directly followed by `v_add_u32 v4, ...` (the second store's
+    address into a data register of the first) and the king-cache rows then held wrong values now
+    and then on the GPU.  A VALU write to the data VGPRs of a store wider than 64 bits needs a wait
+    state; in the ISA of every kernel of the library no such write follows a dwordx3 / dwordx4
+    store directly (the stream's stores are one asm block ending in s_nop)."""
+    import re
+    import shutil
+    import subprocess
+    if not shutil.which("hipcc"):
+        pytest.skip("hipcc not available")
+    hits = []
+    for src in ("stream.hip", "kernels.hip", "gpu_nnue.hip"):
+        asm = tmp_path / (src + ".s")
+        subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "--cuda-device-only", "-w", "-S",
+                        os.path.join(ROOT, "fishnet_amd", "csrc", src), "-o", str(asm)], capture_output=True,
+                       text=True, check=True)
+        seq = [s.strip() for s in asm.read_text().splitlines()]
+        seq = [s for s in seq if s and not s.startswith((";", ".")) and not s.endswith(":")]
+        for k, line in enumerate(seq[:-1]):
+            m = re.match(r"(buffer|global|flat|scratch)_store_dwordx([34])\s+(.*)", line)
+            if not m:
+                continue
+            ops = [o.strip() for o in m.group(3).split(",")]
+            data = _vregs(ops[0] if m.group(1) in ("buffer", "scratch") else ops[1])
+            nxt = seq[k + 1]
+            if nxt.startswith("v_") and not nxt.startswith("v_cmp") and _vregs(nxt.split(None, 1)[1].split(",")[0]) & data:
+                hits.append((src, line, nxt))
+    assert not hits, hits[:6]
