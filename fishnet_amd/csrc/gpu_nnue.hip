@@ -301,6 +301,7 @@ struct Dev {
   DevBuf<int2> pinfo;    // ... and each position's (PSQT value, bucket) for the finish
   int chain_k = 1;          // block length of the current expansion (1: no chaining)
   int slices = 1;           // the current expansion's stream: column slices (3) or whole rows (1)
+  bool part_locked = false; // a pipeline runs: part is in use by a back half (no reallocation)
   // planned expansion (stream.hip): per-parent entry bounds and their scan, the entry
   // lists, tile descriptors, the scratch-slot pool and the error word
   DevBuf<uint64_t> ebound, eoff;
@@ -930,10 +931,18 @@ static int expand_evaluate(gn_ctx *ctx, Dev &d, const gn_board *parents, size_t 
       int slices = d.net[BIG].L1 == 3072 && ctx->stream_slices == 3 ? 3 : 1;
       // the sliced stream's partial sums cost 200 B per position (include/gpu_nnue.h,
       // GN_OPT_STREAM_SLICES); when they do not fit, the whole-row stream gives the same results
-      if (slices > 1 && (d.part.ensure((size_t)GN_PART_SLICES * 16 * (n + total)) != hipSuccess || d.pinfo.ensure(n + total) != hipSuccess)) {
-        (void)hipGetLastError(); // (the failed allocation's error is not the call's)
-        d.part.release(), d.pinfo.release();
-        slices = 1;
+      // (part_locked: a pipelined front, beside the back half of the previous expansion that reads
+      // part -- it may not reallocate it; when it is too small this expansion streams whole rows)
+      if (slices > 1) {
+        const size_t need = (size_t)GN_PART_SLICES * 16 * (n + total);
+        bool ok = d.part_locked ? d.part.cap >= need : d.part.ensure(need) == hipSuccess;
+        ok = ok && d.pinfo.ensure(n + total) == hipSuccess;
+        if (!ok) {
+          (void)hipGetLastError(); // (the failed allocation's error is not the call's)
+          if (!d.part_locked) d.part.release();
+          d.pinfo.release();
+          slices = 1;
+        }
       }
       d.slices = slices;
       // XCD-local block order
@@ -1503,6 +1512,16 @@ static int expand_pipelined(gn_ctx *ctx, Dev &d, const gn_board *d_par, size_t m
     // the front starts after what the device stream holds (the parents' upload / replay)
     if (hipEventRecord(d.ev_streamed, s) != hipSuccess || hipStreamWaitEvent(B, d.ev_streamed, 0) != hipSuccess)
       return fail(GN_E_HIP, "hipStreamWaitEvent failed");
+    // the partial sums sized for the largest chunk now: a later front runs beside a back half that
+    // reads them and may not reallocate them (part_locked)
+    if (d.has[BIG] && d.net[BIG].L1 == 3072 && ctx->stream_slices == 3 &&
+        d.part.ensure((size_t)GN_PART_SLICES * 16 * (maxp + maxc)) != hipSuccess)
+      (void)hipGetLastError(); // (then the chunks that do not fit stream whole rows)
+    d.part_locked = true;
+    struct Unlock {
+      Dev &d;
+      ~Unlock() { d.part_locked = false; }
+    } unlock{d};
     rc = front(0);
     for (size_t c = 0; c + 1 < chunks.size() && rc == GN_OK; ++c) {
       const int k = (int)(c & 1);
@@ -2571,6 +2590,11 @@ int gn_time_expand_device(gn_ctx *ctx, int device_slot, const gn_board *d_parent
     if (he == hipSuccess) he = hipStreamWaitEvent(B, d->ev_streamed, 0);
     if (he == hipSuccess) rc = front(0);
     t = tn;
+    d->part_locked = true; // (front(0) sized the partial sums; later fronts run beside a back half)
+    struct Unlock {
+      Dev &d;
+      ~Unlock() { d.part_locked = false; }
+    } unlock{*d};
     HIP_TRY(d->io_out.ensure(n));
     HIP_TRY(d->io_out2.ensure(std::max<size_t>(t, 1)));
     gn_eval *po = d_parent_out ? d_parent_out : d->io_out.p, *co = d_child_out ? d_child_out : d->io_out2.p;
