@@ -687,8 +687,7 @@ static int evaluate_on(gn_ctx *ctx, Dev &d, const gn_board *b, size_t n, int mod
   }
   auto mark = [&](int k) -> hipError_t { return ev ? hipEventRecord(ev[k], s) : hipSuccess; };
   const gn_eval_params &P = ctx->P;
-  HIP_TRY(mark(0));
-  if (mode == GN_MODE_FULL) HIP_TRY(launch_classify(b, n, P, nsm.p, nbg.p, s));
+  HIP_TRY(mark(0)); // (mode FULL's selection runs inside the small net's launch: launch_eval_net cls)
   const uint32_t *perm = nullptr;
   // a small batch (one game, a handful of in-check replies) gains nothing from the order and
   // would pay the sort's launches on its latency (bench.py secondary.dropin)
@@ -706,9 +705,8 @@ static int evaluate_on(gn_ctx *ctx, Dev &d, const gn_board *b, size_t n, int mod
   const int swz = (ctx->swizzle >> 1) & 1;
   HIP_TRY(mark(1));
   if (mode != GN_MODE_BIG)
-    HIP_TRY(launch_eval_net(d.net[SMALL], b, mode == GN_MODE_FULL ? nsm.p : nullptr, n, osm.p, perm, swz, s,
-                            mode == GN_MODE_SMALL ? rows_out : nullptr));
-  if (mode == GN_MODE_FULL) HIP_TRY(launch_reeval(osm.p, nsm.p, n, P, nbg.p, s));
+    HIP_TRY(launch_eval_net(d.net[SMALL], b, nullptr, n, osm.p, perm, swz, s, mode == GN_MODE_SMALL ? rows_out : nullptr,
+                            mode == GN_MODE_FULL ? &P : nullptr, nsm.p, nbg.p));
   HIP_TRY(mark(2));
   if (mode != GN_MODE_SMALL)
     HIP_TRY(launch_eval_net(d.net[BIG], b, mode == GN_MODE_FULL ? nbg.p : nullptr, n, obg.p, perm, swz, s,

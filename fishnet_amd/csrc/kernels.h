@@ -53,9 +53,13 @@ namespace gn {
 // perm (optional): slot q evaluates boards[perm[q]] and writes out[perm[q]].
 // swz: XCD-aware tile order (each XCD gets a contiguous range of tiles).
 // rows_out (optional): += FT rows the gather reads (common-row base counted once per tile).
+// cls (the small net, mode FULL): the kernel selects the positions itself (classify_kernel's rule:
+// need_small / need_big written for every position, need ignored) and applies reeval_kernel's rule to
+// the small net's outputs (need_big set where |nnue| < reeval_threshold): one launch for three.
 hipError_t launch_eval_net(const NetDevice &net, const gn_board *boards, const uint8_t *need, size_t n,
                            int2 *out, const uint32_t *perm, int swz, hipStream_t s,
-                           unsigned long long *rows_out = nullptr);
+                           unsigned long long *rows_out = nullptr, const gn_eval_params *cls = nullptr,
+                           uint8_t *need_small = nullptr, uint8_t *need_big = nullptr);
 // *out += position-sensitive checksum of bytes at p (caller zeroes *out)
 hipError_t launch_checksum(const void *p, size_t bytes, unsigned long long *out, hipStream_t s);
 // permutation of [0, n) ordering positions by (white king, black king) square, then

@@ -141,6 +141,23 @@ __device__ __forceinline__ void layer_stack_tile(const NetDevice &net, const uin
   }
 }
 
+// ----------------------------------------------------- material (Eval) --
+struct Material {
+  int pawns[2], npm[2];
+};
+
+__device__ __forceinline__ Material material(const Board &B, const gn_eval_params &P) {
+  Material m;
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const Bitboard o = B.byColor[c];
+    m.pawns[c] = popcnt(B.byType[PAWN] & o);
+    m.npm[c] = P.piece_value[1] * popcnt(B.byType[KNIGHT] & o) + P.piece_value[2] * popcnt(B.byType[BISHOP] & o) +
+               P.piece_value[3] * popcnt(B.byType[ROOK] & o) + P.piece_value[4] * popcnt(B.byType[QUEEN] & o);
+  }
+  return m;
+}
+
 // --------------------------------------------------------------- eval_net --
 // Workgroup = 2 * G * PAR threads, G = L1 / 16 threads per (position,
 // perspective): thread j of a perspective group owns accumulator columns
@@ -152,7 +169,8 @@ template <int L1, int PAR>
 __global__ void __launch_bounds__(2 * (L1 / 16) * PAR) __attribute__((amdgpu_waves_per_eu(PAR == 1 ? 1 : GN_SMALL_WPE)))
     eval_net_kernel(NetDevice net, const gn_board *__restrict__ boards, const uint8_t *__restrict__ need,
                     size_t n, int2 *__restrict__ out, const uint32_t *__restrict__ perm, unsigned tiles, int swz,
-                    unsigned long long *__restrict__ rows_out, unsigned tn) {
+                    unsigned long long *__restrict__ rows_out, unsigned tn, gn_eval_params P, int cls,
+                    uint8_t *__restrict__ need_small, uint8_t *__restrict__ need_big) {
   constexpr int G = L1 / 16;
   constexpr int NT = 2 * G * PAR;
   constexpr int NW = NT / 64;
@@ -202,7 +220,28 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR) __attribute__((amdgpu_wav
     const bool in = (unsigned)tid < tn && q < n;
     const size_t i = in ? (perm ? perm[q] : q) : 0;
     gn_board b = {};
-    if (in && (!need || need[i])) b = boards[i];
+    if (PAR > 1 && cls) {
+      // mode FULL's selection folded in (classify_kernel): the small net evaluates the positions
+      // whose |simple_eval| exceeds the threshold, the rest go to the big net; the small net's
+      // re-evaluation rule is applied where its outputs are written (emit, below)
+      if (in) {
+        Board B;
+        uint8_t sm = 0, bg = 0;
+        const gn_board g = boards[i];
+        if (unpack(g, B)) {
+          const Material m = material(B, P);
+          const int us = B.stm;
+          const int simple = P.piece_value[0] * (m.pawns[us] - m.pawns[us ^ 1]) + (m.npm[us] - m.npm[us ^ 1]);
+          sm = abs(simple) > P.small_net_threshold;
+          bg = !sm;
+        }
+        need_small[i] = sm;
+        need_big[i] = bg;
+        if (sm) b = g;
+      }
+    } else if (in && (!need || need[i])) {
+      b = boards[i];
+    }
     tb[tid] = b;
     tix[tid] = (uint32_t)i;
   }
@@ -371,7 +410,13 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR) __attribute__((amdgpu_wav
   // (48 k-steps); small net (2 k-steps): one wave per bucket present runs the whole stack
   // (layer_stack_wave: no LDS partial sums, no further barrier), the other waves are done
   auto valid = [&](int pos, int b) { return (unsigned)pos < tn && base + pos < n && nfeat[pos] && bkt[pos] == b; };
-  auto emit = [&](int pos, int2 v) { out[gidx[pos]] = v; };
+  auto emit = [&](int pos, int2 v) {
+    out[gidx[pos]] = v;
+    if (PAR > 1 && cls) { // (reeval_kernel's rule)
+      const int32_t nnue = wadd(wmul(P.psqt_weight, v.x), wmul(P.positional_weight, v.y)) / 128;
+      if (abs(nnue) < P.reeval_threshold) need_big[gidx[pos]] = 1;
+    }
+  };
   if constexpr (PAR == 1) {
     layer_stack_tile<L1, NW>(net, xt, scratch, psq, (int)threadIdx.x, bmask, valid, emit);
   } else {
@@ -682,7 +727,10 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR) __attribute__((amdgpu_wav
 }
 
 hipError_t launch_eval_net(const NetDevice &net, const gn_board *boards, const uint8_t *need, size_t n, int2 *out,
-                           const uint32_t *perm, int swz, hipStream_t s, unsigned long long *rows_out) {
+                           const uint32_t *perm, int swz, hipStream_t s, unsigned long long *rows_out,
+                           const gn_eval_params *cls, uint8_t *need_small, uint8_t *need_big) {
+  if (cls && (net.L1 != 128 || !need_small || !need_big)) return hipErrorInvalidValue;
+  const gn_eval_params P = cls ? *cls : gn_eval_params{};
   if (!n) return hipSuccess;
   // positions per workgroup: 16, or for a big net (positions one after another in phase 1) and a
   // batch of fewer than 32 k positions, as few as keep >= 2,048 workgroups (>= 2)
@@ -695,13 +743,13 @@ hipError_t launch_eval_net(const NetDevice &net, const gn_board *boards, const u
   const unsigned grid = swz ? 8 * ((tiles + 7) / 8) : tiles;
   if (net.L1 == 3072) {
     hipLaunchKernelGGL((eval_net_kernel<3072, 1>), dim3(grid), dim3(384), 0, s, net, boards, need, n, out, perm, tiles, swz,
-                       rows_out, tn);
+                       rows_out, tn, P, 0, nullptr, nullptr);
   } else if (net.L1 == 128) {
     hipLaunchKernelGGL((eval_net_kernel<128, 16>), dim3(grid), dim3(256), 0, s, net, boards, need, n, out, perm, tiles, swz,
-                       rows_out, tn);
+                       rows_out, tn, P, cls ? 1 : 0, need_small, need_big);
   } else if (net.L1 == 1024) {
     hipLaunchKernelGGL((eval_net_kernel<1024, 1>), dim3(grid), dim3(128), 0, s, net, boards, need, n, out, perm, tiles, swz,
-                       rows_out, tn);
+                       rows_out, tn, P, 0, nullptr, nullptr);
   } else {
     return hipErrorInvalidValue;
   }
@@ -709,22 +757,6 @@ hipError_t launch_eval_net(const NetDevice &net, const gn_board *boards, const u
 }
 
 // -------------------------------------------------------- Eval::evaluate --
-struct Material {
-  int pawns[2], npm[2];
-};
-
-__device__ __forceinline__ Material material(const Board &B, const gn_eval_params &P) {
-  Material m;
-#pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    const Bitboard o = B.byColor[c];
-    m.pawns[c] = popcnt(B.byType[PAWN] & o);
-    m.npm[c] = P.piece_value[1] * popcnt(B.byType[KNIGHT] & o) + P.piece_value[2] * popcnt(B.byType[BISHOP] & o) +
-               P.piece_value[3] * popcnt(B.byType[ROOK] & o) + P.piece_value[4] * popcnt(B.byType[QUEEN] & o);
-  }
-  return m;
-}
-
 __global__ void classify_kernel(const gn_board *__restrict__ boards, size_t n, gn_eval_params P,
                                 uint8_t *__restrict__ need_small, uint8_t *__restrict__ need_big) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1032,7 +1064,8 @@ hipError_t launch_score_replies_fill(const uint32_t *idx, size_t m, const uint64
 // One level of the score rule's replies for a small batch (the drop-in's gn_evaluate_batch,
 // gpu_nnue.hip FastBatch), as one workgroup and no host round trip: position i of boards (records
 // ev) is selected as score_select_kernel does (scored, in check, a legal move); off[i] = the
-// exclusive prefix of the selected positions' legal-move counts (off[n] = their total); the
+// exclusive prefix of the selected positions' legal-move counts (off[n] = their total; both
+// clamped to cap); the
 // replies, in gen_legal order, are rb / rm [off[i], off[i + 1]) -- the boards write_children
 // would make -- and every slot from the total to cap is an empty board (an invalid position for
 // the evaluation that follows, so that launches sized by cap need no count).  A total beyond cap
@@ -1076,7 +1109,11 @@ __global__ void __launch_bounds__(256) reply_level_kernel(const gn_board *__rest
 #pragma unroll 1
   for (uint32_t i = lo; i < hi; ++i) {
     const uint32_t cnt = (uint32_t)off[i];
-    off[i] = base;
+    // (offsets clamped to cap: past an overflow every position's range stays inside the reply
+    // buffers, so the launches after this one -- sized by cap, the call then rerun on the general
+    // path -- never read past them; unclamped, score_reduce_kernel read up to the uncapped total and
+    // faulted, round 6)
+    off[i] = base < cap ? base : cap;
     if (cnt) {
       Board B;
       unpack(boards[i], B);
@@ -1092,7 +1129,7 @@ __global__ void __launch_bounds__(256) reply_level_kernel(const gn_board *__rest
     base += cnt;
   }
   if (t == 0) {
-    off[n] = total;
+    off[n] = total < cap ? total : cap;
     if (first) *flag = total > cap ? 1u : 0u;
     else if (total > cap) atomicOr(flag, 1u);
   }
