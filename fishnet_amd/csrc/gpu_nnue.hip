@@ -203,7 +203,7 @@ struct EvalBufs {
 // makes a level's replies; every launch after it is sized by the level's capacity, its unused
 // slots empty boards, so nothing waits for a count), the two reductions, and the download of
 // the records with the overflow flag behind them.  One synchronisation per call.  A level with
-// more replies than its capacity (2 nb + 256, nb + 256: far beyond a game's) sets the flag and
+// more replies than its capacity (nb / 2 + 256, nb / 4 + 256: beyond a game's) sets the flag and
 // the call reruns on the general path.  Positions beyond n are empty boards (BAD_FEN records,
 // never read back).
 constexpr size_t FAST_NB0 = 128, FAST_MAX = 4096;
@@ -443,7 +443,7 @@ struct gn_ctx {
   } co;
   bool coalesce = true;
   bool fast_batch = true;                  // GN_OPT_FAST_BATCH
-  int pipeline = 1;                        // GN_OPT_EXPAND_PIPELINE (2: the next front beside the stream)
+  int pipeline = 2;                        // GN_OPT_EXPAND_PIPELINE (2: the next front beside the stream)
   std::atomic<uint64_t> graph_gen{0};      // bumped by every option / parameter change: the small-
                                            // batch graphs captured before it are rebuilt
   std::atomic<uint64_t> fast_runs{0}, fast_fallbacks{0};
@@ -1112,7 +1112,10 @@ static int for_each_device(gn_ctx *ctx, F &&f) {
 
 // A FastBatch for nb positions in mode: buffers, pinned staging, the captured graph (d.mu held).
 static int fast_build(gn_ctx *ctx, Dev &d, FastBatch &f, size_t nb, int mode) {
-  f.nb = nb, f.c1 = 2 * nb + 256, f.c2 = nb + 256, f.mode = mode, f.gen = ctx->graph_gen.load();
+  // reply capacities: a lichess game has ~4 % of its positions in check with ~4 replies each (a
+  // 128-position class: ~12 replies against 320); every launch after a level is sized by its
+  // capacity, so a smaller one is cheaper, and a batch beyond it reruns on the general path
+  f.nb = nb, f.c1 = nb / 2 + 256, f.c2 = nb / 4 + 256, f.mode = mode, f.gen = ctx->graph_gen.load();
   const size_t ne = std::max(nb, f.c1);
   HIP_TRY(hipHostMalloc((void **)&f.h_in, nb * sizeof(gn_board), hipHostMallocDefault));
   HIP_TRY(hipHostMalloc((void **)&f.h_out, (nb + 1) * sizeof(gn_eval), hipHostMallocDefault));

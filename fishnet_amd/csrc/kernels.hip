@@ -165,12 +165,13 @@ __device__ __forceinline__ Material material(const Board &B, const gn_eval_param
 // product needs no data exchange.  Big net: G = 192, PAR = 1 (384 threads, the
 // 16 positions of the tile one after another); small net: G = 8, PAR = 16
 // (256 threads, all 16 positions at once).
-template <int L1, int PAR>
+template <int L1, int PAR, bool CLS = false>
 __global__ void __launch_bounds__(2 * (L1 / 16) * PAR) __attribute__((amdgpu_waves_per_eu(PAR == 1 ? 1 : GN_SMALL_WPE)))
     eval_net_kernel(NetDevice net, const gn_board *__restrict__ boards, const uint8_t *__restrict__ need,
                     size_t n, int2 *__restrict__ out, const uint32_t *__restrict__ perm, unsigned tiles, int swz,
-                    unsigned long long *__restrict__ rows_out, unsigned tn, gn_eval_params P, int cls,
+                    unsigned long long *__restrict__ rows_out, unsigned tn, gn_eval_params P,
                     uint8_t *__restrict__ need_small, uint8_t *__restrict__ need_big) {
+  static_assert(!CLS || PAR > 1, "the folded selection is the small net's (mode FULL)");
   constexpr int G = L1 / 16;
   constexpr int NT = 2 * G * PAR;
   constexpr int NW = NT / 64;
@@ -220,7 +221,7 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR) __attribute__((amdgpu_wav
     const bool in = (unsigned)tid < tn && q < n;
     const size_t i = in ? (perm ? perm[q] : q) : 0;
     gn_board b = {};
-    if (PAR > 1 && cls) {
+    if (CLS) {
       // mode FULL's selection folded in (classify_kernel): the small net evaluates the positions
       // whose |simple_eval| exceeds the threshold, the rest go to the big net; the small net's
       // re-evaluation rule is applied where its outputs are written (emit, below)
@@ -412,7 +413,7 @@ __global__ void __launch_bounds__(2 * (L1 / 16) * PAR) __attribute__((amdgpu_wav
   auto valid = [&](int pos, int b) { return (unsigned)pos < tn && base + pos < n && nfeat[pos] && bkt[pos] == b; };
   auto emit = [&](int pos, int2 v) {
     out[gidx[pos]] = v;
-    if (PAR > 1 && cls) { // (reeval_kernel's rule)
+    if (CLS) { // (reeval_kernel's rule)
       const int32_t nnue = wadd(wmul(P.psqt_weight, v.x), wmul(P.positional_weight, v.y)) / 128;
       if (abs(nnue) < P.reeval_threshold) need_big[gidx[pos]] = 1;
     }
@@ -743,13 +744,17 @@ hipError_t launch_eval_net(const NetDevice &net, const gn_board *boards, const u
   const unsigned grid = swz ? 8 * ((tiles + 7) / 8) : tiles;
   if (net.L1 == 3072) {
     hipLaunchKernelGGL((eval_net_kernel<3072, 1>), dim3(grid), dim3(384), 0, s, net, boards, need, n, out, perm, tiles, swz,
-                       rows_out, tn, P, 0, nullptr, nullptr);
+                       rows_out, tn, P, nullptr, nullptr);
   } else if (net.L1 == 128) {
-    hipLaunchKernelGGL((eval_net_kernel<128, 16>), dim3(grid), dim3(256), 0, s, net, boards, need, n, out, perm, tiles, swz,
-                       rows_out, tn, P, cls ? 1 : 0, need_small, need_big);
+    if (cls)
+      hipLaunchKernelGGL((eval_net_kernel<128, 16, true>), dim3(grid), dim3(256), 0, s, net, boards, need, n, out, perm,
+                         tiles, swz, rows_out, tn, P, need_small, need_big);
+    else
+      hipLaunchKernelGGL((eval_net_kernel<128, 16>), dim3(grid), dim3(256), 0, s, net, boards, need, n, out, perm, tiles,
+                         swz, rows_out, tn, P, nullptr, nullptr);
   } else if (net.L1 == 1024) {
     hipLaunchKernelGGL((eval_net_kernel<1024, 1>), dim3(grid), dim3(128), 0, s, net, boards, need, n, out, perm, tiles, swz,
-                       rows_out, tn, P, 0, nullptr, nullptr);
+                       rows_out, tn, P, nullptr, nullptr);
   } else {
     return hipErrorInvalidValue;
   }

@@ -84,15 +84,16 @@ extern "C" {
                                          per call); 0: the general path (a launch sequence with
                                          a host round trip per reply level).  Results are
                                          identical either way.                              */
-#define GN_OPT_EXPAND_PIPELINE 10     /* 1 (default): consecutive planned expansions of one call
+#define GN_OPT_EXPAND_PIPELINE 10     /* 1: consecutive planned expansions of one call
                                          (gn_time_expand_device's iterations, the host-buffer
                                          pipeline's chunks) overlap: expansion k + 1's child
                                          generation and plan run on a second stream while
                                          expansion k's finalize and score rule run (two
-                                         buffer sets); 2: the next child generation and
-                                         plan start while expansion k's row stream still
-                                         runs; 0: one after another.  Results are identical
-                                         for every value.                                   */
+                                         buffer sets); 2 (default): the next child
+                                         generation and plan start while expansion k's row
+                                         stream still runs (151.3 against 153.9 ms per bench
+                                         step unpipelined); 0: one after another.  Results
+                                         are identical for every value.                     */
 #define GN_OPT_INCREMENTAL_CHILDREN 1 /* 1 (default): children from the parent accumulators
                                          by add/sub deltas; 0: full refresh per child    */
 #define GN_OPT_XCD_SWIZZLE 2          /* bit mask, default 9: each XCD takes a contiguous

@@ -759,8 +759,9 @@ def test_pipeline_chunks_equal_one_chunk(gpu_ctx):
     the device output buffers, the drain threads' downloads on the copy stream, chunk cuts at game
     starts) returns byte-identical results to one chunk: gn_evaluate_games with children (cuts at
     game starts, skipped positions inside chunks) and gn_expand_and_evaluate (cuts every 81), with
-    the chunks overlapped (GN_OPT_EXPAND_PIPELINE, the default: chunk c + 1's children and plan on
-    the second stream while chunk c finishes) and one after another."""
+    the chunks overlapped (GN_OPT_EXPAND_PIPELINE 1: chunk c + 1's children and plan on the second
+    stream while chunk c finishes; 2, the default: beside chunk c's row stream) and one after
+    another."""
     from fishnet_amd import gpu_nnue as G
     ucis = G.random_games_uci(0x5EED0123, 0, 40, 80)
     start = "rnbqkbnr/pppppppp/8/8/8/8/PPPPPPPP/RNBQKBNR w KQkq - 0 1"
@@ -769,17 +770,17 @@ def test_pipeline_chunks_equal_one_chunk(gpu_ctx):
     fens = [G.board_to_fen(b) for b in G.random_positions(0x5EED0456, 0, 700, 160)]
     try:
         out = {}
-        for chunk, pipe in ((0, 1), (100, 1), (250, 1), (100, 0), (250, 0), (100, 2)):
+        for chunk, pipe in ((0, 2), (100, 1), (250, 1), (100, 0), (250, 0), (100, 2), (250, 2)):
             gpu_ctx.set_option(G.OPT_CHUNK_PARENTS, chunk)
             gpu_ctx.set_option(G.OPT_EXPAND_PIPELINE, pipe)
             res = gpu_ctx.evaluate_games_arrays(arr, len(games), 0, children=True)
             out[chunk, pipe] = ([np.copy(x) for x in res[:6]], [np.copy(x) for x in gpu_ctx.expand_and_evaluate(fens, 1)])
-        for key in ((100, 1), (250, 1), (100, 0), (250, 0), (100, 2)):
-            for a, b in zip(out[0, 1][0] + out[0, 1][1], out[key][0] + out[key][1]):
+        for key in ((100, 1), (250, 1), (100, 0), (250, 0), (100, 2), (250, 2)):
+            for a, b in zip(out[0, 2][0] + out[0, 2][1], out[key][0] + out[key][1]):
                 assert a.tobytes() == b.tobytes(), key
     finally:
         gpu_ctx.set_option(G.OPT_CHUNK_PARENTS, 0)
-        gpu_ctx.set_option(G.OPT_EXPAND_PIPELINE, 1)
+        gpu_ctx.set_option(G.OPT_EXPAND_PIPELINE, 2)
 
 
 def test_concurrent_batches_coalesce(gpu_ctx):
@@ -1018,7 +1019,7 @@ def test_fast_batch_graph_equals_general_path(gpu_ctx, oracle_nets, oracle_lib):
     checks = [f for f, x in zip(pool, fl) if x & G.FLAG_IN_CHECK and not x & G.FLAG_NO_MOVES]
     assert len(checks) >= 50
     batches = games + [pool[:1], pool[:127], pool[:128], pool[:129], pool[:1000], pool[:4096], pool[:4097]]
-    overflow = (checks * 40)[:1000]  # 1,000 in-check positions: their replies exceed 2 * 1024 + 256
+    overflow = (checks * 40)[:1000]  # 1,000 in-check positions: their replies exceed 1024 / 2 + 256
 
     def run(fens, mode, fast):
         gpu_ctx.set_option(G.OPT_FAST_BATCH, fast)
@@ -1108,7 +1109,7 @@ def test_expand_pipeline_equals_serial(gpu_ctx, oracle_nets, oracle_lib):
         return tuple(gpu_ctx.checksum_device(out[b], nb) for b, nb in
                      (("po", n * G.EVAL_SIZE), ("off", (n + 1) * 4), ("mv", t * 2), ("co", t * G.EVAL_SIZE)))
 
-    assert gpu_ctx.get_option(G.OPT_EXPAND_PIPELINE) == 1
+    assert gpu_ctx.get_option(G.OPT_EXPAND_PIPELINE) == 2
     try:
         for mode in (1, 0):
             serial = run(1, 0, mode)
@@ -1117,8 +1118,8 @@ def test_expand_pipeline_equals_serial(gpu_ctx, oracle_nets, oracle_lib):
                 assert run(3, pipe, mode) == serial, (mode, pipe)
             assert run(3, 0, mode) == serial, mode
     finally:
-        gpu_ctx.set_option(G.OPT_EXPAND_PIPELINE, 1)
-    run(3, 1, 1)  # pipelined, mode BIG: sampled parents with all their children against the oracle
+        gpu_ctx.set_option(G.OPT_EXPAND_PIPELINE, 2)
+    run(3, 2, 1)  # pipelined, mode BIG: sampled parents with all their children against the oracle
     big, small = oracle_nets
     parents = d_b.download(G.BOARD_DTYPE, n)
     offs = out["off"].download(np.uint32, n + 1)
