@@ -618,7 +618,15 @@ static int create(const uint8_t *big, size_t big_len, const uint8_t *small, size
     HIP_TRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
     HIP_TRY(hipEventCreateWithFlags(&d.done, hipEventDisableTiming));
     HIP_TRY(hipStreamCreateWithFlags(&d.copy, hipStreamNonBlocking));
+#ifdef GN_AB_FRONT_PRIORITY // A/B: the pipeline's front stream at the device's highest priority
+    {
+      int least = 0, greatest = 0;
+      HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
+      HIP_TRY(hipStreamCreateWithPriority(&d.front, hipStreamNonBlocking, greatest));
+    }
+#else
     HIP_TRY(hipStreamCreateWithFlags(&d.front, hipStreamNonBlocking));
+#endif
     HIP_TRY(hipEventCreateWithFlags(&d.ev_streamed, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&d.ev_planned, hipEventDisableTiming));
     for (int i = 0; i < 2; ++i) HIP_TRY(hipEventCreateWithFlags(&d.cev[i], hipEventDisableTiming));
