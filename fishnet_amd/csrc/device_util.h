@@ -334,8 +334,10 @@ __device__ __forceinline__ int2 slice_finish_from(const NetDevice &net, const in
   uint32_t x[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
   for (int r = 0; r < 15; ++r) {
-    const long long s2 = ((long long)v[r] * v[r]) >> 19;
-    const uint32_t a = s2 < 127 ? (uint32_t)s2 : 127u, c = (uint32_t)clampi(v[r] >> 6, 0, 127);
+    // min(v^2 >> 19, 127) in 32 bits: |v| >= 8160 gives 127 (8160^2 >> 19 = 127, 8159^2 >> 19 =
+    // 126), so |v| clamped to 8160 squares below 2^26 -- one 24-bit multiply, no 64-bit product
+    const uint32_t u = v[r] < 0 ? 0u - (uint32_t)v[r] : (uint32_t)v[r], m = u < 8160u ? u : 8160u;
+    const uint32_t a = (m * m) >> 19, c = (uint32_t)clampi(v[r] >> 6, 0, 127);
     x[r >> 2] |= a << (8 * (r & 3));
     x[(15 + r) >> 2] |= c << (8 * ((15 + r) & 3));
   }

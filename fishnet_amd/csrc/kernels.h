@@ -29,6 +29,17 @@
 #ifndef GN_SCR_GAP // (the plan serves both streams: the deeper ring's distance)
 #define GN_SCR_GAP (GN_RING > GN_SLICE_RING ? GN_RING : GN_SLICE_RING)
 #endif
+// Workgroup size of the expansion's front kernels (count_children, child_moves, child_boards,
+// block_keys, plan_kernel).  The expansion pipeline runs them beside the row stream, whose
+// 2-wave workgroups hold every wave slot of a CU: a front workgroup is dispatched only where
+// enough stream workgroups have ended at once.  2 waves (128): per step 150.8 against 151.9 ms
+// with 4 (256) and 153.0 with 1 (64), which runs the front fully beside the stream and slows
+// the stream by as much (round 6, profiles/r06/ab_r06p_front_wg.log).
+#ifndef GN_FRONT_WG
+#define GN_FRONT_WG 128
+#endif
+static_assert(GN_FRONT_WG == 64 || GN_FRONT_WG == 128 || GN_FRONT_WG == 256, "front workgroups of 1, 2 or 4 waves");
+
 // Spare entries at the end of each block's entry region (plan_kernel, stream_eval_kernel): the
 // stream's scalar prefetch of the entries two ring revolutions ahead reads up to 2 * ring + 8 - 1
 // entries past its position, so a list ending at the region less the spares never reads past it.

@@ -1075,18 +1075,25 @@ hipError_t launch_score_replies_fill(const uint32_t *idx, size_t m, const uint64
 // would make -- and every slot from the total to cap is an empty board (an invalid position for
 // the evaluation that follows, so that launches sized by cap need no count).  A total beyond cap
 // sets *flag (the caller then takes the general path); first: *flag is set, else or'd.
-// 256 threads (a 1,024-thread version spilled 35 VGPRs around gen_legal and took 36 us per launch,
-// the drop-in's largest kernel); positions per thread <= 64 (n <= 16,384: level 2 takes level 1's
-// capacity, 2 * 4,096 + 256).  A thread's counts wait in off[] (its own entries) between the passes.
+// 256 threads (a 1,024-thread version spilled 35 VGPRs around gen_legal and took 36 us per launch);
+// positions per thread <= 64 (n <= 16,384: level 2 takes level 1's capacity, 2 * 4,096 + 256).
+// One move generation per position: a thread keeps its positions' legal moves (and which of its
+// positions each belongs to) in its LDS segment of MAXM entries, and after the scan every thread
+// makes the replies r = t, t + 256, ... -- the thread owning r by a binary search over the scan --
+// so that a position's ~30 do_move + pack run on 30 lanes, not one after another on one.  (Two
+// move generations and a serial write per in-check position took 40 us per launch, the drop-in's
+// largest kernel.)  A thread whose replies overflow its segment writes them itself, as before.
 __global__ void __launch_bounds__(256) reply_level_kernel(const gn_board *__restrict__ boards,
                                                            const gn_eval *__restrict__ ev, uint32_t n,
                                                            const Tables *__restrict__ tables, uint64_t *__restrict__ off,
                                                            uint32_t cap, gn_board *__restrict__ rb,
                                                            uint16_t *__restrict__ rm, uint32_t *__restrict__ flag,
                                                            int first) {
-  constexpr uint32_t NT = 256;
+  constexpr uint32_t NT = 256, MAXM = 64;
   __shared__ Tables T;
   __shared__ uint32_t part[NT];
+  __shared__ uint16_t smv[NT][MAXM]; // a thread's replies' moves ...
+  __shared__ uint8_t spos[NT][MAXM]; // ... and their positions (offsets from the thread's first)
   load_tables(T, tables);
   const uint32_t t = threadIdx.x, q = (n + NT - 1) / NT, lo = t * q, hi = lo + q < n ? lo + q : n;
   uint32_t c = 0;
@@ -1096,7 +1103,11 @@ __global__ void __launch_bounds__(256) reply_level_kernel(const gn_board *__rest
     const uint32_t f = ev[i].flags;
     if ((f & GN_FLAG_IN_CHECK) && !(f & (GN_FLAG_NO_MOVES | GN_FLAG_NO_SCORE | GN_FLAG_BAD_FEN))) {
       Board B;
-      if (unpack(boards[i], B)) gen_legal(B, T, [&](uint16_t) { ++cnt; });
+      if (unpack(boards[i], B))
+        gen_legal(B, T, [&](uint16_t m) {
+          if (c + cnt < MAXM) smv[t][c + cnt] = m, spos[t][c + cnt] = (uint8_t)(i - lo);
+          ++cnt;
+        });
     }
     off[i] = cnt;
     c += cnt;
@@ -1111,6 +1122,7 @@ __global__ void __launch_bounds__(256) reply_level_kernel(const gn_board *__rest
   }
   const uint32_t total = part[NT - 1];
   uint32_t base = part[t] - c;
+  const bool spill = c > MAXM;
 #pragma unroll 1
   for (uint32_t i = lo; i < hi; ++i) {
     const uint32_t cnt = (uint32_t)off[i];
@@ -1119,7 +1131,7 @@ __global__ void __launch_bounds__(256) reply_level_kernel(const gn_board *__rest
     // path -- never read past them; unclamped, score_reduce_kernel read up to the uncapped total and
     // faulted, round 6)
     off[i] = base < cap ? base : cap;
-    if (cnt) {
+    if (spill && cnt) { // this thread's replies did not fit its segment: made here, in order
       Board B;
       unpack(boards[i], B);
       uint32_t r = base;
@@ -1132,6 +1144,22 @@ __global__ void __launch_bounds__(256) reply_level_kernel(const gn_board *__rest
       });
     }
     base += cnt;
+  }
+  const uint32_t lim = total < cap ? total : cap;
+#pragma unroll 1
+  for (uint32_t r = t; r < lim; r += NT) {
+    uint32_t u = 0; // the first thread u with part[u] > r (part: inclusive, nondecreasing)
+#pragma unroll
+    for (uint32_t step = NT / 2; step; step >>= 1)
+      if (part[u + step - 1] <= r) u += step;
+    const uint32_t cu = part[u] - (u ? part[u - 1] : 0u);
+    if (cu > MAXM) continue; // (a spilled thread's, written above)
+    const uint32_t k = r - (part[u] - cu);
+    const uint16_t m = smv[u][k];
+    Board B;
+    unpack(boards[u * q + spos[u][k]], B);
+    pack(do_move(B, m, nullptr), rb[r]);
+    rm[r] = m;
   }
   if (t == 0) {
     off[n] = total < cap ? total : cap;
@@ -1295,12 +1323,17 @@ __global__ void child_boards_kernel(const gn_board *__restrict__ boards, size_t 
     nr = d.king_moved ? popcnt(C.byType[0]) + d.n_rem + d.n_add : 2 * (d.n_rem + d.n_add);
   }
   if (rows) { // one atomic per workgroup
-    __shared__ unsigned long long part[4];
+    __shared__ unsigned long long part[GN_FRONT_WG / 64];
 #pragma unroll
     for (int off = 32; off; off >>= 1) nr += __shfl_down(nr, off, 64);
     if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = nr;
     __syncthreads();
-    if (threadIdx.x == 0) atomicAdd(rows, part[0] + part[1] + part[2] + part[3]);
+    if (threadIdx.x == 0) {
+      unsigned long long t = 0;
+#pragma unroll
+      for (int w = 0; w < GN_FRONT_WG / 64; ++w) t += part[w];
+      atomicAdd(rows, t);
+    }
   }
 }
 
@@ -1476,7 +1509,7 @@ __global__ void offsets_u32_kernel(const uint64_t *__restrict__ in, size_t n, ui
 hipError_t launch_count_children(const gn_board *boards, size_t n, const Tables *tables, uint64_t *counts,
                                  hipStream_t s, uint64_t *ebound) {
   if (!n) return hipSuccess;
-  hipLaunchKernelGGL(count_children_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, boards, n, tables, counts,
+  hipLaunchKernelGGL(count_children_kernel, dim3(blocks_for(n, GN_FRONT_WG)), dim3(GN_FRONT_WG), 0, s, boards, n, tables, counts,
                      ebound);
   return hipGetLastError();
 }
@@ -1487,10 +1520,10 @@ hipError_t launch_write_children(const gn_board *boards, size_t n, const Tables 
                                  hipStream_t s, Board *unpacked) {
   if (!n) return hipSuccess;
   if (!moves || !owner) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(child_moves_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, boards, n, tables, offsets, moves,
+  hipLaunchKernelGGL(child_moves_kernel, dim3(blocks_for(n, GN_FRONT_WG)), dim3(GN_FRONT_WG), 0, s, boards, n, tables, offsets, moves,
                      owner, next_slot, chain_k, rows, unpacked);
   if (nc)
-    hipLaunchKernelGGL(child_boards_kernel, dim3(blocks_for(nc, 256)), dim3(256), 0, s, boards, c0, nc, moves, owner,
+    hipLaunchKernelGGL(child_boards_kernel, dim3(blocks_for(nc, GN_FRONT_WG)), dim3(GN_FRONT_WG), 0, s, boards, c0, nc, moves, owner,
                        children, deltas, rows, unpacked);
   return hipGetLastError();
 }
@@ -1596,7 +1629,7 @@ __global__ void block_keys_kernel(const gn_board *__restrict__ parents, size_t n
 hipError_t block_order(const gn_board *parents, size_t n, uint32_t K, uint32_t nblk, uint16_t *keys, uint32_t *idx,
                        uint16_t *keys_out, uint32_t *order, void *&temp, size_t &temp_bytes, hipStream_t s) {
   if (!nblk) return hipSuccess;
-  hipLaunchKernelGGL(block_keys_kernel, dim3(blocks_for(nblk, 256)), dim3(256), 0, s, parents, n, K, nblk, keys, idx);
+  hipLaunchKernelGGL(block_keys_kernel, dim3(blocks_for(nblk, GN_FRONT_WG)), dim3(GN_FRONT_WG), 0, s, parents, n, K, nblk, keys, idx);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   size_t need = 0;

@@ -108,7 +108,8 @@ __device__ int gn_fault_armed = 1;
 
 namespace gn {
 namespace ps {
-constexpr uint32_t H_K0 = 1u << 16, H_K1 = 1u << 17, H_LAST = 1u << 18, H_X = 1u << 19,
+// (bits 16-17 of the header word: the kind field HZ / HP / HB below)
+constexpr uint32_t H_LAST = 1u << 18, H_X = 1u << 19,
                    H_PAR_E = H_X | 1u << 20, H_KST = H_X | 1u << 21, H_LDS_SH = 22;
 constexpr uint32_t L_SCR = 1u << 31; // (in lo)
 // Each put site knows its entry's kind, so hi is a constant mask or'd with the slot / side
@@ -143,8 +144,9 @@ __device__ __forceinline__ void wave_sync() {
 } // namespace ps
 
 // ------------------------------------------------------------------- plan --
+constexpr int PLAN_WAVES = GN_FRONT_WG / 64; // one block per wave, no workgroup barriers
 template <int L1>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLAN_WPE)))
+__global__ void __launch_bounds__(GN_FRONT_WG) __attribute__((amdgpu_waves_per_eu(GN_PLAN_WPE)))
     plan_kernel(NetDevice net, const gn_board *__restrict__ parents, const uint64_t *__restrict__ offsets,
                 const ChildDelta *__restrict__ deltas, const uint8_t *__restrict__ need_parent,
                 const uint8_t *__restrict__ need_child, const uint8_t *__restrict__ next_slot, uint32_t np, uint32_t K,
@@ -153,13 +155,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GN_PLA
                 unsigned long long *__restrict__ pads_out, uint32_t *__restrict__ err, int2 *__restrict__ pinfo,
                 uint32_t xu, uint32_t hu) {
   using namespace ps;
-  __shared__ uint32_t ksnap[4][128][8]; // per wave: placement (64 nibbles) of each king-cache row
-  __shared__ uint16_t prow_s[4][2][32];
-  __shared__ uint32_t jrow_s[4][4][64]; // per wave: the first four jobs' (row + 1) | pos << 16 | cpc << 24, lane = square
+  __shared__ uint32_t ksnap[PLAN_WAVES][128][8]; // per wave: placement (64 nibbles) of each king-cache row
+  __shared__ uint16_t prow_s[PLAN_WAVES][2][32];
+  __shared__ uint32_t jrow_s[PLAN_WAVES][4][64]; // per wave: the first four jobs' (row + 1) | pos << 16 | cpc << 24, lane = square
   // (w via readfirstlane: the compiler then knows that blk, p and every bound derived from them
   // are wave-uniform, so they live in SGPRs and their branches are scalar)
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  const uint32_t blk = b0 + blockIdx.x * 4 + (uint32_t)w; // this launch plans blocks [b0, b1)
+  const uint32_t blk = b0 + blockIdx.x * PLAN_WAVES + (uint32_t)w; // this launch plans blocks [b0, b1)
   if (blk >= b1) return; // the whole wave (no workgroup barriers in this kernel)
   const __amdgpu_buffer_rsrc_t pst = __builtin_amdgcn_make_buffer_rsrc(
       (void *)net.psqt, 0, (int)((size_t)PSQT_BUCKETS * FT_ROWS * 4), 0x00020000);
@@ -1556,7 +1558,7 @@ hipError_t launch_plan_stream(const NetDevice &net, const gn_board *parents, siz
   const int scr = K > 1 && kc; // the king cache's rows (the chained walk itself needs no scratch)
   if (b1 > (n + K - 1) / K) return hipErrorInvalidValue;
   const uint32_t nb = (uint32_t)(b1 - b0), B0 = (uint32_t)b0, B1 = (uint32_t)b1;
-  const unsigned pg = (nb + 3) / 4, g = swz == 1 ? 8 * ((nb + 7) / 8) : nb + nb / 16 + 8; // (stream_eval_kernel: claims)
+  const unsigned pg = (nb + PLAN_WAVES - 1) / PLAN_WAVES, g = swz == 1 ? 8 * ((nb + 7) / 8) : nb + nb / 16 + 8; // (stream_eval_kernel: claims)
   if (net.L1 == 3072) {
     const bool sliced = slices == 3 && part && pinfo;
     if (do_plan) {
@@ -1564,7 +1566,7 @@ hipError_t launch_plan_stream(const NetDevice &net, const gn_board *parents, siz
         hipError_t e = hipMemsetAsync(pinfo, 0xFF, npos * sizeof(int2), s);
         if (e != hipSuccess) return e;
       }
-      hipLaunchKernelGGL((plan_kernel<3072>), dim3(pg), dim3(256), 0, s, net, parents, offsets, deltas, need_parent,
+      hipLaunchKernelGGL((plan_kernel<3072>), dim3(pg), dim3(GN_FRONT_WG), 0, s, net, parents, offsets, deltas, need_parent,
                          need_child, K > 1 ? next_slot : nullptr, (uint32_t)n, K, B0, B1, K > 1 ? kc : 0, eoff, ent,
                          tiles, btiles, rows_out, pads_out, err, sliced ? pinfo : nullptr,
                          sliced ? ps::field_xu(3072, 3) : ps::field_xu(3072, 1), sliced ? ps::field_hu(3072, 3) : ps::field_hu(3072, 1));
@@ -1589,7 +1591,7 @@ hipError_t launch_plan_stream(const NetDevice &net, const gn_board *parents, siz
     }
   } else if (net.L1 == 1024) {
     if (do_plan) {
-      hipLaunchKernelGGL((plan_kernel<1024>), dim3(pg), dim3(256), 0, s, net, parents, offsets, deltas, need_parent,
+      hipLaunchKernelGGL((plan_kernel<1024>), dim3(pg), dim3(GN_FRONT_WG), 0, s, net, parents, offsets, deltas, need_parent,
                          need_child, K > 1 ? next_slot : nullptr, (uint32_t)n, K, B0, B1, K > 1 ? kc : 0, eoff, ent,
                          tiles, btiles, rows_out, pads_out, err, nullptr, ps::field_xu(1024, 1), ps::field_hu(1024, 1));
       if (mid) (void)hipEventRecord(mid, s);

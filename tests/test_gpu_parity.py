@@ -1004,7 +1004,8 @@ def test_two_device_slots_games_at_scale(synth_big_path, synth_small_path, oracl
 def test_fast_batch_graph_equals_general_path(gpu_ctx, oracle_nets, oracle_lib):
     """The drop-in's small-batch graphs (GN_OPT_FAST_BATCH, gpu_nnue.hip FastBatch): one lichess
     game per call as GpuEvalStub sends it, batches at the size-class edges, every mode, a batch
-    whose in-check replies overflow the graph's capacity (rerun on the general path), and new
+    whose in-check replies overflow the graph's capacity (rerun on the general path), one whose
+    in-check positions are packed together (reply_level_kernel's per-thread overflow), and new
     eval params (the graphs are recaptured) -- every record equal to the general path's, and a
     sample of games against the oracle."""
     from fishnet_amd import gpu_nnue as G
@@ -1018,7 +1019,11 @@ def test_fast_batch_graph_equals_general_path(gpu_ctx, oracle_nets, oracle_lib):
     fl = gpu_ctx.evaluate_batch(pool, 1)["flags"]
     checks = [f for f, x in zip(pool, fl) if x & G.FLAG_IN_CHECK and not x & G.FLAG_NO_MOVES]
     assert len(checks) >= 50
-    batches = games + [pool[:1], pool[:127], pool[:128], pool[:129], pool[:1000], pool[:4096], pool[:4097]]
+    quiet = [f for f, x in zip(pool, fl) if not x & G.FLAG_IN_CHECK]
+    # in-check positions packed together: reply_level_kernel's threads hold 16 positions each at
+    # 4,096, so the first threads' replies overflow their LDS segments (written by the thread itself)
+    dense = (checks * 2)[:60] + quiet[:4096 - 60]
+    batches = games + [pool[:1], pool[:127], pool[:128], pool[:129], pool[:1000], pool[:4096], dense, pool[:4097]]
     overflow = (checks * 40)[:1000]  # 1,000 in-check positions: their replies exceed 1024 / 2 + 256
 
     def run(fens, mode, fast):
