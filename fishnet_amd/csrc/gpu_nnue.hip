@@ -221,10 +221,7 @@ struct FastBatch {
   DevBuf<uint16_t> m1, m2;
   DevBuf<int32_t> sv1, sv2;
   EvalBufs eb;
-  hipEvent_t fork[2] = {nullptr, nullptr}; // mode FULL: the big net on a branch of its own
   ~FastBatch() {
-    for (hipEvent_t e : fork)
-      if (e) (void)hipEventDestroy(e);
     if (exec) (void)hipGraphExecDestroy(exec);
     if (graph) (void)hipGraphDestroy(graph);
     if (h_in) (void)hipHostFree(h_in);
@@ -680,14 +677,9 @@ struct KernelTimes {
 // in-check ones) rather than child records; counts (optional): their legal-move counts.
 // eb (optional): the net outputs and selections in these buffers instead of the device's (the
 // drop-in's captured small-batch graphs own theirs, FastBatch); sort false: no king sort.
-// side / fork (optional, mode FULL): the big net runs on stream side for every position, beside
-// the small net instead of after it (fork: two events; finalize still takes each position's
-// output by the small net's selection, so the records are the same).  For the small-batch graphs,
-// whose launches are latency-bound: the small net leaves the big net's critical path.
 static int evaluate_on(gn_ctx *ctx, Dev &d, const gn_board *b, size_t n, int mode, gn_eval *out, hipStream_t s,
                        hipEvent_t *ev, unsigned long long *rows_out = nullptr, int score = 1,
-                       const uint64_t *counts = nullptr, EvalBufs *eb = nullptr, bool sort = true,
-                       hipStream_t side = nullptr, hipEvent_t *fork = nullptr) {
+                       const uint64_t *counts = nullptr, EvalBufs *eb = nullptr, bool sort = true) {
   if (mode < GN_MODE_FULL || mode > GN_MODE_SMALL) return fail(GN_E_INVALID, "bad mode %d", mode);
   if ((mode != GN_MODE_SMALL && !d.has[BIG]) || (mode != GN_MODE_BIG && !d.has[SMALL]))
     return fail(GN_E_NONET, "mode %d needs a network that is not loaded", mode);
@@ -720,20 +712,11 @@ static int evaluate_on(gn_ctx *ctx, Dev &d, const gn_board *b, size_t n, int mod
   }
   const int swz = (ctx->swizzle >> 1) & 1;
   HIP_TRY(mark(1));
-  const bool branch = side && fork && mode == GN_MODE_FULL;
-  if (branch) {
-    HIP_TRY(hipEventRecord(fork[0], s));
-    HIP_TRY(hipStreamWaitEvent(side, fork[0], 0));
-    HIP_TRY(launch_eval_net(d.net[BIG], b, nullptr, n, obg.p, perm, swz, side, rows_out));
-    HIP_TRY(hipEventRecord(fork[1], side));
-  }
   if (mode != GN_MODE_BIG)
     HIP_TRY(launch_eval_net(d.net[SMALL], b, nullptr, n, osm.p, perm, swz, s, mode == GN_MODE_SMALL ? rows_out : nullptr,
                             mode == GN_MODE_FULL ? &P : nullptr, nsm.p, nbg.p));
   HIP_TRY(mark(2));
-  if (branch)
-    HIP_TRY(hipStreamWaitEvent(s, fork[1], 0));
-  else if (mode != GN_MODE_SMALL)
+  if (mode != GN_MODE_SMALL)
     HIP_TRY(launch_eval_net(d.net[BIG], b, mode == GN_MODE_FULL ? nbg.p : nullptr, n, obg.p, perm, swz, s,
                             rows_out));
   HIP_TRY(mark(3));
@@ -1162,28 +1145,25 @@ static int fast_build(gn_ctx *ctx, Dev &d, FastBatch &f, size_t nb, int mode) {
   HIP_TRY(f.eb.nbg.ensure(ne));
   const hipStream_t s = d.stream;
   uint32_t *flag = reinterpret_cast<uint32_t *>(f.out.p + nb);
-#ifndef GN_AB_FAST_SERIAL_NETS // A/B: the big net after the small net, as the general path
-  hipStream_t side = d.front;
-  for (hipEvent_t &e : f.fork) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-#else
-  hipStream_t side = nullptr;
-#endif
+  // (round 6: the big net on a graph branch of its own, beside the small net, measured slower --
+  // p50 0.200 against 0.180 ms, the join's cross-queue wait costing more than the overlap gave)
   HIP_TRY(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
   auto seq = [&]() -> int {
     HIP_TRY(hipMemcpyAsync(f.in.p, f.h_in, nb * sizeof(gn_board), hipMemcpyHostToDevice, s));
-    int rc = evaluate_on(ctx, d, f.in.p, nb, mode, f.out.p, s, nullptr, nullptr, 1, nullptr, &f.eb, false, side, f.fork);
+    int rc = evaluate_on(ctx, d, f.in.p, nb, mode, f.out.p, s, nullptr, nullptr, 1, nullptr, &f.eb, false);
     if (rc) return rc;
     // level 1: the replies of the in-check positions; level 2: those of the replies in check
     HIP_TRY(launch_reply_level(f.in.p, f.out.p, nb, d.tables, f.off0.p, f.c1, f.r1.p, f.m1.p, flag, 1, s));
-    if ((rc = evaluate_on(ctx, d, f.r1.p, f.c1, mode, f.e1.p, s, nullptr, nullptr, 1, nullptr, &f.eb, false, side,
-                          f.fork)))
-      return rc;
+    if ((rc = evaluate_on(ctx, d, f.r1.p, f.c1, mode, f.e1.p, s, nullptr, nullptr, 1, nullptr, &f.eb, false))) return rc;
     HIP_TRY(launch_reply_level(f.r1.p, f.e1.p, f.c1, d.tables, f.off1.p, f.c2, f.r2.p, f.m2.p, flag, 0, s));
-    if ((rc = evaluate_on(ctx, d, f.r2.p, f.c2, mode, f.e2.p, s, nullptr, nullptr, 1, nullptr, &f.eb, false, side,
-                          f.fork)))
-      return rc;
+    if ((rc = evaluate_on(ctx, d, f.r2.p, f.c2, mode, f.e2.p, s, nullptr, nullptr, 1, nullptr, &f.eb, false))) return rc;
+#ifndef GN_AB_FAST_TWO_REDUCES // A/B: the two reductions as two launches
+    HIP_TRY(launch_score_reduce2(f.r1.p, f.c1, f.off1.p, f.m2.p, f.e2.p, f.sv2.p, f.e1.p, f.sv1.p, f.in.p, nb, f.off0.p,
+                                 f.m1.p, ctx->P, f.out.p, s));
+#else
     HIP_TRY(launch_score_reduce(f.r1.p, f.c1, nullptr, f.off1.p, f.m2.p, f.e2.p, f.sv2.p, ctx->P, f.e1.p, f.sv1.p, s));
     HIP_TRY(launch_score_reduce(f.in.p, nb, nullptr, f.off0.p, f.m1.p, f.e1.p, f.sv1.p, ctx->P, f.out.p, nullptr, s));
+#endif
     HIP_TRY(hipMemcpyAsync(f.h_out, f.out.p, (nb + 1) * sizeof(gn_eval), hipMemcpyDeviceToHost, s));
     return GN_OK;
   };

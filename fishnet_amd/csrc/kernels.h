@@ -187,6 +187,13 @@ hipError_t launch_score_replies_fill(const uint32_t *idx, size_t m, const uint64
 hipError_t launch_score_reduce(const gn_board *sb, size_t m, const uint32_t *idx, const uint64_t *off,
                                const uint16_t *moves, const gn_eval *ce, const int32_t *csv, const gn_eval_params &P,
                                gn_eval *out, int32_t *sv, hipStream_t s);
+// The small-batch graph's two reductions in one workgroup (idx NULL for both): level 1's positions
+// sb1 [0, m1) from their replies (moves2 / ce2 / csv2 at off1) into out1 / sv1, then level 0's sb0
+// [0, m0) from level 1's records and values (moves1 at off0) into out0.
+hipError_t launch_score_reduce2(const gn_board *sb1, size_t m1, const uint64_t *off1, const uint16_t *moves2,
+                                const gn_eval *ce2, const int32_t *csv2, gn_eval *out1, int32_t *sv1,
+                                const gn_board *sb0, size_t m0, const uint64_t *off0, const uint16_t *moves1,
+                                const gn_eval_params &P, gn_eval *out0, hipStream_t s);
 // One level of the score rule's replies for a small batch in one launch (reply_level_kernel,
 // kernels.hip): n <= 16,384 positions; replies into rb / rm [0, cap) (empty boards after the last),
 // off = n + 1 offsets; *flag set (first) / or'd when the replies exceed cap.

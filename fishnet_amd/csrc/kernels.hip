@@ -736,9 +736,12 @@ hipError_t launch_eval_net(const NetDevice &net, const gn_board *boards, const u
   // positions per workgroup: 16, or for a big net (positions one after another in phase 1) and a
   // batch of fewer than 32 k positions, as few as keep >= 2,048 workgroups (>= 2)
   unsigned tn = 16;
+#ifndef GN_TN_MIN
+#define GN_TN_MIN 2
+#endif
 #ifndef GN_AB_TN16 // A/B: 16 positions per workgroup at every batch size
   if (net.L1 != 128)
-    while (tn > 2 && (n + tn - 1) / tn < 2048) tn >>= 1;
+    while (tn > GN_TN_MIN && (n + tn - 1) / tn < 2048) tn >>= 1;
 #endif
   const unsigned tiles = (unsigned)((n + tn - 1) / tn);
   const unsigned grid = swz ? 8 * ((tiles + 7) / 8) : tiles;
@@ -951,14 +954,14 @@ __global__ void score_replies_kernel(const uint32_t *__restrict__ idx, size_t m,
 // value = max over the replies c of negate_ply(rule_value(c)) (ties: the smaller move), then
 // score / flags / best_move of selected position j; sv (optional) receives the value for
 // the level above
-__global__ void score_reduce_kernel(const gn_board *__restrict__ sb, size_t m, const uint32_t *__restrict__ idx,
-                                    const uint64_t *__restrict__ off, const uint16_t *__restrict__ moves,
-                                    const gn_eval *__restrict__ ce, const int32_t *__restrict__ csv,
-                                    gn_eval_params P, gn_eval *__restrict__ out, int32_t *__restrict__ sv) {
-  const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void score_reduce_one(size_t j, const gn_board *__restrict__ sb, const uint32_t *__restrict__ idx,
+                                                 const uint64_t *__restrict__ off, const uint16_t *__restrict__ moves,
+                                                 const gn_eval *__restrict__ ce, const int32_t *__restrict__ csv,
+                                                 const gn_eval_params &P, gn_eval *__restrict__ out,
+                                                 int32_t *__restrict__ sv) {
   // (idx NULL: every position j of sb, those without replies left as they are -- the drop-in's
   // small-batch path, reply_level_kernel, keeps positions in place instead of compacting them)
-  if (j >= m || off[j] == off[j + 1]) return;
+  if (off[j] == off[j + 1]) return;
   int32_t best = INT32_MIN;
   uint32_t bm = 0xFFFFu;
   for (uint64_t c = off[j]; c < off[j + 1]; ++c) {
@@ -977,6 +980,36 @@ __global__ void score_reduce_kernel(const gn_board *__restrict__ sb, size_t m, c
   e.best_move = (uint16_t)bm;
   out[i] = e;
   if (sv) sv[i] = best;
+}
+
+__global__ void score_reduce_kernel(const gn_board *__restrict__ sb, size_t m, const uint32_t *__restrict__ idx,
+                                    const uint64_t *__restrict__ off, const uint16_t *__restrict__ moves,
+                                    const gn_eval *__restrict__ ce, const int32_t *__restrict__ csv,
+                                    gn_eval_params P, gn_eval *__restrict__ out, int32_t *__restrict__ sv) {
+  const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j < m) score_reduce_one(j, sb, idx, off, moves, ce, csv, P, out, sv);
+}
+
+// Both reductions of the small-batch graph in one workgroup (its two launches, one after the
+// other, were ~12 us of a one-game call): level 1's positions (a, their replies' records from
+// level 2) and then, after a barrier, level 0's (b, from level 1's records and values the first
+// phase wrote -- the same workgroup, so the barrier orders them).
+struct ReduceLevel {
+  const gn_board *sb;
+  size_t m;
+  const uint64_t *off;
+  const uint16_t *moves;
+  const gn_eval *ce;
+  const int32_t *csv;
+  gn_eval *out;
+  int32_t *sv;
+};
+__global__ void __launch_bounds__(1024) score_reduce2_kernel(ReduceLevel a, ReduceLevel b, gn_eval_params P) {
+  for (size_t j = threadIdx.x; j < a.m; j += blockDim.x)
+    score_reduce_one(j, a.sb, nullptr, a.off, a.moves, a.ce, a.csv, P, a.out, a.sv);
+  __syncthreads();
+  for (size_t j = threadIdx.x; j < b.m; j += blockDim.x)
+    score_reduce_one(j, b.sb, nullptr, b.off, b.moves, b.ce, b.csv, P, b.out, b.sv);
 }
 
 static inline unsigned blocks_for(size_t n, int bs) { return (unsigned)((n + bs - 1) / bs); }
@@ -1174,6 +1207,15 @@ hipError_t launch_reply_level(const gn_board *boards, const gn_eval *ev, size_t 
   if (!n || n > 16384 || cap >= 0x80000000ull) return hipErrorInvalidValue;
   hipLaunchKernelGGL(reply_level_kernel, dim3(1), dim3(256), 0, s, boards, ev, (uint32_t)n, tables, off,
                      (uint32_t)cap, rb, rm, flag, first);
+  return hipGetLastError();
+}
+
+hipError_t launch_score_reduce2(const gn_board *sb1, size_t m1, const uint64_t *off1, const uint16_t *moves2,
+                                const gn_eval *ce2, const int32_t *csv2, gn_eval *out1, int32_t *sv1,
+                                const gn_board *sb0, size_t m0, const uint64_t *off0, const uint16_t *moves1,
+                                const gn_eval_params &P, gn_eval *out0, hipStream_t s) {
+  const ReduceLevel a = {sb1, m1, off1, moves2, ce2, csv2, out1, sv1}, b = {sb0, m0, off0, moves1, out1, sv1, out0, nullptr};
+  hipLaunchKernelGGL(score_reduce2_kernel, dim3(1), dim3(1024), 0, s, a, b, P);
   return hipGetLastError();
 }
 
