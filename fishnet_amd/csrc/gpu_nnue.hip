@@ -198,11 +198,12 @@ struct EvalBufs {
 // 36-47, src/main.rs:306-338: a chunk per worker call), ~80 positions, a few of them in check.
 // The general path costs ~20 launches and three host round trips per call (the score rule's
 // reply counts); on a one-device context a batch of <= 4,096 positions runs instead as one
-// captured HIP graph per (size class, mode): upload from pinned memory, the evaluation, both
-// levels of the in-check replies (reply_level_kernel: one workgroup selects, counts, scans and
-// makes a level's replies; every launch after it is sized by the level's capacity, its unused
-// slots empty boards, so nothing waits for a count), the two reductions, and the download of
-// the records with the overflow flag behind them.  One synchronisation per call.  A level with
+// captured HIP graph per (size class, mode): upload from pinned memory, both levels of the
+// in-check replies (reply_level_kernel: one workgroup selects from the boards, counts, scans and
+// makes a level's replies; the levels are sized by their capacities, unused slots empty boards,
+// so nothing waits for a count), one evaluation of the positions and both levels together, the
+// two reductions (one workgroup), and the download of the overflow flag and the records.  One
+// synchronisation per call.  A level with
 // more replies than its capacity (nb / 2 + 256, nb / 4 + 256: beyond a game's) sets the flag and
 // the call reruns on the general path.  Positions beyond n are empty boards (BAD_FEN records,
 // never read back).
@@ -214,9 +215,13 @@ struct FastBatch {
   hipGraph_t graph = nullptr;
   hipGraphExec_t exec = nullptr;
   gn_board *h_in = nullptr; // pinned: nb boards
-  gn_eval *h_out = nullptr; // pinned: nb records + one holding the overflow flag
-  DevBuf<gn_board> in, r1, r2;
-  DevBuf<gn_eval> out, e1, e2;
+  gn_eval *h_out = nullptr; // pinned: one record holding the overflow flag, then nb records
+  // the three levels one after another (in: nb boards, r1: c1 replies, r2: c2 replies of replies)
+  // and their records behind the flag record, so that one evaluation covers them all
+  DevBuf<gn_board> all;
+  DevBuf<gn_eval> rec;
+  gn_board *in = nullptr, *r1 = nullptr, *r2 = nullptr;
+  gn_eval *out = nullptr, *e1 = nullptr, *e2 = nullptr;
   DevBuf<uint64_t> off0, off1;
   DevBuf<uint16_t> m1, m2;
   DevBuf<int32_t> sv1, sv2;
@@ -226,7 +231,7 @@ struct FastBatch {
     if (graph) (void)hipGraphDestroy(graph);
     if (h_in) (void)hipHostFree(h_in);
     if (h_out) (void)hipHostFree(h_out);
-    in.release(), r1.release(), r2.release(), out.release(), e1.release(), e2.release();
+    all.release(), rec.release();
     off0.release(), off1.release(), m1.release(), m2.release(), sv1.release(), sv2.release();
     eb.release();
   }
@@ -1121,50 +1126,48 @@ static int for_each_device(gn_ctx *ctx, F &&f) {
 // A FastBatch for nb positions in mode: buffers, pinned staging, the captured graph (d.mu held).
 static int fast_build(gn_ctx *ctx, Dev &d, FastBatch &f, size_t nb, int mode) {
   // reply capacities: a lichess game has ~4 % of its positions in check with ~4 replies each (a
-  // 128-position class: ~12 replies against 320); every launch after a level is sized by its
-  // capacity, so a smaller one is cheaper, and a batch beyond it reruns on the general path
+  // 128-position class: ~12 replies against 320); the evaluation is sized by the capacities, so a
+  // smaller one is cheaper, and a batch beyond them reruns on the general path
   f.nb = nb, f.c1 = nb / 2 + 256, f.c2 = nb / 4 + 256, f.mode = mode, f.gen = ctx->graph_gen.load();
-  const size_t ne = std::max(nb, f.c1);
+  const size_t na = nb + f.c1 + f.c2;
   HIP_TRY(hipHostMalloc((void **)&f.h_in, nb * sizeof(gn_board), hipHostMallocDefault));
   HIP_TRY(hipHostMalloc((void **)&f.h_out, (nb + 1) * sizeof(gn_eval), hipHostMallocDefault));
-  HIP_TRY(f.in.ensure(nb));
-  HIP_TRY(f.out.ensure(nb + 1));
-  HIP_TRY(f.r1.ensure(f.c1));
-  HIP_TRY(f.e1.ensure(f.c1));
+  HIP_TRY(f.all.ensure(na));
+  HIP_TRY(f.rec.ensure(na + 1));
+  f.in = f.all.p, f.r1 = f.in + nb, f.r2 = f.r1 + f.c1;
+  f.out = f.rec.p + 1, f.e1 = f.out + nb, f.e2 = f.e1 + f.c1;
   HIP_TRY(f.m1.ensure(f.c1));
   HIP_TRY(f.sv1.ensure(f.c1));
-  HIP_TRY(f.r2.ensure(f.c2));
-  HIP_TRY(f.e2.ensure(f.c2));
   HIP_TRY(f.m2.ensure(f.c2));
   HIP_TRY(f.sv2.ensure(f.c2));
   HIP_TRY(f.off0.ensure(nb + 1));
   HIP_TRY(f.off1.ensure(f.c1 + 1));
-  HIP_TRY(f.eb.osm.ensure(ne));
-  HIP_TRY(f.eb.obg.ensure(ne));
-  HIP_TRY(f.eb.nsm.ensure(ne));
-  HIP_TRY(f.eb.nbg.ensure(ne));
+  HIP_TRY(f.eb.osm.ensure(na));
+  HIP_TRY(f.eb.obg.ensure(na));
+  HIP_TRY(f.eb.nsm.ensure(na));
+  HIP_TRY(f.eb.nbg.ensure(na));
   const hipStream_t s = d.stream;
-  uint32_t *flag = reinterpret_cast<uint32_t *>(f.out.p + nb);
+  uint32_t *flag = reinterpret_cast<uint32_t *>(f.rec.p);
   // (round 6: the big net on a graph branch of its own, beside the small net, measured slower --
   // p50 0.200 against 0.180 ms, the join's cross-queue wait costing more than the overlap gave)
   HIP_TRY(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
   auto seq = [&]() -> int {
-    HIP_TRY(hipMemcpyAsync(f.in.p, f.h_in, nb * sizeof(gn_board), hipMemcpyHostToDevice, s));
-    int rc = evaluate_on(ctx, d, f.in.p, nb, mode, f.out.p, s, nullptr, nullptr, 1, nullptr, &f.eb, false);
+    HIP_TRY(hipMemcpyAsync(f.in, f.h_in, nb * sizeof(gn_board), hipMemcpyHostToDevice, s));
+    // level 1: the replies of the in-check positions; level 2: those of the replies in check --
+    // both from the boards alone (the selection is board properties), so that one evaluation
+    // then covers the three levels (round 6: three evaluations, one per level, nine launches)
+    HIP_TRY(launch_reply_level(f.in, nb, d.tables, f.off0.p, f.c1, f.r1, f.m1.p, flag, 1, s));
+    HIP_TRY(launch_reply_level(f.r1, f.c1, d.tables, f.off1.p, f.c2, f.r2, f.m2.p, flag, 0, s));
+    int rc = evaluate_on(ctx, d, f.all.p, na, mode, f.out, s, nullptr, nullptr, 1, nullptr, &f.eb, false);
     if (rc) return rc;
-    // level 1: the replies of the in-check positions; level 2: those of the replies in check
-    HIP_TRY(launch_reply_level(f.in.p, f.out.p, nb, d.tables, f.off0.p, f.c1, f.r1.p, f.m1.p, flag, 1, s));
-    if ((rc = evaluate_on(ctx, d, f.r1.p, f.c1, mode, f.e1.p, s, nullptr, nullptr, 1, nullptr, &f.eb, false))) return rc;
-    HIP_TRY(launch_reply_level(f.r1.p, f.e1.p, f.c1, d.tables, f.off1.p, f.c2, f.r2.p, f.m2.p, flag, 0, s));
-    if ((rc = evaluate_on(ctx, d, f.r2.p, f.c2, mode, f.e2.p, s, nullptr, nullptr, 1, nullptr, &f.eb, false))) return rc;
 #ifndef GN_AB_FAST_TWO_REDUCES // A/B: the two reductions as two launches
-    HIP_TRY(launch_score_reduce2(f.r1.p, f.c1, f.off1.p, f.m2.p, f.e2.p, f.sv2.p, f.e1.p, f.sv1.p, f.in.p, nb, f.off0.p,
-                                 f.m1.p, ctx->P, f.out.p, s));
+    HIP_TRY(launch_score_reduce2(f.r1, f.c1, f.off1.p, f.m2.p, f.e2, f.sv2.p, f.e1, f.sv1.p, f.in, nb, f.off0.p, f.m1.p,
+                                 ctx->P, f.out, s));
 #else
-    HIP_TRY(launch_score_reduce(f.r1.p, f.c1, nullptr, f.off1.p, f.m2.p, f.e2.p, f.sv2.p, ctx->P, f.e1.p, f.sv1.p, s));
-    HIP_TRY(launch_score_reduce(f.in.p, nb, nullptr, f.off0.p, f.m1.p, f.e1.p, f.sv1.p, ctx->P, f.out.p, nullptr, s));
+    HIP_TRY(launch_score_reduce(f.r1, f.c1, nullptr, f.off1.p, f.m2.p, f.e2, f.sv2.p, ctx->P, f.e1, f.sv1.p, s));
+    HIP_TRY(launch_score_reduce(f.in, nb, nullptr, f.off0.p, f.m1.p, f.e1, f.sv1.p, ctx->P, f.out, nullptr, s));
 #endif
-    HIP_TRY(hipMemcpyAsync(f.h_out, f.out.p, (nb + 1) * sizeof(gn_eval), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(f.h_out, f.rec.p, (nb + 1) * sizeof(gn_eval), hipMemcpyDeviceToHost, s));
     return GN_OK;
   };
   const int rc = seq();
@@ -1208,13 +1211,13 @@ static int fast_run(gn_ctx *ctx, Dev &d, const gn_board *boards, size_t n, int m
     HIP_TRY(sg.finish());
   }
   uint32_t flag;
-  memcpy(&flag, f.h_out + nb, sizeof(flag));
+  memcpy(&flag, f.h_out, sizeof(flag));
   ++ctx->fast_runs;
   if (flag) {
     ++ctx->fast_fallbacks;
     return GN_OK;
   }
-  memcpy(out, f.h_out, n * sizeof(gn_eval));
+  memcpy(out, f.h_out + 1, n * sizeof(gn_eval));
   *done = true;
   return GN_OK;
 }

@@ -195,10 +195,11 @@ hipError_t launch_score_reduce2(const gn_board *sb1, size_t m1, const uint64_t *
                                 const gn_board *sb0, size_t m0, const uint64_t *off0, const uint16_t *moves1,
                                 const gn_eval_params &P, gn_eval *out0, hipStream_t s);
 // One level of the score rule's replies for a small batch in one launch (reply_level_kernel,
-// kernels.hip): n <= 16,384 positions; replies into rb / rm [0, cap) (empty boards after the last),
-// off = n + 1 offsets; *flag set (first) / or'd when the replies exceed cap.
-hipError_t launch_reply_level(const gn_board *boards, const gn_eval *ev, size_t n, const Tables *tables, uint64_t *off,
-                              size_t cap, gn_board *rb, uint16_t *rm, uint32_t *flag, int first, hipStream_t s);
+// kernels.hip): n <= 16,384 positions, selected from their boards (valid, in check, a legal move);
+// replies into rb / rm [0, cap) (empty boards after the last), off = n + 1 offsets; *flag set
+// (first) / or'd when the replies exceed cap.
+hipError_t launch_reply_level(const gn_board *boards, size_t n, const Tables *tables, uint64_t *off, size_t cap,
+                              gn_board *rb, uint16_t *rm, uint32_t *flag, int first, hipStream_t s);
 // legal-move counts per board (invalid boards: 0); ebound (optional): per parent an
 // upper bound of the planned expansion's list entries (stream.hip)
 hipError_t launch_count_children(const gn_board *boards, size_t n, const Tables *tables, uint64_t *counts,

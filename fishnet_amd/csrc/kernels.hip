@@ -735,10 +735,11 @@ hipError_t launch_eval_net(const NetDevice &net, const gn_board *boards, const u
   if (!n) return hipSuccess;
   // positions per workgroup: 16, or for a big net (positions one after another in phase 1) and a
   // batch of fewer than 32 k positions, as few as keep >= 2,048 workgroups (>= 2; 1 for a batch of
-  // <= 512 positions, the drop-in's one game per call: p50 0.176 -> 0.169 ms, r06s)
+  // <= 1,024 positions, the drop-in's one game per call with its reply levels: p50 0.176 -> 0.169
+  // ms, r06s)
   unsigned tn = 16;
 #ifndef GN_TN_MIN
-#define GN_TN_MIN (n <= 512 ? 1u : 2u)
+#define GN_TN_MIN (n <= 1024 ? 1u : 2u)
 #endif
 #ifndef GN_AB_TN16 // A/B: 16 positions per workgroup at every batch size
   if (net.L1 != 128)
@@ -1101,8 +1102,10 @@ hipError_t launch_score_replies_fill(const uint32_t *idx, size_t m, const uint64
 }
 
 // One level of the score rule's replies for a small batch (the drop-in's gn_evaluate_batch,
-// gpu_nnue.hip FastBatch), as one workgroup and no host round trip: position i of boards (records
-// ev) is selected as score_select_kernel does (scored, in check, a legal move); off[i] = the
+// gpu_nnue.hip FastBatch), as one workgroup and no host round trip: position i of boards is
+// selected as score_select_kernel selects its record -- a valid board, in check, with a legal
+// move (every position of the graph is a scored one) -- from the board alone, so that the levels
+// need no evaluation before them; off[i] = the
 // exclusive prefix of the selected positions' legal-move counts (off[n] = their total; both
 // clamped to cap); the
 // replies, in gen_legal order, are rb / rm [off[i], off[i + 1]) -- the boards write_children
@@ -1117,8 +1120,7 @@ hipError_t launch_score_replies_fill(const uint32_t *idx, size_t m, const uint64
 // so that a position's ~30 do_move + pack run on 30 lanes, not one after another on one.  (Two
 // move generations and a serial write per in-check position took 40 us per launch, the drop-in's
 // largest kernel.)  A thread whose replies overflow its segment writes them itself, as before.
-__global__ void __launch_bounds__(256) reply_level_kernel(const gn_board *__restrict__ boards,
-                                                           const gn_eval *__restrict__ ev, uint32_t n,
+__global__ void __launch_bounds__(256) reply_level_kernel(const gn_board *__restrict__ boards, uint32_t n,
                                                            const Tables *__restrict__ tables, uint64_t *__restrict__ off,
                                                            uint32_t cap, gn_board *__restrict__ rb,
                                                            uint16_t *__restrict__ rm, uint32_t *__restrict__ flag,
@@ -1134,15 +1136,12 @@ __global__ void __launch_bounds__(256) reply_level_kernel(const gn_board *__rest
 #pragma unroll 1
   for (uint32_t i = lo; i < hi; ++i) {
     uint32_t cnt = 0;
-    const uint32_t f = ev[i].flags;
-    if ((f & GN_FLAG_IN_CHECK) && !(f & (GN_FLAG_NO_MOVES | GN_FLAG_NO_SCORE | GN_FLAG_BAD_FEN))) {
-      Board B;
-      if (unpack(boards[i], B))
-        gen_legal(B, T, [&](uint16_t m) {
-          if (c + cnt < MAXM) smv[t][c + cnt] = m, spos[t][c + cnt] = (uint8_t)(i - lo);
-          ++cnt;
-        });
-    }
+    Board B;
+    if (unpack(boards[i], B) && in_check(B, T))
+      gen_legal(B, T, [&](uint16_t m) {
+        if (c + cnt < MAXM) smv[t][c + cnt] = m, spos[t][c + cnt] = (uint8_t)(i - lo);
+        ++cnt;
+      });
     off[i] = cnt;
     c += cnt;
   }
@@ -1203,10 +1202,10 @@ __global__ void __launch_bounds__(256) reply_level_kernel(const gn_board *__rest
   for (uint32_t r = total + t; r < cap; r += NT) rb[r] = gn_board{};
 }
 
-hipError_t launch_reply_level(const gn_board *boards, const gn_eval *ev, size_t n, const Tables *tables, uint64_t *off,
-                              size_t cap, gn_board *rb, uint16_t *rm, uint32_t *flag, int first, hipStream_t s) {
+hipError_t launch_reply_level(const gn_board *boards, size_t n, const Tables *tables, uint64_t *off, size_t cap,
+                              gn_board *rb, uint16_t *rm, uint32_t *flag, int first, hipStream_t s) {
   if (!n || n > 16384 || cap >= 0x80000000ull) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(reply_level_kernel, dim3(1), dim3(256), 0, s, boards, ev, (uint32_t)n, tables, off,
+  hipLaunchKernelGGL(reply_level_kernel, dim3(1), dim3(256), 0, s, boards, (uint32_t)n, tables, off,
                      (uint32_t)cap, rb, rm, flag, first);
   return hipGetLastError();
 }
