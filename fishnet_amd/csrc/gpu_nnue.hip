@@ -214,6 +214,8 @@ struct FastBatch {
   uint64_t gen = 0;
   hipGraph_t graph = nullptr;
   hipGraphExec_t exec = nullptr;
+  hipEvent_t done = nullptr; // recorded behind each launch (the caller waits for it without d.mu)
+  bool busy = false;         // a launch of this instance is in flight (d.mu)
   gn_board *h_in = nullptr; // pinned: nb boards
   gn_eval *h_out = nullptr; // pinned: one record holding the overflow flag, then nb records
   // the three levels one after another (in: nb boards, r1: c1 replies, r2: c2 replies of replies)
@@ -227,6 +229,7 @@ struct FastBatch {
   DevBuf<int32_t> sv1, sv2;
   EvalBufs eb;
   ~FastBatch() {
+    if (done) (void)hipEventDestroy(done);
     if (exec) (void)hipGraphExecDestroy(exec);
     if (graph) (void)hipGraphDestroy(graph);
     if (h_in) (void)hipHostFree(h_in);
@@ -357,8 +360,10 @@ struct Dev {
   DevBuf<uint32_t> gidx;
   // stage times of the last host-buffer call on this device (GN_STAT_HOST_*), ms
   double t_upload = 0, t_replay = 0, t_compute = 0, t_download = 0, t_tail = 0;
-  // the drop-in's small-batch graphs (FastBatch): one per size class (128 << k positions) and mode
-  std::unique_ptr<FastBatch> fast[6][3];
+  // the drop-in's small-batch graphs (FastBatch): two per size class (128 << k positions) and mode,
+  // so that a second call's launch queues on the stream behind a first one in flight
+  std::unique_ptr<FastBatch> fast[6][3][2];
+  std::condition_variable fast_cv; // an instance's launch completed (its busy flag cleared; d.mu)
   // the expansion pipeline: the other buffer set, the front's stream and its two events (the
   // back's row stream done: the front may overwrite the plan's lists; the plan done)
   ExpSet alt;
@@ -424,6 +429,14 @@ struct SeqGuard { // seq_begin now, seq_end when the scope ends (d.mu held throu
   }
 };
 
+// Merged launches running at once (evaluate_coalesced).  Two (-DGN_MAX_LEADERS=2: a second
+// leader's launch queues on the stream behind the first's, the small-batch graphs having two
+// instances per class) measured the same 16-caller rate with 50 % more, smaller launches
+// (round 6, profiles/r06/dropin_ab_r06w.txt): one at a time.
+#ifndef GN_MAX_LEADERS
+#define GN_MAX_LEADERS 1
+#endif
+constexpr int MAX_LEADERS = GN_MAX_LEADERS;
 // One gn_evaluate_batch call waiting for, or in, a merged launch (evaluate_coalesced).
 struct BatchReq {
   const gn_board *boards;
@@ -432,6 +445,7 @@ struct BatchReq {
   gn_eval *out;
   int rc = GN_OK;
   bool done = false;
+  bool taken = false; // in a leader's launch (its thread waits for the result)
   char err[256] = ""; // (fixed size: copied while another caller's launch is marked busy, noexcept)
 };
 
@@ -443,7 +457,7 @@ struct gn_ctx {
     std::mutex mu;
     std::condition_variable cv;
     std::vector<BatchReq *> q; // calls waiting for a launch
-    bool busy = false;         // a launch is running
+    int active = 0;            // launches running (<= MAX_LEADERS)
     uint64_t launches = 0, calls = 0;
   } co;
   bool coalesce = true;
@@ -574,7 +588,8 @@ static void destroy(gn_ctx *ctx) {
     d.bkeys.release(), d.bkeys2.release(), d.bidx.release(), d.border.release();
     d.lv[0].release(), d.lv[1].release();
     for (auto &row : d.fast)
-      for (auto &f : row) f.reset();
+      for (auto &pair : row)
+        for (auto &f : pair) f.reset();
     for (int i = 0; i < 2; ++i) {
       d.po2[i].release(), d.co2[i].release(), d.cc2[i].release(), d.mv2[i].release();
       if (d.cev[i]) (void)hipEventDestroy(d.cev[i]);
@@ -1130,6 +1145,7 @@ static int fast_build(gn_ctx *ctx, Dev &d, FastBatch &f, size_t nb, int mode) {
   // smaller one is cheaper, and a batch beyond them reruns on the general path
   f.nb = nb, f.c1 = nb / 2 + 256, f.c2 = nb / 4 + 256, f.mode = mode, f.gen = ctx->graph_gen.load();
   const size_t na = nb + f.c1 + f.c2;
+  HIP_TRY(hipEventCreateWithFlags(&f.done, hipEventDisableTiming));
   HIP_TRY(hipHostMalloc((void **)&f.h_in, nb * sizeof(gn_board), hipHostMallocDefault));
   HIP_TRY(hipHostMalloc((void **)&f.h_out, (nb + 1) * sizeof(gn_eval), hipHostMallocDefault));
   HIP_TRY(f.all.ensure(na));
@@ -1183,17 +1199,22 @@ static int fast_build(gn_ctx *ctx, Dev &d, FastBatch &f, size_t nb, int mode) {
   return GN_OK;
 }
 
-// One small batch through its graph (one device, d.mu held).  *done = false: a reply level
-// overflowed and nothing was written (the caller runs the general path).
-static int fast_run(gn_ctx *ctx, Dev &d, const gn_board *boards, size_t n, int mode, gn_eval *out, bool *done) {
+// One small batch through its graph (one device; lk holds d.mu, released while the launch runs).
+// *done = false: a reply level overflowed and nothing was written (the caller runs the general
+// path).  With both instances of the class in flight, the call waits for one.
+static int fast_run(gn_ctx *ctx, Dev &d, std::unique_lock<std::mutex> &lk, const gn_board *boards, size_t n, int mode,
+                    gn_eval *out, bool *done) {
   *done = false;
   size_t nb = FAST_NB0;
   int k = 0;
   while (nb < n) nb <<= 1, ++k;
-  std::unique_ptr<FastBatch> &fp = d.fast[k][mode];
+  auto &inst = d.fast[k][mode];
+  auto busy = [&](int i) { return inst[i] && inst[i]->busy; };
+  while (busy(0) && busy(1)) d.fast_cv.wait(lk);
+  std::unique_ptr<FastBatch> &fp = inst[busy(0) ? 1 : 0];
   HIP_TRY(hipSetDevice(d.id));
   if (!fp || fp->gen != ctx->graph_gen.load()) {
-    if (fp) HIP_TRY(hipStreamSynchronize(d.stream)); // (its last launch is done: the call synchronised)
+    if (fp) HIP_TRY(hipEventSynchronize(fp->done)); // (its last launch is done: the call waited for it)
     fp.reset(new FastBatch());
     const int rc = fast_build(ctx, d, *fp, nb, mode);
     if (rc) {
@@ -1208,16 +1229,26 @@ static int fast_run(gn_ctx *ctx, Dev &d, const gn_board *boards, size_t n, int m
     SeqGuard sg(d, d.stream);
     HIP_TRY(sg.e);
     HIP_TRY(hipGraphLaunch(f.exec, d.stream));
-    HIP_TRY(sg.finish());
+    HIP_TRY(hipEventRecord(f.done, d.stream));
   }
-  uint32_t flag;
-  memcpy(&flag, f.h_out, sizeof(flag));
+  // wait without the device's lock: another call's launch queues behind this one meanwhile
+  f.busy = true;
+  lk.unlock();
+  const hipError_t e = hipEventSynchronize(f.done);
+  uint32_t flag = 1;
+  if (e == hipSuccess) {
+    memcpy(&flag, f.h_out, sizeof(flag));
+    if (!flag) memcpy(out, f.h_out + 1, n * sizeof(gn_eval));
+  }
+  lk.lock();
+  f.busy = false;
+  d.fast_cv.notify_all();
+  HIP_TRY(e);
   ++ctx->fast_runs;
   if (flag) {
     ++ctx->fast_fallbacks;
     return GN_OK;
   }
-  memcpy(out, f.h_out + 1, n * sizeof(gn_eval));
   *done = true;
   return GN_OK;
 }
@@ -1227,11 +1258,11 @@ static int evaluate_boards_host(gn_ctx *ctx, const gn_board *boards, size_t n, i
   if (!n) return GN_OK;
   if (ctx->fast_batch && n <= FAST_MAX && ctx->devs.size() == 1 && mode >= GN_MODE_FULL && mode <= GN_MODE_SMALL) {
     Dev &d = *ctx->devs[0];
-    std::lock_guard<std::mutex> lk(d.mu);
+    std::unique_lock<std::mutex> lk(d.mu);
     bool done = false;
     int rc;
     try {
-      rc = fast_run(ctx, d, boards, n, mode, out, &done);
+      rc = fast_run(ctx, d, lk, boards, n, mode, out, &done);
     } catch (const std::bad_alloc &) {
       rc = fail(GN_E_NOMEM, "host allocation failed");
     }
@@ -1295,7 +1326,7 @@ static int evaluate_coalesced(gn_ctx *ctx, const gn_board *boards, size_t n, int
     }
   } dq{C, &me};
   while (!me.done) {
-    if (C.busy) {
+    if (me.taken || C.active >= MAX_LEADERS) {
       C.cv.wait(lk);
       continue;
     }
@@ -1309,15 +1340,16 @@ static int evaluate_coalesced(gn_ctx *ctx, const gn_board *boards, size_t n, int
     }
     for (BatchReq *r : C.q) (r->mode == mode ? mine : rest).push_back(r);
     C.q.swap(rest);
-    C.busy = true;
+    for (BatchReq *r : mine) r->taken = true;
+    ++C.active;
     lk.unlock();
-    // from here to the re-lock nothing may throw outside the try block: C.busy is true and only
-    // this thread clears it
+    // from here to the re-lock nothing may throw outside the try block: this launch is counted in
+    // C.active and only this thread takes it out
     int rc = GN_OK;
     char err[256] = "";
     try {
-      if (mine.size() == 1) {
-        rc = evaluate_boards_host(ctx, me.boards, me.n, mode, me.out);
+      if (mine.size() == 1) { // (this call's own request: it was queued and not taken)
+        rc = evaluate_boards_host(ctx, mine[0]->boards, mine[0]->n, mode, mine[0]->out);
       } else {
         size_t tot = 0;
         for (BatchReq *r : mine) tot += r->n;
@@ -1339,7 +1371,7 @@ static int evaluate_coalesced(gn_ctx *ctx, const gn_board *boards, size_t n, int
     lk.lock();
     for (BatchReq *r : mine) r->rc = rc, memcpy(r->err, err, sizeof err), r->done = true;
     ++C.launches, C.calls += mine.size();
-    C.busy = false;
+    --C.active;
     C.cv.notify_all();
   }
   const int rc = me.rc;

@@ -786,12 +786,13 @@ def test_pipeline_chunks_equal_one_chunk(gpu_ctx):
 def test_concurrent_batches_coalesce(gpu_ctx):
     """16 threads calling gn_evaluate_batch at once on one context (fishnet's workers, one
     chunk each): the calls are merged into shared launches (GN_OPT_COALESCE) and every caller
-    gets exactly the records of a call on its own, with coalescing on and off."""
+    gets exactly the records of a call on its own, with coalescing on and off; the threads use all
+    three modes (merged launches of different modes run at once, two per class in flight)."""
     import threading
     from fishnet_amd import gpu_nnue as G
     lists = [[G.board_to_fen(b) for b in G.random_positions(0x5EED0900 + t, 0, 81, 160)] for t in range(16)]
     lists[3][5] = "not a fen"  # a bad FEN is flagged in its own call only
-    ref = [gpu_ctx.evaluate_batch(fl, 0) for fl in lists]
+    ref = [gpu_ctx.evaluate_batch(fl, t % 3) for t, fl in enumerate(lists)]
     assert ref[3][5]["flags"] & G.FLAG_BAD_FEN
     for coalesce in (1, 0):
         gpu_ctx.set_option(G.OPT_COALESCE, coalesce)
@@ -803,7 +804,7 @@ def test_concurrent_batches_coalesce(gpu_ctx):
             try:
                 go.wait()
                 for _ in range(4):
-                    got[t] = gpu_ctx.evaluate_batch(lists[t], 0)
+                    got[t] = gpu_ctx.evaluate_batch(lists[t], t % 3)
             except Exception as e:  # surfaced below
                 errs.append(e)
 
