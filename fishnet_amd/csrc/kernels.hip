@@ -1112,20 +1112,26 @@ hipError_t launch_score_replies_fill(const uint32_t *idx, size_t m, const uint64
 // would make -- and every slot from the total to cap is an empty board (an invalid position for
 // the evaluation that follows, so that launches sized by cap need no count).  A total beyond cap
 // sets *flag (the caller then takes the general path); first: *flag is set, else or'd.
-// 256 threads (a 1,024-thread version spilled 35 VGPRs around gen_legal and took 36 us per launch);
-// positions per thread <= 64 (n <= 16,384: level 2 takes level 1's capacity, 2 * 4,096 + 256).
+// GN_RL_THREADS threads (a 1,024-thread version spilled 35 VGPRs around gen_legal and took 36 us per
+// launch); positions per thread <= 16,384 / threads (n <= 16,384: level 2 takes level 1's capacity).
 // One move generation per position: a thread keeps its positions' legal moves (and which of its
 // positions each belongs to) in its LDS segment of MAXM entries, and after the scan every thread
-// makes the replies r = t, t + 256, ... -- the thread owning r by a binary search over the scan --
+// makes the replies r = t, t + NT, ... -- the thread owning r by a binary search over the scan --
 // so that a position's ~30 do_move + pack run on 30 lanes, not one after another on one.  (Two
 // move generations and a serial write per in-check position took 40 us per launch, the drop-in's
 // largest kernel.)  A thread whose replies overflow its segment writes them itself, as before.
-__global__ void __launch_bounds__(256) reply_level_kernel(const gn_board *__restrict__ boards, uint32_t n,
+// reply_level_kernel's workgroup: 512 threads (two positions per thread at the 1,024-position
+// class): p50 0.135 -> 0.130 ms, 16 coalesced callers 2.8 -> 3.15 M positions/s against 256
+// (round 6, profiles/r06/dropin_ab_r06x.txt); the LDS segments hold 16,384 moves either way
+#ifndef GN_RL_THREADS
+#define GN_RL_THREADS 512
+#endif
+__global__ void __launch_bounds__(GN_RL_THREADS) reply_level_kernel(const gn_board *__restrict__ boards, uint32_t n,
                                                            const Tables *__restrict__ tables, uint64_t *__restrict__ off,
                                                            uint32_t cap, gn_board *__restrict__ rb,
                                                            uint16_t *__restrict__ rm, uint32_t *__restrict__ flag,
                                                            int first) {
-  constexpr uint32_t NT = 256, MAXM = 64;
+  constexpr uint32_t NT = GN_RL_THREADS, MAXM = 16384 / NT;
   __shared__ Tables T;
   __shared__ uint32_t part[NT];
   __shared__ uint16_t smv[NT][MAXM]; // a thread's replies' moves ...
@@ -1205,7 +1211,7 @@ __global__ void __launch_bounds__(256) reply_level_kernel(const gn_board *__rest
 hipError_t launch_reply_level(const gn_board *boards, size_t n, const Tables *tables, uint64_t *off, size_t cap,
                               gn_board *rb, uint16_t *rm, uint32_t *flag, int first, hipStream_t s) {
   if (!n || n > 16384 || cap >= 0x80000000ull) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(reply_level_kernel, dim3(1), dim3(256), 0, s, boards, (uint32_t)n, tables, off,
+  hipLaunchKernelGGL(reply_level_kernel, dim3(1), dim3(GN_RL_THREADS), 0, s, boards, (uint32_t)n, tables, off,
                      (uint32_t)cap, rb, rm, flag, first);
   return hipGetLastError();
 }
