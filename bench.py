@@ -642,6 +642,8 @@ def run_dropin(c: Ctx, games: int, threads: int, calls_per_thread: int, check: i
     nn.set_option(G.OPT_COALESCE, 1)
     co = r[f"{threads}_callers_coalesced"]
     co["speedup_vs_serial"] = round(co["positions_per_s"] / r[f"{threads}_callers_serial"]["positions_per_s"], 3)
+    if c.world == 1:  # the same calls from native threads (tools/dropin_native.c): no interpreter lock
+        r[f"{threads}_callers_native"] = run_dropin_native(c, calls, threads, calls_per_thread)
     if check:  # the last records of sampled games (every game's last call wrote them) vs the oracle
         O, big, small = c.oracle_nets()
         idx = np.random.default_rng(55 + c.rank).choice(len(calls), size=min(check, len(calls)), replace=False)
@@ -651,6 +653,33 @@ def run_dropin(c: Ctx, games: int, threads: int, calls_per_thread: int, check: i
         r["oracle_check"] = {"games": len(idx), "positions": len(fens),
                              "mismatches": int(np.count_nonzero(got != exp)), "of": "the concurrent calls' records"}
     return r
+
+
+def run_dropin_native(c: Ctx, calls, threads: int, calls_per_thread: int):
+    """secondary.dropin's 16 callers as native threads: fishnet's workers call the C-ABI from Rust
+    with no interpreter lock between them, while the Python threads above hold the GIL around every
+    ctypes call.  tools/dropin_native.c (built by fishnet_amd/build.py) loads the same nets into its
+    own context on this GPU, checks every call's records against a single-threaded pass of the same
+    game, and times `threads` x `calls_per_thread` calls after a barrier (coalescing on)."""
+    import subprocess
+    import tempfile
+    from fishnet_amd import build, synthnet
+    exe = build.DROPIN_NATIVE
+    if not os.path.exists(exe):
+        return {"skipped": "tools/dropin_native.c not built (fishnet_amd/build.py build_dropin_native)"}
+    big_p, small_p, _ = synthnet.net_paths()
+    with tempfile.NamedTemporaryFile("w", suffix=".txt", delete=False) as f:
+        for x in calls:
+            f.write("|".join(x[3]) + "\n")
+        path = f.name
+    try:
+        p = subprocess.run([exe, big_p, small_p, path, str(threads), str(calls_per_thread), "1"], capture_output=True,
+                           text=True, timeout=180)
+    finally:
+        os.unlink(path)
+    if p.returncode:
+        raise RuntimeError(f"dropin_native failed ({p.returncode}): {p.stderr[-2000:]}")
+    return json.loads(p.stdout.strip().splitlines()[-1])
 
 
 def cpu_baseline_eval(c: Ctx, boards, mode, budget_s):

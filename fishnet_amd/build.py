@@ -114,6 +114,24 @@ def build_odd(force: bool = False, verbose: bool = False) -> str:
     return build(force=force, verbose=verbose, defines=ODD_DEFINES, out=ODD_LIB)
 
 
+DROPIN_NATIVE = os.path.join(LIBDIR, "dropin_native")
+
+
+def build_dropin_native(force: bool = False) -> str:
+    """tools/dropin_native.c (bench.py secondary.dropin's native 16-caller line) against the built
+    library; rebuilt when the source or the library is newer than the binary."""
+    lib = build()
+    src = os.path.join(os.path.dirname(HERE), "tools", "dropin_native.c")
+    out = DROPIN_NATIVE
+    if not force and os.path.exists(out) and os.path.getmtime(out) >= max(os.path.getmtime(src), os.path.getmtime(lib)):
+        return out
+    tmp = out + f".{os.getpid()}"
+    subprocess.run(["gcc", "-O2", "-std=gnu11", "-Wall", "-o", tmp, src, f"-L{LIBDIR}", "-lgpu_nnue", "-lpthread",
+                    "-Wl,-rpath,$ORIGIN", "-Wl,-rpath-link,/opt/rocm/lib"], check=True)
+    os.replace(tmp, out)
+    return out
+
+
 if __name__ == "__main__":
     defs = [a for a in sys.argv[1:] if a.startswith("-D")]
     outs = [a[len("--out="):] for a in sys.argv[1:] if a.startswith("--out=")]
